@@ -1,0 +1,63 @@
+"""Pin the CPU oracle (oracle/render_oracle.py) to the reference's golden vectors.
+
+The fixtures were produced by the reference's own code (tests/golden/gen_golden.py); the
+oracle restates that code op for op, so forward outputs and gradients must agree to fp32
+rounding of identical op graphs (in practice bit-exact).
+"""
+
+import pytest
+import torch
+
+from golden_io import RENDER_CASES, field_from, load
+from oracle import render_oracle as orc
+
+
+def _run_oracle(d, meta):
+    field = field_from(d, meta)
+    field.planes = field.planes.clone().requires_grad_()
+    field.palette = field.palette.clone().requires_grad_()
+    ncg = bool(meta['force_no_cam_grad'])
+    cam = d['cam'].clone().requires_grad_(not ncg)
+    focal = d.get('focal')
+    if focal is not None:
+        focal = focal.clone().requires_grad_(not ncg)
+    rgb, depth, mask = orc.render(field, meta['H'], meta['W'], cam, focal, d.get('center'),
+                                  d.get('bbox'), meta['S'], randomize=bool(meta['randomize']),
+                                  white_background=bool(meta['white_bg']),
+                                  force_no_cam_grad=ncg, u_coarse=d['u_coarse'],
+                                  u_fine=d['u_fine'])
+    loss = (rgb * d['g_rgb']).sum() + (mask * d['g_mask']).sum()
+    loss.backward()
+    return rgb, depth, mask, field, cam, focal
+
+
+@pytest.mark.parametrize('case', RENDER_CASES)
+def test_oracle_render_matches_reference(case):
+    d, meta = load(f'render_{case}')
+    rgb, depth, mask, field, cam, focal = _run_oracle(d, meta)
+    tol = dict(rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(rgb.detach(), d['rgb'], **tol)
+    torch.testing.assert_close(depth.detach(), d['depth'], **tol)
+    torch.testing.assert_close(mask.detach(), d['mask'], **tol)
+    torch.testing.assert_close(field.planes.grad, d['d_planes'], **tol)
+    torch.testing.assert_close(field.palette.grad, d['d_palette'], **tol)
+    if 'd_cam' in d:
+        torch.testing.assert_close(cam.grad, d['d_cam'], rtol=1e-5, atol=1e-5)
+    if 'd_focal' in d:
+        torch.testing.assert_close(focal.grad, d['d_focal'], rtol=1e-5, atol=1e-5)
+
+
+def test_oracle_near_far_matches_reference():
+    d, _ = load('stages')
+    near, far = orc.compute_near_far_planes(d['nf_ro'], d['nf_rd'], 1.4)
+    assert torch.equal(near, d['nf_near'])
+    assert torch.equal(far, d['nf_far'])
+
+
+def test_oracle_sample_pdf_matches_reference():
+    d, _ = load('stages')
+    S = d['pdf_bins'].shape[-1] + 1
+    det = orc.sample_pdf(d['pdf_bins'], d['pdf_w'], S, deterministic=True)
+    rnd = orc.sample_pdf(d['pdf_bins'], d['pdf_w'], S, deterministic=False, u=d['pdf_u'])
+    assert torch.equal(det, d['pdf_det'])
+    assert torch.equal(rnd, d['pdf_rnd'])
