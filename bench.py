@@ -1,0 +1,196 @@
+"""Benchmark of the nfi renderer on MI355X (driver contract: one JSON line from rank 0).
+
+Metric (BASELINE.json): Msamples/s of the renderer fwd+bwd at 128x128, 64 coarse + 64 fine
+samples per ray (sample = one radiance-field evaluation; 2,097,152 per 128^2 image).
+Workload (config 'p3d_fwdbwd', default): p3d_car setting (scene_range 1.4, perspective,
+camera_flipped, black background), B=8 images per GPU, the inversion step's renderer:
+rays -> coarse field -> sample_pdf -> fine field -> composite, then backward to the planes,
+the palette and the camera (pose).  Synthetic seeded inputs at the real sizes (planes
+[8,3,32,256,256] fp32).  The tri-plane producer (synthesis network) and the LPIPS loss are
+outside the timed path.
+
+One step = one fwd+bwd render of the per-GPU batch.  Multi-GPU: one process per GPU
+(torchrun), each rank renders its own images (weak scaling, no data-path collective).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, 'nerf-from-image_amd')):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # name: (scene_range, white_bg, flipped, B, H, S, pose_grad, backward)
+    'p3d_fwdbwd': (1.4, False, True, 8, 128, 64, True, True),
+    'p3d_fwd': (1.4, False, True, 8, 128, 64, False, False),            # BASELINE configs[1]
+    'shapenet_fwdbwd': (0.55, True, False, 16, 128, 64, False, True),   # BASELINE configs[2]
+    'imagenet_256': (1.4, False, True, 8, 256, 128, True, True),        # BASELINE configs[4] per GPU slice
+}
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s
+TAP_BYTES = 3 * 4 * 32 * 4  # 1,536 B per sample per tap pass
+
+
+def make_inputs(cfg, dev, seed):
+    from nfi.synthetic import inversion_batch
+    sr, wbg, flipped, B, H, S, pose, bwd = cfg
+    return inversion_batch(B, H, H, S, 256, sr, seed, flipped=flipped, device=dev)
+
+
+def run_step(nfi, batch, cfg, backward: bool):
+    sr, wbg, flipped, B, H, S, pose, bwd = cfg
+    f = batch['field']
+    f.planes.grad = None
+    f.palette.grad = None
+    cam = batch['cam'].detach().requires_grad_(pose and backward)
+    focal = batch['focal'].detach().requires_grad_(pose and backward)
+    rgb, depth, mask, _, _, _ = nfi.render(f, H, H, cam, focal, None, None, None, S, randomize=True)
+    if backward:
+        loss = (rgb * batch['g_rgb']).sum() + (mask * batch['g_mask']).sum()
+        loss.backward()
+    return rgb
+
+
+def cpu_baseline(args):
+    """The CPU oracle (oracle/render_oracle.py, the reference's op graph in PyTorch) timed on this
+    host's cores on a bounded sample of the same workload: ONE 128x128 image, 64+64 samples,
+    fwd+bwd with plane/palette/pose gradients."""
+    from oracle import render_oracle as orc
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from gpu_helpers import synthetic_inputs
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    H = args.cpu_res
+    inp, meta = synthetic_inputs(B=1, H=H, W=H, S=64, R=256, scene_range=1.4, seed=0)
+    field = orc.Field(planes=inp['planes'].clone().requires_grad_(), w1=inp['w1'], b1=inp['b1'],
+                      w2=inp['w2'], b2=inp['b2'], palette=inp['palette'].clone().requires_grad_(),
+                      alpha=inp['alpha'], beta=inp['beta'], scene_range=1.4)
+
+    def once():
+        cam = inp['cam'].clone().requires_grad_()
+        focal = inp['focal'].clone().requires_grad_()
+        rgb, depth, mask = orc.render(field, H, H, cam, focal, None, None, 64, randomize=True)
+        ((rgb * inp['g_rgb']).sum() + (mask * inp['g_mask']).sum()).backward()
+
+    once()  # warm-up
+    times = []
+    for _ in range(args.cpu_reps):
+        t0 = time.perf_counter()
+        once()
+        times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    samples = H * H * 128
+    model = ''
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {'value': samples / t / 1e6, 'unit': 'Msamples/s', 'cores': cores, 'kind': 'port',
+            'sample': f'1 image {H}x{H}, 64+64 samples/ray, fwd+bwd (planes, palette, pose grads), '
+                      f'median of {args.cpu_reps} after 1 warm-up; {model or platform.processor()}',
+            'seconds_per_image_step': t}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--config', default='p3d_fwdbwd', choices=sorted(CONFIGS))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-reps', type=int, default=2)
+    ap.add_argument('--cpu-res', type=int, default=128)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    import nfi
+    from nfi import ops
+    cfg = CONFIGS[args.config]
+    sr, wbg, flipped, B, H, S, pose, bwd = cfg
+    nfi.configure(scene_range=sr, white_background=wbg, fine_sampling=True)
+    batch = make_inputs(cfg, dev, seed=1234 + rank)
+
+    for _ in range(args.warmup):
+        run_step(nfi, batch, cfg, bwd)
+    torch.cuda.synchronize()
+    ops.KERNEL_TIMERS = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_step(nfi, batch, cfg, bwd)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
+    kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}  # ms/launch
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = B * H * H * 2 * S
+    value = world * samples_per_step * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # roofline of the dominant kernel (SURVEY §8(d) algorithmic tap bytes per sample)
+    per_sample = {'render_fwd': TAP_BYTES, 'render_bwd': TAP_BYTES * (2 if pose else 1)}
+    dom = max(kern, key=kern.get)
+    achieved = samples_per_step * per_sample[dom] / (kern[dom] * 1e-3) / 1e9
+    roof = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+            'bytes_per_sample': per_sample[dom], 'ms_per_launch': {k: round(v, 4) for k, v in kern.items()}}
+
+    out = {
+        'metric': 'Msamples/sec fwd+bwd (128^2, 64+64 samples/ray)' if bwd else 'Msamples/sec fwd (128^2, 64+64)',
+        'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+        'config': {'workload': args.config, 'global_batch': B * world, 'resolution': H,
+                   'samples_per_ray': f'{S}+{S}', 'plane_res': 256, 'pose_grad': pose,
+                   'backward': bwd, 'parallelism': f'dp{world} (one process per GPU, no collective)'},
+        'renderer_s_per_image_30step': round(30 * ms_per_step / 1e3 / B, 5),
+        'roofline': roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args)
+        out['cpu_baseline'] = cb
+        out['speedup_vs_cpu'] = round(value / cb['value'], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

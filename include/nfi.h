@@ -1,0 +1,145 @@
+/*
+ * nfi.h — C-ABI of the MI355X-native volume renderer for the SDF-NeRF inversion loop of
+ * yuliangguo/nerf-from-image (reference @ 2024-10-08).
+ *
+ * The reference has no FFI: its renderer is plain Python/PyTorch.  The seams this library
+ * replaces are:
+ *   render()                                run.py:176-350
+ *   nerf_utils.get_ray_bundle               lib/nerf_utils.py:28-93
+ *   nerf_utils.compute_near_far_planes      lib/nerf_utils.py:227-275
+ *   nerf_utils.compute_query_points_from_rays  lib/nerf_utils.py:96-122
+ *   Generator.forward's `sampler` closure   models/generator.py:587-681
+ *   TriplanarDecoder.forward                models/generator.py:301-331
+ *   nerf_utils.render_volume_density_weights_only + EG3D smoothing  nerf_utils.py:166-182, run.py:261-272
+ *   nerf_utils.sample_pdf                   lib/nerf_utils.py:185-224
+ *   sort/merge of coarse+fine samples       run.py:283-288, 312-319
+ *   nerf_utils.render_volume_density        lib/nerf_utils.py:125-163
+ * and their autograd backward passes.  INTEGRATION.md shows the ctypes binding the
+ * reference side would add (nerf-from-image_amd/nfi/_lib.py is that binding).
+ *
+ * Conventions: all pointers are DEVICE pointers to fp32 (unless stated), contiguous in the
+ * layout given; `stream` is a hipStream_t (NULL = default stream).  Functions are
+ * asynchronous on `stream`, allocate nothing, keep no state, and are safe to call from
+ * several host threads on different streams/devices.  Return 0 on success, a negative
+ * code on a bad argument (nothing launched) or a HIP launch failure; nfi_last_error()
+ * returns a thread-local message.
+ */
+#ifndef NFI_H
+#define NFI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NFI_ABI_VERSION 1
+#define NFI_DEC_SIZE 3088 /* floats in the packed decoder buffer */
+
+enum {
+  NFI_OK = 0,
+  NFI_EINVAL = -1,   /* bad argument / unsupported configuration */
+  NFI_ELAUNCH = -2,  /* HIP launch error */
+};
+
+/* Camera batch (nerf_utils.py:28-93): cam2world [B,4,4]; focal [B] (NULL = orthographic
+ * projection, nerf_utils.py:67-91); optional center [B,2] (:43-47) and bbox [B,2,2] (:52-56). */
+typedef struct nfi_camera {
+  const float* cam;
+  const float* focal;
+  const float* center;
+  const float* bbox;
+  int32_t B, H, W;
+  int32_t _pad;
+} nfi_camera;
+
+/* Radiance field (generator.py:288-331, 587-681; stylegan.py:148-180).
+ * planes: texel-major tri-planes; element (b, plane q, row y, col x, channel c) lives at
+ *   planes[b*sb + q*sq + (y*R + x)*st + c]   (c contiguous; 32 channels; q = xy, xz, yz).
+ * dec: packed, gain-scaled decoder from nfi_decoder_pack().
+ * palette: attention values [B,10,3] (AttentionMapper output, generator.py:455-462).
+ * inv_alpha = 1/Generator.alpha, beta = Generator.beta (generator.py:397-399, 629-636). */
+typedef struct nfi_field {
+  const float* planes;
+  int64_t sb, sq, st;
+  int32_t R;
+  int32_t _pad;
+  const float* dec;
+  const float* palette;
+  float inv_alpha, beta, scene_range;
+  int32_t _pad2;
+} nfi_field;
+
+/* One render call: rays of B images × HW pixels, S coarse samples (+ S fine if fine). */
+typedef struct nfi_render_args {
+  nfi_field field;
+  const float* ro;     /* [B*HW,3] ray origins */
+  const float* rd;     /* [B*HW,3] unit ray directions (after F.normalize, run.py:196) */
+  const float* near_;  /* [B*HW] */
+  const float* far_;   /* [B*HW] */
+  int32_t B, HW, S;
+  int32_t fine;        /* args.fine_sampling (run.py:259) */
+  int32_t white_bg;    /* dataset_config['white_background'] */
+  int32_t randomize;   /* stratified jitter + random u in sample_pdf (else linspace) */
+  uint64_t seed, offset;       /* Philox stream when u_* are NULL */
+  const float* u_coarse;       /* optional [B*HW,S] injected jitter (nerf_utils.py:120) */
+  const float* u_fine;         /* optional [B*HW,S] injected u (nerf_utils.py:202-205) */
+  /* forward outputs */
+  float* rgb;          /* [B*HW,3] */
+  float* depth;        /* [B*HW]   */
+  float* mask;         /* [B*HW]   */
+  /* per-ray state kept for backward: merged, sorted samples (N = fine ? 2S : S) */
+  float* t_saved;      /* [B*HW,N]   */
+  float* sigma_saved;  /* [B*HW,N]   */
+  float* rgb_saved;    /* [B*HW,3,N] */
+  float* z_coarse;     /* optional [B*HW,S] debug: coarse depths */
+  float* z_fine;       /* optional [B*HW,S] debug: fine depths, sorted */
+} nfi_render_args;
+
+typedef struct nfi_render_grad_args {
+  const float* g_rgb;   /* [B*HW,3] dL/d rgb  */
+  const float* g_mask;  /* [B*HW]   dL/d mask (depth carries no gradient, nerf_utils.py:151) */
+  float* d_planes;      /* same layout/strides as field.planes; ACCUMULATED into (zero it) */
+  float* d_palette_ray; /* [B*HW,30] per-ray partial dL/d palette (reduce with nfi_segment_sum) */
+  float* g_ro;          /* [B*HW,3] dL/d ray origins  (NULL: skip coordinate gradients) */
+  float* g_rd;          /* [B*HW,3] dL/d unit ray directions */
+} nfi_render_grad_args;
+
+int32_t nfi_abi_version(void);
+const char* nfi_last_error(void);
+
+/* EqualizedLinear parameters (stylegan.py:173-176) -> packed, gain-scaled decoder:
+ * W1s = w1*g1 [64,32], b1s = b1*gb, W2s = w2*g2 [11,64], b2s = b2*gb. */
+int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, const float* b2,
+                         float g1, float g2, float gb, float* dec, void* stream);
+
+/* [B,3,32,R,R] channel-major planes (generator.py:476-477) <-> texel-major [B,3,R,R,32]. */
+int32_t nfi_planes_to_texel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream);
+int32_t nfi_planes_to_channel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream);
+
+/* get_ray_bundle + F.normalize + compute_near_far_planes (run.py:193-200).
+ * Outputs ro, rd (unit) [B*H*W,3], near, far [B*H*W].  ws: 2 uint32 of device scratch. */
+int32_t nfi_rays_forward(const nfi_camera* cam, float scene_range, float* ro, float* rd,
+                         float* near_, float* far_, uint32_t* ws, void* stream);
+
+/* Backward of get_ray_bundle + F.normalize: g_ro, g_rd [B*H*W,3] -> per-pixel partials
+ * contrib [B*H*W,16] = {d cam[0..2][0..3] (12), d cam[3][3], d focal, 0, 0}. */
+int32_t nfi_rays_backward(const nfi_camera* cam, const float* g_ro, const float* g_rd,
+                          float* contrib, void* stream);
+
+/* out[b,k] = sum_m in[b,m,k]  (deterministic two-pass); ws >= B*64*K floats. */
+int32_t nfi_segment_sum(const float* in, int32_t B, int32_t M, int32_t K, float* out, float* ws,
+                        void* stream);
+
+/* Fused forward: stratified samples -> field -> coarse weights + EG3D smoothing -> sample_pdf
+ * -> fine samples -> field -> sort/merge -> compositing.  Supported S: 32, 64, 128
+ * (fine) or 32, 64, 128, 256 (no fine). */
+int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
+
+/* Fused backward of nfi_render_forward from its saved state (recomputes the field). */
+int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NFI_H */

@@ -1,0 +1,110 @@
+// nfi — MI355X-native volume renderer for the SDF-NeRF inversion loop of
+// yuliangguo/nerf-from-image.  Shared device helpers (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nfi {
+
+constexpr int WAVE = 64;
+constexpr int NC = 32;     // tri-plane channels (generator.py:476-477)
+constexpr int NH = 64;     // decoder hidden width (generator.py:293)
+constexpr int NO = 11;     // decoder outputs: 1 distance + 10 attention logits (generator.py:380-385)
+constexpr int NA = 10;     // attention values (palette rows)
+
+// Packed decoder: per hidden unit o a 48-float record {W1s[o][0..31], W2s^T[o][0..10], b1[o], pad}
+// so that one unit is three s_load_dwordx16 from a wave-uniform address; b2 follows.
+constexpr int DEC_UNIT = 48;
+constexpr int DEC_W2T = 32;
+constexpr int DEC_B1 = 43;
+constexpr int DEC_B2 = NH * DEC_UNIT;          // 11 floats
+constexpr int DEC_SIZE = DEC_B2 + 16;          // 3088 floats
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 64 lanes; result in every lane.  DPP inside rows of 16, then cross-row swaps.
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]  (xor 1)
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]  (xor 2)
+  v += dpp_mov<0x141>(v);   // row_half_mirror      (8-lane groups)
+  v += dpp_mov<0x140>(v);   // row_mirror           (16-lane rows)
+  v += __shfl_xor(v, 16);
+  auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(s[0]) + __int_as_float(s[1]);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+  for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Inclusive prefix sum / product over lanes 0..63 (Hillis-Steele).
+__device__ __forceinline__ float wave_incl_sum(float v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    float t = __shfl_up(v, d);
+    if (l >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ float wave_incl_prod(float v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    float t = __shfl_up(v, d);
+    if (l >= d) v *= t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float readlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// torch.sign
+__device__ __forceinline__ float tsign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
+
+// torch.lerp CPU formula (ATen Lerp.h): weight < 0.5 ? start + w*(end-start) : end - (end-start)*(1-w)
+__device__ __forceinline__ float tlerp(float a, float b, float w) {
+  return (fabsf(w) < 0.5f) ? a + w * (b - a) : b - (b - a) * (1.f - w);
+}
+
+// torch.linspace(0, 1, steps) element idx (ATen RangeFactoriesKernel: symmetric halves)
+__device__ __forceinline__ float tlinspace01(int idx, int steps) {
+  if (steps == 1) return 0.f;
+  const float step = 1.0f / (float)(steps - 1);
+  const int halfway = steps / 2;
+  return (idx < halfway) ? step * (float)idx : 1.0f - step * (float)(steps - idx - 1);
+}
+
+// Philox-4x32-10 counter-based RNG (Salmon et al. 2011) for randomize=True sampling.
+__device__ __forceinline__ uint4 philox4x32(uint4 ctr, uint2 key) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, ctr.x), lo0 = 0xD2511F53u * ctr.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, ctr.z), lo1 = 0xCD9E8D57u * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += 0x9E3779B9u;
+    key.y += 0xBB67AE85u;
+  }
+  return ctr;
+}
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// One uniform [0,1) per (ray, sample, stream) triple.
+__device__ __forceinline__ float rng_uniform(unsigned long long seed, unsigned long long offset,
+                                             long long ray, int sample, int stream) {
+  uint4 c = make_uint4((uint32_t)ray, (uint32_t)((unsigned long long)ray >> 32),
+                       (uint32_t)sample | ((uint32_t)stream << 24), (uint32_t)offset);
+  uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(offset >> 32));
+  return u01(philox4x32(c, k).x);
+}
+
+}  // namespace nfi

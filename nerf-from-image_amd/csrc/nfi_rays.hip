@@ -1,0 +1,422 @@
+// Ray bundle, near/far planes, their backward, per-image reductions, decoder packing and
+// plane layout conversion.  gfx950 (MI355X).  All kernels are simple per-element
+// HBM-streaming kernels; the hot path is nfi_render.hip.
+#include <string.h>
+#include <cmath>
+#include <string>
+
+#include "nfi_common.h"
+#include "nfi_host.h"
+
+namespace nfi {
+
+static thread_local std::string g_err;
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+// ---------------------------------------------------------------------------------------
+// Ray bundle (nerf_utils.py:28-93) + F.normalize (run.py:196) + slab test (nerf_utils.py:227-275)
+// ---------------------------------------------------------------------------------------
+
+struct PixelRay {
+  float dir[3];      // camera-space direction (perspective) or origin (ortho), before rotation
+  float ii, jj;      // pixel coordinates after center/bbox adjustment, before /focal
+};
+
+// Camera-space quantities of pixel (x, y) of image b, exactly as nerf_utils.py computes them.
+__device__ __forceinline__ void pixel_coords(const nfi_camera& c, int b, int x, int y, float& ii,
+                                             float& jj) {
+  ii = (float)x / (float)c.W;   // arange(W)/W  (meshgrid indexing='xy': ii varies along W)
+  jj = (float)y / (float)c.H;
+  if (c.focal) {
+    if (c.center) {
+      ii = ii - 0.5f * (2.f * c.center[b * 2 + 0] - 1.f) - 0.5f;
+      jj = jj - 0.5f * (2.f * c.center[b * 2 + 1] - 1.f) - 0.5f;
+    } else {
+      ii = ii - 0.5f;
+      jj = jj - 0.5f;
+    }
+    if (c.bbox) {
+      const float* bb = c.bbox + b * 4;   // bbox[b][i][j] = bb[i*2+j]
+      ii = (bb[2] * (ii + 0.5f) + bb[0]) * 0.5f;
+      jj = -(bb[3] * (-jj + 0.5f) + bb[1]) * 0.5f;
+    }
+  } else {
+    ii = (ii - 0.5f) * 2.f;
+    jj = (jj - 0.5f) * 2.f;
+    if (c.bbox) {
+      const float* bb = c.bbox + b * 4;
+      ii = bb[2] * (ii / 2.f + 0.5f) + bb[0];
+      jj = -(bb[3] * (-jj / 2.f + 0.5f) + bb[1]);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t fkey(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float fdecode(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+__global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, float* __restrict__ ro,
+                                                       float* __restrict__ rd, float* __restrict__ nearp,
+                                                       float* __restrict__ farp, uint32_t* __restrict__ ws,
+                                                       int* __restrict__ hitflag) {
+  const int HW = c.H * c.W;
+  const long long n = (long long)c.B * HW;
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  float nr = INFINITY, fr = -INFINITY;
+  bool hit = false;
+  if (r < n) {
+    const int b = (int)(r / HW);
+    const int p = (int)(r % HW);
+    const int y = p / c.W, x = p % c.W;
+    const float* M = c.cam + b * 16;
+    float ii, jj;
+    pixel_coords(c, b, x, y, ii, jj);
+    float o[3], d[3];
+    if (c.focal) {
+      const float f = c.focal[b];
+      ii = ii / f;
+      jj = jj / f;
+      const float dc[3] = {ii, -jj, -1.f};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        d[i] = dc[0] * M[i * 4 + 0] + dc[1] * M[i * 4 + 1] + dc[2] * M[i * 4 + 2];
+        o[i] = M[i * 4 + 3];
+      }
+    } else {
+      const float oc[3] = {ii, -jj, 0.f};
+      const float dc[3] = {0.f, 0.f, -1.f};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        o[i] = (oc[0] * M[i * 4 + 0] + oc[1] * M[i * 4 + 1] + oc[2] * M[i * 4 + 2]) + M[i * 4 + 3];
+        d[i] = (dc[0] * M[i * 4 + 0] + dc[1] * M[i * 4 + 1] + dc[2] * M[i * 4 + 2]) / M[15];
+      }
+    }
+    // F.normalize: x / max(||x||, 1e-12)
+    const float nrm = fmaxf(sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]), 1e-12f);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      d[i] = d[i] / nrm;
+      ro[r * 3 + i] = o[i];
+      rd[r * 3 + i] = d[i];
+    }
+    // slab test against [-sr, sr]^3 (nerf_utils.py:235-258)
+    float tmin[3], tmax[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float inv = 1.f / d[i];
+      const bool neg = inv < 0.f;
+      tmin[i] = ((neg ? sr : -sr) - o[i]) * inv;
+      tmax[i] = ((neg ? -sr : sr) - o[i]) * inv;
+    }
+    hit = !((tmin[0] > tmax[1]) || (tmin[1] > tmax[0]));
+    nr = fmaxf(tmin[0], tmin[1]);
+    fr = fminf(tmax[0], tmax[1]);
+    hit = hit && !((nr > tmax[2]) || (tmin[2] > fr));
+    nr = fmaxf(nr, tmin[2]);
+    fr = fminf(fr, tmax[2]);
+    nearp[r] = nr;
+    farp[r] = fr;
+    hitflag[r] = hit ? 1 : 0;
+  }
+  // min near / max far over hits of the whole call (nerf_utils.py:260-261)
+  uint32_t kmin = hit ? fkey(nr) : 0xFFFFFFFFu;
+  uint32_t kmax = hit ? fkey(fr) : 0u;
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (kmin != 0xFFFFFFFFu) atomicMin(ws + 0, kmin);
+    if (kmax != 0u) atomicMax(ws + 1, kmax);
+  }
+}
+
+__global__ void __launch_bounds__(256) rays_fix_kernel(long long n, float* __restrict__ nearp,
+                                                       float* __restrict__ farp,
+                                                       const uint32_t* __restrict__ ws,
+                                                       const int* __restrict__ hitflag) {
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  float nr = nearp[r], fr = farp[r];
+  if (!hitflag[r]) {
+    nr = fdecode(ws[0]);
+    fr = fdecode(ws[1]);
+  }
+  nr = fmaxf(nr, 0.1f);   // clamp_(min=0.1)  (nerf_utils.py:264-265)
+  fr = fmaxf(fr, 0.1f);
+  if ((fr - nr) < 1e-3f) fr = nr + 1e-3f;   // (nerf_utils.py:268-270)
+  nearp[r] = nr;
+  farp[r] = fr;
+}
+
+// Backward of get_ray_bundle + F.normalize; per-pixel partials of d cam / d focal.
+__global__ void __launch_bounds__(256) rays_bwd_kernel(nfi_camera c, const float* __restrict__ g_ro,
+                                                       const float* __restrict__ g_rd,
+                                                       float* __restrict__ contrib) {
+  const int HW = c.H * c.W;
+  const long long n = (long long)c.B * HW;
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int b = (int)(r / HW);
+  const int p = (int)(r % HW);
+  const int y = p / c.W, x = p % c.W;
+  const float* M = c.cam + b * 16;
+  float ii, jj;
+  pixel_coords(c, b, x, y, ii, jj);
+  float out[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) out[i] = 0.f;
+  float dc[3], d[3];
+  float f = 1.f;
+  if (c.focal) {
+    f = c.focal[b];
+    dc[0] = ii / f;
+    dc[1] = -(jj / f);
+    dc[2] = -1.f;
+  } else {
+    dc[0] = 0.f;
+    dc[1] = 0.f;
+    dc[2] = -1.f;
+  }
+  float u[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) u[i] = dc[0] * M[i * 4 + 0] + dc[1] * M[i * 4 + 1] + dc[2] * M[i * 4 + 2];
+  const float c33 = c.focal ? 1.f : M[15];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d[i] = u[i] / c33;
+  // normalize backward: g_raw = (g - y (y.g)) / n
+  const float nn = sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+  const float nrm = fmaxf(nn, 1e-12f);
+  float yv[3], g[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    yv[i] = d[i] / nrm;
+    g[i] = g_rd[r * 3 + i];
+  }
+  const float yg = yv[0] * g[0] + yv[1] * g[1] + yv[2] * g[2];
+  float graw[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) graw[i] = (nn > 1e-12f) ? (g[i] - yv[i] * yg) / nrm : g[i] / nrm;
+  const float gro[3] = {g_ro[r * 3 + 0], g_ro[r * 3 + 1], g_ro[r * 3 + 2]};
+  if (c.focal) {
+    // d = sum_k dc[k] M[i][k]
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) out[i * 4 + k] = graw[i] * dc[k];
+      out[i * 4 + 3] = gro[i];
+    }
+    float gdc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gdc[k] = graw[0] * M[0 * 4 + k] + graw[1] * M[1 * 4 + k] + graw[2] * M[2 * 4 + k];
+    // dc0 = ii/f, dc1 = -(jj/f)
+    out[13] = gdc[0] * (-(ii / f) / f) + gdc[1] * ((jj / f) / f);
+  } else {
+    const float oc[3] = {ii, -jj, 0.f};
+    float gu[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gu[i] = graw[i] / c33;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) out[i * 4 + k] = gro[i] * oc[k] + gu[i] * dc[k];
+      out[i * 4 + 3] = gro[i];
+    }
+    out[12] = -(graw[0] * u[0] + graw[1] * u[1] + graw[2] * u[2]) / (c33 * c33);
+  }
+  float4* o4 = reinterpret_cast<float4*>(contrib + r * 16);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o4[i] = make_float4(out[i * 4], out[i * 4 + 1], out[i * 4 + 2], out[i * 4 + 3]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Deterministic per-image reduction: out[b,k] = sum_m in[b,m,k]
+// ---------------------------------------------------------------------------------------
+constexpr int SEG_CHUNKS = 64;
+
+__global__ void __launch_bounds__(256) segsum_pass1(const float* __restrict__ in, int M, int K,
+                                                    float* __restrict__ part) {
+  __shared__ float red[256];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int rows = (M + SEG_CHUNKS - 1) / SEG_CHUNKS;
+  const int m0 = ch * rows, m1 = min(M, m0 + rows);
+  const int per = 256 / K;             // threads per k
+  const int tid = threadIdx.x;
+  const int k = tid % K, s = tid / K;
+  float acc = 0.f;
+  if (s < per) {
+    for (int m = m0 + s; m < m1; m += per) acc += in[((long long)b * M + m) * K + k];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < K) {
+    float t = 0.f;
+    for (int j = 0; j < per; ++j) t += red[j * K + tid];
+    part[((long long)b * SEG_CHUNKS + ch) * K + tid] = t;
+  }
+}
+
+__global__ void __launch_bounds__(64) segsum_pass2(const float* __restrict__ part, int K,
+                                                   float* __restrict__ out) {
+  const int b = blockIdx.x;
+  for (int k = threadIdx.x; k < K; k += 64) {
+    float t = 0.f;
+    for (int j = 0; j < SEG_CHUNKS; ++j) t += part[((long long)b * SEG_CHUNKS + j) * K + k];
+    out[b * K + k] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Decoder packing (EqualizedLinear gains, stylegan.py:173-176)
+// ---------------------------------------------------------------------------------------
+__global__ void decoder_pack_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                    const float* __restrict__ w2, const float* __restrict__ b2, float g1,
+                                    float g2, float gb, float* __restrict__ dec) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < NH * DEC_UNIT) {
+    const int o = t / DEC_UNIT, j = t % DEC_UNIT;
+    float v = 0.f;
+    if (j < NC) v = w1[o * NC + j] * g1;
+    else if (j < DEC_W2T + NO) v = w2[(j - DEC_W2T) * NH + o] * g2;
+    else if (j == DEC_B1) v = b1[o] * gb;
+    dec[t] = v;
+  } else if (t < DEC_SIZE) {
+    const int k = t - DEC_B2;
+    dec[t] = (k < NO) ? b2[k] * gb : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Plane layout: [B,3,32,R,R] <-> [B,3,R,R,32]  (LDS-tiled transpose, 32 ch x 64 texels)
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) planes_c2t_kernel(const float* __restrict__ src, int RR,
+                                                         float* __restrict__ dst) {
+  __shared__ float tile[NC][65];
+  const long long bq = blockIdx.y;              // b*3 + q
+  const int t0 = blockIdx.x * 64;
+  const float* s = src + bq * NC * (long long)RR;
+  float* d = dst + bq * NC * (long long)RR;
+  for (int i = threadIdx.x; i < NC * 64; i += 256) {
+    const int c = i / 64, t = i % 64;
+    tile[c][t] = (t0 + t < RR) ? s[(long long)c * RR + t0 + t] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NC * 64; i += 256) {
+    const int t = i / NC, c = i % NC;
+    if (t0 + t < RR) d[(long long)(t0 + t) * NC + c] = tile[c][t];
+  }
+}
+
+__global__ void __launch_bounds__(256) planes_t2c_kernel(const float* __restrict__ src, int RR,
+                                                         float* __restrict__ dst) {
+  __shared__ float tile[NC][65];
+  const long long bq = blockIdx.y;
+  const int t0 = blockIdx.x * 64;
+  const float* s = src + bq * NC * (long long)RR;
+  float* d = dst + bq * NC * (long long)RR;
+  for (int i = threadIdx.x; i < NC * 64; i += 256) {
+    const int t = i / NC, c = i % NC;
+    tile[c][t] = (t0 + t < RR) ? s[(long long)(t0 + t) * NC + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NC * 64; i += 256) {
+    const int c = i / 64, t = i % 64;
+    if (t0 + t < RR) d[(long long)c * RR + t0 + t] = tile[c][t];
+  }
+}
+
+}  // namespace nfi
+
+using namespace nfi;
+
+extern "C" {
+
+int32_t nfi_abi_version(void) { return NFI_ABI_VERSION; }
+const char* nfi_last_error(void) { return nfi::g_err.c_str(); }
+
+static int check_cam(const nfi_camera* c) {
+  NFI_REQUIRE(c && c->cam, "camera: null cam pointer");
+  NFI_REQUIRE(c->B > 0 && c->H > 0 && c->W > 0, "camera: bad shape B=%d H=%d W=%d", c->B, c->H, c->W);
+  return NFI_OK;
+}
+
+int32_t nfi_rays_forward(const nfi_camera* cam, float scene_range, float* ro, float* rd, float* near_,
+                         float* far_, uint32_t* ws, void* stream) {
+  int e = check_cam(cam);
+  if (e) return e;
+  NFI_REQUIRE(ro && rd && near_ && far_ && ws, "rays_forward: null output");
+  NFI_REQUIRE(scene_range > 0.f && std::isfinite(scene_range), "rays_forward: bad scene_range");
+  hipStream_t s = (hipStream_t)stream;
+  const long long n = (long long)cam->B * cam->H * cam->W;
+  // ws layout: [0]=min-key, [1]=max-key, [2..] = per-ray hit flags (int)
+  NFI_REQUIRE(hipMemsetAsync(ws, 0xFF, 4, s) == hipSuccess && hipMemsetAsync(ws + 1, 0, 4, s) == hipSuccess,
+              "rays_forward: hipMemsetAsync failed");
+  const int blocks = (int)((n + 255) / 256);
+  int* hit = reinterpret_cast<int*>(ws + 2);
+  rays_fwd_kernel<<<blocks, 256, 0, s>>>(*cam, scene_range, ro, rd, near_, far_, ws, hit);
+  NFI_CHECK_LAUNCH("rays_fwd_kernel");
+  rays_fix_kernel<<<blocks, 256, 0, s>>>(n, near_, far_, ws, hit);
+  NFI_CHECK_LAUNCH("rays_fix_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_rays_backward(const nfi_camera* cam, const float* g_ro, const float* g_rd, float* contrib,
+                          void* stream) {
+  int e = check_cam(cam);
+  if (e) return e;
+  NFI_REQUIRE(g_ro && g_rd && contrib, "rays_backward: null pointer");
+  const long long n = (long long)cam->B * cam->H * cam->W;
+  rays_bwd_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(*cam, g_ro, g_rd, contrib);
+  NFI_CHECK_LAUNCH("rays_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_segment_sum(const float* in, int32_t B, int32_t M, int32_t K, float* out, float* ws,
+                        void* stream) {
+  NFI_REQUIRE(in && out && ws, "segment_sum: null pointer");
+  NFI_REQUIRE(B > 0 && M > 0 && K > 0 && K <= 256, "segment_sum: bad shape B=%d M=%d K=%d", B, M, K);
+  hipStream_t s = (hipStream_t)stream;
+  segsum_pass1<<<dim3(SEG_CHUNKS, B), 256, 0, s>>>(in, M, K, ws);
+  NFI_CHECK_LAUNCH("segsum_pass1");
+  segsum_pass2<<<B, 64, 0, s>>>(ws, K, out);
+  NFI_CHECK_LAUNCH("segsum_pass2");
+  return NFI_OK;
+}
+
+int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, const float* b2, float g1,
+                         float g2, float gb, float* dec, void* stream) {
+  NFI_REQUIRE(w1 && b1 && w2 && b2 && dec, "decoder_pack: null pointer");
+  decoder_pack_kernel<<<(DEC_SIZE + 255) / 256, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1, g2, gb,
+                                                                                dec);
+  NFI_CHECK_LAUNCH("decoder_pack_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_planes_to_texel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream) {
+  NFI_REQUIRE(src && dst && B > 0 && R > 1, "planes_to_texel_major: bad args");
+  const int RR = R * R;
+  planes_c2t_kernel<<<dim3((RR + 63) / 64, B * 3), 256, 0, (hipStream_t)stream>>>(src, RR, dst);
+  NFI_CHECK_LAUNCH("planes_c2t_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_planes_to_channel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream) {
+  NFI_REQUIRE(src && dst && B > 0 && R > 1, "planes_to_channel_major: bad args");
+  const int RR = R * R;
+  planes_t2c_kernel<<<dim3((RR + 63) / 64, B * 3), 256, 0, (hipStream_t)stream>>>(src, RR, dst);
+  NFI_CHECK_LAUNCH("planes_t2c_kernel");
+  return NFI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+"""ctypes binding of the nfi C-ABI (include/nfi.h) — the binding a reference-side maintainer
+would add.  Loads the in-tree HIP library `libnfi_hip.so`; there is no
+fallback: if the library is missing or was built for another ABI, importing the renderer
+raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libnfi_hip.so')
+ABI_VERSION = 1
+DEC_SIZE = 3088
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_void_p = ctypes.c_void_p
+
+
+class NfiCamera(ctypes.Structure):
+    _fields_ = [('cam', c_void_p), ('focal', c_void_p), ('center', c_void_p), ('bbox', c_void_p),
+                ('B', ctypes.c_int32), ('H', ctypes.c_int32), ('W', ctypes.c_int32),
+                ('_pad', ctypes.c_int32)]
+
+
+class NfiField(ctypes.Structure):
+    _fields_ = [('planes', c_void_p), ('sb', ctypes.c_int64), ('sq', ctypes.c_int64),
+                ('st', ctypes.c_int64), ('R', ctypes.c_int32), ('_pad', ctypes.c_int32),
+                ('dec', c_void_p), ('palette', c_void_p), ('inv_alpha', ctypes.c_float),
+                ('beta', ctypes.c_float), ('scene_range', ctypes.c_float),
+                ('_pad2', ctypes.c_int32)]
+
+
+class NfiRenderArgs(ctypes.Structure):
+    _fields_ = [('field', NfiField), ('ro', c_void_p), ('rd', c_void_p), ('near_', c_void_p),
+                ('far_', c_void_p), ('B', ctypes.c_int32), ('HW', ctypes.c_int32),
+                ('S', ctypes.c_int32), ('fine', ctypes.c_int32), ('white_bg', ctypes.c_int32),
+                ('randomize', ctypes.c_int32), ('seed', ctypes.c_uint64),
+                ('offset', ctypes.c_uint64), ('u_coarse', c_void_p), ('u_fine', c_void_p),
+                ('rgb', c_void_p), ('depth', c_void_p), ('mask', c_void_p),
+                ('t_saved', c_void_p), ('sigma_saved', c_void_p), ('rgb_saved', c_void_p),
+                ('z_coarse', c_void_p), ('z_fine', c_void_p)]
+
+
+class NfiRenderGradArgs(ctypes.Structure):
+    _fields_ = [('g_rgb', c_void_p), ('g_mask', c_void_p), ('d_planes', c_void_p),
+                ('d_palette_ray', c_void_p), ('g_ro', c_void_p), ('g_rd', c_void_p)]
+
+
+# symbol -> (restype, argtypes); every entry point of include/nfi.h
+SIGNATURES = {
+    'nfi_abi_version': (ctypes.c_int32, []),
+    'nfi_last_error': (ctypes.c_char_p, []),
+    'nfi_decoder_pack': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
+                                          ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
+    'nfi_planes_to_texel_major': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                   c_void_p, c_void_p]),
+    'nfi_planes_to_channel_major': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                     c_void_p, c_void_p]),
+    'nfi_rays_forward': (ctypes.c_int32, [ctypes.POINTER(NfiCamera), ctypes.c_float, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    'nfi_rays_backward': (ctypes.c_int32, [ctypes.POINTER(NfiCamera), c_void_p, c_void_p,
+                                           c_void_p, c_void_p]),
+    'nfi_segment_sum': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         c_void_p, c_void_p, c_void_p]),
+    'nfi_render_forward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs), c_void_p]),
+    'nfi_render_backward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
+                                             ctypes.POINTER(NfiRenderGradArgs), c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NfiError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load and type the library once.  Raises NfiError if it is absent or mismatched."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NfiError(f'nfi HIP library not found at {path}; build it with '
+                           f'`python __graft_entry__.py` (build()) — there is no CPU fallback')
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.nfi_abi_version()
+        if v != ABI_VERSION:
+            raise NfiError(f'nfi ABI mismatch: library {v}, binding {ABI_VERSION}')
+        _lib = lib
+        return lib
+
+
+def check(code: int, what: str):
+    if code != 0:
+        msg = _lib.nfi_last_error().decode() if _lib is not None else ''
+        raise NfiError(f'{what} failed ({code}): {msg}')

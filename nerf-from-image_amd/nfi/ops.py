@@ -1,0 +1,307 @@
+"""Autograd operators over the nfi C-ABI (HIP kernels).  Device tensors only — there is no
+CPU path: every op raises if its inputs are not on a HIP device.
+
+Operators (reference function each one replaces, file:line in yuliangguo/nerf-from-image):
+  planes_texel_major   layout of generator.py:476-477 planes for the tap kernels
+  rays                 nerf_utils.get_ray_bundle (:28-93) + F.normalize (run.py:196)
+                       + nerf_utils.compute_near_far_planes (:227-275, no grad)
+  volume_render        run.py:202-348 from the rays onward: compute_query_points_from_rays,
+                       sampler (generator.py:587-681) coarse + fine, weights/smoothing,
+                       sample_pdf, sort/merge, render_volume_density — fused
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+# Optional live kernel timing (bench.py): name -> list of (start, end) events recorded on the
+# stream the C-ABI call launches on.  Off by default (no events, no overhead).
+KERNEL_TIMERS: Optional[dict] = None
+
+
+class _timed:
+    def __init__(self, name, dev):
+        self.name, self.dev = name, dev
+
+    def __enter__(self):
+        if KERNEL_TIMERS is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record(torch.cuda.current_stream(self.dev))
+        return self
+
+    def __exit__(self, *exc):
+        if KERNEL_TIMERS is not None:
+            self.e1.record(torch.cuda.current_stream(self.dev))
+            KERNEL_TIMERS.setdefault(self.name, []).append((self.e0, self.e1))
+        return False
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('nfi ops run on HIP devices only (got a CPU tensor); '
+                               'the CPU path of the reference is not part of this package')
+        if t is not None and t.dtype != torch.float32:
+            raise RuntimeError(f'nfi ops need float32 tensors (got {t.dtype})')
+
+
+# ----------------------------------------------------------------------------------------
+# Plane layout
+# ----------------------------------------------------------------------------------------
+
+class _PlanesTexelMajor(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, planes):
+        lib = _lib.load()
+        B, three, C, R, R2 = planes.shape
+        src = planes.contiguous()
+        out = torch.empty((B, 3, R, R, C), device=planes.device, dtype=planes.dtype)
+        _lib.check(lib.nfi_planes_to_texel_major(_ptr(src), B, R, _ptr(out), _stream(planes.device)),
+                   'nfi_planes_to_texel_major')
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        g = g.contiguous()
+        B, _, R, _, C = g.shape
+        out = torch.empty((B, 3, C, R, R), device=g.device, dtype=g.dtype)
+        _lib.check(lib.nfi_planes_to_channel_major(_ptr(g), B, R, _ptr(out), _stream(g.device)),
+                   'nfi_planes_to_channel_major')
+        return out
+
+
+def planes_texel_major(planes: torch.Tensor) -> torch.Tensor:
+    """[B,3,32,R,R] planes (generator.py:476-477) -> texel-major [B,3,R,R,32] view/copy.
+    A channels_last producer output is re-viewed without a copy."""
+    _require_device(planes)
+    if planes.dim() != 5 or planes.shape[1] != 3 or planes.shape[2] != 32 or planes.shape[3] != planes.shape[4]:
+        raise ValueError(f'planes must be [B,3,32,R,R], got {tuple(planes.shape)}')
+    tm = planes.permute(0, 1, 3, 4, 2)
+    if tm.stride(-1) == 1 and tm.stride(2) == tm.shape[3] * tm.stride(3):
+        return tm
+    return _PlanesTexelMajor.apply(planes)
+
+
+# ----------------------------------------------------------------------------------------
+# Rays
+# ----------------------------------------------------------------------------------------
+
+def _camera_struct(cam, focal, center, bbox, H, W):
+    return _lib.NfiCamera(cam=_ptr(cam), focal=_ptr(focal), center=_ptr(center), bbox=_ptr(bbox),
+                          B=cam.shape[0], H=H, W=W, _pad=0)
+
+
+class _Rays(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cam, focal, center, bbox, H: int, W: int, scene_range: float):
+        lib = _lib.load()
+        B = cam.shape[0]
+        dev = cam.device
+        n = B * H * W
+        cam_c = cam.contiguous()
+        foc_c = None if focal is None else focal.contiguous()
+        cen_c = None if center is None else center.contiguous()
+        bb_c = None if bbox is None else bbox.contiguous()
+        ro = torch.empty((B, H, W, 3), device=dev)
+        rd = torch.empty((B, H, W, 3), device=dev)
+        near = torch.empty((B, H, W), device=dev)
+        far = torch.empty((B, H, W), device=dev)
+        ws = torch.empty((2 + n,), device=dev, dtype=torch.int32)
+        cs = _camera_struct(cam_c, foc_c, cen_c, bb_c, H, W)
+        _lib.check(lib.nfi_rays_forward(ctypes.byref(cs), float(scene_range), _ptr(ro), _ptr(rd),
+                                        _ptr(near), _ptr(far), _ptr(ws), _stream(dev)),
+                   'nfi_rays_forward')
+        ctx.save_for_backward(cam_c, foc_c, cen_c, bb_c)
+        ctx.HW = (H, W)
+        ctx.mark_non_differentiable(near, far)
+        return ro, rd, near, far
+
+    @staticmethod
+    def backward(ctx, g_ro, g_rd, g_near, g_far):
+        lib = _lib.load()
+        cam, focal, center, bbox = ctx.saved_tensors
+        H, W = ctx.HW
+        B = cam.shape[0]
+        dev = cam.device
+        n = B * H * W
+        g_ro = torch.zeros((n, 3), device=dev) if g_ro is None else g_ro.contiguous()
+        g_rd = torch.zeros((n, 3), device=dev) if g_rd is None else g_rd.contiguous()
+        contrib = torch.empty((n, 16), device=dev)
+        cs = _camera_struct(cam, focal, center, bbox, H, W)
+        st = _stream(dev)
+        _lib.check(lib.nfi_rays_backward(ctypes.byref(cs), _ptr(g_ro), _ptr(g_rd), _ptr(contrib), st),
+                   'nfi_rays_backward')
+        red = torch.empty((B, 16), device=dev)
+        ws = torch.empty((B * 64 * 16,), device=dev)
+        _lib.check(lib.nfi_segment_sum(_ptr(contrib), B, H * W, 16, _ptr(red), _ptr(ws), st),
+                   'nfi_segment_sum')
+        d_cam = torch.zeros((B, 4, 4), device=dev)
+        d_cam[:, :3, :] = red[:, :12].view(B, 3, 4)
+        d_cam[:, 3, 3] = red[:, 12]
+        d_focal = red[:, 13].clone() if focal is not None else None
+        return d_cam, d_focal, None, None, None, None, None
+
+
+def rays(cam, focal, center, bbox, H: int, W: int, scene_range: float):
+    """get_ray_bundle + F.normalize + near/far (run.py:193-200) -> ro, rd [B,H,W,3], near, far."""
+    _require_device(cam, focal, center, bbox)
+    return _Rays.apply(cam, focal, center, bbox, int(H), int(W), float(scene_range))
+
+
+# ----------------------------------------------------------------------------------------
+# Fused volume render
+# ----------------------------------------------------------------------------------------
+
+@dataclass
+class RenderOptions:
+    samples: int                 # depth_samples_per_ray (coarse; fine adds as many)
+    fine: bool = True            # args.fine_sampling
+    white_background: bool = False
+    randomize: bool = True
+    scene_range: float = 1.0
+    inv_alpha: float = 1.0       # 1 / Generator.alpha
+    beta: float = 0.1            # Generator.beta
+
+
+def pack_decoder(w1, b1, w2, b2, lr_multiplier: float = 1.0) -> torch.Tensor:
+    """EqualizedLinear gains (stylegan.py:173-176) folded into the packed decoder buffer."""
+    _require_device(w1, b1, w2, b2)
+    lib = _lib.load()
+    dec = torch.empty((_lib.DEC_SIZE,), device=w1.device)
+    g1 = float(torch.tensor(lr_multiplier / math.sqrt(w1.shape[1]), dtype=torch.float32))
+    g2 = float(torch.tensor(lr_multiplier / math.sqrt(w2.shape[1]), dtype=torch.float32))
+    gb = float(torch.tensor(lr_multiplier, dtype=torch.float32))
+    _lib.check(lib.nfi_decoder_pack(_ptr(w1.detach().contiguous()), _ptr(b1.detach().contiguous()),
+                                    _ptr(w2.detach().contiguous()), _ptr(b2.detach().contiguous()),
+                                    g1, g2, gb, _ptr(dec), _stream(w1.device)), 'nfi_decoder_pack')
+    return dec
+
+
+class _VolumeRender(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, planes_tm, palette, ro, rd, near, far, dec, opts: RenderOptions,
+                u_coarse, u_fine, seed: int, debug: Optional[dict]):
+        lib = _lib.load()
+        B, _, R, R2, C = planes_tm.shape
+        H, W = ro.shape[1], ro.shape[2]
+        dev = ro.device
+        n = B * H * W
+        S = opts.samples
+        N = 2 * S if opts.fine else S
+        ro_c, rd_c = ro.contiguous(), rd.contiguous()
+        near_c, far_c = near.contiguous(), far.contiguous()
+        pal_c = palette.contiguous()
+        rgb = torch.empty((n, 3), device=dev)
+        depth = torch.empty((n,), device=dev)
+        mask = torch.empty((n,), device=dev)
+        t_saved = torch.empty((n, N), device=dev)
+        s_saved = torch.empty((n, N), device=dev)
+        c_saved = torch.empty((n, 3, N), device=dev)
+        zc = zf = None
+        if debug is not None:
+            zc = torch.empty((n, S), device=dev)
+            zf = torch.empty((n, S), device=dev) if opts.fine else None
+        uc = None if u_coarse is None else u_coarse.contiguous()
+        uf = None if u_fine is None else u_fine.contiguous()
+        args = _VolumeRender._args(planes_tm, dec, pal_c, ro_c, rd_c, near_c, far_c, opts, B, H * W,
+                                   uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, zc, zf)
+        with _timed('render_fwd', dev):
+            _lib.check(lib.nfi_render_forward(ctypes.byref(args), _stream(dev)), 'nfi_render_forward')
+        if debug is not None:
+            debug['z_coarse'] = zc
+            debug['z_fine'] = zf
+            debug['t_sorted'] = t_saved
+            debug['sigma_sorted'] = s_saved
+            debug['rgb_sorted'] = c_saved
+        ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved)
+        ctx.opts = opts
+        ctx.shape = (B, H, W)
+        ctx.mark_non_differentiable(depth)
+        return rgb.view(B, H, W, 3), depth.view(B, H, W), mask.view(B, H, W)
+
+    @staticmethod
+    def _args(planes_tm, dec, pal, ro, rd, near, far, opts, B, HW, uc, uf, seed, rgb, depth, mask,
+              t_saved, s_saved, c_saved, zc, zf):
+        R = planes_tm.shape[2]
+        field = _lib.NfiField(planes=_ptr(planes_tm), sb=planes_tm.stride(0), sq=planes_tm.stride(1),
+                              st=planes_tm.stride(3), R=R, _pad=0, dec=_ptr(dec), palette=_ptr(pal),
+                              inv_alpha=float(opts.inv_alpha), beta=float(opts.beta),
+                              scene_range=float(opts.scene_range), _pad2=0)
+        return _lib.NfiRenderArgs(field=field, ro=_ptr(ro), rd=_ptr(rd), near_=_ptr(near), far_=_ptr(far),
+                                  B=B, HW=HW, S=opts.samples, fine=int(opts.fine),
+                                  white_bg=int(opts.white_background), randomize=int(opts.randomize),
+                                  seed=seed & ((1 << 64) - 1), offset=0, u_coarse=_ptr(uc),
+                                  u_fine=_ptr(uf), rgb=_ptr(rgb), depth=_ptr(depth), mask=_ptr(mask),
+                                  t_saved=_ptr(t_saved), sigma_saved=_ptr(s_saved),
+                                  rgb_saved=_ptr(c_saved), z_coarse=_ptr(zc), z_fine=_ptr(zf))
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_mask):
+        lib = _lib.load()
+        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved = ctx.saved_tensors
+        opts = ctx.opts
+        B, H, W = ctx.shape
+        dev = ro.device
+        n = B * H * W
+        g_rgb = torch.zeros((n, 3), device=dev) if g_rgb is None else g_rgb.contiguous()
+        g_mask = torch.zeros((n,), device=dev) if g_mask is None else g_mask.contiguous()
+        d_planes = torch.zeros_like(planes_tm)   # preserves (texel-major) strides
+        d_pal_ray = torch.empty((n, 30), device=dev)
+        need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        g_ro = torch.empty((n, 3), device=dev) if need_coords else None
+        g_rd = torch.empty((n, 3), device=dev) if need_coords else None
+        args = _VolumeRender._args(planes_tm, dec, pal, ro, rd, near, far, opts, B, H * W, None, None, 0,
+                                   None, None, None, t_saved, s_saved, c_saved, None, None)
+        gargs = _lib.NfiRenderGradArgs(g_rgb=_ptr(g_rgb), g_mask=_ptr(g_mask), d_planes=_ptr(d_planes),
+                                       d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd))
+        st = _stream(dev)
+        with _timed('render_bwd', dev):
+            _lib.check(lib.nfi_render_backward(ctypes.byref(args), ctypes.byref(gargs), st),
+                       'nfi_render_backward')
+        d_pal = torch.empty((B, 30), device=dev)
+        ws = torch.empty((B * 64 * 30,), device=dev)
+        _lib.check(lib.nfi_segment_sum(_ptr(d_pal_ray), B, H * W, 30, _ptr(d_pal), _ptr(ws), st),
+                   'nfi_segment_sum')
+        d_ro = g_ro.view(B, H, W, 3) if need_coords else None
+        d_rd = g_rd.view(B, H, W, 3) if need_coords else None
+        return (d_planes, d_pal.view(B, 10, 3), d_ro, d_rd, None, None, None, None, None, None, None, None)
+
+
+def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOptions,
+                  u_coarse=None, u_fine=None, seed: Optional[int] = None, debug: Optional[dict] = None):
+    """Fused coarse+fine render of rays (run.py:202-348).  planes_tm: texel-major
+    [B,3,R,R,32] (see planes_texel_major); palette [B,10,3]; ro, rd [B,H,W,3]; near, far
+    [B,H,W].  Returns rgb [B,H,W,3], depth [B,H,W] (no grad), mask [B,H,W]."""
+    _require_device(planes_tm, palette, ro, rd, near, far, dec, u_coarse, u_fine)
+    if planes_tm.dim() != 5 or planes_tm.shape[-1] != 32 or planes_tm.stride(-1) != 1:
+        raise ValueError('planes_tm must be texel-major [B,3,R,R,32] with unit channel stride')
+    if planes_tm.stride(2) != planes_tm.shape[3] * planes_tm.stride(3):
+        raise ValueError('planes_tm rows must be dense (stride(2) == R*stride(3))')
+    B = planes_tm.shape[0]
+    if ro.shape[0] != B or palette.shape != (B, 10, 3):
+        raise ValueError('batch mismatch between planes, palette and rays')
+    n = ro.shape[0] * ro.shape[1] * ro.shape[2]
+    for name, u in (('u_coarse', u_coarse), ('u_fine', u_fine)):
+        if u is not None and u.numel() != n * opts.samples:
+            raise ValueError(f'{name} must have B*H*W*S = {n * opts.samples} elements')
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if opts.randomize else 0
+    return _VolumeRender.apply(planes_tm, palette, ro, rd, near, far, dec, opts, u_coarse, u_fine, seed, debug)

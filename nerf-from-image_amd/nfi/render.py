@@ -1,0 +1,169 @@
+"""Drop-in `render()` for run.py:176-350 on MI355X.
+
+`render(target_model, height, width, tform_cam2world, focal_length, center, bbox, model_input,
+depth_samples_per_ray, randomize=True, compute_normals=False, compute_semantics=False,
+compute_coords=False, extra_model_outputs=[], extra_model_inputs={}, force_no_cam_grad=False)`
+keeps the reference's signature, argument meaning and 6-tuple return
+`(rgb, depth, mask, normals, semantics, model_outputs)`.  The reference reads the globals
+`args` (use_viewdir, fine_sampling, use_sdf, attention_values) and `dataset_config`
+(scene_range, white_background); here they come from `configure(args=..., dataset_config=...)`.
+
+Everything from the camera to the composited pixel runs in the HIP kernels of
+`nerf-from-image_amd/csrc` (see ops.py); the tri-plane producer (synthesis network) and
+the palette producer (AttentionMapper) stay the caller's PyTorch modules.
+"""
+
+from __future__ import annotations
+
+import types
+from dataclasses import dataclass, field as dc_field
+from typing import Any, Optional, Sequence
+
+import torch
+
+from . import ops
+
+
+@dataclass
+class RenderConfig:
+    scene_range: float = 1.4
+    white_background: bool = False
+    fine_sampling: bool = True
+    use_sdf: bool = True
+    attention_values: int = 10
+    use_viewdir: bool = False
+
+
+_CONFIG = RenderConfig()
+
+
+def configure(args: Any = None, dataset_config: Optional[dict] = None, **overrides) -> RenderConfig:
+    """Set the reference's globals: `args` (arguments.py namespace) and `dataset_config`
+    (loaders.get_dataset_config dict), or individual fields as keywords."""
+    if args is not None:
+        for k in ('fine_sampling', 'use_sdf', 'attention_values', 'use_viewdir'):
+            if hasattr(args, k):
+                setattr(_CONFIG, k, getattr(args, k))
+    if dataset_config is not None:
+        _CONFIG.scene_range = float(dataset_config['scene_range'])
+        _CONFIG.white_background = bool(dataset_config['white_background'])
+    for k, v in overrides.items():
+        if not hasattr(_CONFIG, k):
+            raise KeyError(k)
+        setattr(_CONFIG, k, v)
+    return _CONFIG
+
+
+def get_config() -> RenderConfig:
+    return _CONFIG
+
+
+@dataclass
+class TriplaneField:
+    """The inputs the renderer reads from a Generator (generator.py:392-503)."""
+    planes: torch.Tensor                 # [B,3,32,R,R] (contiguous or channels_last producer output)
+    palette: torch.Tensor                # [B,10,3] attention values
+    w1: torch.Tensor                     # decoder.net[0].weight [64,32]
+    b1: torch.Tensor                     # decoder.net[0].bias   [64]
+    w2: torch.Tensor                     # decoder.net[2].weight [11,64]
+    b2: torch.Tensor                     # decoder.net[2].bias   [11]
+    alpha: float = 1.0                   # Generator.alpha (sigma = laplace_cdf / alpha)
+    beta: float = 0.1                    # Generator.beta
+    model_outputs: dict = dc_field(default_factory=dict)
+
+
+def _as_float(x) -> float:
+    return float(x.detach().reshape(-1)[0].item()) if torch.is_tensor(x) else float(x)
+
+
+def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
+                         extra_model_inputs: Optional[dict] = None) -> TriplaneField:
+    """Runs the parts of Generator.forward (generator.py:423-503) that produce the path's
+    inputs — ws, AttentionMapper palette, synthesis tri-planes — on the reference's own
+    modules, for the inversion configuration (attention_values=10, use_sdf, no viewdir,
+    no encoder, unconditional)."""
+    extra_model_inputs = extra_model_inputs or {}
+    for k in extra_model_inputs:
+        if k not in ('freeze_noise', 'attention_values', 'attention_values_bias'):
+            raise AssertionError(k)
+    if getattr(gen, 'use_encoder', False) or getattr(gen, 'num_classes', None):
+        raise NotImplementedError('encoder-/class-conditioned generators are outside the inversion path')
+    if getattr(gen, 'attention_values', 0) != 10 or not getattr(gen, 'use_sdf', False) \
+            or getattr(gen, 'use_viewdir', False):
+        raise NotImplementedError('nfi renders the SDF + 10-value attention field of the inversion path')
+    if c.dim() == 3:
+        ws = c.expand(-1, gen.mapping_network.backbone.num_ws, -1).contiguous() if c.shape[1] == 1 else c
+    else:
+        ws = gen.mapping_network(c, None)
+    assert ws.shape[1] == 15
+    w_tex, w_syn = ws[:, 14], ws[:, :14]
+    if 'attention_values' in extra_model_inputs:
+        palette = extra_model_inputs['attention_values']
+    else:
+        palette = gen.texture_mapper(w_tex)
+        if 'attention_values_bias' in extra_model_inputs:
+            palette = palette + extra_model_inputs['attention_values_bias']
+    kw = {'noise_mode': 'const'} if extra_model_inputs.get('freeze_noise') else {}
+    planes = gen.synthesis_network(w_syn, **kw)
+    planes = planes.view(c.shape[0], 3, 32, planes.shape[-2], planes.shape[-1])
+    outs = {}
+    if 'attention_values' in extra_model_outputs:
+        outs['attention_values'] = palette
+    for k in extra_model_outputs:
+        if k not in ('attention_values',):
+            raise NotImplementedError(f'model output {k!r} (training regulariser) is outside the path')
+    dec = gen.decoder.net
+    return TriplaneField(planes=planes, palette=palette, w1=dec[0].weight, b1=dec[0].bias,
+                         w2=dec[2].weight, b2=dec[2].bias, alpha=_as_float(gen.alpha),
+                         beta=_as_float(gen.beta), model_outputs=outs)
+
+
+def _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs) -> TriplaneField:
+    if isinstance(target_model, TriplaneField):
+        return target_model
+    if hasattr(target_model, 'nfi_field'):
+        return target_model.nfi_field(model_input, extra_model_outputs, extra_model_inputs)
+    if hasattr(target_model, 'synthesis_network') and hasattr(target_model, 'decoder'):
+        return field_from_generator(target_model, model_input, extra_model_outputs, extra_model_inputs)
+    raise TypeError('target_model must be a TriplaneField, provide nfi_field(), or be a '
+                    'reference-style Generator (synthesis_network + decoder)')
+
+
+def _check_frozen(f: TriplaneField):
+    if torch.is_grad_enabled():
+        for name in ('w1', 'b1', 'w2', 'b2'):
+            if getattr(f, name).requires_grad:
+                raise NotImplementedError(
+                    f'decoder parameter {name} requires grad: nfi differentiates the inversion '
+                    f'path, where the generator is frozen (run.py:630-632); call requires_grad_(False)')
+
+
+def render(target_model, height, width, tform_cam2world, focal_length, center, bbox, model_input,
+           depth_samples_per_ray, randomize=True, compute_normals=False, compute_semantics=False,
+           compute_coords=False, extra_model_outputs=[], extra_model_inputs={},
+           force_no_cam_grad=False, *, u_coarse=None, u_fine=None, seed=None, debug=None):
+    """run.py:176-350.  Extra keyword-only arguments (not in the reference) inject the random
+    draws for parity testing (`u_coarse` [B,H,W,S], `u_fine` [B*H*W,S]) or fix the Philox
+    seed; `debug` (a dict) receives intermediate depths."""
+    cfg = _CONFIG
+    if compute_normals or compute_semantics or compute_coords:
+        raise NotImplementedError('normals/semantics/coords outputs are SURVEY §8(f) #3 (next), not built')
+    if cfg.use_viewdir or not cfg.use_sdf or cfg.attention_values != 10:
+        raise NotImplementedError('only the inversion field (use_sdf, attention_values=10, no viewdir)')
+    f = _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs)
+    _check_frozen(f)
+    ro, rd, near, far = ops.rays(tform_cam2world, focal_length, center, bbox, height, width,
+                                 cfg.scene_range)
+    if force_no_cam_grad:
+        # run.py:211-214 detaches query points and directions (the reference's fine points keep a
+        # gradient path to ray origins; its callers of this mode run under no_grad)
+        ro, rd = ro.detach(), rd.detach()
+    planes_tm = ops.planes_texel_major(f.planes)
+    dec = ops.pack_decoder(f.w1, f.b1, f.w2, f.b2)
+    opts = ops.RenderOptions(samples=int(depth_samples_per_ray), fine=bool(cfg.fine_sampling),
+                             white_background=bool(cfg.white_background), randomize=bool(randomize),
+                             scene_range=float(cfg.scene_range), inv_alpha=1.0 / float(f.alpha),
+                             beta=float(f.beta))
+    rgb, depth, mask = ops.volume_render(planes_tm, f.palette, ro, rd, near, far, dec, opts,
+                                         u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug)
+    return rgb, depth, mask, None, None, dict(f.model_outputs)

@@ -1,0 +1,67 @@
+"""Seeded synthetic inversion inputs at the real sizes for bench.py and the
+multi-GPU harness: no datasets or checkpoints exist offline, so planes are N(0, 1.87^2)
+(the measured std of the random-init synthesis output), the decoder is a random
+EqualizedLinear init with the -0.97 SDF bias shift, the palette is
+wide_sigmoid_rescaled(N(0,1)), and cameras sit on a sphere of radius 3.3*scene_range with
+focal 1.859 (pose_utils.pose_to_matrix convention)."""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .render import TriplaneField
+
+
+def quaternion_to_matrix(q):
+    """pose_utils.py:30-45 (caller-side camera math)."""
+    v = torch.eye(3, device=q.device).unsqueeze(0).expand(q.shape[0], -1, -1)
+    qvec = q[:, 1:].unsqueeze(1).expand(-1, 3, -1)
+    uv = torch.cross(qvec, v, dim=2)
+    uuv = torch.cross(qvec, uv, dim=2)
+    return v + 2 * (q[:, :1].unsqueeze(1) * uv + uuv)
+
+
+def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
+    """pose_utils.py:48-75: (z0, t2, s, q) -> cam2world [B,4,4], focal (perspective) or None."""
+    R = quaternion_to_matrix(q)
+    mat = torch.zeros((q.shape[0], 4, 4), device=R.device)
+    mat[:, 3, 3] = 1
+    mat[:, :3, :3] = R
+    if z0 is not None:
+        f = 1 + z0.exp()
+        t3 = torch.cat((t2 / s.unsqueeze(-1), (f / s).unsqueeze(-1)), dim=-1)
+        mat[:, :3, 3] = (t3[:, None, :] * R).sum(dim=-1)
+        if camera_flipped:
+            mat[:, :3, 1:] *= -1
+        return mat, f / 2
+    t3 = torch.cat((t2, torch.ones_like(t2[:, :1])), dim=-1) / s
+    mat[:, :3, 3] = (t3[:, None, :] * R).sum(dim=-1)
+    if camera_flipped:
+        mat[:, :3, 1:] *= -1
+    return mat, None
+
+
+def inversion_batch(B, H, W, S, R, scene_range, seed, flipped=True, device='cuda'):
+    g = torch.Generator(device=device).manual_seed(seed)
+    dev = torch.device(device)
+    planes = 1.87 * torch.randn((B, 3, 32, R, R), generator=g, device=dev)
+    w1 = torch.randn((64, 32), generator=g, device=dev)
+    w2 = torch.randn((11, 64), generator=g, device=dev)
+    b1 = torch.zeros(64, device=dev)
+    b2 = torch.zeros(11, device=dev)
+    b2[0] -= 0.97
+    palette = torch.sigmoid(torch.randn((B, 10, 3), generator=g, device=dev)) * 2.004 - 1.002
+    q = F.normalize(torch.randn((B, 4), generator=g, device=dev), dim=-1)
+    t2 = 0.05 * torch.randn((B, 2), generator=g, device=dev)
+    f = 2 * 1.859
+    s = torch.full((B,), f / (3.3 * scene_range), device=dev)
+    z0 = torch.full((B,), math.log(f - 1), device=dev)
+    cam, focal = pose_to_matrix(z0, t2, s, q, flipped)
+    field = TriplaneField(planes=planes.requires_grad_(), palette=palette.requires_grad_(),
+                          w1=w1, b1=b1, w2=w2, b2=b2, alpha=1.0, beta=0.1)
+    return {'field': field, 'cam': cam, 'focal': focal,
+            'g_rgb': torch.randn((B, H, W, 3), generator=g, device=dev),
+            'g_mask': torch.randn((B, H, W), generator=g, device=dev)}

@@ -1,0 +1,58 @@
+"""Host-side logic of the drop-in boundary (no GPU): configuration mirroring the reference's
+globals, loud failure on CPU tensors (no silent CPU fallback), unsupported variants."""
+
+import pytest
+import torch
+
+import nfi
+from nfi import ops
+
+
+def _field(dev='cpu'):
+    return nfi.TriplaneField(planes=torch.zeros(1, 3, 32, 8, 8), palette=torch.zeros(1, 10, 3),
+                             w1=torch.zeros(64, 32), b1=torch.zeros(64), w2=torch.zeros(11, 64),
+                             b2=torch.zeros(11))
+
+
+def test_configure_from_reference_globals():
+    class A:
+        fine_sampling = True
+        use_sdf = True
+        attention_values = 10
+        use_viewdir = False
+    cfg = nfi.configure(args=A(), dataset_config={'scene_range': 0.55, 'white_background': True})
+    assert cfg.scene_range == 0.55 and cfg.white_background and cfg.fine_sampling
+    nfi.configure(scene_range=1.4, white_background=False)
+
+
+def test_cpu_tensors_fail_loudly():
+    cam = torch.eye(4).unsqueeze(0)
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        nfi.render(_field(), 8, 8, cam, torch.ones(1), None, None, None, 32)
+
+
+def test_unsupported_outputs_raise():
+    with pytest.raises(NotImplementedError):
+        nfi.render(_field(), 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32,
+                   compute_normals=True)
+
+
+def test_viewdir_variant_raises():
+    nfi.configure(use_viewdir=True)
+    try:
+        with pytest.raises(NotImplementedError):
+            nfi.render(_field(), 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
+    finally:
+        nfi.configure(use_viewdir=False)
+
+
+def test_frozen_decoder_required():
+    f = _field()
+    f.w1.requires_grad_()
+    with pytest.raises(NotImplementedError, match='frozen'):
+        nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
+
+
+def test_planes_shape_checked():
+    with pytest.raises(RuntimeError):
+        ops.planes_texel_major(torch.zeros(1, 3, 32, 8, 8))
