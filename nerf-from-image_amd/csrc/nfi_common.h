@@ -71,17 +71,31 @@ __device__ __forceinline__ int readlane(int v, int l) { return __builtin_amdgcn_
 // torch.sign
 __device__ __forceinline__ float tsign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 
-// torch.lerp CPU formula (ATen Lerp.h): weight < 0.5 ? start + w*(end-start) : end - (end-start)*(1-w)
+// Explicitly rounded fp32 ops (no FMA contraction): geometry that decides box-mask and texel
+// membership is evaluated in exactly ATen's CPU rounding order (see DESIGN.md "bit-faithful
+// geometry"), so a sample on the box surface is classified as the reference classifies it.
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+
+// torch.lerp on CPU (ATen LerpKernel lerp_vec): |w| < 0.5 ? fma(w, e-s, s) : fma(w-1, e-s, e)
 __device__ __forceinline__ float tlerp(float a, float b, float w) {
-  return (fabsf(w) < 0.5f) ? a + w * (b - a) : b - (b - a) * (1.f - w);
+  const float d = fsub(b, a);
+  return (fabsf(w) < 0.5f) ? fmaf(w, d, a) : fmaf(w - 1.f, d, b);
 }
 
-// torch.linspace(0, 1, steps) element idx (ATen RangeFactoriesKernel: symmetric halves)
+// torch.linspace(0, 1, steps) on CPU: step*idx below halfway, fma(-step, steps-1-idx, 1) above
 __device__ __forceinline__ float tlinspace01(int idx, int steps) {
   if (steps == 1) return 0.f;
   const float step = 1.0f / (float)(steps - 1);
   const int halfway = steps / 2;
-  return (idx < halfway) ? step * (float)idx : 1.0f - step * (float)(steps - idx - 1);
+  return (idx < halfway) ? fmul(step, (float)idx) : fmaf(-step, (float)(steps - idx - 1), 1.0f);
+}
+
+// torch.linalg.vector_norm(x, 2) of a 3-vector on CPU: sqrt(fma(z,z, fma(y,y, x*x)))
+__device__ __forceinline__ float tnorm3(float x, float y, float z) {
+  return sqrtf(fmaf(z, z, fmaf(y, y, fmul(x, x))));
 }
 
 // Philox-4x32-10 counter-based RNG (Salmon et al. 2011) for randomize=True sampling.

@@ -24,38 +24,39 @@ void set_error(const char* fmt, ...) {
 // Ray bundle (nerf_utils.py:28-93) + F.normalize (run.py:196) + slab test (nerf_utils.py:227-275)
 // ---------------------------------------------------------------------------------------
 
-struct PixelRay {
-  float dir[3];      // camera-space direction (perspective) or origin (ortho), before rotation
-  float ii, jj;      // pixel coordinates after center/bbox adjustment, before /focal
-};
 
 // Camera-space quantities of pixel (x, y) of image b, exactly as nerf_utils.py computes them.
 __device__ __forceinline__ void pixel_coords(const nfi_camera& c, int b, int x, int y, float& ii,
                                              float& jj) {
-  ii = (float)x / (float)c.W;   // arange(W)/W  (meshgrid indexing='xy': ii varies along W)
-  jj = (float)y / (float)c.H;
+  ii = fdiv((float)x, (float)c.W);   // arange(W)/W  (meshgrid indexing='xy': ii varies along W)
+  jj = fdiv((float)y, (float)c.H);
   if (c.focal) {
     if (c.center) {
-      ii = ii - 0.5f * (2.f * c.center[b * 2 + 0] - 1.f) - 0.5f;
-      jj = jj - 0.5f * (2.f * c.center[b * 2 + 1] - 1.f) - 0.5f;
+      ii = fsub(fsub(ii, fmul(0.5f, fsub(fmul(2.f, c.center[b * 2 + 0]), 1.f))), 0.5f);
+      jj = fsub(fsub(jj, fmul(0.5f, fsub(fmul(2.f, c.center[b * 2 + 1]), 1.f))), 0.5f);
     } else {
-      ii = ii - 0.5f;
-      jj = jj - 0.5f;
+      ii = fsub(ii, 0.5f);
+      jj = fsub(jj, 0.5f);
     }
     if (c.bbox) {
       const float* bb = c.bbox + b * 4;   // bbox[b][i][j] = bb[i*2+j]
-      ii = (bb[2] * (ii + 0.5f) + bb[0]) * 0.5f;
-      jj = -(bb[3] * (-jj + 0.5f) + bb[1]) * 0.5f;
+      ii = fmul(fadd(fmul(bb[2], fadd(ii, 0.5f)), bb[0]), 0.5f);
+      jj = fmul(-fadd(fmul(bb[3], fadd(-jj, 0.5f)), bb[1]), 0.5f);
     }
   } else {
-    ii = (ii - 0.5f) * 2.f;
-    jj = (jj - 0.5f) * 2.f;
+    ii = fmul(fsub(ii, 0.5f), 2.f);
+    jj = fmul(fsub(jj, 0.5f), 2.f);
     if (c.bbox) {
       const float* bb = c.bbox + b * 4;
-      ii = bb[2] * (ii / 2.f + 0.5f) + bb[0];
-      jj = -(bb[3] * (-jj / 2.f + 0.5f) + bb[1]);
+      ii = fadd(fmul(bb[2], fadd(fdiv(ii, 2.f), 0.5f)), bb[0]);
+      jj = -fadd(fmul(bb[3], fadd(fdiv(-jj, 2.f), 0.5f)), bb[1]);
     }
   }
+}
+
+// sum_k v[k] * M[i][k] as torch.sum(v[...,None,:] * M, -1) on CPU: rounded products, left to right
+__device__ __forceinline__ float rowdot3(const float v[3], const float* __restrict__ Mi) {
+  return fadd(fadd(fmul(v[0], Mi[0]), fmul(v[1], Mi[1])), fmul(v[2], Mi[2]));
 }
 
 __device__ __forceinline__ uint32_t fkey(float f) {
@@ -85,12 +86,12 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
     float o[3], d[3];
     if (c.focal) {
       const float f = c.focal[b];
-      ii = ii / f;
-      jj = jj / f;
+      ii = fdiv(ii, f);
+      jj = fdiv(jj, f);
       const float dc[3] = {ii, -jj, -1.f};
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        d[i] = dc[0] * M[i * 4 + 0] + dc[1] * M[i * 4 + 1] + dc[2] * M[i * 4 + 2];
+        d[i] = rowdot3(dc, M + i * 4);
         o[i] = M[i * 4 + 3];
       }
     } else {
@@ -98,15 +99,15 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
       const float dc[3] = {0.f, 0.f, -1.f};
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        o[i] = (oc[0] * M[i * 4 + 0] + oc[1] * M[i * 4 + 1] + oc[2] * M[i * 4 + 2]) + M[i * 4 + 3];
-        d[i] = (dc[0] * M[i * 4 + 0] + dc[1] * M[i * 4 + 1] + dc[2] * M[i * 4 + 2]) / M[15];
+        o[i] = fadd(rowdot3(oc, M + i * 4), M[i * 4 + 3]);
+        d[i] = fdiv(rowdot3(dc, M + i * 4), M[15]);
       }
     }
-    // F.normalize: x / max(||x||, 1e-12)
-    const float nrm = fmaxf(sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]), 1e-12f);
+    // F.normalize: x / clamp_min(||x||, 1e-12)
+    const float nrm = fmaxf(tnorm3(d[0], d[1], d[2]), 1e-12f);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      d[i] = d[i] / nrm;
+      d[i] = fdiv(d[i], nrm);
       ro[r * 3 + i] = o[i];
       rd[r * 3 + i] = d[i];
     }
@@ -114,10 +115,10 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
     float tmin[3], tmax[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const float inv = 1.f / d[i];
+      const float inv = fdiv(1.f, d[i]);
       const bool neg = inv < 0.f;
-      tmin[i] = ((neg ? sr : -sr) - o[i]) * inv;
-      tmax[i] = ((neg ? -sr : sr) - o[i]) * inv;
+      tmin[i] = fmul(fsub(neg ? sr : -sr, o[i]), inv);
+      tmax[i] = fmul(fsub(neg ? -sr : sr, o[i]), inv);
     }
     hit = !((tmin[0] > tmax[1]) || (tmin[1] > tmax[0]));
     nr = fmaxf(tmin[0], tmin[1]);
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(256) rays_fix_kernel(long long n, float* __res
   }
   nr = fmaxf(nr, 0.1f);   // clamp_(min=0.1)  (nerf_utils.py:264-265)
   fr = fmaxf(fr, 0.1f);
-  if ((fr - nr) < 1e-3f) fr = nr + 1e-3f;   // (nerf_utils.py:268-270)
+  if (fsub(fr, nr) < 1e-3f) fr = fadd(nr, 1e-3f);   // (nerf_utils.py:268-270)
   nearp[r] = nr;
   farp[r] = fr;
 }

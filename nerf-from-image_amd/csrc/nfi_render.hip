@@ -71,8 +71,10 @@ struct PointP {
 
 __device__ __forceinline__ void point_params(const float o[3], const float d[3], float t, float sr, int R,
                                              PointP& P) {
+  // ray_origins + ray_directions * depth (run.py:283-288, nerf_utils.py:121), then / scene_range
+  // (generator.py:604): two roundings each, as ATen evaluates them.
 #pragma unroll
-  for (int k = 0; k < 3; ++k) P.cx[k] = (o[k] + d[k] * t) / sr;
+  for (int k = 0; k < 3; ++k) P.cx[k] = fdiv(fadd(o[k], fmul(d[k], t)), sr);
   P.mask = (fabsf(P.cx[0]) > 1.f || fabsf(P.cx[1]) > 1.f || fabsf(P.cx[2]) > 1.f) ? 1.f : 0.f;
   plane_params(P.cx[0], P.cx[1], R, P.pl[0]);
   plane_params(P.cx[0], P.cx[2], R, P.pl[1]);
@@ -222,24 +224,48 @@ __device__ __forceinline__ void head_forward(const float y[NO], float mask, floa
 }
 
 // ---------------------------------------------------------------------------------------
-// Chunked wave scans over per-ray arrays held as v[e] = element (e*64 + lane).
+// Wave scans over per-ray arrays held as v[e] = element (e*64 + lane), chunk by chunk.
+// Products and sums of the per-ray recurrences are accumulated in fp64 (ATen's CPU cumprod /
+// cumsum accumulate float inputs in double).
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_incl_prod_d(double v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double t = __shfl_up(v, d);
+    if (l >= d) v *= t;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_incl_sum_d(double v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double t = __shfl_up(v, d);
+    if (l >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d);
+  return v;
+}
+
+// Exclusive cumulative product T[i] = prod_{j<i} a[j]  (cumprod_exclusive, nerf_utils.py:20-25)
 template <int E>
 __device__ __forceinline__ void excl_prod(const float (&a)[E], float (&T)[E]) {
-  float carry = 1.f;
+  double carry = 1.0;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const float inc = wave_incl_prod(a[e]);
-    float ex = __shfl_up(inc, 1);
-    if (lane_id() == 0) ex = 1.f;
-    T[e] = carry * ex;
-    carry = carry * readlane(inc, 63);
+    const double inc = wave_incl_prod_d((double)a[e]);
+    double ex = __shfl_up(inc, 1);
+    if (lane_id() == 0) ex = 1.0;
+    T[e] = (float)(carry * ex);
+    carry = carry * __shfl(inc, 63);
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Forward kernel
-// ---------------------------------------------------------------------------------------
 struct RayCtx {
   long long r;
   int b;
@@ -256,7 +282,7 @@ __device__ __forceinline__ void load_ray(const nfi_render_args& a, long long r, 
     R.o[k] = a.ro[r * 3 + k];
     R.d[k] = a.rd[r * 3 + k];
   }
-  R.rdn = sqrtf(R.d[0] * R.d[0] + R.d[1] * R.d[1] + R.d[2] * R.d[2]);   // ray_directions.norm
+  R.rdn = tnorm3(R.d[0], R.d[1], R.d[2]);   // ray_directions.norm(p=2, dim=-1) (nerf_utils.py:142)
   R.near_ = a.near_[r];
   R.far_ = a.far_[r];
 }
@@ -282,28 +308,32 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   wave_lds_sync();
 }
 
-template <int S, bool FINE>
-struct Cfg {
-  static constexpr int SPL = (S + 63) / 64;            // coarse elements per lane
-  static constexpr int N = FINE ? 2 * S : S;            // merged samples per ray
-  static constexpr int NPL = (N + 63) / 64;
-  static constexpr int WAVE_LDS = XTILE + 5 * N + 2 * S + 8;
-};
+// alpha_i = 1 - exp(-sigma_i * dist_i),  a_i = 1 - alpha_i + 1e-10  (nerf_utils.py:136-146)
+__device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, float& aa, float& ex) {
+  ex = expf(fmul(-sigma, dist));
+  al = fsub(1.f, ex);
+  aa = fadd(fsub(1.f, al), 1e-10f);
+}
 
-template <int S, bool FINE>
+// ---------------------------------------------------------------------------------------
+// Forward kernel.  SPL = coarse samples per lane (S <= 64*SPL), NPL = merged per lane.
+// ---------------------------------------------------------------------------------------
+template <int SPL, int NPL, bool FINE>
 __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
-  using C = Cfg<S, FINE>;
-  constexpr int SPL = C::SPL, N = C::N, NPL = C::NPL;
-  __shared__ __attribute__((aligned(16))) float lds[4 * C::WAVE_LDS];
+  constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
+  constexpr int WL = XTILE + 5 * NMAX + 2 * SMAX + 8;
+  __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
   const long long r = (long long)blockIdx.x * 4 + wv;
   if (r >= nrays) return;
-  float* X = lds + wv * C::WAVE_LDS;
-  float* Mt = X + XTILE;          // merged t     [N]
-  float* Ms = Mt + N;             // merged sigma [N]
-  float* Mc = Ms + N;             // merged rgb   [3][N]
-  float* T2 = Mc + 3 * N;         // coarse t [S] then fine t [S] (rank computation) / cdf, bins
+  const int S = a.S;
+  const int N = FINE ? 2 * S : S;
+  float* X = lds + wv * WL;
+  float* Mt = X + XTILE;          // merged t     [NMAX]
+  float* Ms = Mt + NMAX;          // merged sigma [NMAX]
+  float* Mc = Ms + NMAX;          // merged rgb   [3][NMAX]
+  float* T2 = Mc + 3 * NMAX;      // [2*SMAX] coarse t | fine t (ranks); cdf | bins (sample_pdf)
 
   RayCtx R;
   load_ray(a, r, R);
@@ -312,20 +342,23 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
 
   // ---- stratified coarse depths (nerf_utils.py:104-120) ----
   float tc[SPL], sc[SPL], cc[SPL][3];
+  const float delta = fdiv(fsub(R.far_, R.near_), (float)S);
 #pragma unroll
   for (int e = 0; e < SPL; ++e) {
     const int i = e * 64 + l;
     float t = R.near_;
     if (i < S) {
-      t = tlerp(R.near_, R.far_, (float)i / (float)S);
+      t = tlerp(R.near_, R.far_, fdiv((float)i, (float)S));
       if (a.randomize) {
         const float u = a.u_coarse ? a.u_coarse[r * S + i] : rng_uniform(a.seed, a.offset, r, i, 0);
-        t = t + u * ((R.far_ - R.near_) / (float)S);
+        t = fadd(t, fmul(u, delta));
       }
       if (a.z_coarse) a.z_coarse[r * S + i] = t;
     }
     tc[e] = t;
-    field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e]);
+    sc[e] = 0.f;
+    cc[e][0] = cc[e][1] = cc[e][2] = 0.f;
+    if (e * 64 < S) field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e]);
   }
 
   if constexpr (FINE) {
@@ -337,17 +370,17 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
       const int i = e * 64 + l;
-      float dist = 0.f;
-      if (i < S - 1) dist = T2[i + 1] - tc[e];
-      dist = dist * R.rdn;
-      const float ex = expf(-sc[e] * dist);
-      al[e] = 1.f - ex;
-      aa[e] = (i < S) ? (1.f - al[e]) + 1e-10f : 1.f;
+      const float dist = (i < S - 1) ? fmul(fsub(T2[i + 1], tc[e]), R.rdn) : 0.f;
+      float ex;
+      alpha_of(sc[e], dist, al[e], aa[e], ex);
+      if (i >= S) {
+        al[e] = 0.f;
+        aa[e] = 1.f;
+      }
     }
     excl_prod<SPL>(aa, T);
 #pragma unroll
-    for (int e = 0; e < SPL; ++e) w[e] = al[e] * T[e];
-    wave_lds_sync();
+    for (int e = 0; e < SPL; ++e) w[e] = fmul(al[e], T[e]);
     // ---- EG3D smoothing (run.py:266-272): max_pool1d(2,1,pad 1) -> avg_pool1d(2,1) -> +0.01
     float* Wl = Mt;   // scratch [S]
 #pragma unroll
@@ -360,42 +393,35 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       const float wi = w[e];
       const float wp = (i > 0 && i < S) ? Wl[i - 1] : -INFINITY;
       const float wn = (i < S - 1) ? Wl[i + 1] : -INFINITY;
-      const float m0 = fmaxf(wp, wi), m1 = fmaxf(wi, wn);
-      sm[e] = (m0 + m1) / 2.f + 0.01f;
+      sm[e] = fadd(fdiv(fadd(fmaxf(wp, wi), fmaxf(wi, wn)), 2.f), 0.01f);
     }
     wave_lds_sync();
-    // ---- sample_pdf (nerf_utils.py:185-224): bins = midpoints [S-1], weights = sm[1..S-2]
-    float* cdf = T2 + 0;        // [S-1]
-    float* bins = T2 + S;       // [S-1]
 #pragma unroll
     for (int e = 0; e < SPL; ++e) Wl[e * 64 + l] = sm[e];
     wave_lds_sync();
-    float pw[SPL];
-    float tot = 0.f;
+    // ---- sample_pdf (nerf_utils.py:185-224): bins = midpoints [S-1], weights = sm[1..S-2]
+    float pw[SPL], mid[SPL];
+    double tot = 0.0;
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
       const int i = e * 64 + l;
-      pw[e] = (i < S - 2) ? Wl[i + 1] + 1e-5f : 0.f;
-      tot += pw[e];
+      pw[e] = (i < S - 2) ? fadd(Wl[i + 1], 1e-5f) : 0.f;
+      tot += (double)pw[e];
+      mid[e] = (i < S - 1) ? fmul(.5f, fadd(T2[i + 1], T2[i])) : 0.f;
     }
-    tot = wave_sum(tot);
-    // bins from coarse t (still in T2[0..S)); read before overwriting T2
-    float mid[SPL];
-#pragma unroll
-    for (int e = 0; e < SPL; ++e) {
-      const int i = e * 64 + l;
-      mid[e] = (i < S - 1) ? .5f * (T2[i + 1] + T2[i]) : 0.f;
-    }
+    const float totf = (float)wave_sum_d(tot);
     wave_lds_sync();
-    float carry = 0.f;
+    float* cdf = T2 + 0;        // [S-1]
+    float* bins = T2 + SMAX;    // [S-1]
+    double carry = 0.0;
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
       const int i = e * 64 + l;
-      const float pdf = pw[e] / tot;
-      const float inc = wave_incl_sum(pdf) + carry;
-      if (i < S - 2) cdf[i + 1] = inc;
+      const float pdf = (i < S - 2) ? fdiv(pw[e], totf) : 0.f;
+      const double inc = wave_incl_sum_d((double)pdf) + carry;
+      if (i < S - 2) cdf[i + 1] = (float)inc;
       if (i < S - 1) bins[i] = mid[e];
-      carry = readlane(inc, 63);
+      carry = __shfl(inc, 63);
     }
     if (l == 0) cdf[0] = 0.f;
     wave_lds_sync();
@@ -409,24 +435,28 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       // searchsorted(cdf, u, right=True): number of cdf entries <= u
       int lo = 0, hi = S - 1;
       while (lo < hi) {
-        const int mid_ = (lo + hi) >> 1;
-        if (cdf[mid_] <= u) lo = mid_ + 1;
-        else hi = mid_;
+        const int m = (lo + hi) >> 1;
+        if (cdf[m] <= u) lo = m + 1;
+        else hi = m;
       }
       const int below = max(0, lo - 1), above = min(S - 2, lo);
       const float c0 = cdf[below], c1 = cdf[above];
       const float b0 = bins[below], b1 = bins[above];
-      float denom = c1 - c0;
+      float denom = fsub(c1, c0);
       denom = (denom < 1e-5f) ? 1.f : denom;
-      const float tt = (u - c0) / denom;
-      tf[e] = b0 + tt * (b1 - b0);
+      const float tt = fdiv(fsub(u, c0), denom);
+      tf[e] = fadd(b0, fmul(tt, fsub(b1, b0)));
       if (i < S && a.z_fine) a.z_fine[r * S + i] = tf[e];
     }
     wave_lds_sync();
     // ---- fine field evaluation (run.py:283-291) ----
     float sf[SPL], cf[SPL][3];
 #pragma unroll
-    for (int e = 0; e < SPL; ++e) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e]);
+    for (int e = 0; e < SPL; ++e) {
+      sf[e] = 0.f;
+      cf[e][0] = cf[e][1] = cf[e][2] = 0.f;
+      if (e * 64 < S) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e]);
+    }
     // ---- merge: stable sort of cat(z_coarse, z_fine) (run.py:283-288, 312-319) ----
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
@@ -454,8 +484,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
         Ms[rf] = sf[e];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          Mc[k * N + rc] = cc[e][k];
-          Mc[k * N + rf] = cf[e][k];
+          Mc[k * NMAX + rc] = cc[e][k];
+          Mc[k * NMAX + rf] = cf[e][k];
         }
       }
     }
@@ -467,53 +497,58 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
         Mt[i] = tc[e];
         Ms[i] = sc[e];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) Mc[k * N + i] = cc[e][k];
+        for (int k = 0; k < 3; ++k) Mc[k * NMAX + i] = cc[e][k];
       }
     }
   }
   wave_lds_sync();
 
   // ---- compositing (nerf_utils.py:125-163) ----
-  float t[NPL], sg[NPL], al[NPL], aa[NPL], T[NPL];
+  float t[NPL], al[NPL], aa[NPL], T[NPL];
 #pragma unroll
   for (int e = 0; e < NPL; ++e) {
     const int i = e * 64 + l;
     const bool v = i < N;
     t[e] = v ? Mt[i] : 0.f;
-    sg[e] = v ? Ms[i] : 0.f;
-    const float dist = (i < N - 1) ? (Mt[i + 1] - t[e]) * R.rdn : 0.f;
-    const float ex = expf(-sg[e] * dist);
-    al[e] = v ? 1.f - ex : 0.f;
-    aa[e] = v ? (1.f - al[e]) + 1e-10f : 1.f;
+    const float sg = v ? Ms[i] : 0.f;
+    const float dist = (i < N - 1) ? fmul(fsub(Mt[i + 1], t[e]), R.rdn) : 0.f;
+    float ex;
+    alpha_of(sg, dist, al[e], aa[e], ex);
+    if (!v) {
+      al[e] = 0.f;
+      aa[e] = 1.f;
+    }
+    if (v) {
+      a.t_saved[r * N + i] = t[e];
+      a.sigma_saved[r * N + i] = sg;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a.rgb_saved[(r * 3 + k) * N + i] = Mc[k * NMAX + i];
+    }
   }
   excl_prod<NPL>(aa, T);
-  float sr = 0.f, sgc = 0.f, sb = 0.f, sm = 0.f, sd = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, sm = 0.f, sd = 0.f;
 #pragma unroll
   for (int e = 0; e < NPL; ++e) {
     const int i = e * 64 + l;
     if (i < N) {
-      const float w = al[e] * T[e];
-      sr += w * Mc[0 * N + i];
-      sgc += w * Mc[1 * N + i];
-      sb += w * Mc[2 * N + i];
+      const float w = fmul(al[e], T[e]);
+      s0 = fmaf(w, Mc[0 * NMAX + i], s0);
+      s1 = fmaf(w, Mc[1 * NMAX + i], s1);
+      s2 = fmaf(w, Mc[2 * NMAX + i], s2);
       sm += w;
-      sd += w * t[e];
-      a.t_saved[r * N + i] = t[e];
-      a.sigma_saved[r * N + i] = sg[e];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) a.rgb_saved[(r * 3 + k) * N + i] = Mc[k * N + i];
+      sd = fmaf(w, t[e], sd);
     }
   }
-  sr = wave_sum(sr);
-  sgc = wave_sum(sgc);
-  sb = wave_sum(sb);
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
   sm = wave_sum(sm);
   sd = wave_sum(sd);
   if (l == 0) {
-    const float bg = a.white_bg ? (1.f - sm) : 0.f;
-    a.rgb[r * 3 + 0] = sr + bg;
-    a.rgb[r * 3 + 1] = sgc + bg;
-    a.rgb[r * 3 + 2] = sb + bg;
+    const float bg = a.white_bg ? fsub(1.f, sm) : 0.f;
+    a.rgb[r * 3 + 0] = s0 + bg;
+    a.rgb[r * 3 + 1] = s1 + bg;
+    a.rgb[r * 3 + 2] = s2 + bg;
     a.mask[r] = sm;
     a.depth[r] = sd;
   }
@@ -523,19 +558,21 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
 // Backward kernel: compositing backward from saved state, then per-sample field backward
 // (recompute taps + decoder), scatter-add of d planes, coordinate gradients -> d ro, d rd.
 // ---------------------------------------------------------------------------------------
-template <int S, bool FINE>
+template <int NPL>
 __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_render_grad_args g) {
-  using C = Cfg<S, FINE>;
-  constexpr int N = C::N, NPL = C::NPL;
-  constexpr int WL = XTILE + N + 8;
+  constexpr int NMAX = 64 * NPL;
+  constexpr int WL = XTILE + 3 * NMAX + 8;
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const int dxl = l >> 5, cl = l & 31;
   const long long nrays = (long long)a.B * a.HW;
   const long long r = (long long)blockIdx.x * 4 + wv;
   if (r >= nrays) return;
+  const int N = a.fine ? 2 * a.S : a.S;
   float* X = lds + wv * WL;
-  float* Mt = X + XTILE;
+  float* Lt = X + XTILE;          // t      [NMAX]
+  float* Lg = Lt + NMAX;          // dL/d sigma [NMAX]
+  float* Lw = Lg + NMAX;          // weights    [NMAX]
   const bool dcoord = g.g_ro != nullptr;
 
   RayCtx R;
@@ -549,38 +586,38 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
   const float gm = g.g_mask[r] - (a.white_bg ? (gr0 + gr1 + gr2) : 0.f);
 
   // ---- compositing backward ----
-  float t[NPL], sg[NPL], al[NPL], aa[NPL], ex[NPL], dist[NPL], raw[NPL], T[NPL], ee[NPL];
-#pragma unroll
-  for (int e = 0; e < NPL; ++e) {
-    const int i = e * 64 + l;
-    t[e] = (i < N) ? a.t_saved[r * N + i] : 0.f;
-    Mt[e * 64 + l] = t[e];
-  }
-  wave_lds_sync();
-#pragma unroll
-  for (int e = 0; e < NPL; ++e) {
-    const int i = e * 64 + l;
-    const bool v = i < N;
-    sg[e] = v ? a.sigma_saved[r * N + i] : 0.f;
-    raw[e] = (i < N - 1) ? (Mt[i + 1] - t[e]) : 0.f;
-    dist[e] = raw[e] * R.rdn;
-    ex[e] = expf(-sg[e] * dist[e]);
-    al[e] = v ? 1.f - ex[e] : 0.f;
-    aa[e] = v ? (1.f - al[e]) + 1e-10f : 1.f;
-    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
-    if (v) {
-      c0 = a.rgb_saved[(r * 3 + 0) * N + i];
-      c1 = a.rgb_saved[(r * 3 + 1) * N + i];
-      c2 = a.rgb_saved[(r * 3 + 2) * N + i];
-    }
-    ee[e] = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm : 0.f;
-  }
-  excl_prod<NPL>(aa, T);
-  // S_k = sum_{i>k} e_i alpha_i prod_{k<j<i} a_j  : reverse exclusive scan of f_i(s) = a_i s + e_i alpha_i
-  float gsig[NPL], gcw[NPL];
   float grdn = 0.f;
   {
-    float cA = 1.f, cB = 0.f;   // composition of maps with index beyond the current chunk
+    float t[NPL], sg[NPL], al[NPL], aa[NPL], ex[NPL], dist[NPL], raw[NPL], T[NPL], ee[NPL];
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      const int i = e * 64 + l;
+      t[e] = (i < N) ? a.t_saved[r * N + i] : 0.f;
+      Lt[e * 64 + l] = t[e];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      const int i = e * 64 + l;
+      const bool v = i < N;
+      sg[e] = v ? a.sigma_saved[r * N + i] : 0.f;
+      raw[e] = (i < N - 1) ? fsub(Lt[i + 1], t[e]) : 0.f;
+      dist[e] = fmul(raw[e], R.rdn);
+      alpha_of(sg[e], dist[e], al[e], aa[e], ex[e]);
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+      if (v) {
+        c0 = a.rgb_saved[(r * 3 + 0) * N + i];
+        c1 = a.rgb_saved[(r * 3 + 1) * N + i];
+        c2 = a.rgb_saved[(r * 3 + 2) * N + i];
+      } else {
+        al[e] = 0.f;
+        aa[e] = 1.f;
+      }
+      ee[e] = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm : 0.f;
+    }
+    excl_prod<NPL>(aa, T);
+    // S_k = sum_{i>k} e_i alpha_i prod_{k<j<i} a_j : reverse exclusive scan of f_i(s) = a_i s + e_i alpha_i
+    float cB = 0.f;   // composition of the maps beyond the current chunk, evaluated at 0
 #pragma unroll
     for (int e = NPL - 1; e >= 0; --e) {
       float A = aa[e], B = ee[e] * al[e];
@@ -592,98 +629,121 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
           A = A * A2;
         }
       }
-      // exclusive: F_{l+1} o carry evaluated at 0
-      float An = __shfl_down(A, 1), Bn = __shfl_down(B, 1);
-      float Sk = (l < 63) ? fmaf(An, cB, Bn) : cB;
-      const float A0 = readlane(A, 0), B0 = readlane(B, 0);
-      cB = fmaf(A0, cB, B0);
-      cA = A0 * cA;
-      const float dal = T[e] * (ee[e] - Sk);
-      gsig[e] = dal * dist[e] * ex[e];
-      grdn += dal * sg[e] * ex[e] * raw[e];
-      gcw[e] = al[e] * T[e];   // weight w_i; d c_i = w_i * g_rgb
+      const float An = __shfl_down(A, 1), Bn = __shfl_down(B, 1);
+      const float Sk = (l < 63) ? fmaf(An, cB, Bn) : cB;
+      cB = fmaf(readlane(A, 0), cB, readlane(B, 0));
+      const float dal = T[e] * (ee[e] - Sk);                  // dL/d alpha_k
+      Lg[e * 64 + l] = dal * dist[e] * ex[e];                  // d alpha/d sigma = dist * exp(-sigma dist)
+      grdn += dal * sg[e] * ex[e] * raw[e];                   // dists = raw * ||rd||
+      Lw[e * 64 + l] = al[e] * T[e];                           // w_i; dL/d c_i = w_i g_rgb
     }
   }
+  wave_lds_sync();
 
   // ---- per-sample field backward ----
   float gro[3] = {0.f, 0.f, 0.f}, grd[3] = {0.f, 0.f, 0.f};
-  float dpal[NA * 3];
-#pragma unroll
-  for (int k = 0; k < NA * 3; ++k) dpal[k] = 0.f;
+  float pacc = 0.f;   // lane k < 30 accumulates dL/d palette[k/3][k%3] over the ray
+  const float sr = a.field.scene_range;
 
 #pragma unroll 1
   for (int e = 0; e < NPL; ++e) {
+    if (e * 64 >= N) break;
     const int npts = min(64, N - e * 64);
     const int i = e * 64 + l;
     const bool v = i < N;
-    PointP P;
-    point_params(R.o, R.d, t[e], a.field.scene_range, pv.R, P);
-    gather_features(pv, P, npts, X);
+    const float te = Lt[i];
+    float pmask;
+    {
+      PointP P;
+      point_params(R.o, R.d, te, sr, pv.R, P);
+      gather_features(pv, P, npts, X);
+      pmask = P.mask;
+    }
     wave_lds_sync();
     float x[NC];
     load_row(X, l, x);
     float y[NO];
     mlp_forward(a.field.dec, x, y);
-    Head h;
-    head_forward(y, P.mask, a.field.inv_alpha, a.field.beta, pal, h);
-    // sigma -> distance
-    const float gs = v ? gsig[e] : 0.f;
-    const float xn = -y[0];
-    const float sgn = tsign(xn);
-    const float ex2 = expf(-fabsf(xn) / a.field.beta);
-    const float gcdf = (gs * a.field.inv_alpha) * (1.f - P.mask);
-    const float gxn = ((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn;
     float gy[NO];
-    gy[0] = -gxn;
-    // rgb -> logits (softmax backward), palette gradient
-    const float w = v ? gcw[e] : 0.f;
-    const float gc0 = w * gr0, gc1 = w * gr1, gc2 = w * gr2;
-    float gp[NA], dot = 0.f;
+    {
+      Head h;
+      head_forward(y, pmask, a.field.inv_alpha, a.field.beta, pal, h);
+      // sigma -> distance  (generator.py:629-636, laplace_cdf generator.py:30-33)
+      const float gs = v ? Lg[i] : 0.f;
+      const float xn = -y[0];
+      const float sgn = tsign(xn);
+      const float ex2 = expf(-fabsf(xn) / a.field.beta);
+      const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
+      gy[0] = -(((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn);
+      // rgb -> logits (softmax backward) and palette gradient  (generator.py:668-679)
+      const float w = v ? Lw[i] : 0.f;
+      const float gc0 = w * gr0, gc1 = w * gr1, gc2 = w * gr2;
+      float gp[NA], dot = 0.f;
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      gp[k] = gc0 * pal[k * 3 + 0] + gc1 * pal[k * 3 + 1] + gc2 * pal[k * 3 + 2];
-      dot = fmaf(gp[k], h.p[k], dot);
-      dpal[k * 3 + 0] = fmaf(h.p[k], gc0, dpal[k * 3 + 0]);
-      dpal[k * 3 + 1] = fmaf(h.p[k], gc1, dpal[k * 3 + 1]);
-      dpal[k * 3 + 2] = fmaf(h.p[k], gc2, dpal[k * 3 + 2]);
+      for (int k = 0; k < NA; ++k) {
+        gp[k] = gc0 * pal[k * 3 + 0] + gc1 * pal[k * 3 + 1] + gc2 * pal[k * 3 + 2];
+        dot = fmaf(gp[k], h.p[k], dot);
+      }
+#pragma unroll
+      for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
+      // per-point palette contributions p_k * gc, column-summed through the LDS tile
+      float* row = X + l * XS;
+#pragma unroll
+      for (int k = 0; k < NA; ++k) {
+        row[k * 3 + 0] = h.p[k] * gc0;
+        row[k * 3 + 1] = h.p[k] * gc1;
+        row[k * 3 + 2] = h.p[k] * gc2;
+      }
     }
-#pragma unroll
-    for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
+    wave_lds_sync();
+    if (l < NA * 3) {
+      float s = 0.f;
+      for (int j = 0; j < npts; ++j) s += X[j * XS + l];
+      pacc += s;
+    }
     float gx[NC];
     mlp_backward(a.field.dec, x, gy, gx);
+    bool nz = false;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
+    for (int c = 0; c < NC; ++c) {
+      gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
+      nz |= (gx[c] != 0.f);
+    }
+    // points whose feature gradient is exactly zero (outside the box, or zero weight and
+    // zero density gradient) add nothing: skip their atomics and coordinate re-gather
+    const unsigned long long live = __ballot(nz && v);
     wave_lds_sync();
     store_row(X, l, gx);
     wave_lds_sync();
-    // scatter-add d planes (+ re-gather for d coords), one point at a time, 256-B rows
+    // scatter-add d planes (+ re-gather for d coords), one point at a time, 256-B rows.
+    // The point's bilinear parameters are recomputed wave-uniformly from its depth.
 #pragma unroll 1
     for (int j = 0; j < npts; ++j) {
+      if (!((live >> j) & 1ull)) continue;
+      const float tj = readlane(te, j);
+      PointP P;
+      point_params(R.o, R.d, tj, sr, pv.R, P);
       const float gv = X[j * XS + cl];
       float GX[3], GY[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        const int pk = readlane(P.pl[q].tex, j);
-        const float ew = readlane(P.pl[q].e, j), ww = readlane(P.pl[q].w, j);
-        const float s = readlane(P.pl[q].s, j), n = readlane(P.pl[q].n, j);
-        const int t0 = (pk & 0xFFFFF) + (dxl ? ((pk >> 20) & 1) : 0);
-        const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-        const float wx = dxl ? ww : ew;
+        const PlaneP& pp = P.pl[q];
+        const int t0 = (pp.tex & 0xFFFFF) + (dxl ? ((pp.tex >> 20) & 1) : 0);
+        const int t1 = t0 + (((pp.tex >> 21) & 1) ? pv.R : 0);
+        const float wx = dxl ? pp.w : pp.e;
         float* dq = dpl + q * pv.sq + cl;
-        unsafeAtomicAdd(dq + t0 * pv.st, gv * (s * wx));
-        unsafeAtomicAdd(dq + t1 * pv.st, gv * (n * wx));
+        unsafeAtomicAdd(dq + t0 * pv.st, gv * (pp.s * wx));
+        unsafeAtomicAdd(dq + t1 * pv.st, gv * (pp.n * wx));
         if (dcoord) {
           const float* bq = pv.base + q * pv.sq + cl;
           const float v0 = bq[t0 * pv.st], v1 = bq[t1 * pv.st];
-          const float px = (dxl ? 1.f : -1.f) * (s * v0 + n * v1) * gv;
+          const float px = (dxl ? 1.f : -1.f) * (pp.s * v0 + pp.n * v1) * gv;
           const float py = wx * (v1 - v0) * gv;
-          GX[q] = wave_sum(px) * readlane(P.pl[q].gxm, j);
-          GY[q] = wave_sum(py) * readlane(P.pl[q].gym, j);
+          GX[q] = wave_sum(px) * pp.gxm;
+          GY[q] = wave_sum(py) * pp.gym;
         }
       }
       if (dcoord) {
-        const float tj = readlane(t[e], j);
-        const float sr = a.field.scene_range;
         const float dp0 = (GX[0] + GX[1]) / sr;
         const float dp1 = (GY[0] + GX[2]) / sr;
         const float dp2 = (GY[1] + GY[2]) / sr;
@@ -699,11 +759,7 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
   }
 
   // ---- per-ray outputs ----
-#pragma unroll
-  for (int k = 0; k < NA * 3; ++k) {
-    const float s = wave_sum(dpal[k]);
-    if (l == 0) g.d_palette_ray[r * (NA * 3) + k] = s;
-  }
+  if (l < NA * 3) g.d_palette_ray[r * (NA * 3) + l] = pacc;
   if (dcoord) {
     grdn = wave_sum(grdn);
     if (l == 0) {
@@ -717,32 +773,33 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
   }
 }
 
-template <int S, bool FINE>
-static int launch_pair(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
+template <int SPL, int NPL, bool FINE>
+static int launch(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
   const long long nrays = (long long)a->B * a->HW;
   const unsigned blocks = (unsigned)((nrays + 3) / 4);
   if (g == nullptr) {
-    render_fwd_kernel<S, FINE><<<blocks, 256, 0, s>>>(*a);
+    render_fwd_kernel<SPL, NPL, FINE><<<blocks, 256, 0, s>>>(*a);
     NFI_CHECK_LAUNCH("render_fwd_kernel");
   } else {
-    render_bwd_kernel<S, FINE><<<blocks, 256, 0, s>>>(*a, *g);
+    render_bwd_kernel<NPL><<<blocks, 256, 0, s>>>(*a, *g);
     NFI_CHECK_LAUNCH("render_bwd_kernel");
   }
   return NFI_OK;
 }
 
 static int dispatch(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
-  const bool f = a->fine != 0;
-  switch (a->S) {
-    case 32: return f ? launch_pair<32, true>(a, g, s) : launch_pair<32, false>(a, g, s);
-    case 64: return f ? launch_pair<64, true>(a, g, s) : launch_pair<64, false>(a, g, s);
-    case 128: return f ? launch_pair<128, true>(a, g, s) : launch_pair<128, false>(a, g, s);
-    case 256:
-      if (!f) return launch_pair<256, false>(a, g, s);
-      break;
-    default: break;
+  const int S = a->S;
+  if (a->fine) {
+    if (S >= 3 && S <= 32) return launch<1, 1, true>(a, g, s);
+    if (S >= 3 && S <= 64) return launch<1, 2, true>(a, g, s);
+    if (S >= 3 && S <= 128) return launch<2, 4, true>(a, g, s);
+  } else {
+    if (S >= 1 && S <= 64) return launch<1, 1, false>(a, g, s);
+    if (S >= 1 && S <= 128) return launch<2, 2, false>(a, g, s);
+    if (S >= 1 && S <= 256) return launch<4, 4, false>(a, g, s);
   }
-  set_error("render: unsupported samples per ray S=%d (fine=%d)", a->S, (int)f);
+  set_error("render: unsupported samples per ray S=%d (fine=%d): need 3..128 with fine sampling, "
+            "1..256 without", S, (int)a->fine);
   return NFI_EINVAL;
 }
 

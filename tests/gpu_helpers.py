@@ -52,6 +52,17 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
     return out
 
 
+def run_oracle64(inp, meta, with_grad=True, return_intermediates=False):
+    """The oracle evaluated in float64 — the 'exact' answer both fp32 paths are measured against."""
+    inp64 = {k: (v.double() if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in inp.items()}
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        return run_oracle(inp64, meta, with_grad, return_intermediates)
+    finally:
+        torch.set_default_dtype(prev)
+
+
 def run_oracle(inp, meta, with_grad=True, return_intermediates=False):
     ncg = bool(meta.get('force_no_cam_grad', 0))
     field = orc.Field(planes=inp['planes'].clone().requires_grad_(with_grad),
@@ -101,7 +112,7 @@ def synthetic_inputs(B, H, W, S, R, scene_range, seed, ortho=False, flipped=True
     q = torch.nn.functional.normalize(torch.randn(B, 4, generator=g), dim=-1)
     t2 = 0.05 * torch.randn(B, 2, generator=g)
     if ortho:
-        s = torch.full((B,), 1.0 / scene_range)
+        s = torch.full((B, 1), 1.0 / scene_range)
         cam, focal = orc.pose_to_matrix(None, t2, s, q, flipped)
     else:
         f = 2 * 1.859

@@ -1,61 +1,75 @@
-"""Parity of the HIP renderer (through the C-ABI) against the reference's golden vectors and
-the CPU oracle.  fp32 tolerances, written per assertion:
-  rgb, mask   |d| <= 2e-5 + 2e-5 |ref|      depth |d| <= 1e-4 + 1e-4 |ref|
-  d palette, d cam, d focal: relative L2 <= 1e-4;  d planes: relative L2 <= 1e-3
-(summation order: wave-tree sums and float atomics vs ATen's sequential CPU loops).
+"""Parity of the HIP renderer (called through the C-ABI) against the reference.
+
+Truth is the oracle evaluated in float64 (`oracle64`).  The reference's own fp32 result
+(golden vectors, or the fp32 oracle which is pinned to them bit for bit) has an error
+`err_ref` against that truth; the HIP fp32 result must satisfy
+    err_hip <= max(FLOOR, K * err_ref),   K = 4
+i.e. the HIP path is as accurate as the reference's own fp32 path.  This matters because
+the reference is ill-conditioned in places (a deterministic first sample lies exactly on
+the box surface, where the (|x|>1) mask flips with one ulp; d focal is a sum with heavy
+cancellation: fp32-vs-fp64 differences of 1e-3..7e-2 in the reference itself).
+FLOORs (fp32): rgb/mask max|d| 2e-5, depth 1e-4, d palette / d cam / d focal
+rel-L2 1e-4, d planes rel-L2 1e-3.
 """
 
 import pytest
 import torch
 
 from golden_io import RENDER_CASES, load
-from gpu_helpers import rel_l2, run_hip, run_oracle, synthetic_inputs
+from gpu_helpers import rel_l2, run_hip, run_oracle, run_oracle64, synthetic_inputs
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device('cuda:0')
+K = 4.0
+FLOOR = {'rgb': 2e-5, 'mask': 2e-5, 'depth': 1e-4, 'd_planes': 1e-3, 'd_palette': 1e-4,
+         'd_cam': 1e-4, 'd_focal': 1e-4}
+ELEMENTWISE = ('rgb', 'mask', 'depth')
 
-TOL_PIX = dict(rtol=2e-5, atol=2e-5)
-TOL_DEPTH = dict(rtol=1e-4, atol=1e-4)
+
+def _err(a, b, key):
+    if key in ELEMENTWISE:
+        return float((a.double().cpu() - b.double().cpu()).abs().max())
+    return rel_l2(a, b)
 
 
-def _compare(out, ref, grad_tol_planes=1e-3, grad_tol=1e-4):
-    torch.testing.assert_close(out['rgb'], ref['rgb'], **TOL_PIX)
-    torch.testing.assert_close(out['mask'], ref['mask'], **TOL_PIX)
-    torch.testing.assert_close(out['depth'], ref['depth'], **TOL_DEPTH)
-    if 'd_planes' in ref:
-        assert rel_l2(out['d_planes'], ref['d_planes']) <= grad_tol_planes
-        assert rel_l2(out['d_palette'], ref['d_palette']) <= grad_tol
-    for k in ('d_cam', 'd_focal'):
-        if k in ref:
-            assert rel_l2(out[k], ref[k]) <= grad_tol, (k, rel_l2(out[k], ref[k]))
+def check(hip, ref32, ref64):
+    report = {}
+    for key, floor in FLOOR.items():
+        if key not in ref64 or key not in hip:
+            continue
+        e_hip = _err(hip[key], ref64[key], key)
+        e_ref = _err(ref32[key], ref64[key], key)
+        report[key] = (e_hip, e_ref)
+        print(f'  {key:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
+        assert e_hip <= max(floor, K * e_ref), f'{key}: hip err {e_hip:.3g} vs ref fp32 err {e_ref:.3g}'
+    return report
 
 
 @pytest.mark.parametrize('case', RENDER_CASES)
 def test_golden_render(case):
-    """HIP path vs the reference's own outputs and gradients (tests/golden)."""
+    """HIP path vs the reference's own fp32 outputs/gradients (tests/golden) and fp64 truth."""
     d, meta = load(f'render_{case}')
-    out = run_hip(d, meta, DEV)
-    _compare(out, d)
+    hip = run_hip(d, meta, DEV)
+    check(hip, d, run_oracle64(d, meta))
 
 
-@pytest.mark.parametrize('S,fine', [(32, True), (64, True), (128, True), (64, False), (256, False)])
+@pytest.mark.parametrize('S,fine', [(8, True), (32, True), (48, True), (64, True), (100, True),
+                                    (128, True), (64, False), (200, False), (256, False)])
 def test_oracle_seeded(S, fine):
-    """Every kernel specialisation vs the oracle on seeded inputs (multi-chunk rays included)."""
+    """Every kernel specialisation (1/2/4 samples per lane, partial chunks) vs the oracle."""
     inp, meta = synthetic_inputs(B=2, H=8, W=8, S=S, R=32, scene_range=1.4, seed=S + fine)
     meta['fine'] = int(fine)
-    out = run_hip(inp, meta, DEV)
-    ref = run_oracle(inp, meta)
-    _compare(out, ref)
+    check(run_hip(inp, meta, DEV), run_oracle(inp, meta), run_oracle64(inp, meta))
 
 
 def test_intermediate_depths():
-    """Coarse depths, fine (sample_pdf) depths and merged order vs the oracle's intermediates."""
+    """Coarse depths are bit-faithful; fine (sample_pdf) and merged depths within 1e-5 of the span."""
     inp, meta = synthetic_inputs(B=2, H=8, W=8, S=64, R=32, scene_range=1.4, seed=3)
     dbg = {}
     run_hip(inp, meta, DEV, debug=dbg, with_grad=False)
     ref = run_oracle(inp, meta, with_grad=False, return_intermediates=True)['inter']
     n = 2 * 8 * 8
-    torch.testing.assert_close(dbg['z_coarse'].cpu(), ref['z_coarse'].reshape(n, -1), rtol=1e-6, atol=1e-6)
+    assert torch.equal(dbg['z_coarse'].cpu(), ref['z_coarse'].reshape(n, -1))
     span = (ref['far'] - ref['near']).reshape(n, 1)
     err = (dbg['z_fine'].cpu() - ref['z_fine'].reshape(n, -1)).abs() / span
     assert float(err.max()) <= 1e-5
@@ -66,21 +80,15 @@ def test_intermediate_depths():
 def test_deterministic_mode_and_white_background():
     inp, meta = synthetic_inputs(B=2, H=8, W=8, S=32, R=16, scene_range=0.55, seed=11, white_bg=True,
                                  randomize=False, flipped=False)
-    out = run_hip(inp, meta, DEV)
-    ref = run_oracle(inp, meta)
-    _compare(out, ref)
+    check(run_hip(inp, meta, DEV), run_oracle(inp, meta), run_oracle64(inp, meta))
 
 
 def test_full_plane_resolution():
     """Real plane size (R=256, 25 MB/image) and 64+64 samples on a 24x24 crop of rays."""
     inp, meta = synthetic_inputs(B=1, H=24, W=24, S=64, R=256, scene_range=1.4, seed=5)
-    out = run_hip(inp, meta, DEV)
-    ref = run_oracle(inp, meta)
-    _compare(out, ref)
+    check(run_hip(inp, meta, DEV), run_oracle(inp, meta), run_oracle64(inp, meta))
 
 
 def test_ortho_camera():
     inp, meta = synthetic_inputs(B=2, H=8, W=8, S=32, R=16, scene_range=2.0, seed=8, ortho=True)
-    out = run_hip(inp, meta, DEV)
-    ref = run_oracle(inp, meta)
-    _compare(out, ref)
+    check(run_hip(inp, meta, DEV), run_oracle(inp, meta), run_oracle64(inp, meta))
