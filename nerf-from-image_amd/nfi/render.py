@@ -154,6 +154,8 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
     _check_frozen(f)
     ro, rd, near, far = ops.rays(tform_cam2world, focal_length, center, bbox, height, width,
                                  cfg.scene_range)
+    if debug is not None:
+        debug.update(ro=ro.detach(), rd=rd.detach(), near=near, far=far)
     if force_no_cam_grad:
         # run.py:211-214 detaches query points and directions (the reference's fine points keep a
         # gradient path to ray origins; its callers of this mode run under no_grad)

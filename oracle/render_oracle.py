@@ -282,7 +282,8 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
     sigma, rgb = sampler(field, query_points)
     sigma = sigma.view(*query_points.shape[:-1], -1)
     rgb = rgb.view(*query_points.shape[:-1], -1)
-    inter = {'near': near_thresh, 'far': far_thresh, 'z_coarse': depth_values}
+    inter = {'near': near_thresh, 'far': far_thresh, 'z_coarse': depth_values,
+             'ro': ray_origins.detach(), 'rd': ray_directions.detach()}
     if fine_sampling:
         z_vals = depth_values
         with torch.no_grad():
