@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 1
+#define NFI_ABI_VERSION 2
 #define NFI_DEC_SIZE 3088 /* floats in the packed decoder buffer */
 
 enum {
@@ -103,6 +103,8 @@ typedef struct nfi_render_grad_args {
   float* d_palette_ray; /* [B*HW,30] per-ray partial dL/d palette (reduce with nfi_segment_sum) */
   float* g_ro;          /* [B*HW,3] dL/d ray origins  (NULL: skip coordinate gradients) */
   float* g_rd;          /* [B*HW,3] dL/d unit ray directions */
+  void* workspace;      /* device scratch of nfi_render_backward_workspace_bytes() bytes */
+  int64_t workspace_bytes;
 } nfi_render_grad_args;
 
 int32_t nfi_abi_version(void);
@@ -118,7 +120,7 @@ int32_t nfi_planes_to_texel_major(const float* src, int32_t B, int32_t R, float*
 int32_t nfi_planes_to_channel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream);
 
 /* get_ray_bundle + F.normalize + compute_near_far_planes (run.py:193-200).
- * Outputs ro, rd (unit) [B*H*W,3], near, far [B*H*W].  ws: 2 uint32 of device scratch. */
+ * Outputs ro, rd (unit) [B*H*W,3], near, far [B*H*W].  ws: 2 + B*H*W uint32 of device scratch. */
 int32_t nfi_rays_forward(const nfi_camera* cam, float scene_range, float* ro, float* rd,
                          float* near_, float* far_, uint32_t* ws, void* stream);
 
@@ -132,11 +134,14 @@ int32_t nfi_segment_sum(const float* in, int32_t B, int32_t M, int32_t K, float*
                         void* stream);
 
 /* Fused forward: stratified samples -> field -> coarse weights + EG3D smoothing -> sample_pdf
- * -> fine samples -> field -> sort/merge -> compositing.  Supported S: 32, 64, 128
- * (fine) or 32, 64, 128, 256 (no fine). */
+ * -> fine samples -> field -> sort/merge -> compositing.  Supported S: 3..128 with fine
+ * sampling (N = 2S merged samples), 1..256 without. */
 int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
 
-/* Fused backward of nfi_render_forward from its saved state (recomputes the field). */
+/* Backward of nfi_render_forward from its saved state: per-ray compositing + field backward
+ * (recomputes taps and decoder) writes per-sample feature gradients; d planes is then summed
+ * per 16x16-cell plane tile in LDS (samples binned by tile) and flushed once per tile. */
+int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 
 #ifdef __cplusplus

@@ -74,10 +74,24 @@ __device__ __forceinline__ float tsign(float x) { return (x > 0.f) ? 1.f : ((x <
 // Explicitly rounded fp32 ops (no FMA contraction): geometry that decides box-mask and texel
 // membership is evaluated in exactly ATen's CPU rounding order (see DESIGN.md "bit-faithful
 // geometry"), so a sample on the box surface is classified as the reference classifies it.
-__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
-__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+// (`#pragma clang fp contract(off)` keeps the instructions free of the `contract` flag, so the
+// backend cannot fuse them into an FMA after inlining — __fmul_rn alone does not prevent it.)
+__device__ __forceinline__ float fmul(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float fadd(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float fsub(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+__device__ __forceinline__ float fdiv(float a, float b) {
+#pragma clang fp contract(off)
+  return a / b;
+}
 
 // torch.lerp on CPU (ATen LerpKernel lerp_vec): |w| < 0.5 ? fma(w, e-s, s) : fma(w-1, e-s, e)
 __device__ __forceinline__ float tlerp(float a, float b, float w) {

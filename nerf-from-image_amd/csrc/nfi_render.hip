@@ -558,8 +558,17 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
 // Backward kernel: compositing backward from saved state, then per-sample field backward
 // (recompute taps + decoder), scatter-add of d planes, coordinate gradients -> d ro, d rd.
 // ---------------------------------------------------------------------------------------
+struct BwdArgs {
+  const float* g_rgb;
+  const float* g_mask;
+  float* d_palette_ray;
+  float* g_ro;
+  float* g_rd;
+  float* gfeat;         // [rays][N][32] per-sample dL/d(tap feature of each plane) = dL/dx / 3
+};
+
 template <int NPL>
-__global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_render_grad_args g) {
+__global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, BwdArgs g) {
   constexpr int NMAX = 64 * NPL;
   constexpr int WL = XTILE + 3 * NMAX + 8;
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
@@ -579,7 +588,6 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
   load_ray(a, r, R);
   const PlaneView pv{a.field.planes + (long long)R.b * a.field.sb, (int)a.field.sq, (int)a.field.st,
                      a.field.R};
-  float* __restrict__ dpl = g.d_planes + (long long)R.b * a.field.sb;
   const float* pal = a.field.palette + R.b * (NA * 3);
 
   const float gr0 = g.g_rgb[r * 3 + 0], gr1 = g.g_rgb[r * 3 + 1], gr2 = g.g_rgb[r * 3 + 2];
@@ -703,38 +711,38 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
     }
     float gx[NC];
     mlp_backward(a.field.dec, x, gy, gx);
-    bool nz = false;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
-      nz |= (gx[c] != 0.f);
+    for (int c = 0; c < NC; ++c) gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
+    // per-sample feature gradient -> G[ray][i][32]; d planes is summed per tile later
+    if (v) {
+      float4* gr = reinterpret_cast<float4*>(g.gfeat + (r * N + i) * NC);
+#pragma unroll
+      for (int k = 0; k < NC / 4; ++k) gr[k] = make_float4(gx[4 * k], gx[4 * k + 1], gx[4 * k + 2], gx[4 * k + 3]);
     }
-    // points whose feature gradient is exactly zero (outside the box, or zero weight and
-    // zero density gradient) add nothing: skip their atomics and coordinate re-gather
-    const unsigned long long live = __ballot(nz && v);
-    wave_lds_sync();
-    store_row(X, l, gx);
-    wave_lds_sync();
-    // scatter-add d planes (+ re-gather for d coords), one point at a time, 256-B rows.
-    // The point's bilinear parameters are recomputed wave-uniformly from its depth.
-#pragma unroll 1
-    for (int j = 0; j < npts; ++j) {
-      if (!((live >> j) & 1ull)) continue;
-      const float tj = readlane(te, j);
-      PointP P;
-      point_params(R.o, R.d, tj, sr, pv.R, P);
-      const float gv = X[j * XS + cl];
-      float GX[3], GY[3];
+    if (dcoord) {
+      bool nz = false;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const PlaneP& pp = P.pl[q];
-        const int t0 = (pp.tex & 0xFFFFF) + (dxl ? ((pp.tex >> 20) & 1) : 0);
-        const int t1 = t0 + (((pp.tex >> 21) & 1) ? pv.R : 0);
-        const float wx = dxl ? pp.w : pp.e;
-        float* dq = dpl + q * pv.sq + cl;
-        unsafeAtomicAdd(dq + t0 * pv.st, gv * (pp.s * wx));
-        unsafeAtomicAdd(dq + t1 * pv.st, gv * (pp.n * wx));
-        if (dcoord) {
+      for (int c = 0; c < NC; ++c) nz |= (gx[c] != 0.f);
+      // points with an exactly-zero feature gradient move no coordinate: skip their re-gather
+      const unsigned long long live = __ballot(nz && v);
+      wave_lds_sync();
+      store_row(X, l, gx);
+      wave_lds_sync();
+      // d coords: re-gather the taps, grid_sampler_2d_backward's d grid (one point at a time)
+#pragma unroll 1
+      for (int j = 0; j < npts; ++j) {
+        if (!((live >> j) & 1ull)) continue;
+        const float tj = readlane(te, j);
+        PointP P;
+        point_params(R.o, R.d, tj, sr, pv.R, P);
+        const float gv = X[j * XS + cl];
+        float GX[3], GY[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const PlaneP& pp = P.pl[q];
+          const int t0 = (pp.tex & 0xFFFFF) + (dxl ? ((pp.tex >> 20) & 1) : 0);
+          const int t1 = t0 + (((pp.tex >> 21) & 1) ? pv.R : 0);
+          const float wx = dxl ? pp.w : pp.e;
           const float* bq = pv.base + q * pv.sq + cl;
           const float v0 = bq[t0 * pv.st], v1 = bq[t1 * pv.st];
           const float px = (dxl ? 1.f : -1.f) * (pp.s * v0 + pp.n * v1) * gv;
@@ -742,8 +750,6 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
           GX[q] = wave_sum(px) * pp.gxm;
           GY[q] = wave_sum(py) * pp.gym;
         }
-      }
-      if (dcoord) {
         const float dp0 = (GX[0] + GX[1]) / sr;
         const float dp1 = (GY[0] + GX[2]) / sr;
         const float dp2 = (GY[1] + GY[2]) / sr;
@@ -773,34 +779,322 @@ __global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, nfi_
   }
 }
 
-template <int SPL, int NPL, bool FINE>
-static int launch(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
-  const long long nrays = (long long)a->B * a->HW;
-  const unsigned blocks = (unsigned)((nrays + 3) / 4);
-  if (g == nullptr) {
-    render_fwd_kernel<SPL, NPL, FINE><<<blocks, 256, 0, s>>>(*a);
-    NFI_CHECK_LAUNCH("render_fwd_kernel");
-  } else {
-    render_bwd_kernel<NPL><<<blocks, 256, 0, s>>>(*a, *g);
-    NFI_CHECK_LAUNCH("render_bwd_kernel");
+// ---------------------------------------------------------------------------------------
+// d planes by plane tile: every (sample, plane) contribution is binned by the 16x16-cell tile
+// of the plane its bilinear cell lies in; one workgroup sums a chunk of a tile's samples in a
+// 17x17x32 LDS image (ds_add_f32) and flushes it with one float atomic per texel channel.
+// Global atomic traffic drops from 1,536 B per sample to ~37 KB per (tile, chunk).
+// ---------------------------------------------------------------------------------------
+constexpr int TS = 16;            // cells per tile side
+constexpr int TT = TS + 1;        // texels per tile side
+constexpr int CHUNK = 2048;       // (sample, plane) entries per accumulation workgroup
+
+struct BinArgs {
+  const float* ro;
+  const float* rd;
+  const float* t;        // [rays][N] merged depths (saved by the forward)
+  long long nsamp;       // rays * N
+  int N, HW, R, T;       // T = tiles per plane side
+  float sr;
+  int* counts;           // [K]
+  int* cursor;           // [K]
+  int* list;             // [3 * nsamp]
+};
+
+__device__ __forceinline__ int tile_of(int cell, int T) { return min(cell / TS, T - 1); }
+
+// Tile keys of sample s for the three planes; false for samples outside the box (their
+// gradient is exactly zero: sigma * (1 - mask) and weight 0).
+__device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int key[3]) {
+  const long long ray = s / A.N;
+  const int b = (int)(ray / A.HW);
+  float o[3], d[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    o[k] = A.ro[ray * 3 + k];
+    d[k] = A.rd[ray * 3 + k];
   }
+  PointP P;
+  point_params(o, d, A.t[s], A.sr, A.R, P);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int cell = P.pl[q].tex & 0xFFFFF;
+    const int y0 = cell / A.R, x0 = cell % A.R;
+    key[q] = ((b * 3 + q) * A.T + tile_of(y0, A.T)) * A.T + tile_of(x0, A.T);
+  }
+  return P.mask == 0.f;
+}
+
+// Wave-aggregated atomicAdd of 1 per lane on base[key]; returns each lane's slot.
+__device__ __forceinline__ int agg_increment(int* base, int key, bool valid) {
+  const int l = lane_id();
+  unsigned long long active = __ballot(valid);
+  int pos = 0;
+  while (active) {
+    const int leader = __ffsll((long long)active) - 1;
+    const int k = __shfl(key, leader);
+    const unsigned long long m = __ballot(valid && key == k) & active;
+    int old = 0;
+    if (l == leader) old = atomicAdd(base + k, __popcll(m));
+    old = __shfl(old, leader);
+    if ((m >> l) & 1ull) pos = old + __popcll(m & ((1ull << l) - 1ull));
+    active &= ~m;
+  }
+  return pos;
+}
+
+__global__ void __launch_bounds__(256) bin_count_kernel(BinArgs A) {
+  const long long s = (long long)blockIdx.x * 256 + threadIdx.x;
+  int key[3] = {0, 0, 0};
+  bool v = s < A.nsamp;
+  if (v) v = sample_keys(A, s, key);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) agg_increment(A.counts, key[q], v);
+}
+
+__global__ void __launch_bounds__(256) bin_fill_kernel(BinArgs A) {
+  const long long s = (long long)blockIdx.x * 256 + threadIdx.x;
+  int key[3] = {0, 0, 0};
+  bool v = s < A.nsamp;
+  if (v) v = sample_keys(A, s, key);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int pos = agg_increment(A.cursor, key[q], v);
+    if (v) A.list[pos] = (int)(s * 3 + q);
+  }
+}
+
+// Exclusive scans over the K tile counts: offsets (entry starts; cursor := offsets) and
+// chunk starts (ceil(count / CHUNK) workgroup chunks per tile); total chunks -> meta[0].
+__global__ void __launch_bounds__(1024) bin_scan_kernel(const int* __restrict__ counts, int K,
+                                                        int* __restrict__ offsets, int* __restrict__ cursor,
+                                                        int* __restrict__ chunk_start, int* __restrict__ meta) {
+  __shared__ int s_off[1024], s_chk[1024];
+  const int tid = threadIdx.x;
+  const int per = (K + 1023) / 1024;
+  const int k0 = tid * per, k1 = min(K, k0 + per);
+  int so = 0, sc = 0;
+  for (int k = k0; k < k1; ++k) {
+    so += counts[k];
+    sc += (counts[k] + CHUNK - 1) / CHUNK;
+  }
+  s_off[tid] = so;
+  s_chk[tid] = sc;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int a = (tid >= d) ? s_off[tid - d] : 0;
+    const int c = (tid >= d) ? s_chk[tid - d] : 0;
+    __syncthreads();
+    s_off[tid] += a;
+    s_chk[tid] += c;
+    __syncthreads();
+  }
+  int o = s_off[tid] - so, c = s_chk[tid] - sc;
+  for (int k = k0; k < k1; ++k) {
+    offsets[k] = o;
+    cursor[k] = o;
+    chunk_start[k] = c;
+    o += counts[k];
+    c += (counts[k] + CHUNK - 1) / CHUNK;
+  }
+  if (tid == 1023) {
+    offsets[K] = s_off[1023];
+    chunk_start[K] = s_chk[1023];
+    meta[0] = s_chk[1023];
+  }
+}
+
+struct TileArgs {
+  const float* ro;
+  const float* rd;
+  const float* t;
+  const float* gfeat;     // [nsamp][32]
+  const int* counts;
+  const int* offsets;
+  const int* chunk_start; // [K+1]
+  const int* meta;        // meta[0] = total chunks
+  const int* list;
+  float* dplanes;
+  long long sb;
+  int sq, st;
+  int K, N, HW, R, T;
+  float sr;
+};
+
+__global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
+  __shared__ __attribute__((aligned(16))) float acc[TT * TT * NC];
+  const int tid = threadIdx.x, wv = tid >> 6, l = lane_id();
+  const int dxl = l >> 5, cl = l & 31;
+  const int total = A.meta[0];
+  for (int c = blockIdx.x; c < total; c += gridDim.x) {
+    // chunk -> tile: last k with chunk_start[k] <= c
+    int lo = 0, hi = A.K - 1;
+    while (lo < hi) {
+      const int m = (lo + hi + 1) >> 1;
+      if (A.chunk_start[m] <= c) lo = m;
+      else hi = m - 1;
+    }
+    const int tile = lo;
+    const int first = A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK;
+    const int last = min(A.offsets[tile] + A.counts[tile], first + CHUNK);
+    const int tx = tile % A.T, ty = (tile / A.T) % A.T, bq = tile / (A.T * A.T);
+    const int q = bq % 3, b = bq / 3;
+    for (int k = tid; k < TT * TT * NC; k += 256) acc[k] = 0.f;
+    __syncthreads();
+    for (int base = first + wv * 64; base < last; base += 256) {
+      const int n = min(64, last - base);
+      // lane j: bilinear parameters of entry base + j on plane q
+      int cell = 0, sidx = 0;
+      float pw = 0.f, pn = 0.f;
+      int flags = 0;
+      if (l < n) {
+        const int ent = A.list[base + l];
+        const long long s = ent / 3;
+        const long long ray = s / A.N;
+        float o[3], d[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          o[k] = A.ro[ray * 3 + k];
+          d[k] = A.rd[ray * 3 + k];
+        }
+        const float ts = A.t[s];
+        float cx[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(o[k], fmul(d[k], ts)), A.sr);
+        // plane q samples (x,y), (x,z), (y,z)  (generator.py:312-326)
+        PlaneP pp;
+        plane_params(q == 2 ? cx[1] : cx[0], q == 0 ? cx[1] : cx[2], A.R, pp);
+        cell = pp.tex & 0xFFFFF;
+        flags = pp.tex >> 20;
+        pw = pp.w;
+        pn = pp.n;
+        sidx = (int)s;
+      }
+      for (int j = 0; j < n; ++j) {
+        const int cj = readlane(cell, j), fj = readlane(flags, j), sj = readlane(sidx, j);
+        const float w = readlane(pw, j), nn = readlane(pn, j);
+        const float e = 1.f - w, s_ = 1.f - nn;
+        const int y0 = cj / A.R, x0 = cj % A.R;
+        const int lx = x0 - tx * TS + (dxl ? (fj & 1) : 0);
+        const int ly = y0 - ty * TS;
+        const int oy = (fj >> 1) & 1;
+        const float gv = A.gfeat[(long long)sj * NC + cl];
+        const float wx = dxl ? w : e;
+        atomicAdd(&acc[(ly * TT + lx) * NC + cl], gv * (s_ * wx));
+        atomicAdd(&acc[((ly + oy) * TT + lx) * NC + cl], gv * (nn * wx));
+      }
+    }
+    __syncthreads();
+    float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
+    for (int k = tid; k < TT * TT * NC; k += 256) {
+      const float v = acc[k];
+      const int texel = k / NC, ch = k % NC;
+      const int gy = ty * TS + texel / TT, gx = tx * TS + texel % TT;
+      if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
+    }
+    __syncthreads();
+  }
+}
+
+struct Workspace {
+  float* gfeat;
+  int* counts;
+  int* cursor;
+  int* offsets;
+  int* chunk_start;
+  int* meta;
+  int* list;
+  long long bytes;
+};
+
+static Workspace carve(const nfi_render_args* a, void* base) {
+  const long long nrays = (long long)a->B * a->HW;
+  const int N = a->fine ? 2 * a->S : a->S;
+  const long long nsamp = nrays * N;
+  const int T = (a->field.R - 1 + TS - 1) / TS;
+  const long long K = (long long)a->B * 3 * T * T;
+  char* p = static_cast<char*>(base);
+  Workspace w;
+  auto take = [&](long long bytes) {
+    char* q = p;
+    p += (bytes + 255) / 256 * 256;
+    return q;
+  };
+  w.gfeat = reinterpret_cast<float*>(take(nsamp * NC * 4));
+  w.counts = reinterpret_cast<int*>(take(K * 4));
+  w.cursor = reinterpret_cast<int*>(take(K * 4));
+  w.offsets = reinterpret_cast<int*>(take((K + 1) * 4));
+  w.chunk_start = reinterpret_cast<int*>(take((K + 1) * 4));
+  w.meta = reinterpret_cast<int*>(take(16));
+  w.list = reinterpret_cast<int*>(take(3 * nsamp * 4));
+  w.bytes = p - static_cast<char*>(base);
+  return w;
+}
+
+template <int SPL, int NPL, bool FINE>
+static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
+  const long long nrays = (long long)a->B * a->HW;
+  render_fwd_kernel<SPL, NPL, FINE><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
+  NFI_CHECK_LAUNCH("render_fwd_kernel");
   return NFI_OK;
 }
 
-static int dispatch(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
+static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
+  const long long nrays = (long long)a->B * a->HW;
+  const int N = a->fine ? 2 * a->S : a->S;
+  const long long nsamp = nrays * N;
+  const int T = (a->field.R - 1 + TS - 1) / TS;
+  const int K = a->B * 3 * T * T;
+  Workspace w = carve(a, g->workspace);
+  NFI_REQUIRE(w.bytes <= g->workspace_bytes, "render_backward: workspace too small (%lld < %lld)",
+              (long long)g->workspace_bytes, w.bytes);
+  NFI_REQUIRE(nsamp * 3 < (1LL << 31), "render_backward: too many samples per call (%lld)", nsamp);
+  // 1) bin (sample, plane) entries by plane tile from the saved depths
+  BinArgs B{a->ro, a->rd, a->t_saved, nsamp, N, a->HW, a->field.R, T, a->field.scene_range,
+            w.counts, w.cursor, w.list};
+  NFI_REQUIRE(hipMemsetAsync(w.counts, 0, (size_t)K * 4, s) == hipSuccess, "render_backward: memset failed");
+  const unsigned sb = (unsigned)((nsamp + 255) / 256);
+  bin_count_kernel<<<sb, 256, 0, s>>>(B);
+  NFI_CHECK_LAUNCH("bin_count_kernel");
+  bin_scan_kernel<<<1, 1024, 0, s>>>(w.counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
+  NFI_CHECK_LAUNCH("bin_scan_kernel");
+  bin_fill_kernel<<<sb, 256, 0, s>>>(B);
+  NFI_CHECK_LAUNCH("bin_fill_kernel");
+  // 2) per-ray compositing + field backward -> per-sample feature gradients, d palette, d rays
+  BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat};
+  const unsigned rb = (unsigned)((nrays + 3) / 4);
+  const int NPL = (N + 63) / 64;
+  if (NPL <= 1) render_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
+  else if (NPL <= 2) render_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
+  else render_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
+  NFI_CHECK_LAUNCH("render_bwd_kernel");
+  // 3) per-tile LDS accumulation of d planes
+  TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, w.counts, w.offsets, w.chunk_start, w.meta, w.list,
+              g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,
+              a->field.scene_range};
+  tile_accum_kernel<<<2048, 256, 0, s>>>(TA);
+  NFI_CHECK_LAUNCH("tile_accum_kernel");
+  return NFI_OK;
+}
+
+static int dispatch_fwd(const nfi_render_args* a, hipStream_t s) {
   const int S = a->S;
   if (a->fine) {
-    if (S >= 3 && S <= 32) return launch<1, 1, true>(a, g, s);
-    if (S >= 3 && S <= 64) return launch<1, 2, true>(a, g, s);
-    if (S >= 3 && S <= 128) return launch<2, 4, true>(a, g, s);
+    if (S >= 3 && S <= 32) return launch_fwd<1, 1, true>(a, s);
+    if (S >= 3 && S <= 64) return launch_fwd<1, 2, true>(a, s);
+    if (S >= 3 && S <= 128) return launch_fwd<2, 4, true>(a, s);
   } else {
-    if (S >= 1 && S <= 64) return launch<1, 1, false>(a, g, s);
-    if (S >= 1 && S <= 128) return launch<2, 2, false>(a, g, s);
-    if (S >= 1 && S <= 256) return launch<4, 4, false>(a, g, s);
+    if (S >= 1 && S <= 64) return launch_fwd<1, 1, false>(a, s);
+    if (S >= 1 && S <= 128) return launch_fwd<2, 2, false>(a, s);
+    if (S >= 1 && S <= 256) return launch_fwd<4, 4, false>(a, s);
   }
   set_error("render: unsupported samples per ray S=%d (fine=%d): need 3..128 with fine sampling, "
             "1..256 without", S, (int)a->fine);
   return NFI_EINVAL;
+}
+
+static bool supported_S(const nfi_render_args* a) {
+  return a->fine ? (a->S >= 3 && a->S <= 128) : (a->S >= 1 && a->S <= 256);
 }
 
 static int validate(const nfi_render_args* a) {
@@ -814,6 +1108,8 @@ static int validate(const nfi_render_args* a) {
   NFI_REQUIRE(a->ro && a->rd && a->near_ && a->far_, "render: null ray pointer");
   NFI_REQUIRE(a->B > 0 && a->HW > 0, "render: bad shape B=%d HW=%d", a->B, a->HW);
   NFI_REQUIRE(a->t_saved && a->sigma_saved && a->rgb_saved, "render: null saved-state pointer");
+  NFI_REQUIRE(supported_S(a), "render: unsupported samples per ray S=%d (fine=%d): need 3..128 with fine "
+              "sampling, 1..256 without", a->S, (int)a->fine);
   return NFI_OK;
 }
 
@@ -825,15 +1121,21 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
   int e = nfi::validate(a);
   if (e) return e;
   NFI_REQUIRE(a->rgb && a->depth && a->mask, "render_forward: null output");
-  return nfi::dispatch(a, nullptr, (hipStream_t)stream);
+  return nfi::dispatch_fwd(a, (hipStream_t)stream);
+}
+
+int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {
+  if (nfi::validate(a)) return -1;
+  return nfi::carve(a, nullptr).bytes;
 }
 
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream) {
   int e = nfi::validate(a);
   if (e) return e;
-  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray, "render_backward: null grad pointer");
+  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
+              "render_backward: null grad pointer");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
-  return nfi::dispatch(a, g, (hipStream_t)stream);
+  return nfi::launch_bwd(a, g, (hipStream_t)stream);
 }
 
 }  // extern "C"

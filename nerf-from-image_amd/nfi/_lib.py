@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 1
+ABI_VERSION = 2
 DEC_SIZE = 3088
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -46,7 +46,8 @@ class NfiRenderArgs(ctypes.Structure):
 
 class NfiRenderGradArgs(ctypes.Structure):
     _fields_ = [('g_rgb', c_void_p), ('g_mask', c_void_p), ('d_planes', c_void_p),
-                ('d_palette_ray', c_void_p), ('g_ro', c_void_p), ('g_rd', c_void_p)]
+                ('d_palette_ray', c_void_p), ('g_ro', c_void_p), ('g_rd', c_void_p),
+                ('workspace', c_void_p), ('workspace_bytes', ctypes.c_int64)]
 
 
 # symbol -> (restype, argtypes); every entry point of include/nfi.h
@@ -66,6 +67,7 @@ SIGNATURES = {
     'nfi_segment_sum': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          c_void_p, c_void_p, c_void_p]),
     'nfi_render_forward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs), c_void_p]),
+    'nfi_render_backward_workspace_bytes': (ctypes.c_int64, [ctypes.POINTER(NfiRenderArgs)]),
     'nfi_render_backward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
                                              ctypes.POINTER(NfiRenderGradArgs), c_void_p]),
 }

@@ -270,8 +270,13 @@ class _VolumeRender(torch.autograd.Function):
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
         args = _VolumeRender._args(planes_tm, dec, pal, ro, rd, near, far, opts, B, H * W, None, None, 0,
                                    None, None, None, t_saved, s_saved, c_saved, None, None)
+        nbytes = lib.nfi_render_backward_workspace_bytes(ctypes.byref(args))
+        if nbytes < 0:
+            _lib.check(-1, 'nfi_render_backward_workspace_bytes')
+        ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
         gargs = _lib.NfiRenderGradArgs(g_rgb=_ptr(g_rgb), g_mask=_ptr(g_mask), d_planes=_ptr(d_planes),
-                                       d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd))
+                                       d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd),
+                                       workspace=_ptr(ws), workspace_bytes=nbytes)
         st = _stream(dev)
         with _timed('render_bwd', dev):
             _lib.check(lib.nfi_render_backward(ctypes.byref(args), ctypes.byref(gargs), st),

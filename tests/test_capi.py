@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, 'include', 'nfi.h')
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r'^\s*(?:int32_t|const char\*)\s+(nfi_\w+)\s*\(', src, re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int32_t|int64_t|const char\*)\s+(nfi_\w+)\s*\(', src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
