@@ -100,7 +100,8 @@ typedef struct nfi_render_grad_args {
   const float* g_rgb;   /* [B*HW,3] dL/d rgb  */
   const float* g_mask;  /* [B*HW]   dL/d mask (depth carries no gradient, nerf_utils.py:151) */
   float* d_planes;      /* same layout/strides as field.planes; ACCUMULATED into (zero it) */
-  float* d_palette_ray; /* [B*HW,30] per-ray partial dL/d palette (reduce with nfi_segment_sum) */
+  float* d_palette_ray; /* [B*HW*ceil(N/64),30] per-(ray, 64-sample chunk) partial dL/d palette
+                           (reduce per image with nfi_segment_sum, M = HW*ceil(N/64)) */
   float* g_ro;          /* [B*HW,3] dL/d ray origins  (NULL: skip coordinate gradients) */
   float* g_rd;          /* [B*HW,3] dL/d unit ray directions */
   void* workspace;      /* device scratch of nfi_render_backward_workspace_bytes() bytes */

@@ -143,7 +143,13 @@ __device__ __forceinline__ float softplus_grad(float z) {
   return (z > 20.f) ? 1.f : u / (u + 1.f);
 }
 
-__device__ __forceinline__ float dot32(const float x[NC], const float* __restrict__ w) {
+// The packed decoder is read through the constant address space (AS 4): wave-uniform,
+// read-only loads there become s_load into SGPRs even after global stores in the kernel
+// (a plain global pointer would fall back to vector loads into VGPRs once a store may alias).
+typedef const __attribute__((address_space(4))) float* cfloat_p;
+__device__ __forceinline__ cfloat_p as_const(const float* p) { return (cfloat_p)(p); }
+
+__device__ __forceinline__ float dot32(const float x[NC], cfloat_p w) {
   float z0 = 0.f, z1 = 0.f, z2 = 0.f, z3 = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; c += 4) {
@@ -156,13 +162,14 @@ __device__ __forceinline__ float dot32(const float x[NC], const float* __restric
 }
 
 // TriplanarDecoder.net (generator.py:295-299): y = W2s softplus(W1s x + b1) + b2.
-__device__ __forceinline__ void mlp_forward(const float* __restrict__ dec, const float x[NC], float y[NO]) {
+__device__ __forceinline__ void mlp_forward(const float* __restrict__ dec_, const float x[NC], float y[NO]) {
+  const cfloat_p dec = as_const(dec_);
   float acc[NO];
 #pragma unroll
   for (int k = 0; k < NO; ++k) acc[k] = 0.f;
-#pragma unroll 2
+#pragma unroll 1
   for (int o = 0; o < NH; ++o) {
-    const float* u = dec + o * DEC_UNIT;
+    const cfloat_p u = dec + o * DEC_UNIT;
     const float h = softplus(dot32(x, u) + u[DEC_B1]);
 #pragma unroll
     for (int k = 0; k < NO; ++k) acc[k] = fmaf(h, u[DEC_W2T + k], acc[k]);
@@ -172,13 +179,14 @@ __device__ __forceinline__ void mlp_forward(const float* __restrict__ dec, const
 }
 
 // Input-gradient of the decoder (its weights are frozen during inversion, run.py:630-632).
-__device__ __forceinline__ void mlp_backward(const float* __restrict__ dec, const float x[NC],
+__device__ __forceinline__ void mlp_backward(const float* __restrict__ dec_, const float x[NC],
                                              const float gy[NO], float gx[NC]) {
+  const cfloat_p dec = as_const(dec_);
 #pragma unroll
   for (int c = 0; c < NC; ++c) gx[c] = 0.f;
-#pragma unroll 2
+#pragma unroll 1
   for (int o = 0; o < NH; ++o) {
-    const float* u = dec + o * DEC_UNIT;
+    const cfloat_p u = dec + o * DEC_UNIT;
     const float z = dot32(x, u) + u[DEC_B1];
     float gh = 0.f;
 #pragma unroll
@@ -561,221 +569,230 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
 struct BwdArgs {
   const float* g_rgb;
   const float* g_mask;
-  float* d_palette_ray;
-  float* g_ro;
-  float* g_rd;
-  float* gfeat;         // [rays][N][32] per-sample dL/d(tap feature of each plane) = dL/dx / 3
+  float* d_palette_part;  // [rays][NPL][30] per-(ray, chunk) partial dL/d palette
+  float* g_ro;            // [rays][3] (NULL: no coordinate gradients)
+  float* g_rd;            // [rays][3]
+  float* gfeat;           // [rays][N][32] per-sample dL/d(tap feature of each plane) = dL/dx / 3
+  float* gsig;            // [rays][N] dL/d sigma per merged sample
+  float* wts;             // [rays][N] compositing weight per merged sample
+  int npl;                // chunks of 64 per ray
 };
 
+// Compositing backward (nerf_utils.py:125-163 under autograd), one wave per ray:
+// dL/d alpha_k = T_k (e_k - S_k), S_k = sum_{i>k} e_i alpha_i prod_{k<j<i} a_j (reverse affine
+// scan), e_i = g_rgb.c_i + g_mask(-white bg) -> dL/d sigma_i, weights w_i, and the ||rd|| term.
 template <int NPL>
-__global__ void __launch_bounds__(256) render_bwd_kernel(nfi_render_args a, BwdArgs g) {
+__global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, BwdArgs g) {
   constexpr int NMAX = 64 * NPL;
-  constexpr int WL = XTILE + 3 * NMAX + 8;
-  __shared__ __attribute__((aligned(16))) float lds[4 * WL];
+  __shared__ float lds[4 * (NMAX + 8)];
   const int wv = threadIdx.x >> 6, l = lane_id();
-  const int dxl = l >> 5, cl = l & 31;
   const long long nrays = (long long)a.B * a.HW;
   const long long r = (long long)blockIdx.x * 4 + wv;
   if (r >= nrays) return;
   const int N = a.fine ? 2 * a.S : a.S;
-  float* X = lds + wv * WL;
-  float* Lt = X + XTILE;          // t      [NMAX]
-  float* Lg = Lt + NMAX;          // dL/d sigma [NMAX]
-  float* Lw = Lg + NMAX;          // weights    [NMAX]
-  const bool dcoord = g.g_ro != nullptr;
+  float* Lt = lds + wv * (NMAX + 8);
+  RayCtx R;
+  load_ray(a, r, R);
+  const float gr0 = g.g_rgb[r * 3 + 0], gr1 = g.g_rgb[r * 3 + 1], gr2 = g.g_rgb[r * 3 + 2];
+  const float gm = g.g_mask[r] - (a.white_bg ? (gr0 + gr1 + gr2) : 0.f);
+  float t[NPL], sg[NPL], al[NPL], aa[NPL], ex[NPL], dist[NPL], raw[NPL], T[NPL], ee[NPL];
+#pragma unroll
+  for (int e = 0; e < NPL; ++e) {
+    const int i = e * 64 + l;
+    t[e] = (i < N) ? a.t_saved[r * N + i] : 0.f;
+    Lt[e * 64 + l] = t[e];
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int e = 0; e < NPL; ++e) {
+    const int i = e * 64 + l;
+    const bool v = i < N;
+    sg[e] = v ? a.sigma_saved[r * N + i] : 0.f;
+    raw[e] = (i < N - 1) ? fsub(Lt[i + 1], t[e]) : 0.f;
+    dist[e] = fmul(raw[e], R.rdn);
+    alpha_of(sg[e], dist[e], al[e], aa[e], ex[e]);
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+    if (v) {
+      c0 = a.rgb_saved[(r * 3 + 0) * N + i];
+      c1 = a.rgb_saved[(r * 3 + 1) * N + i];
+      c2 = a.rgb_saved[(r * 3 + 2) * N + i];
+    } else {
+      al[e] = 0.f;
+      aa[e] = 1.f;
+    }
+    ee[e] = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm : 0.f;
+  }
+  excl_prod<NPL>(aa, T);
+  float grdn = 0.f;
+  float cB = 0.f;   // composition of the maps beyond the current chunk, evaluated at 0
+#pragma unroll
+  for (int e = NPL - 1; e >= 0; --e) {
+    const int i = e * 64 + l;
+    float A = aa[e], B = ee[e] * al[e];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const float A2 = __shfl_down(A, d), B2 = __shfl_down(B, d);
+      if (l + d < 64) {
+        B = fmaf(A, B2, B);
+        A = A * A2;
+      }
+    }
+    const float An = __shfl_down(A, 1), Bn = __shfl_down(B, 1);
+    const float Sk = (l < 63) ? fmaf(An, cB, Bn) : cB;
+    cB = fmaf(readlane(A, 0), cB, readlane(B, 0));
+    const float dal = T[e] * (ee[e] - Sk);                   // dL/d alpha_k
+    grdn += dal * sg[e] * ex[e] * raw[e];                    // dists = raw * ||rd||
+    if (i < N) {
+      g.gsig[r * N + i] = dal * dist[e] * ex[e];             // d alpha/d sigma = dist * exp(-sigma dist)
+      g.wts[r * N + i] = al[e] * T[e];                       // w_i; dL/d c_i = w_i g_rgb
+    }
+  }
+  if (g.g_ro) {
+    grdn = wave_sum(grdn);
+    if (l < 3) {
+      g.g_ro[r * 3 + l] = 0.f;
+      g.g_rd[r * 3 + l] = grdn * (R.d[l] / R.rdn);           // d rd += d||rd|| * rd / ||rd||
+    }
+  }
+}
 
+// Field backward for one chunk of 64 merged samples of one ray (one wave): recompute taps
+// and decoder, sigma/colour head backward, decoder input-gradient, per-sample feature
+// gradient -> gfeat (d planes is summed per tile afterwards), palette partial, and the
+// grid_sampler_2d d-grid -> d ray origins/directions (re-gather, generator.py:312-326).
+__global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const int dxl = l >> 5, cl = l & 31;
+  const long long nrays = (long long)a.B * a.HW;
+  const long long job = (long long)blockIdx.x * 4 + wv;
+  const long long r = job / g.npl;
+  const int e = (int)(job % g.npl);
+  if (r >= nrays) return;
+  const int N = a.fine ? 2 * a.S : a.S;
+  if (e * 64 >= N) return;
+  float* X = lds + wv * XTILE;
+  const bool dcoord = g.g_ro != nullptr;
+  const float sr = a.field.scene_range;
   RayCtx R;
   load_ray(a, r, R);
   const PlaneView pv{a.field.planes + (long long)R.b * a.field.sb, (int)a.field.sq, (int)a.field.st,
                      a.field.R};
   const float* pal = a.field.palette + R.b * (NA * 3);
-
   const float gr0 = g.g_rgb[r * 3 + 0], gr1 = g.g_rgb[r * 3 + 1], gr2 = g.g_rgb[r * 3 + 2];
-  const float gm = g.g_mask[r] - (a.white_bg ? (gr0 + gr1 + gr2) : 0.f);
 
-  // ---- compositing backward ----
-  float grdn = 0.f;
+  const int npts = min(64, N - e * 64);
+  const int i = e * 64 + l;
+  const bool v = i < N;
+  const float te = v ? a.t_saved[r * N + i] : R.near_;
+  float pmask;
   {
-    float t[NPL], sg[NPL], al[NPL], aa[NPL], ex[NPL], dist[NPL], raw[NPL], T[NPL], ee[NPL];
+    PointP P;
+    point_params(R.o, R.d, te, sr, pv.R, P);
+    gather_features(pv, P, npts, X);
+    pmask = P.mask;
+  }
+  wave_lds_sync();
+  float x[NC];
+  load_row(X, l, x);
+  float y[NO];
+  mlp_forward(a.field.dec, x, y);
+  float gy[NO];
+  {
+    Head h;
+    head_forward(y, pmask, a.field.inv_alpha, a.field.beta, pal, h);
+    // sigma -> distance  (generator.py:629-636, laplace_cdf generator.py:30-33)
+    const float gs = v ? g.gsig[r * N + i] : 0.f;
+    const float xn = -y[0];
+    const float sgn = tsign(xn);
+    const float ex2 = expf(-fabsf(xn) / a.field.beta);
+    const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
+    gy[0] = -(((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn);
+    // rgb -> logits (softmax backward) and palette gradient  (generator.py:668-679)
+    const float w = v ? g.wts[r * N + i] : 0.f;
+    const float gc0 = w * gr0, gc1 = w * gr1, gc2 = w * gr2;
+    float gp[NA], dot = 0.f;
 #pragma unroll
-    for (int e = 0; e < NPL; ++e) {
-      const int i = e * 64 + l;
-      t[e] = (i < N) ? a.t_saved[r * N + i] : 0.f;
-      Lt[e * 64 + l] = t[e];
+    for (int k = 0; k < NA; ++k) {
+      gp[k] = gc0 * pal[k * 3 + 0] + gc1 * pal[k * 3 + 1] + gc2 * pal[k * 3 + 2];
+      dot = fmaf(gp[k], h.p[k], dot);
     }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
+    // per-point palette contributions p_k * gc, column-summed through the LDS tile
     wave_lds_sync();
+    float* row = X + l * XS;
 #pragma unroll
-    for (int e = 0; e < NPL; ++e) {
-      const int i = e * 64 + l;
-      const bool v = i < N;
-      sg[e] = v ? a.sigma_saved[r * N + i] : 0.f;
-      raw[e] = (i < N - 1) ? fsub(Lt[i + 1], t[e]) : 0.f;
-      dist[e] = fmul(raw[e], R.rdn);
-      alpha_of(sg[e], dist[e], al[e], aa[e], ex[e]);
-      float c0 = 0.f, c1 = 0.f, c2 = 0.f;
-      if (v) {
-        c0 = a.rgb_saved[(r * 3 + 0) * N + i];
-        c1 = a.rgb_saved[(r * 3 + 1) * N + i];
-        c2 = a.rgb_saved[(r * 3 + 2) * N + i];
-      } else {
-        al[e] = 0.f;
-        aa[e] = 1.f;
-      }
-      ee[e] = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm : 0.f;
-    }
-    excl_prod<NPL>(aa, T);
-    // S_k = sum_{i>k} e_i alpha_i prod_{k<j<i} a_j : reverse exclusive scan of f_i(s) = a_i s + e_i alpha_i
-    float cB = 0.f;   // composition of the maps beyond the current chunk, evaluated at 0
-#pragma unroll
-    for (int e = NPL - 1; e >= 0; --e) {
-      float A = aa[e], B = ee[e] * al[e];
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const float A2 = __shfl_down(A, d), B2 = __shfl_down(B, d);
-        if (l + d < 64) {
-          B = fmaf(A, B2, B);
-          A = A * A2;
-        }
-      }
-      const float An = __shfl_down(A, 1), Bn = __shfl_down(B, 1);
-      const float Sk = (l < 63) ? fmaf(An, cB, Bn) : cB;
-      cB = fmaf(readlane(A, 0), cB, readlane(B, 0));
-      const float dal = T[e] * (ee[e] - Sk);                  // dL/d alpha_k
-      Lg[e * 64 + l] = dal * dist[e] * ex[e];                  // d alpha/d sigma = dist * exp(-sigma dist)
-      grdn += dal * sg[e] * ex[e] * raw[e];                   // dists = raw * ||rd||
-      Lw[e * 64 + l] = al[e] * T[e];                           // w_i; dL/d c_i = w_i g_rgb
+    for (int k = 0; k < NA; ++k) {
+      row[k * 3 + 0] = h.p[k] * gc0;
+      row[k * 3 + 1] = h.p[k] * gc1;
+      row[k * 3 + 2] = h.p[k] * gc2;
     }
   }
   wave_lds_sync();
-
-  // ---- per-sample field backward ----
-  float gro[3] = {0.f, 0.f, 0.f}, grd[3] = {0.f, 0.f, 0.f};
-  float pacc = 0.f;   // lane k < 30 accumulates dL/d palette[k/3][k%3] over the ray
-  const float sr = a.field.scene_range;
-
-#pragma unroll 1
-  for (int e = 0; e < NPL; ++e) {
-    if (e * 64 >= N) break;
-    const int npts = min(64, N - e * 64);
-    const int i = e * 64 + l;
-    const bool v = i < N;
-    const float te = Lt[i];
-    float pmask;
-    {
-      PointP P;
-      point_params(R.o, R.d, te, sr, pv.R, P);
-      gather_features(pv, P, npts, X);
-      pmask = P.mask;
-    }
-    wave_lds_sync();
-    float x[NC];
-    load_row(X, l, x);
-    float y[NO];
-    mlp_forward(a.field.dec, x, y);
-    float gy[NO];
-    {
-      Head h;
-      head_forward(y, pmask, a.field.inv_alpha, a.field.beta, pal, h);
-      // sigma -> distance  (generator.py:629-636, laplace_cdf generator.py:30-33)
-      const float gs = v ? Lg[i] : 0.f;
-      const float xn = -y[0];
-      const float sgn = tsign(xn);
-      const float ex2 = expf(-fabsf(xn) / a.field.beta);
-      const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
-      gy[0] = -(((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn);
-      // rgb -> logits (softmax backward) and palette gradient  (generator.py:668-679)
-      const float w = v ? Lw[i] : 0.f;
-      const float gc0 = w * gr0, gc1 = w * gr1, gc2 = w * gr2;
-      float gp[NA], dot = 0.f;
-#pragma unroll
-      for (int k = 0; k < NA; ++k) {
-        gp[k] = gc0 * pal[k * 3 + 0] + gc1 * pal[k * 3 + 1] + gc2 * pal[k * 3 + 2];
-        dot = fmaf(gp[k], h.p[k], dot);
-      }
-#pragma unroll
-      for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
-      // per-point palette contributions p_k * gc, column-summed through the LDS tile
-      float* row = X + l * XS;
-#pragma unroll
-      for (int k = 0; k < NA; ++k) {
-        row[k * 3 + 0] = h.p[k] * gc0;
-        row[k * 3 + 1] = h.p[k] * gc1;
-        row[k * 3 + 2] = h.p[k] * gc2;
-      }
-    }
-    wave_lds_sync();
-    if (l < NA * 3) {
-      float s = 0.f;
-      for (int j = 0; j < npts; ++j) s += X[j * XS + l];
-      pacc += s;
-    }
-    float gx[NC];
-    mlp_backward(a.field.dec, x, gy, gx);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
-    // per-sample feature gradient -> G[ray][i][32]; d planes is summed per tile later
-    if (v) {
-      float4* gr = reinterpret_cast<float4*>(g.gfeat + (r * N + i) * NC);
-#pragma unroll
-      for (int k = 0; k < NC / 4; ++k) gr[k] = make_float4(gx[4 * k], gx[4 * k + 1], gx[4 * k + 2], gx[4 * k + 3]);
-    }
-    if (dcoord) {
-      bool nz = false;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) nz |= (gx[c] != 0.f);
-      // points with an exactly-zero feature gradient move no coordinate: skip their re-gather
-      const unsigned long long live = __ballot(nz && v);
-      wave_lds_sync();
-      store_row(X, l, gx);
-      wave_lds_sync();
-      // d coords: re-gather the taps, grid_sampler_2d_backward's d grid (one point at a time)
-#pragma unroll 1
-      for (int j = 0; j < npts; ++j) {
-        if (!((live >> j) & 1ull)) continue;
-        const float tj = readlane(te, j);
-        PointP P;
-        point_params(R.o, R.d, tj, sr, pv.R, P);
-        const float gv = X[j * XS + cl];
-        float GX[3], GY[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const PlaneP& pp = P.pl[q];
-          const int t0 = (pp.tex & 0xFFFFF) + (dxl ? ((pp.tex >> 20) & 1) : 0);
-          const int t1 = t0 + (((pp.tex >> 21) & 1) ? pv.R : 0);
-          const float wx = dxl ? pp.w : pp.e;
-          const float* bq = pv.base + q * pv.sq + cl;
-          const float v0 = bq[t0 * pv.st], v1 = bq[t1 * pv.st];
-          const float px = (dxl ? 1.f : -1.f) * (pp.s * v0 + pp.n * v1) * gv;
-          const float py = wx * (v1 - v0) * gv;
-          GX[q] = wave_sum(px) * pp.gxm;
-          GY[q] = wave_sum(py) * pp.gym;
-        }
-        const float dp0 = (GX[0] + GX[1]) / sr;
-        const float dp1 = (GY[0] + GX[2]) / sr;
-        const float dp2 = (GY[1] + GY[2]) / sr;
-        gro[0] += dp0;
-        gro[1] += dp1;
-        gro[2] += dp2;
-        grd[0] = fmaf(dp0, tj, grd[0]);
-        grd[1] = fmaf(dp1, tj, grd[1]);
-        grd[2] = fmaf(dp2, tj, grd[2]);
-      }
-    }
-    wave_lds_sync();
+  if (l < NA * 3) {
+    float s = 0.f;
+    for (int j = 0; j < npts; ++j) s += X[j * XS + l];
+    g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = s;
   }
-
-  // ---- per-ray outputs ----
-  if (l < NA * 3) g.d_palette_ray[r * (NA * 3) + l] = pacc;
-  if (dcoord) {
-    grdn = wave_sum(grdn);
-    if (l == 0) {
-      // dists * ||rd||  ->  d rd += d||rd|| * rd / ||rd||
+  float gx[NC];
+  mlp_backward(a.field.dec, x, gy, gx);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        g.g_ro[r * 3 + k] = gro[k];
-        g.g_rd[r * 3 + k] = grd[k] + grdn * (R.d[k] / R.rdn);
-      }
+  for (int c = 0; c < NC; ++c) gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
+  if (v) {
+    float4* gr = reinterpret_cast<float4*>(g.gfeat + (r * N + i) * NC);
+#pragma unroll
+    for (int k = 0; k < NC / 4; ++k) gr[k] = make_float4(gx[4 * k], gx[4 * k + 1], gx[4 * k + 2], gx[4 * k + 3]);
+  }
+  if (!dcoord) return;
+  bool nz = false;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) nz |= (gx[c] != 0.f);
+  // points with an exactly-zero feature gradient move no coordinate: skip their re-gather
+  const unsigned long long live = __ballot(nz && v);
+  wave_lds_sync();
+  store_row(X, l, gx);
+  wave_lds_sync();
+  float gro0 = 0.f, gro1 = 0.f, gro2 = 0.f, grd0 = 0.f, grd1 = 0.f, grd2 = 0.f;
+#pragma unroll 1
+  for (int j = 0; j < npts; ++j) {
+    if (!((live >> j) & 1ull)) continue;
+    const float tj = readlane(te, j);
+    PointP P;
+    point_params(R.o, R.d, tj, sr, pv.R, P);
+    const float gv = X[j * XS + cl];
+    float GX[3], GY[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const PlaneP& pp = P.pl[q];
+      const int t0 = (pp.tex & 0xFFFFF) + (dxl ? ((pp.tex >> 20) & 1) : 0);
+      const int t1 = t0 + (((pp.tex >> 21) & 1) ? pv.R : 0);
+      const float wx = dxl ? pp.w : pp.e;
+      const float* bq = pv.base + q * pv.sq + cl;
+      const float v0 = bq[t0 * pv.st], v1 = bq[t1 * pv.st];
+      // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
+      const float px = (dxl ? 1.f : -1.f) * (pp.s * v0 + pp.n * v1) * gv;
+      const float py = wx * (v1 - v0) * gv;
+      GX[q] = wave_sum(px) * pp.gxm;
+      GY[q] = wave_sum(py) * pp.gym;
     }
+    const float dp0 = (GX[0] + GX[1]) / sr;
+    const float dp1 = (GY[0] + GX[2]) / sr;
+    const float dp2 = (GY[1] + GY[2]) / sr;
+    gro0 += dp0;
+    gro1 += dp1;
+    gro2 += dp2;
+    grd0 = fmaf(dp0, tj, grd0);
+    grd1 = fmaf(dp1, tj, grd1);
+    grd2 = fmaf(dp2, tj, grd2);
+  }
+  if (l == 0) {
+    unsafeAtomicAdd(g.g_ro + r * 3 + 0, gro0);
+    unsafeAtomicAdd(g.g_ro + r * 3 + 1, gro1);
+    unsafeAtomicAdd(g.g_ro + r * 3 + 2, gro2);
+    unsafeAtomicAdd(g.g_rd + r * 3 + 0, grd0);
+    unsafeAtomicAdd(g.g_rd + r * 3 + 1, grd1);
+    unsafeAtomicAdd(g.g_rd + r * 3 + 2, grd2);
   }
 }
 
@@ -923,8 +940,10 @@ struct TileArgs {
 
 __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
   __shared__ __attribute__((aligned(16))) float acc[TT * TT * NC];
+  __shared__ __attribute__((aligned(16))) float stage[4][64 * (NC + 4)];
   const int tid = threadIdx.x, wv = tid >> 6, l = lane_id();
   const int dxl = l >> 5, cl = l & 31;
+  float* G = stage[wv];
   const int total = A.meta[0];
   for (int c = blockIdx.x; c < total; c += gridDim.x) {
     // chunk -> tile: last k with chunk_start[k] <= c
@@ -943,46 +962,44 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
     __syncthreads();
     for (int base = first + wv * 64; base < last; base += 256) {
       const int n = min(64, last - base);
-      // lane j: bilinear parameters of entry base + j on plane q
-      int cell = 0, sidx = 0;
+      // lane j: bilinear cell/weights of entry base + j on plane q, and its gradient row -> LDS
+      int lxy = 0, flags = 0;
       float pw = 0.f, pn = 0.f;
-      int flags = 0;
       if (l < n) {
-        const int ent = A.list[base + l];
-        const long long s = ent / 3;
+        const long long s = A.list[base + l] / 3;
         const long long ray = s / A.N;
-        float o[3], d[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          o[k] = A.ro[ray * 3 + k];
-          d[k] = A.rd[ray * 3 + k];
-        }
         const float ts = A.t[s];
         float cx[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(o[k], fmul(d[k], ts)), A.sr);
+        for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(A.ro[ray * 3 + k], fmul(A.rd[ray * 3 + k], ts)), A.sr);
         // plane q samples (x,y), (x,z), (y,z)  (generator.py:312-326)
         PlaneP pp;
         plane_params(q == 2 ? cx[1] : cx[0], q == 0 ? cx[1] : cx[2], A.R, pp);
-        cell = pp.tex & 0xFFFFF;
+        const int cell = pp.tex & 0xFFFFF;
+        const int y0 = cell / A.R, x0 = cell % A.R;
+        lxy = ((y0 - ty * TS) << 8) | (x0 - tx * TS);
         flags = pp.tex >> 20;
         pw = pp.w;
         pn = pp.n;
-        sidx = (int)s;
+        const float4* src = reinterpret_cast<const float4*>(A.gfeat + s * NC);
+        float4* dst = reinterpret_cast<float4*>(G + l * (NC + 4));
+#pragma unroll
+        for (int k = 0; k < NC / 4; ++k) dst[k] = src[k];
       }
+      wave_lds_sync();
       for (int j = 0; j < n; ++j) {
-        const int cj = readlane(cell, j), fj = readlane(flags, j), sj = readlane(sidx, j);
+        const int pj = readlane(lxy, j), fj = readlane(flags, j);
         const float w = readlane(pw, j), nn = readlane(pn, j);
         const float e = 1.f - w, s_ = 1.f - nn;
-        const int y0 = cj / A.R, x0 = cj % A.R;
-        const int lx = x0 - tx * TS + (dxl ? (fj & 1) : 0);
-        const int ly = y0 - ty * TS;
+        const int lx = (pj & 0xFF) + (dxl ? (fj & 1) : 0);
+        const int ly = pj >> 8;
         const int oy = (fj >> 1) & 1;
-        const float gv = A.gfeat[(long long)sj * NC + cl];
+        const float gv = G[j * (NC + 4) + cl];
         const float wx = dxl ? w : e;
         atomicAdd(&acc[(ly * TT + lx) * NC + cl], gv * (s_ * wx));
         atomicAdd(&acc[((ly + oy) * TT + lx) * NC + cl], gv * (nn * wx));
       }
+      wave_lds_sync();
     }
     __syncthreads();
     float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
@@ -998,6 +1015,8 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
 
 struct Workspace {
   float* gfeat;
+  float* gsig;
+  float* wts;
   int* counts;
   int* cursor;
   int* offsets;
@@ -1021,6 +1040,8 @@ static Workspace carve(const nfi_render_args* a, void* base) {
     return q;
   };
   w.gfeat = reinterpret_cast<float*>(take(nsamp * NC * 4));
+  w.gsig = reinterpret_cast<float*>(take(nsamp * 4));
+  w.wts = reinterpret_cast<float*>(take(nsamp * 4));
   w.counts = reinterpret_cast<int*>(take(K * 4));
   w.cursor = reinterpret_cast<int*>(take(K * 4));
   w.offsets = reinterpret_cast<int*>(take((K + 1) * 4));
@@ -1060,14 +1081,16 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   NFI_CHECK_LAUNCH("bin_scan_kernel");
   bin_fill_kernel<<<sb, 256, 0, s>>>(B);
   NFI_CHECK_LAUNCH("bin_fill_kernel");
-  // 2) per-ray compositing + field backward -> per-sample feature gradients, d palette, d rays
-  BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat};
-  const unsigned rb = (unsigned)((nrays + 3) / 4);
+  // 2) per-ray compositing backward, then per-(ray, 64-sample chunk) field backward
   const int NPL = (N + 63) / 64;
-  if (NPL <= 1) render_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
-  else if (NPL <= 2) render_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
-  else render_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
-  NFI_CHECK_LAUNCH("render_bwd_kernel");
+  BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat, w.gsig, w.wts, NPL};
+  const unsigned rb = (unsigned)((nrays + 3) / 4);
+  if (NPL <= 1) composite_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
+  else if (NPL <= 2) composite_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
+  else composite_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
+  NFI_CHECK_LAUNCH("composite_bwd_kernel");
+  field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+  NFI_CHECK_LAUNCH("field_bwd_kernel");
   // 3) per-tile LDS accumulation of d planes
   TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, w.counts, w.offsets, w.chunk_start, w.meta, w.list,
               g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,

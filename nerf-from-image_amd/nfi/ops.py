@@ -264,7 +264,8 @@ class _VolumeRender(torch.autograd.Function):
         g_rgb = torch.zeros((n, 3), device=dev) if g_rgb is None else g_rgb.contiguous()
         g_mask = torch.zeros((n,), device=dev) if g_mask is None else g_mask.contiguous()
         d_planes = torch.zeros_like(planes_tm)   # preserves (texel-major) strides
-        d_pal_ray = torch.empty((n, 30), device=dev)
+        npl = ((2 * opts.samples if opts.fine else opts.samples) + 63) // 64
+        d_pal_ray = torch.empty((n * npl, 30), device=dev)
         need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         g_ro = torch.empty((n, 3), device=dev) if need_coords else None
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
@@ -283,7 +284,7 @@ class _VolumeRender(torch.autograd.Function):
                        'nfi_render_backward')
         d_pal = torch.empty((B, 30), device=dev)
         ws = torch.empty((B * 64 * 30,), device=dev)
-        _lib.check(lib.nfi_segment_sum(_ptr(d_pal_ray), B, H * W, 30, _ptr(d_pal), _ptr(ws), st),
+        _lib.check(lib.nfi_segment_sum(_ptr(d_pal_ray), B, H * W * npl, 30, _ptr(d_pal), _ptr(ws), st),
                    'nfi_segment_sum')
         d_ro = g_ro.view(B, H, W, 3) if need_coords else None
         d_rd = g_rd.view(B, H, W, 3) if need_coords else None
