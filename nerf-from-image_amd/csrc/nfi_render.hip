@@ -797,13 +797,18 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
 }
 
 // ---------------------------------------------------------------------------------------
-// d planes by plane tile: every (sample, plane) contribution is binned by the 16x16-cell tile
-// of the plane its bilinear cell lies in; one workgroup sums a chunk of a tile's samples in a
-// 17x17x32 LDS image (ds_add_f32) and flushes it with one float atomic per texel channel.
-// Global atomic traffic drops from 1,536 B per sample to ~37 KB per (tile, chunk).
+// d planes by plane tile: every (sample, plane) contribution is binned by the 8x8-cell tile
+// of the plane its bilinear cell lies in; a workgroup sums a chunk of a tile's entries into
+// 9x9x32 LDS images — one private image per wave, updated by plain read-modify-write (LDS
+// executes a wave's instructions in order, so no atomics are needed; gfx950's ds_add_f32 costs
+// ~200 cycles per wave-instruction per CU against ~25 for the RMW, scripts/ubench/lds_atomic.hip)
+// with consecutive same-cell entries merged in registers first — then merges the four images
+// and flushes them with one float atomic per nonzero texel channel.  Global atomic traffic
+// drops from 1,536 B per sample to ~10 KB per (tile, chunk).
 // ---------------------------------------------------------------------------------------
-constexpr int TS = 16;            // cells per tile side
+constexpr int TS = 8;             // cells per tile side
 constexpr int TT = TS + 1;        // texels per tile side
+constexpr int TILE_F = TT * TT * NC + NC;   // floats per wave image (+1 trash texel)
 constexpr int CHUNK = 2048;       // (sample, plane) entries per accumulation workgroup
 
 struct BinArgs {
@@ -938,12 +943,23 @@ struct TileArgs {
   float sr;
 };
 
+__device__ __forceinline__ void tile_rmw(float* __restrict__ img, int key, int dxl, int cl, float a0, float a1) {
+  // key = ly << 16 | lx << 8 | flags(ox | oy << 1); dx=1 lanes of an edge cell (ox = 0) would
+  // alias the dx=0 texel inside one instruction: send them (weight 0) to the trash texel
+  const int lx = (key >> 8) & 0xFF, ly = key >> 16, ox = key & 1, oy = (key >> 1) & 1;
+  const int t0 = (dxl && !ox) ? TT * TT : ly * TT + lx + dxl;
+  const int t1 = (dxl && !ox) ? TT * TT : (ly + oy) * TT + lx + dxl;
+  float* p0 = img + t0 * NC + cl;
+  *p0 = *p0 + a0;
+  float* p1 = img + t1 * NC + cl;
+  *p1 = *p1 + a1;
+}
+
 __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
-  __shared__ __attribute__((aligned(16))) float acc[TT * TT * NC];
-  __shared__ __attribute__((aligned(16))) float stage[4][64 * (NC + 4)];
+  __shared__ __attribute__((aligned(16))) float acc[4 * TILE_F];
   const int tid = threadIdx.x, wv = tid >> 6, l = lane_id();
   const int dxl = l >> 5, cl = l & 31;
-  float* G = stage[wv];
+  float* img = acc + wv * TILE_F;
   const int total = A.meta[0];
   for (int c = blockIdx.x; c < total; c += gridDim.x) {
     // chunk -> tile: last k with chunk_start[k] <= c
@@ -958,12 +974,14 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
     const int last = min(A.offsets[tile] + A.counts[tile], first + CHUNK);
     const int tx = tile % A.T, ty = (tile / A.T) % A.T, bq = tile / (A.T * A.T);
     const int q = bq % 3, b = bq / 3;
-    for (int k = tid; k < TT * TT * NC; k += 256) acc[k] = 0.f;
+    for (int k = tid; k < 4 * TILE_F; k += 256) acc[k] = 0.f;
     __syncthreads();
+    int cur = -1;
+    float a0 = 0.f, a1 = 0.f;
     for (int base = first + wv * 64; base < last; base += 256) {
       const int n = min(64, last - base);
-      // lane j: bilinear cell/weights of entry base + j on plane q, and its gradient row -> LDS
-      int lxy = 0, flags = 0;
+      // lane j: cell key, weights and sample index of entry base + j on plane q
+      int key = 0, sidx = 0;
       float pw = 0.f, pn = 0.f;
       if (l < n) {
         const long long s = A.list[base + l] / 3;
@@ -977,34 +995,44 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
         plane_params(q == 2 ? cx[1] : cx[0], q == 0 ? cx[1] : cx[2], A.R, pp);
         const int cell = pp.tex & 0xFFFFF;
         const int y0 = cell / A.R, x0 = cell % A.R;
-        lxy = ((y0 - ty * TS) << 8) | (x0 - tx * TS);
-        flags = pp.tex >> 20;
+        key = ((y0 - ty * TS) << 16) | ((x0 - tx * TS) << 8) | (pp.tex >> 20);
         pw = pp.w;
         pn = pp.n;
-        const float4* src = reinterpret_cast<const float4*>(A.gfeat + s * NC);
-        float4* dst = reinterpret_cast<float4*>(G + l * (NC + 4));
+        sidx = (int)s;
+      }
+      for (int j0 = 0; j0 < n; j0 += 8) {
+        float gv[8];
 #pragma unroll
-        for (int k = 0; k < NC / 4; ++k) dst[k] = src[k];
+        for (int u = 0; u < 8; ++u) {
+          const int sj = readlane(sidx, min(j0 + u, 63));
+          gv[u] = (j0 + u < n) ? A.gfeat[(long long)sj * NC + cl] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + u;
+          if (j < n) {
+            const int kj = readlane(key, j);
+            const float w = readlane(pw, j), nn = readlane(pn, j);
+            const float wx = dxl ? w : 1.f - w;
+            const float c0 = gv[u] * ((1.f - nn) * wx), c1 = gv[u] * (nn * wx);
+            if (kj == cur) {
+              a0 += c0;
+              a1 += c1;
+            } else {
+              if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
+              cur = kj;
+              a0 = c0;
+              a1 = c1;
+            }
+          }
+        }
       }
-      wave_lds_sync();
-      for (int j = 0; j < n; ++j) {
-        const int pj = readlane(lxy, j), fj = readlane(flags, j);
-        const float w = readlane(pw, j), nn = readlane(pn, j);
-        const float e = 1.f - w, s_ = 1.f - nn;
-        const int lx = (pj & 0xFF) + (dxl ? (fj & 1) : 0);
-        const int ly = pj >> 8;
-        const int oy = (fj >> 1) & 1;
-        const float gv = G[j * (NC + 4) + cl];
-        const float wx = dxl ? w : e;
-        atomicAdd(&acc[(ly * TT + lx) * NC + cl], gv * (s_ * wx));
-        atomicAdd(&acc[((ly + oy) * TT + lx) * NC + cl], gv * (nn * wx));
-      }
-      wave_lds_sync();
     }
+    if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
     __syncthreads();
     float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
     for (int k = tid; k < TT * TT * NC; k += 256) {
-      const float v = acc[k];
+      const float v = (acc[k] + acc[TILE_F + k]) + (acc[2 * TILE_F + k] + acc[3 * TILE_F + k]);
       const int texel = k / NC, ch = k % NC;
       const int gy = ty * TS + texel / TT, gx = tx * TS + texel % TT;
       if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
