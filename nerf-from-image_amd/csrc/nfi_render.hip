@@ -87,28 +87,57 @@ struct PlaneView {
 };
 
 // Gather + interpolate + mean-of-3 for points 0..npts-1 of the wave (point j's parameters live
-// in lane j); writes X[j][c] (j < npts) into the wave's LDS tile.
+// in lane j); writes X[j][0..31] (j < npts) into the wave's LDS tile.
+//
+// Lane layout ("quad" gather): lane = (sub = l>>4, dx = (l>>3)&1, q4 = l&7).  One wave
+// instruction serves four points (sub), each a bilinear row pair of 2 texels x 32 channels
+// (dx selects x0 / x0+1, q4 a float4 of channels): 4 x 256 contiguous bytes per 1-KiB load.
+// Point parameters arrive by ds_bpermute from the owning lane; the two texels of a row are
+// combined with a DPP row_ror:8 (lanes l and l^8 of a 16-lane row).
+__device__ __forceinline__ float4 ror8_add(float4 v) {
+  v.x += dpp_mov<0x128>(v.x);
+  v.y += dpp_mov<0x128>(v.y);
+  v.z += dpp_mov<0x128>(v.z);
+  v.w += dpp_mov<0x128>(v.w);
+  return v;
+}
+
 __device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
                                                 float* __restrict__ X) {
   const int l = lane_id();
-  const int dx = l >> 5, c = l & 31;
+  const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
+  const int ngrp = (npts + 3) >> 2;
 #pragma unroll 2
-  for (int j = 0; j < npts; ++j) {
-    float E[3];
+  for (int gi = 0; gi < ngrp; ++gi) {
+    const int j = 4 * gi + sub;
+    float4 E[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const int pk = readlane(P.pl[q].tex, j);
-      const float e = readlane(P.pl[q].e, j), w = readlane(P.pl[q].w, j);
-      const float s = readlane(P.pl[q].s, j), n = readlane(P.pl[q].n, j);
+      const int pk = __shfl(P.pl[q].tex, j);
+      const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
+      const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
       const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
       const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-      const float* b = pv.base + q * pv.sq + c;
-      const float v0 = b[t0 * pv.st];
-      const float v1 = b[t1 * pv.st];
+      const float* b = pv.base + q * pv.sq + 4 * q4;
+      const float4 v0 = *reinterpret_cast<const float4*>(b + t0 * pv.st);
+      const float4 v1 = *reinterpret_cast<const float4*>(b + t1 * pv.st);
       const float wx = dx ? w : e;
-      E[q] = sum_halves(v0 * (s * wx) + v1 * (n * wx));
+      const float w0 = s * wx, w1 = n * wx;
+      float4 pr;
+      pr.x = v0.x * w0 + v1.x * w1;
+      pr.y = v0.y * w0 + v1.y * w1;
+      pr.z = v0.z * w0 + v1.z * w1;
+      pr.w = v0.w * w0 + v1.w * w1;
+      E[q] = ror8_add(pr);
     }
-    if (l < 32) X[j * XS + c] = ((E[0] + E[1]) + E[2]) / 3.f;
+    if (dx == 0 && j < npts) {
+      float4 f;
+      f.x = ((E[0].x + E[1].x) + E[2].x) / 3.f;
+      f.y = ((E[0].y + E[1].y) + E[2].y) / 3.f;
+      f.z = ((E[0].z + E[1].z) + E[2].z) / 3.f;
+      f.w = ((E[0].w + E[1].w) + E[2].w) / 3.f;
+      *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
+    }
   }
 }
 
@@ -753,39 +782,56 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   wave_lds_sync();
   store_row(X, l, gx);
   wave_lds_sync();
-  float gro0 = 0.f, gro1 = 0.f, gro2 = 0.f, grd0 = 0.f, grd1 = 0.f, grd2 = 0.f;
-#pragma unroll 1
-  for (int j = 0; j < npts; ++j) {
-    if (!((live >> j) & 1ull)) continue;
-    const float tj = readlane(te, j);
+  // d ray origin / direction: dL/dp_j = sum_q (d grid_q) * (R-1)/2 * inbound / scene_range and
+  // dL/d ro = sum_j dL/dp_j, dL/d rd = sum_j t_j dL/dp_j are linear in the per-lane products,
+  // so every lane accumulates its share over all points and the wave is reduced once.
+  // Re-gather in the quad layout of gather_features (4 points per wave instruction).
+  float aro0 = 0.f, aro1 = 0.f, aro2 = 0.f, ard0 = 0.f, ard1 = 0.f, ard2 = 0.f;
+  {
     PointP P;
-    point_params(R.o, R.d, tj, sr, pv.R, P);
-    const float gv = X[j * XS + cl];
-    float GX[3], GY[3];
+    point_params(R.o, R.d, te, sr, pv.R, P);
+    const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
+    const int ngrp = (npts + 3) >> 2;
+#pragma unroll 1
+    for (int gi = 0; gi < ngrp; ++gi) {
+      if (((live >> (4 * gi)) & 0xFull) == 0ull) continue;
+      const int j = 4 * gi + sub;
+      const bool lj = (live >> j) & 1ull;
+      const float tj = __shfl(te, j);
+      const float4 gv = *reinterpret_cast<const float4*>(X + j * XS + 4 * q4);
+      float GX[3], GY[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const PlaneP& pp = P.pl[q];
-      const int t0 = (pp.tex & 0xFFFFF) + (dxl ? ((pp.tex >> 20) & 1) : 0);
-      const int t1 = t0 + (((pp.tex >> 21) & 1) ? pv.R : 0);
-      const float wx = dxl ? pp.w : pp.e;
-      const float* bq = pv.base + q * pv.sq + cl;
-      const float v0 = bq[t0 * pv.st], v1 = bq[t1 * pv.st];
-      // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
-      const float px = (dxl ? 1.f : -1.f) * (pp.s * v0 + pp.n * v1) * gv;
-      const float py = wx * (v1 - v0) * gv;
-      GX[q] = wave_sum(px) * pp.gxm;
-      GY[q] = wave_sum(py) * pp.gym;
+      for (int q = 0; q < 3; ++q) {
+        const int pk = __shfl(P.pl[q].tex, j);
+        const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
+        const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
+        const float gxm = __shfl(P.pl[q].gxm, j), gym = __shfl(P.pl[q].gym, j);
+        const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
+        const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
+        const float* b = pv.base + q * pv.sq + 4 * q4;
+        const float4 v0 = *reinterpret_cast<const float4*>(b + t0 * pv.st);
+        const float4 v1 = *reinterpret_cast<const float4*>(b + t1 * pv.st);
+        const float wx = dx ? w : e;
+        // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
+        const float ax = (s * v0.x + n * v1.x) * gv.x + (s * v0.y + n * v1.y) * gv.y +
+                         (s * v0.z + n * v1.z) * gv.z + (s * v0.w + n * v1.w) * gv.w;
+        const float ay = (v1.x - v0.x) * gv.x + (v1.y - v0.y) * gv.y + (v1.z - v0.z) * gv.z +
+                         (v1.w - v0.w) * gv.w;
+        GX[q] = lj ? (dx ? ax : -ax) * gxm : 0.f;
+        GY[q] = lj ? wx * ay * gym : 0.f;
+      }
+      // coords (x, y, z) of planes xy, xz, yz
+      const float d0 = GX[0] + GX[1], d1 = GY[0] + GX[2], d2 = GY[1] + GY[2];
+      aro0 += d0;
+      aro1 += d1;
+      aro2 += d2;
+      ard0 = fmaf(d0, tj, ard0);
+      ard1 = fmaf(d1, tj, ard1);
+      ard2 = fmaf(d2, tj, ard2);
     }
-    const float dp0 = (GX[0] + GX[1]) / sr;
-    const float dp1 = (GY[0] + GX[2]) / sr;
-    const float dp2 = (GY[1] + GY[2]) / sr;
-    gro0 += dp0;
-    gro1 += dp1;
-    gro2 += dp2;
-    grd0 = fmaf(dp0, tj, grd0);
-    grd1 = fmaf(dp1, tj, grd1);
-    grd2 = fmaf(dp2, tj, grd2);
   }
+  const float gro0 = wave_sum(aro0) / sr, gro1 = wave_sum(aro1) / sr, gro2 = wave_sum(aro2) / sr;
+  const float grd0 = wave_sum(ard0) / sr, grd1 = wave_sum(ard1) / sr, grd2 = wave_sum(ard2) / sr;
   if (l == 0) {
     unsafeAtomicAdd(g.g_ro + r * 3 + 0, gro0);
     unsafeAtomicAdd(g.g_ro + r * 3 + 1, gro1);

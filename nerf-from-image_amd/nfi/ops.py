@@ -301,6 +301,9 @@ def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOption
         raise ValueError('planes_tm must be texel-major [B,3,R,R,32] with unit channel stride')
     if planes_tm.stride(2) != planes_tm.shape[3] * planes_tm.stride(3):
         raise ValueError('planes_tm rows must be dense (stride(2) == R*stride(3))')
+    if planes_tm.data_ptr() % 16 or any(st % 4 for st in planes_tm.stride()[:4]):
+        raise ValueError('planes_tm must be 16-byte aligned with texel/plane/batch strides '
+                         'divisible by 4 (the kernels load channel quads as float4)')
     B = planes_tm.shape[0]
     if ro.shape[0] != B or palette.shape != (B, 10, 3):
         raise ValueError('batch mismatch between planes, palette and rays')
