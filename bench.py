@@ -163,12 +163,27 @@ def main():
     value = world * samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel (SURVEY §8(d) algorithmic tap bytes per sample)
-    per_sample = {'render_fwd': TAP_BYTES, 'render_bwd': TAP_BYTES * (2 if pose else 1)}
+    # roofline of the dominant kernel (SURVEY §8(d) algorithmic bytes per sample):
+    # forward tap 1,536 B; field backward: coordinate re-gather 1,536 B (pose) / 0; tile
+    # accumulation: d planes scatter-add 1,536 B; binning: 12 B of keys/ids.
+    per_sample = {'render_fwd': TAP_BYTES, 'bwd_field': TAP_BYTES if pose else 4 * 32,
+                  'bwd_tiles': TAP_BYTES, 'bwd_bins': 12}
+    kernel_of = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
+                 'bwd_tiles': 'tile_accum_kernel', 'bwd_bins': 'bin_fill_kernel'}
     dom = max(kern, key=kern.get)
     achieved = samples_per_step * per_sample[dom] / (kern[dom] * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, 'profiles', 'latest_counters.json')) as fh:
+            ctr = json.load(fh)['kernels'].get(kernel_of[dom])
+        if ctr is not None and args.config == 'p3d_fwdbwd' and B == 8:
+            traffic = round(ctr['hbm_bytes_corrected'] / 1e9, 3)
+    except (OSError, ValueError, KeyError):
+        pass
     roof = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
+            'traffic': traffic, 'traffic_unit': 'GB per launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE, '
+                                                'profiles/latest_counters.json)',
             'bytes_per_sample': per_sample[dom], 'ms_per_launch': {k: round(v, 4) for k, v in kern.items()}}
 
     out = {

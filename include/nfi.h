@@ -144,6 +144,12 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
  * per 16x16-cell plane tile in LDS (samples binned by tile) and flushed once per tile. */
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
+/* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
+ * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,
+ * 1 = compositing + field backward (d palette, d rays, per-sample feature gradients),
+ * 2 = per-tile d planes accumulation. */
+int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_grad_args* g, int32_t stage,
+                                  void* stream);
 
 #ifdef __cplusplus
 }

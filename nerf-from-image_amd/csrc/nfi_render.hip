@@ -23,6 +23,15 @@ namespace nfi {
 constexpr int XS = 36;                  // LDS row stride (floats) of the point x channel tile
 constexpr int XTILE = WAVE * XS;        // 2304 floats
 
+// XCD-aware block order (MI355X: 8 XCDs with private 4 MB L2s; blocks are dealt round-robin,
+// so blocks b and b+8 share an XCD).  Logical block = (b % 8)-th contiguous range + b / 8, so
+// each XCD walks a contiguous range of rays (≈ one image of a B=8 batch) and its L2 holds
+// that image's planes.  Bijective for any grid size (cdna_hip_programming.md §5.5 T1).
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
+  const unsigned q = nb >> 3, r8 = nb & 7, x = b & 7;
+  return (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -362,7 +371,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
-  const long long r = (long long)blockIdx.x * 4 + wv;
+  const long long r = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
   if (r >= nrays) return;
   const int S = a.S;
   const int N = FINE ? 2 * S : S;
@@ -694,7 +703,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   const int wv = threadIdx.x >> 6, l = lane_id();
   const int dxl = l >> 5, cl = l & 31;
   const long long nrays = (long long)a.B * a.HW;
-  const long long job = (long long)blockIdx.x * 4 + wv;
+  const long long job = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
   const long long r = job / g.npl;
   const int e = (int)(job % g.npl);
   if (r >= nrays) return;
@@ -1007,7 +1016,10 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
   const int dxl = l >> 5, cl = l & 31;
   float* img = acc + wv * TILE_F;
   const int total = A.meta[0];
-  for (int c = blockIdx.x; c < total; c += gridDim.x) {
+  // contiguous chunk range per (XCD-remapped) block: tiles are ordered (image, plane, ty, tx)
+  const long long L = xcd_remap(blockIdx.x, gridDim.x);
+  const int c0 = (int)(L * total / gridDim.x), c1 = (int)((L + 1) * total / gridDim.x);
+  for (int c = c0; c < c1; ++c) {
     // chunk -> tile: last k with chunk_start[k] <= c
     int lo = 0, hi = A.K - 1;
     while (lo < hi) {
@@ -1134,7 +1146,7 @@ static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
   return NFI_OK;
 }
 
-static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s) {
+static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, hipStream_t s, int stage) {
   const long long nrays = (long long)a->B * a->HW;
   const int N = a->fine ? 2 * a->S : a->S;
   const long long nsamp = nrays * N;
@@ -1145,32 +1157,39 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
               (long long)g->workspace_bytes, w.bytes);
   NFI_REQUIRE(nsamp * 3 < (1LL << 31), "render_backward: too many samples per call (%lld)", nsamp);
   // 1) bin (sample, plane) entries by plane tile from the saved depths
+  const bool do_bins = stage < 0 || stage == 0, do_field = stage < 0 || stage == 1, do_tiles = stage < 0 || stage == 2;
   BinArgs B{a->ro, a->rd, a->t_saved, nsamp, N, a->HW, a->field.R, T, a->field.scene_range,
             w.counts, w.cursor, w.list};
-  NFI_REQUIRE(hipMemsetAsync(w.counts, 0, (size_t)K * 4, s) == hipSuccess, "render_backward: memset failed");
-  const unsigned sb = (unsigned)((nsamp + 255) / 256);
-  bin_count_kernel<<<sb, 256, 0, s>>>(B);
-  NFI_CHECK_LAUNCH("bin_count_kernel");
-  bin_scan_kernel<<<1, 1024, 0, s>>>(w.counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
-  NFI_CHECK_LAUNCH("bin_scan_kernel");
-  bin_fill_kernel<<<sb, 256, 0, s>>>(B);
-  NFI_CHECK_LAUNCH("bin_fill_kernel");
+  if (do_bins) {
+    NFI_REQUIRE(hipMemsetAsync(w.counts, 0, (size_t)K * 4, s) == hipSuccess, "render_backward: memset failed");
+    const unsigned sb = (unsigned)((nsamp + 255) / 256);
+    bin_count_kernel<<<sb, 256, 0, s>>>(B);
+    NFI_CHECK_LAUNCH("bin_count_kernel");
+    bin_scan_kernel<<<1, 1024, 0, s>>>(w.counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
+    NFI_CHECK_LAUNCH("bin_scan_kernel");
+    bin_fill_kernel<<<sb, 256, 0, s>>>(B);
+    NFI_CHECK_LAUNCH("bin_fill_kernel");
+  }
   // 2) per-ray compositing backward, then per-(ray, 64-sample chunk) field backward
   const int NPL = (N + 63) / 64;
   BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat, w.gsig, w.wts, NPL};
   const unsigned rb = (unsigned)((nrays + 3) / 4);
-  if (NPL <= 1) composite_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
-  else if (NPL <= 2) composite_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
-  else composite_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
-  NFI_CHECK_LAUNCH("composite_bwd_kernel");
-  field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
-  NFI_CHECK_LAUNCH("field_bwd_kernel");
+  if (do_field) {
+    if (NPL <= 1) composite_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
+    else if (NPL <= 2) composite_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
+    else composite_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
+    NFI_CHECK_LAUNCH("composite_bwd_kernel");
+    field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+    NFI_CHECK_LAUNCH("field_bwd_kernel");
+  }
   // 3) per-tile LDS accumulation of d planes
   TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, w.counts, w.offsets, w.chunk_start, w.meta, w.list,
               g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,
               a->field.scene_range};
-  tile_accum_kernel<<<2048, 256, 0, s>>>(TA);
-  NFI_CHECK_LAUNCH("tile_accum_kernel");
+  if (do_tiles) {
+    tile_accum_kernel<<<2048, 256, 0, s>>>(TA);
+    NFI_CHECK_LAUNCH("tile_accum_kernel");
+  }
   return NFI_OK;
 }
 
@@ -1232,7 +1251,18 @@ int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args
   NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
               "render_backward: null grad pointer");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
-  return nfi::launch_bwd(a, g, (hipStream_t)stream);
+  return nfi::launch_bwd(a, g, (hipStream_t)stream, -1);
+}
+
+int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_grad_args* g, int32_t stage,
+                                  void* stream) {
+  int e = nfi::validate(a);
+  if (e) return e;
+  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
+              "render_backward: null grad pointer");
+  NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
+  NFI_REQUIRE(stage >= 0 && stage <= 2, "render_backward_stage: stage %d not in 0..2", stage);
+  return nfi::launch_bwd(a, g, (hipStream_t)stream, stage);
 }
 
 }  // extern "C"

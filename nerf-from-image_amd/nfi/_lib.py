@@ -70,6 +70,9 @@ SIGNATURES = {
     'nfi_render_backward_workspace_bytes': (ctypes.c_int64, [ctypes.POINTER(NfiRenderArgs)]),
     'nfi_render_backward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
                                              ctypes.POINTER(NfiRenderGradArgs), c_void_p]),
+    'nfi_render_backward_stage': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
+                                                   ctypes.POINTER(NfiRenderGradArgs), ctypes.c_int32,
+                                                   c_void_p]),
 }
 
 _lib = None

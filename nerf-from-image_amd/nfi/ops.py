@@ -279,9 +279,10 @@ class _VolumeRender(torch.autograd.Function):
                                        d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd),
                                        workspace=_ptr(ws), workspace_bytes=nbytes)
         st = _stream(dev)
-        with _timed('render_bwd', dev):
-            _lib.check(lib.nfi_render_backward(ctypes.byref(args), ctypes.byref(gargs), st),
-                       'nfi_render_backward')
+        for stage, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
+            with _timed(name, dev):
+                _lib.check(lib.nfi_render_backward_stage(ctypes.byref(args), ctypes.byref(gargs), stage, st),
+                           'nfi_render_backward_stage')
         d_pal = torch.empty((B, 30), device=dev)
         ws = torch.empty((B * 64 * 30,), device=dev)
         _lib.check(lib.nfi_segment_sum(_ptr(d_pal_ray), B, H * W * npl, 30, _ptr(d_pal), _ptr(ws), st),

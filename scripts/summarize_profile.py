@@ -36,4 +36,18 @@ for r in stats:
                  f"{'' if f is None else f'{f:.4g}'} | {'' if f is None else f'{2*f*1024/1e9:.3f} GB'} | "
                  f"{'' if w is None else f'{w:.4g}'} |")
 open(out, 'w').write('\n'.join(lines) + '\n')
+# machine-readable per-launch HBM counters for bench.py's roofline.traffic
+import json
+kern = {}
+for r in stats:
+    n = r['Name']
+    short = n.split('(')[0].replace('void ', '').split('<')[0].replace('nfi::', '')
+    f, w = fetch.get(n), write.get(n)
+    if f is None or w is None:
+        continue
+    kern[short] = {'avg_us': float(r['AverageNs']) / 1e3, 'fetch_kib': f, 'write_kib': w,
+                   'hbm_bytes_corrected': 2 * f * 1024 + w * 1024}
+json.dump({'tag': tag, 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), '
+           'FETCH_SIZE x2 per MI355X_MICROARCH.md HBM section', 'kernels': kern},
+          open(os.path.join(root, 'profiles', 'latest_counters.json'), 'w'), indent=1)
 print(out)
