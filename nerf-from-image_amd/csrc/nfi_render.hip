@@ -23,15 +23,6 @@ namespace nfi {
 constexpr int XS = 36;                  // LDS row stride (floats) of the point x channel tile
 constexpr int XTILE = WAVE * XS;        // 2304 floats
 
-// XCD-aware block order (MI355X: 8 XCDs with private 4 MB L2s; blocks are dealt round-robin,
-// so blocks b and b+8 share an XCD).  Logical block = (b % 8)-th contiguous range + b / 8, so
-// each XCD walks a contiguous range of rays (≈ one image of a B=8 batch) and its L2 holds
-// that image's planes.  Bijective for any grid size (cdna_hip_programming.md §5.5 T1).
-__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nb) {
-  const unsigned q = nb >> 3, r8 = nb & 7, x = b & 7;
-  return (x < r8 ? x * (q + 1) : r8 * (q + 1) + (x - r8) * q) + (b >> 3);
-}
-
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -371,7 +362,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
-  const long long r = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+  const long long r = (long long)blockIdx.x * 4 + wv;
   if (r >= nrays) return;
   const int S = a.S;
   const int N = FINE ? 2 * S : S;
@@ -703,7 +694,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   const int wv = threadIdx.x >> 6, l = lane_id();
   const int dxl = l >> 5, cl = l & 31;
   const long long nrays = (long long)a.B * a.HW;
-  const long long job = (long long)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+  const long long job = (long long)blockIdx.x * 4 + wv;
   const long long r = job / g.npl;
   const int e = (int)(job % g.npl);
   if (r >= nrays) return;
@@ -1016,10 +1007,7 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
   const int dxl = l >> 5, cl = l & 31;
   float* img = acc + wv * TILE_F;
   const int total = A.meta[0];
-  // contiguous chunk range per (XCD-remapped) block: tiles are ordered (image, plane, ty, tx)
-  const long long L = xcd_remap(blockIdx.x, gridDim.x);
-  const int c0 = (int)(L * total / gridDim.x), c1 = (int)((L + 1) * total / gridDim.x);
-  for (int c = c0; c < c1; ++c) {
+  for (int c = blockIdx.x; c < total; c += gridDim.x) {
     // chunk -> tile: last k with chunk_start[k] <= c
     int lo = 0, hi = A.K - 1;
     while (lo < hi) {
