@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 2
+#define NFI_ABI_VERSION 3
 #define NFI_DEC_SIZE 3088 /* floats in the packed decoder buffer */
 
 enum {
@@ -92,6 +92,9 @@ typedef struct nfi_render_args {
   float* t_saved;      /* [B*HW,N]   */
   float* sigma_saved;  /* [B*HW,N]   */
   float* rgb_saved;    /* [B*HW,3,N] */
+  float* y_saved;      /* [B*HW,11,N] decoder outputs (distance, 10 logits) in evaluation order:
+                          coarse 0..S-1 then fine S..2S-1 (lets the backward skip the forward MLP) */
+  int16_t* perm;       /* [B*HW,N] merged sample k -> evaluation index */
   float* z_coarse;     /* optional [B*HW,S] debug: coarse depths */
   float* z_fine;       /* optional [B*HW,S] debug: fine depths, sorted */
 } nfi_render_args;

@@ -327,7 +327,7 @@ __device__ __forceinline__ void load_ray(const nfi_render_args& a, long long r, 
 // Evaluate the field at the (up to 64) points t (one per lane; lanes >= npts ignored).
 __device__ __forceinline__ void field_eval(const nfi_render_args& a, const PlaneView& pv, const RayCtx& R,
                                            float t, int npts, float* __restrict__ X, float& sigma,
-                                           float rgb[3]) {
+                                           float rgb[3], int eval_base) {
   PointP P;
   point_params(R.o, R.d, t, a.field.scene_range, pv.R, P);
   gather_features(pv, P, npts, X);
@@ -336,6 +336,12 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   load_row(X, lane_id(), x);
   float y[NO];
   mlp_forward(a.field.dec, x, y);
+  if (lane_id() < npts) {
+    const int N = a.fine ? 2 * a.S : a.S;
+    float* ys = a.y_saved + R.r * NO * N + eval_base + lane_id();
+#pragma unroll
+    for (int k = 0; k < NO; ++k) ys[k * N] = y[k];
+  }
   Head h;
   head_forward(y, P.mask, a.field.inv_alpha, a.field.beta, a.field.palette + R.b * (NA * 3), h);
   sigma = h.sigma;
@@ -358,7 +364,7 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 template <int SPL, int NPL, bool FINE>
 __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
-  constexpr int WL = XTILE + 5 * NMAX + 2 * SMAX + 8;
+  constexpr int WL = XTILE + 6 * NMAX + 2 * SMAX + 8;
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -370,7 +376,8 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   float* Mt = X + XTILE;          // merged t     [NMAX]
   float* Ms = Mt + NMAX;          // merged sigma [NMAX]
   float* Mc = Ms + NMAX;          // merged rgb   [3][NMAX]
-  float* T2 = Mc + 3 * NMAX;      // [2*SMAX] coarse t | fine t (ranks); cdf | bins (sample_pdf)
+  int* Mi = reinterpret_cast<int*>(Mc + 3 * NMAX);   // merged -> evaluation index [NMAX]
+  float* T2 = Mc + 4 * NMAX;      // [2*SMAX] coarse t | fine t (ranks); cdf | bins (sample_pdf)
 
   RayCtx R;
   load_ray(a, r, R);
@@ -395,7 +402,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     tc[e] = t;
     sc[e] = 0.f;
     cc[e][0] = cc[e][1] = cc[e][2] = 0.f;
-    if (e * 64 < S) field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e]);
+    if (e * 64 < S) field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64);
   }
 
   if constexpr (FINE) {
@@ -492,7 +499,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     for (int e = 0; e < SPL; ++e) {
       sf[e] = 0.f;
       cf[e][0] = cf[e][1] = cf[e][2] = 0.f;
-      if (e * 64 < S) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e]);
+      if (e * 64 < S) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64);
     }
     // ---- merge: stable sort of cat(z_coarse, z_fine) (run.py:283-288, 312-319) ----
 #pragma unroll
@@ -517,8 +524,10 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
         }
         Mt[rc] = vc;
         Ms[rc] = sc[e];
+        Mi[rc] = i;
         Mt[rf] = vf;
         Ms[rf] = sf[e];
+        Mi[rf] = S + i;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           Mc[k * NMAX + rc] = cc[e][k];
@@ -533,6 +542,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       if (i < S) {
         Mt[i] = tc[e];
         Ms[i] = sc[e];
+        Mi[i] = i;
 #pragma unroll
         for (int k = 0; k < 3; ++k) Mc[k * NMAX + i] = cc[e][k];
       }
@@ -560,6 +570,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       a.sigma_saved[r * N + i] = sg;
 #pragma unroll
       for (int k = 0; k < 3; ++k) a.rgb_saved[(r * 3 + k) * N + i] = Mc[k * NMAX + i];
+      a.perm[r * N + i] = (int16_t)Mi[i];
     }
   }
   excl_prod<NPL>(aa, T);
@@ -724,8 +735,14 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   wave_lds_sync();
   float x[NC];
   load_row(X, l, x);
+  // decoder outputs saved by the forward (no forward MLP here)
   float y[NO];
-  mlp_forward(a.field.dec, x, y);
+  {
+    const int ei = v ? (int)a.perm[r * N + i] : 0;
+    const float* ys = a.y_saved + r * NO * N + ei;
+#pragma unroll
+    for (int k = 0; k < NO; ++k) y[k] = v ? ys[k * N] : 0.f;
+  }
   float gy[NO];
   {
     Head h;
@@ -1211,7 +1228,8 @@ static int validate(const nfi_render_args* a) {
   NFI_REQUIRE(f.beta > 0.f && std::isfinite(f.inv_alpha) && f.scene_range > 0.f, "render: bad field scalars");
   NFI_REQUIRE(a->ro && a->rd && a->near_ && a->far_, "render: null ray pointer");
   NFI_REQUIRE(a->B > 0 && a->HW > 0, "render: bad shape B=%d HW=%d", a->B, a->HW);
-  NFI_REQUIRE(a->t_saved && a->sigma_saved && a->rgb_saved, "render: null saved-state pointer");
+  NFI_REQUIRE(a->t_saved && a->sigma_saved && a->rgb_saved && a->y_saved && a->perm,
+              "render: null saved-state pointer");
   NFI_REQUIRE(supported_S(a), "render: unsupported samples per ray S=%d (fine=%d): need 3..128 with fine "
               "sampling, 1..256 without", a->S, (int)a->fine);
   return NFI_OK;

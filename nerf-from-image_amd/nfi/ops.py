@@ -215,6 +215,8 @@ class _VolumeRender(torch.autograd.Function):
         t_saved = torch.empty((n, N), device=dev)
         s_saved = torch.empty((n, N), device=dev)
         c_saved = torch.empty((n, 3, N), device=dev)
+        y_saved = torch.empty((n, 11, N), device=dev)
+        perm = torch.empty((n, N), device=dev, dtype=torch.int16)
         zc = zf = None
         if debug is not None:
             zc = torch.empty((n, S), device=dev)
@@ -222,7 +224,8 @@ class _VolumeRender(torch.autograd.Function):
         uc = None if u_coarse is None else u_coarse.contiguous()
         uf = None if u_fine is None else u_fine.contiguous()
         args = _VolumeRender._args(planes_tm, dec, pal_c, ro_c, rd_c, near_c, far_c, opts, B, H * W,
-                                   uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, zc, zf)
+                                   uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, y_saved, perm,
+                                   zc, zf)
         with _timed('render_fwd', dev):
             _lib.check(lib.nfi_render_forward(ctypes.byref(args), _stream(dev)), 'nfi_render_forward')
         if debug is not None:
@@ -231,7 +234,8 @@ class _VolumeRender(torch.autograd.Function):
             debug['t_sorted'] = t_saved
             debug['sigma_sorted'] = s_saved
             debug['rgb_sorted'] = c_saved
-        ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved)
+        ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved,
+                              y_saved, perm)
         ctx.opts = opts
         ctx.shape = (B, H, W)
         ctx.mark_non_differentiable(depth)
@@ -239,7 +243,7 @@ class _VolumeRender(torch.autograd.Function):
 
     @staticmethod
     def _args(planes_tm, dec, pal, ro, rd, near, far, opts, B, HW, uc, uf, seed, rgb, depth, mask,
-              t_saved, s_saved, c_saved, zc, zf):
+              t_saved, s_saved, c_saved, y_saved, perm, zc, zf):
         R = planes_tm.shape[2]
         field = _lib.NfiField(planes=_ptr(planes_tm), sb=planes_tm.stride(0), sq=planes_tm.stride(1),
                               st=planes_tm.stride(3), R=R, _pad=0, dec=_ptr(dec), palette=_ptr(pal),
@@ -251,12 +255,13 @@ class _VolumeRender(torch.autograd.Function):
                                   seed=seed & ((1 << 64) - 1), offset=0, u_coarse=_ptr(uc),
                                   u_fine=_ptr(uf), rgb=_ptr(rgb), depth=_ptr(depth), mask=_ptr(mask),
                                   t_saved=_ptr(t_saved), sigma_saved=_ptr(s_saved),
-                                  rgb_saved=_ptr(c_saved), z_coarse=_ptr(zc), z_fine=_ptr(zf))
+                                  rgb_saved=_ptr(c_saved), y_saved=_ptr(y_saved), perm=_ptr(perm),
+                                  z_coarse=_ptr(zc), z_fine=_ptr(zf))
 
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_mask):
         lib = _lib.load()
-        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved = ctx.saved_tensors
+        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm = ctx.saved_tensors
         opts = ctx.opts
         B, H, W = ctx.shape
         dev = ro.device
@@ -270,7 +275,7 @@ class _VolumeRender(torch.autograd.Function):
         g_ro = torch.empty((n, 3), device=dev) if need_coords else None
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
         args = _VolumeRender._args(planes_tm, dec, pal, ro, rd, near, far, opts, B, H * W, None, None, 0,
-                                   None, None, None, t_saved, s_saved, c_saved, None, None)
+                                   None, None, None, t_saved, s_saved, c_saved, y_saved, perm, None, None)
         nbytes = lib.nfi_render_backward_workspace_bytes(ctypes.byref(args))
         if nbytes < 0:
             _lib.check(-1, 'nfi_render_backward_workspace_bytes')
