@@ -883,14 +883,15 @@ struct BinArgs {
   float sr;
   int* counts;           // [K]
   int* cursor;           // [K]
-  int* list;             // [3 * nsamp]
+  int4* list;            // [3 * nsamp] entries {sample, local cell key, w bits, n bits}
 };
 
 __device__ __forceinline__ int tile_of(int cell, int T) { return min(cell / TS, T - 1); }
 
-// Tile keys of sample s for the three planes; false for samples outside the box (their
-// gradient is exactly zero: sigma * (1 - mask) and weight 0).
-__device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int key[3]) {
+// Tile keys of sample s for the three planes, and each plane's entry record {s, local cell key,
+// w, n} (key = ly << 16 | lx << 8 | ox | oy << 1 inside the tile); false for samples outside
+// the box (their gradient is exactly zero: sigma * (1 - mask) and weight 0).
+__device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int key[3], int4 rec[3]) {
   const long long ray = s / A.N;
   const int b = (int)(ray / A.HW);
   float o[3], d[3];
@@ -905,7 +906,10 @@ __device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int k
   for (int q = 0; q < 3; ++q) {
     const int cell = P.pl[q].tex & 0xFFFFF;
     const int y0 = cell / A.R, x0 = cell % A.R;
-    key[q] = ((b * 3 + q) * A.T + tile_of(y0, A.T)) * A.T + tile_of(x0, A.T);
+    const int ty = tile_of(y0, A.T), tx = tile_of(x0, A.T);
+    key[q] = ((b * 3 + q) * A.T + ty) * A.T + tx;
+    rec[q] = make_int4((int)s, ((y0 - ty * TS) << 16) | ((x0 - tx * TS) << 8) | (P.pl[q].tex >> 20),
+                       __float_as_int(P.pl[q].w), __float_as_int(P.pl[q].n));
   }
   return P.mask == 0.f;
 }
@@ -931,8 +935,9 @@ __device__ __forceinline__ int agg_increment(int* base, int key, bool valid) {
 __global__ void __launch_bounds__(256) bin_count_kernel(BinArgs A) {
   const long long s = (long long)blockIdx.x * 256 + threadIdx.x;
   int key[3] = {0, 0, 0};
+  int4 rec[3];
   bool v = s < A.nsamp;
-  if (v) v = sample_keys(A, s, key);
+  if (v) v = sample_keys(A, s, key, rec);
 #pragma unroll
   for (int q = 0; q < 3; ++q) agg_increment(A.counts, key[q], v);
 }
@@ -940,12 +945,13 @@ __global__ void __launch_bounds__(256) bin_count_kernel(BinArgs A) {
 __global__ void __launch_bounds__(256) bin_fill_kernel(BinArgs A) {
   const long long s = (long long)blockIdx.x * 256 + threadIdx.x;
   int key[3] = {0, 0, 0};
+  int4 rec[3];
   bool v = s < A.nsamp;
-  if (v) v = sample_keys(A, s, key);
+  if (v) v = sample_keys(A, s, key, rec);
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const int pos = agg_increment(A.cursor, key[q], v);
-    if (v) A.list[pos] = (int)(s * 3 + q);
+    if (v) A.list[pos] = rec[q];
   }
 }
 
@@ -998,7 +1004,7 @@ struct TileArgs {
   const int* offsets;
   const int* chunk_start; // [K+1]
   const int* meta;        // meta[0] = total chunks
-  const int* list;
+  const int4* list;
   float* dplanes;
   long long sb;
   int sq, st;
@@ -1020,9 +1026,11 @@ __device__ __forceinline__ void tile_rmw(float* __restrict__ img, int key, int d
 
 __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
   __shared__ __attribute__((aligned(16))) float acc[4 * TILE_F];
+  __shared__ __attribute__((aligned(16))) float stage[4 * 64 * NC];
   const int tid = threadIdx.x, wv = tid >> 6, l = lane_id();
   const int dxl = l >> 5, cl = l & 31;
   float* img = acc + wv * TILE_F;
+  float* G = stage + wv * 64 * NC;
   const int total = A.meta[0];
   for (int c = blockIdx.x; c < total; c += gridDim.x) {
     // chunk -> tile: last k with chunk_start[k] <= c
@@ -1035,62 +1043,56 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
     const int tile = lo;
     const int first = A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK;
     const int last = min(A.offsets[tile] + A.counts[tile], first + CHUNK);
-    const int tx = tile % A.T, ty = (tile / A.T) % A.T, bq = tile / (A.T * A.T);
+    const int bq = tile / (A.T * A.T);
     const int q = bq % 3, b = bq / 3;
+    const int tx = tile % A.T, ty = (tile / A.T) % A.T;
     for (int k = tid; k < 4 * TILE_F; k += 256) acc[k] = 0.f;
     __syncthreads();
     int cur = -1;
     float a0 = 0.f, a1 = 0.f;
-    for (int base = first + wv * 64; base < last; base += 256) {
+    // software pipeline: records + gradient rows of batch k+1 load while batch k is summed
+    int base = first + wv * 64;
+    // (indices clamped to the chunk's last entry: every lane always loads a valid record)
+    int4 rec = A.list[min(base + l, last - 1)];
+    float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
+#define NFI_LOAD_ROW(REC)                                                                       \
+  {                                                                                              \
+    const float4* src_ = reinterpret_cast<const float4*>(A.gfeat + (long long)(REC).x * NC);     \
+    r0 = src_[0]; r1 = src_[1]; r2 = src_[2]; r3 = src_[3];                                      \
+    r4 = src_[4]; r5 = src_[5]; r6 = src_[6]; r7 = src_[7];                                      \
+  }
+    NFI_LOAD_ROW(rec)
+    while (base < last) {
       const int n = min(64, last - base);
-      // lane j: cell key, weights and sample index of entry base + j on plane q
-      int key = 0, sidx = 0;
-      float pw = 0.f, pn = 0.f;
-      if (l < n) {
-        const long long s = A.list[base + l] / 3;
-        const long long ray = s / A.N;
-        const float ts = A.t[s];
-        float cx[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(A.ro[ray * 3 + k], fmul(A.rd[ray * 3 + k], ts)), A.sr);
-        // plane q samples (x,y), (x,z), (y,z)  (generator.py:312-326)
-        PlaneP pp;
-        plane_params(q == 2 ? cx[1] : cx[0], q == 0 ? cx[1] : cx[2], A.R, pp);
-        const int cell = pp.tex & 0xFFFFF;
-        const int y0 = cell / A.R, x0 = cell % A.R;
-        key = ((y0 - ty * TS) << 16) | ((x0 - tx * TS) << 8) | (pp.tex >> 20);
-        pw = pp.w;
-        pn = pp.n;
-        sidx = (int)s;
-      }
-      for (int j0 = 0; j0 < n; j0 += 8) {
-        float gv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int sj = readlane(sidx, min(j0 + u, 63));
-          gv[u] = (j0 + u < n) ? A.gfeat[(long long)sj * NC + cl] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int j = j0 + u;
-          if (j < n) {
-            const int kj = readlane(key, j);
-            const float w = readlane(pw, j), nn = readlane(pn, j);
-            const float wx = dxl ? w : 1.f - w;
-            const float c0 = gv[u] * ((1.f - nn) * wx), c1 = gv[u] * (nn * wx);
-            if (kj == cur) {
-              a0 += c0;
-              a1 += c1;
-            } else {
-              if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
-              cur = kj;
-              a0 = c0;
-              a1 = c1;
-            }
-          }
+      float4* dst = reinterpret_cast<float4*>(G + l * NC);
+      dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
+      dst[4] = r4; dst[5] = r5; dst[6] = r6; dst[7] = r7;
+      const int key = rec.y;
+      const float pw = __int_as_float(rec.z), pn = __int_as_float(rec.w);
+      const int nb = base + 256;
+      rec = A.list[min(nb + l, last - 1)];
+      NFI_LOAD_ROW(rec)
+      wave_lds_sync();
+      for (int j = 0; j < n; ++j) {
+        const int kj = readlane(key, j);
+        const float w = readlane(pw, j), nn = readlane(pn, j);
+        const float gv = G[j * NC + cl];
+        const float wx = dxl ? w : 1.f - w;
+        const float c0 = gv * ((1.f - nn) * wx), c1 = gv * (nn * wx);
+        if (kj == cur) {
+          a0 += c0;
+          a1 += c1;
+        } else {
+          if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
+          cur = kj;
+          a0 = c0;
+          a1 = c1;
         }
       }
+      wave_lds_sync();
+      base = nb;
     }
+#undef NFI_LOAD_ROW
     if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
     __syncthreads();
     float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
@@ -1113,7 +1115,7 @@ struct Workspace {
   int* offsets;
   int* chunk_start;
   int* meta;
-  int* list;
+  int4* list;
   long long bytes;
 };
 
@@ -1138,7 +1140,7 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.offsets = reinterpret_cast<int*>(take((K + 1) * 4));
   w.chunk_start = reinterpret_cast<int*>(take((K + 1) * 4));
   w.meta = reinterpret_cast<int*>(take(16));
-  w.list = reinterpret_cast<int*>(take(3 * nsamp * 4));
+  w.list = reinterpret_cast<int4*>(take(3 * nsamp * 16));
   w.bytes = p - static_cast<char*>(base);
   return w;
 }
