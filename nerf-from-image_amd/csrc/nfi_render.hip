@@ -995,6 +995,16 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(const int* __restrict__ 
   }
 }
 
+// chunk -> tile map (one dependent load per chunk in tile_accum instead of a binary search)
+__global__ void __launch_bounds__(256) chunk_map_kernel(const int* __restrict__ counts,
+                                                        const int* __restrict__ chunk_start, int K,
+                                                        int* __restrict__ chunk_tile) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  const int c0 = chunk_start[k], nc = (counts[k] + CHUNK - 1) / CHUNK;
+  for (int j = 0; j < nc; ++j) chunk_tile[c0 + j] = k;
+}
+
 struct TileArgs {
   const float* ro;
   const float* rd;
@@ -1003,6 +1013,7 @@ struct TileArgs {
   const int* counts;
   const int* offsets;
   const int* chunk_start; // [K+1]
+  const int* chunk_tile;  // [total chunks]
   const int* meta;        // meta[0] = total chunks
   const int4* list;
   float* dplanes;
@@ -1033,14 +1044,7 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
   float* G = stage + wv * 64 * NC;
   const int total = A.meta[0];
   for (int c = blockIdx.x; c < total; c += gridDim.x) {
-    // chunk -> tile: last k with chunk_start[k] <= c
-    int lo = 0, hi = A.K - 1;
-    while (lo < hi) {
-      const int m = (lo + hi + 1) >> 1;
-      if (A.chunk_start[m] <= c) lo = m;
-      else hi = m - 1;
-    }
-    const int tile = lo;
+    const int tile = A.chunk_tile[c];
     const int first = A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK;
     const int last = min(A.offsets[tile] + A.counts[tile], first + CHUNK);
     const int bq = tile / (A.T * A.T);
@@ -1114,6 +1118,7 @@ struct Workspace {
   int* cursor;
   int* offsets;
   int* chunk_start;
+  int* chunk_tile;
   int* meta;
   int4* list;
   long long bytes;
@@ -1140,6 +1145,8 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.offsets = reinterpret_cast<int*>(take((K + 1) * 4));
   w.chunk_start = reinterpret_cast<int*>(take((K + 1) * 4));
   w.meta = reinterpret_cast<int*>(take(16));
+  // chunks <= ceil(entries / CHUNK) + K  (each tile wastes at most one partial chunk)
+  w.chunk_tile = reinterpret_cast<int*>(take((3 * nsamp / CHUNK + K + 1) * 4));
   w.list = reinterpret_cast<int4*>(take(3 * nsamp * 16));
   w.bytes = p - static_cast<char*>(base);
   return w;
@@ -1174,6 +1181,8 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     NFI_CHECK_LAUNCH("bin_count_kernel");
     bin_scan_kernel<<<1, 1024, 0, s>>>(w.counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
     NFI_CHECK_LAUNCH("bin_scan_kernel");
+    chunk_map_kernel<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(w.counts, w.chunk_start, K, w.chunk_tile);
+    NFI_CHECK_LAUNCH("chunk_map_kernel");
     bin_fill_kernel<<<sb, 256, 0, s>>>(B);
     NFI_CHECK_LAUNCH("bin_fill_kernel");
   }
@@ -1190,7 +1199,7 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
   // 3) per-tile LDS accumulation of d planes
-  TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, w.counts, w.offsets, w.chunk_start, w.meta, w.list,
+  TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, w.counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list,
               g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,
               a->field.scene_range};
   if (do_tiles) {
