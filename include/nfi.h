@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 3
+#define NFI_ABI_VERSION 4
 #define NFI_DEC_SIZE 3088 /* floats in the packed decoder buffer */
 
 enum {
@@ -95,6 +95,8 @@ typedef struct nfi_render_args {
   float* y_saved;      /* [B*HW,11,N] decoder outputs (distance, 10 logits) in evaluation order:
                           coarse 0..S-1 then fine S..2S-1 (lets the backward skip the forward MLP) */
   int16_t* perm;       /* [B*HW,N] merged sample k -> evaluation index */
+  int32_t* tile_counts; /* optional [nfi_tile_count_size()] per-plane-tile sample counts for the
+                           backward's d-planes binning (zeroed and filled by the forward); NULL = skip */
   float* z_coarse;     /* optional [B*HW,S] debug: coarse depths */
   float* z_fine;       /* optional [B*HW,S] debug: fine depths, sorted */
 } nfi_render_args;
@@ -107,6 +109,7 @@ typedef struct nfi_render_grad_args {
                            (reduce per image with nfi_segment_sum, M = HW*ceil(N/64)) */
   float* g_ro;          /* [B*HW,3] dL/d ray origins  (NULL: skip coordinate gradients) */
   float* g_rd;          /* [B*HW,3] dL/d unit ray directions */
+  const int32_t* tile_counts; /* the forward's tile_counts, or NULL (the backward counts itself) */
   void* workspace;      /* device scratch of nfi_render_backward_workspace_bytes() bytes */
   int64_t workspace_bytes;
 } nfi_render_grad_args;
@@ -146,6 +149,7 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
  * (recomputes taps and decoder) writes per-sample feature gradients; d planes is then summed
  * per 16x16-cell plane tile in LDS (samples binned by tile) and flushed once per tile. */
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
+int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * 3 * ceil((R-1)/8)^2 */
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 /* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
  * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,

@@ -14,6 +14,7 @@
 // in SGPRs (wave-uniform scalar loads).  Backward scatters d planes with the same 256-byte
 // wave-instruction shape, which is the full-rate shape of gfx950 float atomics.
 #include <cmath>
+#include <cstdlib>
 
 #include "nfi_common.h"
 #include "nfi_host.h"
@@ -139,6 +140,54 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
       *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// d planes by plane tile: every (sample, plane) contribution is binned by the 8x8-cell tile
+// of the plane its bilinear cell lies in; a workgroup sums a chunk of a tile's entries into
+// 9x9x32 LDS images — one private image per wave, updated by plain read-modify-write (LDS
+// executes a wave's instructions in order, so no atomics are needed; gfx950's ds_add_f32 costs
+// ~200 cycles per wave-instruction per CU against ~25 for the RMW, scripts/ubench/lds_atomic.hip)
+// with consecutive same-cell entries merged in registers first — then merges the four images
+// and flushes them with one float atomic per nonzero texel channel.  Global atomic traffic
+// drops from 1,536 B per sample to ~10 KB per (tile, chunk).
+// ---------------------------------------------------------------------------------------
+constexpr int TS = 8;             // cells per tile side
+constexpr int TT = TS + 1;        // texels per tile side
+constexpr int TILE_F = TT * TT * NC + NC;   // floats per wave image (+1 trash texel)
+constexpr int CHUNK = 2048;       // (sample, plane) entries per accumulation workgroup
+
+__device__ __forceinline__ int tile_of(int cell, int T) { return min(cell / TS, T - 1); }
+
+// Tile key of plane q for point P of image b, and the entry record {s, local cell key, w, n}
+// (key = ly << 16 | lx << 8 | ox | oy << 1 inside the tile).
+__device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int R, int T, long long s, int4& rec) {
+  const int cell = P.pl[q].tex & 0xFFFFF;
+  const int y0 = cell / R, x0 = cell % R;
+  const int ty = tile_of(y0, T), tx = tile_of(x0, T);
+  rec = make_int4((int)s, ((y0 - ty * TS) << 16) | ((x0 - tx * TS) << 8) | (P.pl[q].tex >> 20),
+                  __float_as_int(P.pl[q].w), __float_as_int(P.pl[q].n));
+  return ((b * 3 + q) * T + ty) * T + tx;
+}
+
+__host__ __device__ __forceinline__ int tiles_per_side(int R) { return (R - 1 + TS - 1) / TS; }
+
+// Wave-aggregated atomicAdd of 1 per lane on base[key]; returns each lane's slot.
+__device__ __forceinline__ int agg_increment(int* base, int key, bool valid) {
+  const int l = lane_id();
+  unsigned long long active = __ballot(valid);
+  int pos = 0;
+  while (active) {
+    const int leader = __ffsll((long long)active) - 1;
+    const int k = __shfl(key, leader);
+    const unsigned long long m = __ballot(valid && key == k) & active;
+    int old = 0;
+    if (l == leader) old = atomicAdd(base + k, __popcll(m));
+    old = __shfl(old, leader);
+    if ((m >> l) & 1ull) pos = old + __popcll(m & ((1ull << l) - 1ull));
+    active &= ~m;
+  }
+  return pos;
 }
 
 __device__ __forceinline__ void load_row(const float* __restrict__ X, int row, float x[NC]) {
@@ -574,6 +623,23 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     }
   }
   excl_prod<NPL>(aa, T);
+  if (a.tile_counts) {
+    // per-tile sample counts for the backward's d-planes binning (same keys as bin_fill)
+    const int Tn = tiles_per_side(pv.R);
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      const int i = e * 64 + l;
+      PointP P;
+      point_params(R.o, R.d, t[e], a.field.scene_range, pv.R, P);
+      const bool v = i < N && P.mask == 0.f;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        int4 rec;
+        const int key = plane_tile_key(P, q, R.b, pv.R, Tn, r * N + i, rec);
+        agg_increment(a.tile_counts, key, v);
+      }
+    }
+  }
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, sm = 0.f, sd = 0.f;
 #pragma unroll
   for (int e = 0; e < NPL; ++e) {
@@ -616,6 +682,9 @@ struct BwdArgs {
   float* gsig;            // [rays][N] dL/d sigma per merged sample
   float* wts;             // [rays][N] compositing weight per merged sample
   int npl;                // chunks of 64 per ray
+  int* cursor;            // [K] tile fill cursors (NULL: bins filled by bin_fill_kernel)
+  int4* list;             // [3*rays*N] tile entries
+  int T;                  // tiles per plane side
 };
 
 // Compositing backward (nerf_utils.py:125-163 under autograd), one wave per ray:
@@ -790,6 +859,19 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
 #pragma unroll
     for (int k = 0; k < NC / 4; ++k) gr[k] = make_float4(gx[4 * k], gx[4 * k + 1], gx[4 * k + 2], gx[4 * k + 3]);
   }
+  if (g.cursor) {
+    // append this sample's three (plane, tile) entries to the d-planes bins
+    PointP P;
+    point_params(R.o, R.d, te, sr, pv.R, P);
+    const bool vb = v && P.mask == 0.f;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      int4 rec;
+      const int key = plane_tile_key(P, q, R.b, pv.R, g.T, r * N + i, rec);
+      const int pos = agg_increment(g.cursor, key, vb);
+      if (vb) g.list[pos] = rec;
+    }
+  }
   if (!dcoord) return;
   bool nz = false;
 #pragma unroll
@@ -859,21 +941,6 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// d planes by plane tile: every (sample, plane) contribution is binned by the 8x8-cell tile
-// of the plane its bilinear cell lies in; a workgroup sums a chunk of a tile's entries into
-// 9x9x32 LDS images — one private image per wave, updated by plain read-modify-write (LDS
-// executes a wave's instructions in order, so no atomics are needed; gfx950's ds_add_f32 costs
-// ~200 cycles per wave-instruction per CU against ~25 for the RMW, scripts/ubench/lds_atomic.hip)
-// with consecutive same-cell entries merged in registers first — then merges the four images
-// and flushes them with one float atomic per nonzero texel channel.  Global atomic traffic
-// drops from 1,536 B per sample to ~10 KB per (tile, chunk).
-// ---------------------------------------------------------------------------------------
-constexpr int TS = 8;             // cells per tile side
-constexpr int TT = TS + 1;        // texels per tile side
-constexpr int TILE_F = TT * TT * NC + NC;   // floats per wave image (+1 trash texel)
-constexpr int CHUNK = 2048;       // (sample, plane) entries per accumulation workgroup
-
 struct BinArgs {
   const float* ro;
   const float* rd;
@@ -885,8 +952,6 @@ struct BinArgs {
   int* cursor;           // [K]
   int4* list;            // [3 * nsamp] entries {sample, local cell key, w bits, n bits}
 };
-
-__device__ __forceinline__ int tile_of(int cell, int T) { return min(cell / TS, T - 1); }
 
 // Tile keys of sample s for the three planes, and each plane's entry record {s, local cell key,
 // w, n} (key = ly << 16 | lx << 8 | ox | oy << 1 inside the tile); false for samples outside
@@ -903,33 +968,8 @@ __device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int k
   PointP P;
   point_params(o, d, A.t[s], A.sr, A.R, P);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int cell = P.pl[q].tex & 0xFFFFF;
-    const int y0 = cell / A.R, x0 = cell % A.R;
-    const int ty = tile_of(y0, A.T), tx = tile_of(x0, A.T);
-    key[q] = ((b * 3 + q) * A.T + ty) * A.T + tx;
-    rec[q] = make_int4((int)s, ((y0 - ty * TS) << 16) | ((x0 - tx * TS) << 8) | (P.pl[q].tex >> 20),
-                       __float_as_int(P.pl[q].w), __float_as_int(P.pl[q].n));
-  }
+  for (int q = 0; q < 3; ++q) key[q] = plane_tile_key(P, q, b, A.R, A.T, s, rec[q]);
   return P.mask == 0.f;
-}
-
-// Wave-aggregated atomicAdd of 1 per lane on base[key]; returns each lane's slot.
-__device__ __forceinline__ int agg_increment(int* base, int key, bool valid) {
-  const int l = lane_id();
-  unsigned long long active = __ballot(valid);
-  int pos = 0;
-  while (active) {
-    const int leader = __ffsll((long long)active) - 1;
-    const int k = __shfl(key, leader);
-    const unsigned long long m = __ballot(valid && key == k) & active;
-    int old = 0;
-    if (l == leader) old = atomicAdd(base + k, __popcll(m));
-    old = __shfl(old, leader);
-    if ((m >> l) & 1ull) pos = old + __popcll(m & ((1ull << l) - 1ull));
-    active &= ~m;
-  }
-  return pos;
 }
 
 __global__ void __launch_bounds__(256) bin_count_kernel(BinArgs A) {
@@ -1016,6 +1056,7 @@ struct TileArgs {
   const int* chunk_tile;  // [total chunks]
   const int* meta;        // meta[0] = total chunks
   const int4* list;
+  int dbg;                // ablation switch (NFI_TILE_DEBUG): 1 no RMW, 2 no entry loop, 4 no flush
   float* dplanes;
   long long sb;
   int sq, st;
@@ -1077,6 +1118,7 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
       rec = A.list[min(nb + l, last - 1)];
       NFI_LOAD_ROW(rec)
       wave_lds_sync();
+      if (A.dbg & 2) { base = nb; continue; }
       for (int j = 0; j < n; ++j) {
         const int kj = readlane(key, j);
         const float w = readlane(pw, j), nn = readlane(pn, j);
@@ -1087,7 +1129,7 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
           a0 += c0;
           a1 += c1;
         } else {
-          if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
+          if (cur >= 0 && !(A.dbg & 1)) tile_rmw(img, cur, dxl, cl, a0, a1);
           cur = kj;
           a0 = c0;
           a1 = c1;
@@ -1104,9 +1146,12 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
       const float v = (acc[k] + acc[TILE_F + k]) + (acc[2 * TILE_F + k] + acc[3 * TILE_F + k]);
       const int texel = k / NC, ch = k % NC;
       const int gy = ty * TS + texel / TT, gx = tx * TS + texel % TT;
-      if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
+      if (v != 0.f && gy < A.R && gx < A.R && !(A.dbg & 4)) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
     }
     __syncthreads();
+  }
+  if (A.dbg) {   // keep the ablated values observable
+    if (threadIdx.x == 0 && blockIdx.x == 0) A.dplanes[0] += 0.f * acc[0];
   }
 }
 
@@ -1155,6 +1200,11 @@ static Workspace carve(const nfi_render_args* a, void* base) {
 template <int SPL, int NPL, bool FINE>
 static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
   const long long nrays = (long long)a->B * a->HW;
+  if (a->tile_counts) {
+    const int T = tiles_per_side(a->field.R);
+    NFI_REQUIRE(hipMemsetAsync(a->tile_counts, 0, (size_t)a->B * 3 * T * T * 4, s) == hipSuccess,
+                "render_forward: memset failed");
+  }
   render_fwd_kernel<SPL, NPL, FINE><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
   NFI_CHECK_LAUNCH("render_fwd_kernel");
   return NFI_OK;
@@ -1170,25 +1220,34 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   NFI_REQUIRE(w.bytes <= g->workspace_bytes, "render_backward: workspace too small (%lld < %lld)",
               (long long)g->workspace_bytes, w.bytes);
   NFI_REQUIRE(nsamp * 3 < (1LL << 31), "render_backward: too many samples per call (%lld)", nsamp);
-  // 1) bin (sample, plane) entries by plane tile from the saved depths
+  // 1) bin (sample, plane) entries by plane tile from the saved depths.  With the forward's
+  //    tile counts only the scan runs here and field_bwd fills the bins (its atomics hide
+  //    behind the MLP); otherwise count here and fill in bin_fill_kernel.
   const bool do_bins = stage < 0 || stage == 0, do_field = stage < 0 || stage == 1, do_tiles = stage < 0 || stage == 2;
+  const bool fwd_counts = g->tile_counts != nullptr;
+  const int* counts = fwd_counts ? g->tile_counts : w.counts;
   BinArgs B{a->ro, a->rd, a->t_saved, nsamp, N, a->HW, a->field.R, T, a->field.scene_range,
             w.counts, w.cursor, w.list};
+  const unsigned sb = (unsigned)((nsamp + 255) / 256);
   if (do_bins) {
-    NFI_REQUIRE(hipMemsetAsync(w.counts, 0, (size_t)K * 4, s) == hipSuccess, "render_backward: memset failed");
-    const unsigned sb = (unsigned)((nsamp + 255) / 256);
-    bin_count_kernel<<<sb, 256, 0, s>>>(B);
-    NFI_CHECK_LAUNCH("bin_count_kernel");
-    bin_scan_kernel<<<1, 1024, 0, s>>>(w.counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
+    if (!fwd_counts) {
+      NFI_REQUIRE(hipMemsetAsync(w.counts, 0, (size_t)K * 4, s) == hipSuccess, "render_backward: memset failed");
+      bin_count_kernel<<<sb, 256, 0, s>>>(B);
+      NFI_CHECK_LAUNCH("bin_count_kernel");
+    }
+    bin_scan_kernel<<<1, 1024, 0, s>>>(counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
     NFI_CHECK_LAUNCH("bin_scan_kernel");
-    chunk_map_kernel<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(w.counts, w.chunk_start, K, w.chunk_tile);
+    chunk_map_kernel<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(counts, w.chunk_start, K, w.chunk_tile);
     NFI_CHECK_LAUNCH("chunk_map_kernel");
-    bin_fill_kernel<<<sb, 256, 0, s>>>(B);
-    NFI_CHECK_LAUNCH("bin_fill_kernel");
+    if (!fwd_counts) {
+      bin_fill_kernel<<<sb, 256, 0, s>>>(B);
+      NFI_CHECK_LAUNCH("bin_fill_kernel");
+    }
   }
   // 2) per-ray compositing backward, then per-(ray, 64-sample chunk) field backward
   const int NPL = (N + 63) / 64;
-  BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat, w.gsig, w.wts, NPL};
+  BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat, w.gsig, w.wts, NPL,
+             fwd_counts ? w.cursor : nullptr, w.list, T};
   const unsigned rb = (unsigned)((nrays + 3) / 4);
   if (do_field) {
     if (NPL <= 1) composite_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
@@ -1199,9 +1258,10 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
   // 3) per-tile LDS accumulation of d planes
-  TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, w.counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list,
-              g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,
+  TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list,
+              0, g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,
               a->field.scene_range};
+  if (const char* dbg = getenv("NFI_TILE_DEBUG")) TA.dbg = atoi(dbg);
   if (do_tiles) {
     tile_accum_kernel<<<2048, 256, 0, s>>>(TA);
     NFI_CHECK_LAUNCH("tile_accum_kernel");
@@ -1255,6 +1315,12 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
   if (e) return e;
   NFI_REQUIRE(a->rgb && a->depth && a->mask, "render_forward: null output");
   return nfi::dispatch_fwd(a, (hipStream_t)stream);
+}
+
+int64_t nfi_tile_count_size(const nfi_render_args* a) {
+  if (nfi::validate(a)) return -1;
+  const int T = nfi::tiles_per_side(a->field.R);
+  return (int64_t)a->B * 3 * T * T;
 }
 
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 3
+ABI_VERSION = 4
 DEC_SIZE = 3088
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -41,14 +41,14 @@ class NfiRenderArgs(ctypes.Structure):
                 ('offset', ctypes.c_uint64), ('u_coarse', c_void_p), ('u_fine', c_void_p),
                 ('rgb', c_void_p), ('depth', c_void_p), ('mask', c_void_p),
                 ('t_saved', c_void_p), ('sigma_saved', c_void_p), ('rgb_saved', c_void_p),
-                ('y_saved', c_void_p), ('perm', c_void_p),
+                ('y_saved', c_void_p), ('perm', c_void_p), ('tile_counts', c_void_p),
                 ('z_coarse', c_void_p), ('z_fine', c_void_p)]
 
 
 class NfiRenderGradArgs(ctypes.Structure):
     _fields_ = [('g_rgb', c_void_p), ('g_mask', c_void_p), ('d_planes', c_void_p),
                 ('d_palette_ray', c_void_p), ('g_ro', c_void_p), ('g_rd', c_void_p),
-                ('workspace', c_void_p), ('workspace_bytes', ctypes.c_int64)]
+                ('tile_counts', c_void_p), ('workspace', c_void_p), ('workspace_bytes', ctypes.c_int64)]
 
 
 # symbol -> (restype, argtypes); every entry point of include/nfi.h
@@ -69,6 +69,7 @@ SIGNATURES = {
                                          c_void_p, c_void_p, c_void_p]),
     'nfi_render_forward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs), c_void_p]),
     'nfi_render_backward_workspace_bytes': (ctypes.c_int64, [ctypes.POINTER(NfiRenderArgs)]),
+    'nfi_tile_count_size': (ctypes.c_int64, [ctypes.POINTER(NfiRenderArgs)]),
     'nfi_render_backward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
                                              ctypes.POINTER(NfiRenderGradArgs), c_void_p]),
     'nfi_render_backward_stage': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),

@@ -32,6 +32,10 @@ def _stream(dev: torch.device):
 
 # Optional live kernel timing (bench.py): name -> list of (start, end) events recorded on the
 # stream the C-ABI call launches on.  Off by default (no events, no overhead).
+# The forward counts the backward's tile bins (nfi_render_args.tile_counts) when True; when
+# False the backward counts them itself (both paths are covered by tests/test_gpu_parity.py).
+FORWARD_TILE_COUNTS = True
+
 KERNEL_TIMERS: Optional[dict] = None
 
 
@@ -226,6 +230,12 @@ class _VolumeRender(torch.autograd.Function):
         args = _VolumeRender._args(planes_tm, dec, pal_c, ro_c, rd_c, near_c, far_c, opts, B, H * W,
                                    uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, y_saved, perm,
                                    zc, zf)
+        tile_counts = None
+        if FORWARD_TILE_COUNTS and ctx.needs_input_grad[0]:
+            # the forward counts the backward's d-planes tile bins while it has the samples
+            tile_counts = torch.empty((lib.nfi_tile_count_size(ctypes.byref(args)),), device=dev,
+                                      dtype=torch.int32)
+            args.tile_counts = _ptr(tile_counts)
         with _timed('render_fwd', dev):
             _lib.check(lib.nfi_render_forward(ctypes.byref(args), _stream(dev)), 'nfi_render_forward')
         if debug is not None:
@@ -235,7 +245,7 @@ class _VolumeRender(torch.autograd.Function):
             debug['sigma_sorted'] = s_saved
             debug['rgb_sorted'] = c_saved
         ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved,
-                              y_saved, perm)
+                              y_saved, perm, tile_counts)
         ctx.opts = opts
         ctx.shape = (B, H, W)
         ctx.mark_non_differentiable(depth)
@@ -261,7 +271,8 @@ class _VolumeRender(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_mask):
         lib = _lib.load()
-        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm = ctx.saved_tensors
+        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm, tile_counts = \
+            ctx.saved_tensors
         opts = ctx.opts
         B, H, W = ctx.shape
         dev = ro.device
@@ -282,7 +293,7 @@ class _VolumeRender(torch.autograd.Function):
         ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
         gargs = _lib.NfiRenderGradArgs(g_rgb=_ptr(g_rgb), g_mask=_ptr(g_mask), d_planes=_ptr(d_planes),
                                        d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd),
-                                       workspace=_ptr(ws), workspace_bytes=nbytes)
+                                       tile_counts=_ptr(tile_counts), workspace=_ptr(ws), workspace_bytes=nbytes)
         st = _stream(dev)
         for stage, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
             with _timed(name, dev):

@@ -92,3 +92,20 @@ def test_full_plane_resolution():
 def test_ortho_camera():
     inp, meta = synthetic_inputs(B=2, H=8, W=8, S=32, R=16, scene_range=2.0, seed=8, ortho=True)
     check(run_hip(inp, meta, DEV), run_oracle(inp, meta), run_oracle64(inp, meta))
+
+
+def test_backward_binning_paths_agree():
+    """d planes binned from the forward's tile counts == binned by the backward's own count pass
+    (nfi_render_grad_args.tile_counts NULL); only the summation order inside a tile differs."""
+    from nfi import ops
+    inp, meta = synthetic_inputs(B=2, H=16, W=16, S=64, R=64, scene_range=1.4, seed=21)
+    a = run_hip(inp, meta, DEV)
+    ops.FORWARD_TILE_COUNTS = False
+    try:
+        b = run_hip(inp, meta, DEV)
+    finally:
+        ops.FORWARD_TILE_COUNTS = True
+    for key in ('rgb', 'depth', 'mask', 'd_palette'):
+        assert torch.equal(a[key], b[key]), key
+    for key in ('d_planes', 'd_cam', 'd_focal'):   # float atomics: order differs run to run
+        assert rel_l2(a[key], b[key]) < 1e-5, key
