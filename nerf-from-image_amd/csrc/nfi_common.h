@@ -135,4 +135,30 @@ __device__ __forceinline__ float rng_uniform(unsigned long long seed, unsigned l
   return u01(philox4x32(c, k).x);
 }
 
+// ---------------------------------------------------------------------------------------
+// Phase timing for profiling builds (-DNFI_STAMPS, scripts/stamps.py): per-wave s_memtime
+// deltas summed into nfi_stamp_acc[slot][phase] (slots spread the atomics).  Compiled out of
+// the product library.
+// ---------------------------------------------------------------------------------------
+constexpr int STAMP_PHASES = 32, STAMP_SLOTS = 1024;
+#ifdef NFI_STAMPS
+extern __device__ unsigned long long nfi_stamp_acc[STAMP_SLOTS * STAMP_PHASES];
+#define NFI_STAMP_INIT unsigned long long nfi_st_ = __builtin_readcyclecounter();
+#define NFI_STAMP(id)                                                                        \
+  {                                                                                          \
+    const unsigned long long n_ = __builtin_readcyclecounter();                             \
+    if (lane_id() == 0)                                                                      \
+      atomicAdd(&nfi::nfi_stamp_acc[(blockIdx.x & (STAMP_SLOTS - 1)) * STAMP_PHASES + (id)], \
+                n_ - nfi_st_);                                                               \
+    nfi_st_ = n_;                                                                            \
+  }
+#define NFI_STAMP_PARAM , unsigned long long& nfi_st_
+#define NFI_STAMP_ARG , nfi_st_
+#else
+#define NFI_STAMP_INIT
+#define NFI_STAMP(id)
+#define NFI_STAMP_PARAM
+#define NFI_STAMP_ARG
+#endif
+
 }  // namespace nfi

@@ -15,11 +15,16 @@
 // wave-instruction shape, which is the full-rate shape of gfx950 float atomics.
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "nfi_common.h"
 #include "nfi_host.h"
 
 namespace nfi {
+
+#ifdef NFI_STAMPS
+__device__ unsigned long long nfi_stamp_acc[STAMP_SLOTS * STAMP_PHASES];
+#endif
 
 constexpr int XS = 36;                  // LDS row stride (floats) of the point x channel tile
 constexpr int XTILE = WAVE * XS;        // 2304 floats
@@ -133,10 +138,10 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
     }
     if (dx == 0 && j < npts) {
       float4 f;
-      f.x = ((E[0].x + E[1].x) + E[2].x) / 3.f;
-      f.y = ((E[0].y + E[1].y) + E[2].y) / 3.f;
-      f.z = ((E[0].z + E[1].z) + E[2].z) / 3.f;
-      f.w = ((E[0].w + E[1].w) + E[2].w) / 3.f;
+      f.x = ((E[0].x + E[1].x) + E[2].x) * (1.f / 3.f);
+      f.y = ((E[0].y + E[1].y) + E[2].y) * (1.f / 3.f);
+      f.z = ((E[0].z + E[1].z) + E[2].z) * (1.f / 3.f);
+      f.w = ((E[0].w + E[1].w) + E[2].w) * (1.f / 3.f);
       *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
     }
   }
@@ -172,22 +177,38 @@ __device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int
 
 __host__ __device__ __forceinline__ int tiles_per_side(int R) { return (R - 1 + TS - 1) / TS; }
 
-// Wave-aggregated atomicAdd of 1 per lane on base[key]; returns each lane's slot.
-__device__ __forceinline__ int agg_increment(int* base, int key, bool valid) {
+// Run-aggregated atomicAdd of 1 per valid lane on base[key]: each run of equal keys in
+// consecutive lanes (samples along a ray are depth-sorted, so a ray meets each tile in one run)
+// takes its slots with ONE atomic by the run's first lane, all runs in one wave instruction —
+// one memory round trip per call whatever the key pattern (a key split over several runs gets
+// one contiguous slot range per run).  Returns each lane's slot.
+struct LaneRuns {
+  int leader;   // first lane of this lane's run
+  int len;      // run length (meaningful in leader lanes)
+  bool start;
+};
+__device__ __forceinline__ LaneRuns lane_runs(int key, bool valid) {
   const int l = lane_id();
-  unsigned long long active = __ballot(valid);
-  int pos = 0;
-  while (active) {
-    const int leader = __ffsll((long long)active) - 1;
-    const int k = __shfl(key, leader);
-    const unsigned long long m = __ballot(valid && key == k) & active;
-    int old = 0;
-    if (l == leader) old = atomicAdd(base + k, __popcll(m));
-    old = __shfl(old, leader);
-    if ((m >> l) & 1ull) pos = old + __popcll(m & ((1ull << l) - 1ull));
-    active &= ~m;
-  }
-  return pos;
+  const int kk = valid ? key : -1;
+  const int prev = __shfl_up(kk, 1);
+  LaneRuns R;
+  R.start = (l == 0) || kk != prev;
+  const unsigned long long starts = __ballot(R.start);
+  const unsigned long long upto = (l == 63) ? ~0ull : ((2ull << l) - 1ull);   // lanes <= l
+  R.leader = 63 - __clzll(starts & upto);
+  const unsigned long long after = starts & ~upto;
+  R.len = (after ? (__ffsll((long long)after) - 1) : 64) - l;
+  return R;
+}
+__device__ __forceinline__ int run_increment(int* base, int key, bool valid) {
+  const LaneRuns R = lane_runs(key, valid);
+  int old = 0;
+  if (R.start && valid) old = atomicAdd(base + key, R.len);
+  return __shfl(old, R.leader) + (lane_id() - R.leader);
+}
+__device__ __forceinline__ void run_count(int* base, int key, bool valid) {
+  const LaneRuns R = lane_runs(key, valid);
+  if (R.start && valid) atomicAdd(base + key, R.len);
 }
 
 __device__ __forceinline__ void load_row(const float* __restrict__ X, int row, float x[NC]) {
@@ -209,69 +230,106 @@ __device__ __forceinline__ void store_row(float* __restrict__ X, int row, const 
 }
 
 // Softplus(beta=1, threshold=20) (generator.py:297) and its derivative (ATen softplus_backward).
+// The correction factor u/(u+1-1) of the accurate log1p and u/(u+1) use the hardware
+// reciprocal (<= 2 ulp) instead of the IEEE division sequence.
 __device__ __forceinline__ float softplus(float z) {
   const float u = __expf(z);
   const float up = 1.f + u;
   const float dd = up - 1.f;
-  const float l1p = (dd == 0.f) ? u : __logf(up) * (u / dd);   // accurate log1p(u)
+  // accurate log1p(u) = log(1+u) * u / ((1+u) - 1), on v_log_f32 / v_rcp_f32 (up >= 1: no denormals)
+  const float lg = __builtin_amdgcn_logf(up) * 0.69314718f;
+  const float l1p = (dd == 0.f) ? u : lg * (u * __builtin_amdgcn_rcpf(dd));
   return (z > 20.f) ? z : l1p;
 }
 __device__ __forceinline__ float softplus_grad(float z) {
   const float u = __expf(z);
-  return (z > 20.f) ? 1.f : u / (u + 1.f);
+  return (z > 20.f) ? 1.f : u * __builtin_amdgcn_rcpf(u + 1.f);
 }
 
 // The packed decoder is read through the constant address space (AS 4): wave-uniform,
 // read-only loads there become s_load into SGPRs even after global stores in the kernel
 // (a plain global pointer would fall back to vector loads into VGPRs once a store may alias).
+// The decoder runs on packed fp32 FMAs (v_pk_fma_f32, two lanes of work per instruction with
+// an SGPR-pair weight operand: the f32 VALU peak, 2x the scalar v_fma_f32 rate).
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(4))) float* cfloat_p;
+typedef const __attribute__((address_space(4))) f2* cf2_p;
 __device__ __forceinline__ cfloat_p as_const(const float* p) { return (cfloat_p)(p); }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
 
-__device__ __forceinline__ float dot32(const float x[NC], cfloat_p w) {
-  float z0 = 0.f, z1 = 0.f, z2 = 0.f, z3 = 0.f;
+// W1 row o . x  (x as 16 channel pairs)
+__device__ __forceinline__ float dot32(const f2 x[NC / 2], cf2_p w) {
+  f2 z0 = splat(0.f), z1 = splat(0.f);
 #pragma unroll
-  for (int c = 0; c < NC; c += 4) {
-    z0 = fmaf(x[c + 0], w[c + 0], z0);
-    z1 = fmaf(x[c + 1], w[c + 1], z1);
-    z2 = fmaf(x[c + 2], w[c + 2], z2);
-    z3 = fmaf(x[c + 3], w[c + 3], z3);
+  for (int c = 0; c < NC / 2; c += 2) {
+    z0 = pfma(x[c], w[c], z0);
+    z1 = pfma(x[c + 1], w[c + 1], z1);
   }
-  return (z0 + z1) + (z2 + z3);
+  const f2 z = z0 + z1;
+  return z.x + z.y;
+}
+
+__device__ __forceinline__ void pack_x(const float x[NC], f2 xv[NC / 2]) {
+#pragma unroll
+  for (int c = 0; c < NC / 2; ++c) xv[c] = f2{x[2 * c], x[2 * c + 1]};
 }
 
 // TriplanarDecoder.net (generator.py:295-299): y = W2s softplus(W1s x + b1) + b2.
+// Unit o of the packed decoder: u[0..31] = W1s row, u[32..42] = W2s column, u[43] = b1s.
 __device__ __forceinline__ void mlp_forward(const float* __restrict__ dec_, const float x[NC], float y[NO]) {
   const cfloat_p dec = as_const(dec_);
-  float acc[NO];
+  f2 xv[NC / 2];
+  pack_x(x, xv);
+  f2 acc[NO / 2];
 #pragma unroll
-  for (int k = 0; k < NO; ++k) acc[k] = 0.f;
+  for (int k = 0; k < NO / 2; ++k) acc[k] = splat(0.f);
+  float acc10 = 0.f;
 #pragma unroll 1
   for (int o = 0; o < NH; ++o) {
     const cfloat_p u = dec + o * DEC_UNIT;
-    const float h = softplus(dot32(x, u) + u[DEC_B1]);
+    const cf2_p u2 = (cf2_p)u;
+    const float h = softplus(dot32(xv, u2) + u[DEC_B1]);
+    const f2 hh = splat(h);
 #pragma unroll
-    for (int k = 0; k < NO; ++k) acc[k] = fmaf(h, u[DEC_W2T + k], acc[k]);
+    for (int k = 0; k < NO / 2; ++k) acc[k] = pfma(hh, u2[DEC_W2T / 2 + k], acc[k]);
+    acc10 = fmaf(h, u[DEC_W2T + NO - 1], acc10);
   }
 #pragma unroll
-  for (int k = 0; k < NO; ++k) y[k] = acc[k] + dec[DEC_B2 + k];
+  for (int k = 0; k < NO / 2; ++k) {
+    y[2 * k] = acc[k].x + dec[DEC_B2 + 2 * k];
+    y[2 * k + 1] = acc[k].y + dec[DEC_B2 + 2 * k + 1];
+  }
+  y[NO - 1] = acc10 + dec[DEC_B2 + NO - 1];
 }
 
 // Input-gradient of the decoder (its weights are frozen during inversion, run.py:630-632).
 __device__ __forceinline__ void mlp_backward(const float* __restrict__ dec_, const float x[NC],
                                              const float gy[NO], float gx[NC]) {
   const cfloat_p dec = as_const(dec_);
+  f2 xv[NC / 2], g2[NC / 2], gyv[NO / 2];
+  pack_x(x, xv);
 #pragma unroll
-  for (int c = 0; c < NC; ++c) gx[c] = 0.f;
+  for (int c = 0; c < NC / 2; ++c) g2[c] = splat(0.f);
+#pragma unroll
+  for (int k = 0; k < NO / 2; ++k) gyv[k] = f2{gy[2 * k], gy[2 * k + 1]};
 #pragma unroll 1
   for (int o = 0; o < NH; ++o) {
     const cfloat_p u = dec + o * DEC_UNIT;
-    const float z = dot32(x, u) + u[DEC_B1];
-    float gh = 0.f;
+    const cf2_p u2 = (cf2_p)u;
+    const float z = dot32(xv, u2) + u[DEC_B1];
+    f2 gh2 = splat(0.f);
 #pragma unroll
-    for (int k = 0; k < NO; ++k) gh = fmaf(gy[k], u[DEC_W2T + k], gh);
-    const float gz = gh * softplus_grad(z);
+    for (int k = 0; k < NO / 2; ++k) gh2 = pfma(gyv[k], u2[DEC_W2T / 2 + k], gh2);
+    const float gh = fmaf(gy[NO - 1], u[DEC_W2T + NO - 1], gh2.x + gh2.y);
+    const f2 gz = splat(gh * softplus_grad(z));
 #pragma unroll
-    for (int c = 0; c < NC; ++c) gx[c] = fmaf(gz, u[c], gx[c]);
+    for (int c = 0; c < NC / 2; ++c) g2[c] = pfma(gz, u2[c], g2[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < NC / 2; ++c) {
+    gx[2 * c] = g2[c].x;
+    gx[2 * c + 1] = g2[c].y;
   }
 }
 
@@ -298,8 +356,9 @@ __device__ __forceinline__ void head_forward(const float y[NO], float mask, floa
     h.p[k] = __expf(y[1 + k] - m);
     sum += h.p[k];
   }
+  const float rs = 1.f / sum;
 #pragma unroll
-  for (int k = 0; k < NA; ++k) h.p[k] = h.p[k] / sum;
+  for (int k = 0; k < NA; ++k) h.p[k] = h.p[k] * rs;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     float a = 0.f;
@@ -376,15 +435,17 @@ __device__ __forceinline__ void load_ray(const nfi_render_args& a, long long r, 
 // Evaluate the field at the (up to 64) points t (one per lane; lanes >= npts ignored).
 __device__ __forceinline__ void field_eval(const nfi_render_args& a, const PlaneView& pv, const RayCtx& R,
                                            float t, int npts, float* __restrict__ X, float& sigma,
-                                           float rgb[3], int eval_base) {
+                                           float rgb[3], int eval_base NFI_STAMP_PARAM) {
   PointP P;
   point_params(R.o, R.d, t, a.field.scene_range, pv.R, P);
   gather_features(pv, P, npts, X);
   wave_lds_sync();
+  NFI_STAMP(1)
   float x[NC];
   load_row(X, lane_id(), x);
   float y[NO];
   mlp_forward(a.field.dec, x, y);
+  NFI_STAMP(2)
   if (lane_id() < npts) {
     const int N = a.fine ? 2 * a.S : a.S;
     float* ys = a.y_saved + R.r * NO * N + eval_base + lane_id();
@@ -398,6 +459,7 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   rgb[1] = h.rgb[1];
   rgb[2] = h.rgb[2];
   wave_lds_sync();
+  NFI_STAMP(3)
 }
 
 // alpha_i = 1 - exp(-sigma_i * dist_i),  a_i = 1 - alpha_i + 1e-10  (nerf_utils.py:136-146)
@@ -419,6 +481,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   const long long nrays = (long long)a.B * a.HW;
   const long long r = (long long)blockIdx.x * 4 + wv;
   if (r >= nrays) return;
+  NFI_STAMP_INIT
   const int S = a.S;
   const int N = FINE ? 2 * S : S;
   float* X = lds + wv * WL;
@@ -432,6 +495,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   load_ray(a, r, R);
   const PlaneView pv{a.field.planes + (long long)R.b * a.field.sb, (int)a.field.sq, (int)a.field.st,
                      a.field.R};
+  NFI_STAMP(0)
 
   // ---- stratified coarse depths (nerf_utils.py:104-120) ----
   float tc[SPL], sc[SPL], cc[SPL][3];
@@ -451,7 +515,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     tc[e] = t;
     sc[e] = 0.f;
     cc[e][0] = cc[e][1] = cc[e][2] = 0.f;
-    if (e * 64 < S) field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64);
+    if (e * 64 < S) field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64 NFI_STAMP_ARG);
   }
 
   if constexpr (FINE) {
@@ -542,13 +606,14 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       if (i < S && a.z_fine) a.z_fine[r * S + i] = tf[e];
     }
     wave_lds_sync();
+    NFI_STAMP(4)
     // ---- fine field evaluation (run.py:283-291) ----
     float sf[SPL], cf[SPL][3];
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
       sf[e] = 0.f;
       cf[e][0] = cf[e][1] = cf[e][2] = 0.f;
-      if (e * 64 < S) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64);
+      if (e * 64 < S) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64 NFI_STAMP_ARG);
     }
     // ---- merge: stable sort of cat(z_coarse, z_fine) (run.py:283-288, 312-319) ----
 #pragma unroll
@@ -598,6 +663,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     }
   }
   wave_lds_sync();
+  NFI_STAMP(5)
 
   // ---- compositing (nerf_utils.py:125-163) ----
   float t[NPL], al[NPL], aa[NPL], T[NPL];
@@ -623,6 +689,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     }
   }
   excl_prod<NPL>(aa, T);
+  NFI_STAMP(6)
   if (a.tile_counts) {
     // per-tile sample counts for the backward's d-planes binning (same keys as bin_fill)
     const int Tn = tiles_per_side(pv.R);
@@ -636,10 +703,11 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       for (int q = 0; q < 3; ++q) {
         int4 rec;
         const int key = plane_tile_key(P, q, R.b, pv.R, Tn, r * N + i, rec);
-        agg_increment(a.tile_counts, key, v);
+        run_count(a.tile_counts, key, v);
       }
     }
   }
+  NFI_STAMP(7)
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, sm = 0.f, sd = 0.f;
 #pragma unroll
   for (int e = 0; e < NPL; ++e) {
@@ -666,6 +734,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
     a.mask[r] = sm;
     a.depth[r] = sd;
   }
+  NFI_STAMP(8)
 }
 
 // ---------------------------------------------------------------------------------------
@@ -772,7 +841,6 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
-  const int dxl = l >> 5, cl = l & 31;
   const long long nrays = (long long)a.B * a.HW;
   const long long job = (long long)blockIdx.x * 4 + wv;
   const long long r = job / g.npl;
@@ -780,6 +848,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   if (r >= nrays) return;
   const int N = a.fine ? 2 * a.S : a.S;
   if (e * 64 >= N) return;
+  NFI_STAMP_INIT
   float* X = lds + wv * XTILE;
   const bool dcoord = g.g_ro != nullptr;
   const float sr = a.field.scene_range;
@@ -789,6 +858,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
                      a.field.R};
   const float* pal = a.field.palette + R.b * (NA * 3);
   const float gr0 = g.g_rgb[r * 3 + 0], gr1 = g.g_rgb[r * 3 + 1], gr2 = g.g_rgb[r * 3 + 2];
+  NFI_STAMP(16)
 
   const int npts = min(64, N - e * 64);
   const int i = e * 64 + l;
@@ -802,6 +872,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     pmask = P.mask;
   }
   wave_lds_sync();
+  NFI_STAMP(17)
   float x[NC];
   load_row(X, l, x);
   // decoder outputs saved by the forward (no forward MLP here)
@@ -850,15 +921,18 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     for (int j = 0; j < npts; ++j) s += X[j * XS + l];
     g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = s;
   }
+  NFI_STAMP(18)
   float gx[NC];
   mlp_backward(a.field.dec, x, gy, gx);
+  NFI_STAMP(19)
 #pragma unroll
-  for (int c = 0; c < NC; ++c) gx[c] = gx[c] / 3.f;   // x = (e1+e2+e3)/3
+  for (int c = 0; c < NC; ++c) gx[c] = gx[c] * (1.f / 3.f);   // x = (e1+e2+e3)/3
   if (v) {
     float4* gr = reinterpret_cast<float4*>(g.gfeat + (r * N + i) * NC);
 #pragma unroll
     for (int k = 0; k < NC / 4; ++k) gr[k] = make_float4(gx[4 * k], gx[4 * k + 1], gx[4 * k + 2], gx[4 * k + 3]);
   }
+  NFI_STAMP(20)
   if (g.cursor) {
     // append this sample's three (plane, tile) entries to the d-planes bins
     PointP P;
@@ -868,10 +942,11 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     for (int q = 0; q < 3; ++q) {
       int4 rec;
       const int key = plane_tile_key(P, q, R.b, pv.R, g.T, r * N + i, rec);
-      const int pos = agg_increment(g.cursor, key, vb);
+      const int pos = run_increment(g.cursor, key, vb);
       if (vb) g.list[pos] = rec;
     }
   }
+  NFI_STAMP(21)
   if (!dcoord) return;
   bool nz = false;
 #pragma unroll
@@ -929,6 +1004,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
       ard2 = fmaf(d2, tj, ard2);
     }
   }
+  NFI_STAMP(22)
   const float gro0 = wave_sum(aro0) / sr, gro1 = wave_sum(aro1) / sr, gro2 = wave_sum(aro2) / sr;
   const float grd0 = wave_sum(ard0) / sr, grd1 = wave_sum(ard1) / sr, grd2 = wave_sum(ard2) / sr;
   if (l == 0) {
@@ -939,6 +1015,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     unsafeAtomicAdd(g.g_rd + r * 3 + 1, grd1);
     unsafeAtomicAdd(g.g_rd + r * 3 + 2, grd2);
   }
+  NFI_STAMP(23)
 }
 
 struct BinArgs {
@@ -979,7 +1056,7 @@ __global__ void __launch_bounds__(256) bin_count_kernel(BinArgs A) {
   bool v = s < A.nsamp;
   if (v) v = sample_keys(A, s, key, rec);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) agg_increment(A.counts, key[q], v);
+  for (int q = 0; q < 3; ++q) run_count(A.counts, key[q], v);
 }
 
 __global__ void __launch_bounds__(256) bin_fill_kernel(BinArgs A) {
@@ -990,7 +1067,7 @@ __global__ void __launch_bounds__(256) bin_fill_kernel(BinArgs A) {
   if (v) v = sample_keys(A, s, key, rec);
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const int pos = agg_increment(A.cursor, key[q], v);
+    const int pos = run_increment(A.cursor, key[q], v);
     if (v) A.list[pos] = rec[q];
   }
 }
@@ -1349,3 +1426,22 @@ int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_gra
 }
 
 }  // extern "C"
+
+// Profiling builds only (-DNFI_STAMPS): per-phase cycle sums, summed over slots, then reset.
+extern "C" int32_t nfi_debug_stamps(uint64_t* out) {
+#ifdef NFI_STAMPS
+  static unsigned long long h[nfi::STAMP_SLOTS * nfi::STAMP_PHASES];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(nfi::nfi_stamp_acc), sizeof(h)) != hipSuccess) return NFI_ELAUNCH;
+  for (int p = 0; p < nfi::STAMP_PHASES; ++p) {
+    unsigned long long t = 0;
+    for (int k = 0; k < nfi::STAMP_SLOTS; ++k) t += h[k * nfi::STAMP_PHASES + p];
+    out[p] = t;
+  }
+  memset(h, 0, sizeof(h));
+  if (hipMemcpyToSymbol(HIP_SYMBOL(nfi::nfi_stamp_acc), h, sizeof(h)) != hipSuccess) return NFI_ELAUNCH;
+  return NFI_OK;
+#else
+  (void)out;
+  return NFI_EINVAL;
+#endif
+}

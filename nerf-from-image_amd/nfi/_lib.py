@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libnfi_hip.so')
+LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
 ABI_VERSION = 4
 DEC_SIZE = 3088
 

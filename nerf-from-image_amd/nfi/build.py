@@ -24,17 +24,21 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
-        return OUT
+def build(force: bool = False, verbose: bool = True, variant: str = '') -> str:
+    """variant 'stamps': profiling library libnfi_hip_stamps.so with per-phase cycle counters
+    (-DNFI_STAMPS, loaded via NFI_LIBRARY by scripts/stamps.py); never the product build."""
+    out = OUT if not variant else OUT.replace('.so', f'_{variant}.so')
+    if not force and not variant and not _stale():
+        return out
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-    cmd = [hipcc] + FLAGS + ['-o', OUT + '.tmp'] + [os.path.join(CSRC, s) for s in SOURCES]
+    extra = {'': [], 'stamps': ['-DNFI_STAMPS']}[variant]
+    cmd = [hipcc] + FLAGS + extra + ['-o', out + '.tmp'] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + '.tmp', OUT)
-    return OUT
+    os.replace(out + '.tmp', out)
+    return out
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv)
+    build(force='--force' in sys.argv, variant='stamps' if '--stamps' in sys.argv else '')
