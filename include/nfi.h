@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 4
+#define NFI_ABI_VERSION 5
 #define NFI_DEC_SIZE 3088 /* floats in the packed decoder buffer */
 
 enum {
@@ -95,6 +95,8 @@ typedef struct nfi_render_args {
   float* y_saved;      /* [B*HW,11,N] decoder outputs (distance, 10 logits) in evaluation order:
                           coarse 0..S-1 then fine S..2S-1 (lets the backward skip the forward MLP) */
   int16_t* perm;       /* [B*HW,N] merged sample k -> evaluation index */
+  float* x_saved;      /* [B*HW*N,32] decoder inputs (mean tap features) in evaluation order; optional
+                          in the forward (NULL: not written), required by the backward */
   int32_t* tile_counts; /* optional [nfi_tile_count_size()] per-plane-tile sample counts for the
                            backward's d-planes binning (zeroed and filled by the forward); NULL = skip */
   float* z_coarse;     /* optional [B*HW,S] debug: coarse depths */

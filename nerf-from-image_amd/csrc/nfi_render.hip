@@ -108,41 +108,58 @@ __device__ __forceinline__ float4 ror8_add(float4 v) {
   return v;
 }
 
+// Loads of GB groups (4*GB points) are issued before any is consumed: the gather is bound by
+// load latency (texels mostly come from MALL/HBM), so the wave keeps 6*GB KiB in flight.
+constexpr int GATHER_GB = 2;
+
 __device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
                                                 float* __restrict__ X) {
   const int l = lane_id();
   const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
   const int ngrp = (npts + 3) >> 2;
-#pragma unroll 2
-  for (int gi = 0; gi < ngrp; ++gi) {
-    const int j = 4 * gi + sub;
-    float4 E[3];
+#pragma unroll 1
+  for (int gb = 0; gb < ngrp; gb += GATHER_GB) {
+    float4 V0[GATHER_GB][3], V1[GATHER_GB][3];
+    float W0[GATHER_GB][3], W1[GATHER_GB][3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int pk = __shfl(P.pl[q].tex, j);
-      const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
-      const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
-      const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
-      const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-      const float* b = pv.base + q * pv.sq + 4 * q4;
-      const float4 v0 = *reinterpret_cast<const float4*>(b + t0 * pv.st);
-      const float4 v1 = *reinterpret_cast<const float4*>(b + t1 * pv.st);
-      const float wx = dx ? w : e;
-      const float w0 = s * wx, w1 = n * wx;
-      float4 pr;
-      pr.x = v0.x * w0 + v1.x * w1;
-      pr.y = v0.y * w0 + v1.y * w1;
-      pr.z = v0.z * w0 + v1.z * w1;
-      pr.w = v0.w * w0 + v1.w * w1;
-      E[q] = ror8_add(pr);
+    for (int u = 0; u < GATHER_GB; ++u) {
+      const int j = min(4 * (gb + u) + sub, WAVE - 1);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int pk = __shfl(P.pl[q].tex, j);
+        const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
+        const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
+        const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
+        const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
+        const float* b = pv.base + q * pv.sq + 4 * q4;
+        V0[u][q] = *reinterpret_cast<const float4*>(b + t0 * pv.st);
+        V1[u][q] = *reinterpret_cast<const float4*>(b + t1 * pv.st);
+        const float wx = dx ? w : e;
+        W0[u][q] = s * wx;
+        W1[u][q] = n * wx;
+      }
     }
-    if (dx == 0 && j < npts) {
-      float4 f;
-      f.x = ((E[0].x + E[1].x) + E[2].x) * (1.f / 3.f);
-      f.y = ((E[0].y + E[1].y) + E[2].y) * (1.f / 3.f);
-      f.z = ((E[0].z + E[1].z) + E[2].z) * (1.f / 3.f);
-      f.w = ((E[0].w + E[1].w) + E[2].w) * (1.f / 3.f);
-      *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u) {
+      const int j = 4 * (gb + u) + sub;
+      float4 E[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        float4 pr;
+        pr.x = V0[u][q].x * W0[u][q] + V1[u][q].x * W1[u][q];
+        pr.y = V0[u][q].y * W0[u][q] + V1[u][q].y * W1[u][q];
+        pr.z = V0[u][q].z * W0[u][q] + V1[u][q].z * W1[u][q];
+        pr.w = V0[u][q].w * W0[u][q] + V1[u][q].w * W1[u][q];
+        E[q] = ror8_add(pr);
+      }
+      if (dx == 0 && j < npts) {
+        float4 f;
+        f.x = ((E[0].x + E[1].x) + E[2].x) * (1.f / 3.f);
+        f.y = ((E[0].y + E[1].y) + E[2].y) * (1.f / 3.f);
+        f.z = ((E[0].z + E[1].z) + E[2].z) * (1.f / 3.f);
+        f.w = ((E[0].w + E[1].w) + E[2].w) * (1.f / 3.f);
+        *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
+      }
     }
   }
 }
@@ -440,6 +457,16 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   point_params(R.o, R.d, t, a.field.scene_range, pv.R, P);
   gather_features(pv, P, npts, X);
   wave_lds_sync();
+  if (a.x_saved) {
+    // decoder inputs for the backward: rows eval_base.. of this ray, one coalesced KiB per store
+    const int N = a.fine ? 2 * a.S : a.S;
+    float4* xs = reinterpret_cast<float4*>(a.x_saved + (R.r * N + eval_base) * NC);
+#pragma unroll
+    for (int k = 0; k < NC / 4; ++k) {
+      const int q = k * 64 + lane_id();
+      if (q < npts * (NC / 4)) xs[q] = *reinterpret_cast<const float4*>(X + (q >> 3) * XS + 4 * (q & 7));
+    }
+  }
   NFI_STAMP(1)
   float x[NC];
   load_row(X, lane_id(), x);
@@ -864,21 +891,30 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   const int i = e * 64 + l;
   const bool v = i < N;
   const float te = v ? a.t_saved[r * N + i] : R.near_;
+  const int ei = v ? (int)a.perm[r * N + i] : 0;
   float pmask;
   {
     PointP P;
     point_params(R.o, R.d, te, sr, pv.R, P);
-    gather_features(pv, P, npts, X);
     pmask = P.mask;
   }
-  wave_lds_sync();
-  NFI_STAMP(17)
+  // decoder inputs saved by the forward (no re-gather here)
   float x[NC];
-  load_row(X, l, x);
+  {
+    const float4* xr = reinterpret_cast<const float4*>(a.x_saved + (r * N + ei) * NC);
+#pragma unroll
+    for (int k = 0; k < NC / 4; ++k) {
+      const float4 q = v ? xr[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[4 * k] = q.x;
+      x[4 * k + 1] = q.y;
+      x[4 * k + 2] = q.z;
+      x[4 * k + 3] = q.w;
+    }
+  }
+  NFI_STAMP(17)
   // decoder outputs saved by the forward (no forward MLP here)
   float y[NO];
   {
-    const int ei = v ? (int)a.perm[r * N + i] : 0;
     const float* ys = a.y_saved + r * NO * N + ei;
 #pragma unroll
     for (int k = 0; k < NO; ++k) y[k] = v ? ys[k * N] : 0.f;
@@ -966,42 +1002,55 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     point_params(R.o, R.d, te, sr, pv.R, P);
     const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
     const int ngrp = (npts + 3) >> 2;
+    constexpr int GB = GATHER_GB;
 #pragma unroll 1
-    for (int gi = 0; gi < ngrp; ++gi) {
-      if (((live >> (4 * gi)) & 0xFull) == 0ull) continue;
-      const int j = 4 * gi + sub;
-      const bool lj = (live >> j) & 1ull;
-      const float tj = __shfl(te, j);
-      const float4 gv = *reinterpret_cast<const float4*>(X + j * XS + 4 * q4);
-      float GX[3], GY[3];
+    for (int gb = 0; gb < ngrp; gb += GB) {
+      if (((live >> (4 * gb)) & ((1ull << (4 * GB)) - 1ull)) == 0ull) continue;
+      float4 V0[GB][3], V1[GB][3];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int pk = __shfl(P.pl[q].tex, j);
-        const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
-        const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
-        const float gxm = __shfl(P.pl[q].gxm, j), gym = __shfl(P.pl[q].gym, j);
-        const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
-        const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-        const float* b = pv.base + q * pv.sq + 4 * q4;
-        const float4 v0 = *reinterpret_cast<const float4*>(b + t0 * pv.st);
-        const float4 v1 = *reinterpret_cast<const float4*>(b + t1 * pv.st);
-        const float wx = dx ? w : e;
-        // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
-        const float ax = (s * v0.x + n * v1.x) * gv.x + (s * v0.y + n * v1.y) * gv.y +
-                         (s * v0.z + n * v1.z) * gv.z + (s * v0.w + n * v1.w) * gv.w;
-        const float ay = (v1.x - v0.x) * gv.x + (v1.y - v0.y) * gv.y + (v1.z - v0.z) * gv.z +
-                         (v1.w - v0.w) * gv.w;
-        GX[q] = lj ? (dx ? ax : -ax) * gxm : 0.f;
-        GY[q] = lj ? wx * ay * gym : 0.f;
+      for (int u = 0; u < GB; ++u) {
+        const int j = min(4 * (gb + u) + sub, WAVE - 1);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int pk = __shfl(P.pl[q].tex, j);
+          const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
+          const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
+          const float* b = pv.base + q * pv.sq + 4 * q4;
+          V0[u][q] = *reinterpret_cast<const float4*>(b + t0 * pv.st);
+          V1[u][q] = *reinterpret_cast<const float4*>(b + t1 * pv.st);
+        }
       }
-      // coords (x, y, z) of planes xy, xz, yz
-      const float d0 = GX[0] + GX[1], d1 = GY[0] + GX[2], d2 = GY[1] + GY[2];
-      aro0 += d0;
-      aro1 += d1;
-      aro2 += d2;
-      ard0 = fmaf(d0, tj, ard0);
-      ard1 = fmaf(d1, tj, ard1);
-      ard2 = fmaf(d2, tj, ard2);
+#pragma unroll
+      for (int u = 0; u < GB; ++u) {
+        const int jr = 4 * (gb + u) + sub, j = min(jr, WAVE - 1);
+        const bool lj = jr < WAVE && ((live >> j) & 1ull);
+        const float tj = __shfl(te, j);
+        const float4 gv = *reinterpret_cast<const float4*>(X + j * XS + 4 * q4);
+        float GX[3], GY[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
+          const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
+          const float gxm = __shfl(P.pl[q].gxm, j), gym = __shfl(P.pl[q].gym, j);
+          const float4 v0 = V0[u][q], v1 = V1[u][q];
+          const float wx = dx ? w : e;
+          // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
+          const float ax = (s * v0.x + n * v1.x) * gv.x + (s * v0.y + n * v1.y) * gv.y +
+                           (s * v0.z + n * v1.z) * gv.z + (s * v0.w + n * v1.w) * gv.w;
+          const float ay = (v1.x - v0.x) * gv.x + (v1.y - v0.y) * gv.y + (v1.z - v0.z) * gv.z +
+                           (v1.w - v0.w) * gv.w;
+          GX[q] = lj ? (dx ? ax : -ax) * gxm : 0.f;
+          GY[q] = lj ? wx * ay * gym : 0.f;
+        }
+        // coords (x, y, z) of planes xy, xz, yz
+        const float d0 = GX[0] + GX[1], d1 = GY[0] + GX[2], d2 = GY[1] + GY[2];
+        aro0 += d0;
+        aro1 += d1;
+        aro2 += d2;
+        ard0 = fmaf(d0, tj, ard0);
+        ard1 = fmaf(d1, tj, ard1);
+        ard2 = fmaf(d2, tj, ard2);
+      }
     }
   }
   NFI_STAMP(22)
@@ -1410,6 +1459,7 @@ int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args
   if (e) return e;
   NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
               "render_backward: null grad pointer");
+  NFI_REQUIRE(a->x_saved, "render_backward: x_saved (decoder inputs saved by the forward) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
   return nfi::launch_bwd(a, g, (hipStream_t)stream, -1);
 }
@@ -1420,6 +1470,7 @@ int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_gra
   if (e) return e;
   NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
               "render_backward: null grad pointer");
+  NFI_REQUIRE(a->x_saved, "render_backward: x_saved (decoder inputs saved by the forward) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
   NFI_REQUIRE(stage >= 0 && stage <= 2, "render_backward_stage: stage %d not in 0..2", stage);
   return nfi::launch_bwd(a, g, (hipStream_t)stream, stage);

@@ -221,6 +221,8 @@ class _VolumeRender(torch.autograd.Function):
         c_saved = torch.empty((n, 3, N), device=dev)
         y_saved = torch.empty((n, 11, N), device=dev)
         perm = torch.empty((n, N), device=dev, dtype=torch.int16)
+        # decoder inputs for the backward (saves it the re-gather), only when a gradient is wanted
+        x_saved = torch.empty((n * N, 32), device=dev) if any(ctx.needs_input_grad) else None
         zc = zf = None
         if debug is not None:
             zc = torch.empty((n, S), device=dev)
@@ -230,6 +232,7 @@ class _VolumeRender(torch.autograd.Function):
         args = _VolumeRender._args(planes_tm, dec, pal_c, ro_c, rd_c, near_c, far_c, opts, B, H * W,
                                    uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, y_saved, perm,
                                    zc, zf)
+        args.x_saved = _ptr(x_saved)
         tile_counts = None
         if FORWARD_TILE_COUNTS and ctx.needs_input_grad[0]:
             # the forward counts the backward's d-planes tile bins while it has the samples
@@ -245,7 +248,7 @@ class _VolumeRender(torch.autograd.Function):
             debug['sigma_sorted'] = s_saved
             debug['rgb_sorted'] = c_saved
         ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved,
-                              y_saved, perm, tile_counts)
+                              y_saved, perm, x_saved, tile_counts)
         ctx.opts = opts
         ctx.shape = (B, H, W)
         ctx.mark_non_differentiable(depth)
@@ -271,8 +274,8 @@ class _VolumeRender(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_rgb, g_depth, g_mask):
         lib = _lib.load()
-        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm, tile_counts = \
-            ctx.saved_tensors
+        planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm, x_saved, \
+            tile_counts = ctx.saved_tensors
         opts = ctx.opts
         B, H, W = ctx.shape
         dev = ro.device
@@ -287,6 +290,7 @@ class _VolumeRender(torch.autograd.Function):
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
         args = _VolumeRender._args(planes_tm, dec, pal, ro, rd, near, far, opts, B, H * W, None, None, 0,
                                    None, None, None, t_saved, s_saved, c_saved, y_saved, perm, None, None)
+        args.x_saved = _ptr(x_saved)
         nbytes = lib.nfi_render_backward_workspace_bytes(ctypes.byref(args))
         if nbytes < 0:
             _lib.check(-1, 'nfi_render_backward_workspace_bytes')
