@@ -151,7 +151,7 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
  * (recomputes taps and decoder) writes per-sample feature gradients; d planes is then summed
  * per 16x16-cell plane tile in LDS (samples binned by tile) and flushed once per tile. */
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
-int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * 3 * ceil((R-1)/8)^2 */
+int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * 3 * ((R-2)/7+1) * ((R-2)/4+1) */
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 /* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
  * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,

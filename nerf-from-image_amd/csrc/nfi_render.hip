@@ -165,34 +165,48 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
 }
 
 // ---------------------------------------------------------------------------------------
-// d planes by plane tile: every (sample, plane) contribution is binned by the 8x8-cell tile
-// of the plane its bilinear cell lies in; a workgroup sums a chunk of a tile's entries into
-// 9x9x32 LDS images — one private image per wave, updated by plain read-modify-write (LDS
-// executes a wave's instructions in order, so no atomics are needed; gfx950's ds_add_f32 costs
-// ~200 cycles per wave-instruction per CU against ~25 for the RMW, scripts/ubench/lds_atomic.hip)
-// with consecutive same-cell entries merged in registers first — then merges the four images
-// and flushes them with one float atomic per nonzero texel channel.  Global atomic traffic
-// drops from 1,536 B per sample to ~10 KB per (tile, chunk).
+// d planes by plane tile: every (sample, plane) contribution is binned by the 7x4-cell tile of
+// the plane its bilinear cell lies in, and a workgroup sums a chunk of one tile's entries in
+// REGISTERS: lane (h, c) of a wave holds channel c of texel rows ly + h of the tile's 8x5 texels
+// as a 32-float vector (half h = 1 stores row y at slot y - 1, so an entry's two rows sit at the
+// same wave-uniform slot ly*8 + lx in both halves), updated through M0-indexed VGPR moves
+// (s_set_gpr_idx).  No LDS atomics (gfx950 ds_add_f32: ~200 cycles per wave-instruction per CU)
+// and no LDS read-modify-write chain; the waves' images are merged once through LDS and flushed
+// with one global float atomic per nonzero texel channel.
+//
+// Cells are normalized so the bilinear cell is interior (x0, y0 <= R-2): a border-clipped point
+// (x0 = R-1, w = 0) becomes (x0 = R-2, w = 1), which puts the same weights on the same texels.
 // ---------------------------------------------------------------------------------------
-constexpr int TS = 8;             // cells per tile side
-constexpr int TT = TS + 1;        // texels per tile side
-constexpr int TILE_F = TT * TT * NC + NC;   // floats per wave image (+1 trash texel)
-constexpr int CHUNK = 2048;       // (sample, plane) entries per accumulation workgroup
+constexpr int TSX = 7, TSY = 4;               // cells per tile
+constexpr int TTX = TSX + 1, TTY = TSY + 1;   // texels per tile (8 x 5)
+constexpr int CHUNK = 2048;                   // (sample, plane) entries per accumulation workgroup
 
-__device__ __forceinline__ int tile_of(int cell, int T) { return min(cell / TS, T - 1); }
+struct TileGrid {
+  int nx, ny;
+};
+__host__ __device__ __forceinline__ TileGrid tile_grid(int R) { return {(R - 2) / TSX + 1, (R - 2) / TSY + 1}; }
 
-// Tile key of plane q for point P of image b, and the entry record {s, local cell key, w, n}
-// (key = ly << 16 | lx << 8 | ox | oy << 1 inside the tile).
-__device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int R, int T, long long s, int4& rec) {
+// Tile key of plane q for point P of image b, and the entry record {s, slot | flags, w, n}:
+// slot = ly*8 + lx inside the tile, flags bit 8/9 = grid-gradient multiplier gxm/gym nonzero.
+__device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int R, TileGrid G, long long s,
+                                              int4& rec) {
   const int cell = P.pl[q].tex & 0xFFFFF;
-  const int y0 = cell / R, x0 = cell % R;
-  const int ty = tile_of(y0, T), tx = tile_of(x0, T);
-  rec = make_int4((int)s, ((y0 - ty * TS) << 16) | ((x0 - tx * TS) << 8) | (P.pl[q].tex >> 20),
-                  __float_as_int(P.pl[q].w), __float_as_int(P.pl[q].n));
-  return ((b * 3 + q) * T + ty) * T + tx;
+  int y0 = cell / R, x0 = cell % R;
+  float w = P.pl[q].w, n = P.pl[q].n;
+  if (x0 == R - 1) {
+    x0 = R - 2;
+    w = 1.f;
+  }
+  if (y0 == R - 1) {
+    y0 = R - 2;
+    n = 1.f;
+  }
+  const int tx = x0 / TSX, ty = y0 / TSY;
+  const int slot = (y0 - ty * TSY) * TTX + (x0 - tx * TSX);
+  rec = make_int4((int)s, slot | (P.pl[q].gxm != 0.f ? 0x100 : 0) | (P.pl[q].gym != 0.f ? 0x200 : 0),
+                  __float_as_int(w), __float_as_int(n));
+  return ((b * 3 + q) * G.ny + ty) * G.nx + tx;
 }
-
-__host__ __device__ __forceinline__ int tiles_per_side(int R) { return (R - 1 + TS - 1) / TS; }
 
 // Run-aggregated atomicAdd of 1 per valid lane on base[key]: each run of equal keys in
 // consecutive lanes (samples along a ray are depth-sorted, so a ray meets each tile in one run)
@@ -719,7 +733,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
   NFI_STAMP(6)
   if (a.tile_counts) {
     // per-tile sample counts for the backward's d-planes binning (same keys as bin_fill)
-    const int Tn = tiles_per_side(pv.R);
+    const TileGrid Tg = tile_grid(pv.R);
 #pragma unroll
     for (int e = 0; e < NPL; ++e) {
       const int i = e * 64 + l;
@@ -729,7 +743,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         int4 rec;
-        const int key = plane_tile_key(P, q, R.b, pv.R, Tn, r * N + i, rec);
+        const int key = plane_tile_key(P, q, R.b, pv.R, Tg, r * N + i, rec);
         run_count(a.tile_counts, key, v);
       }
     }
@@ -780,7 +794,7 @@ struct BwdArgs {
   int npl;                // chunks of 64 per ray
   int* cursor;            // [K] tile fill cursors (NULL: bins filled by bin_fill_kernel)
   int4* list;             // [3*rays*N] tile entries
-  int T;                  // tiles per plane side
+  TileGrid tg;            // tile grid of a plane
 };
 
 // Compositing backward (nerf_utils.py:125-163 under autograd), one wave per ray:
@@ -977,7 +991,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       int4 rec;
-      const int key = plane_tile_key(P, q, R.b, pv.R, g.T, r * N + i, rec);
+      const int key = plane_tile_key(P, q, R.b, pv.R, g.tg, r * N + i, rec);
       const int pos = run_increment(g.cursor, key, vb);
       if (vb) g.list[pos] = rec;
     }
@@ -1072,7 +1086,8 @@ struct BinArgs {
   const float* rd;
   const float* t;        // [rays][N] merged depths (saved by the forward)
   long long nsamp;       // rays * N
-  int N, HW, R, T;       // T = tiles per plane side
+  int N, HW, R;
+  TileGrid tg;
   float sr;
   int* counts;           // [K]
   int* cursor;           // [K]
@@ -1094,7 +1109,7 @@ __device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int k
   PointP P;
   point_params(o, d, A.t[s], A.sr, A.R, P);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) key[q] = plane_tile_key(P, q, b, A.R, A.T, s, rec[q]);
+  for (int q = 0; q < 3; ++q) key[q] = plane_tile_key(P, q, b, A.R, A.tg, s, rec[q]);
   return P.mask == 0.f;
 }
 
@@ -1172,9 +1187,6 @@ __global__ void __launch_bounds__(256) chunk_map_kernel(const int* __restrict__ 
 }
 
 struct TileArgs {
-  const float* ro;
-  const float* rd;
-  const float* t;
   const float* gfeat;     // [nsamp][32]
   const int* counts;
   const int* offsets;
@@ -1182,102 +1194,109 @@ struct TileArgs {
   const int* chunk_tile;  // [total chunks]
   const int* meta;        // meta[0] = total chunks
   const int4* list;
-  int dbg;                // ablation switch (NFI_TILE_DEBUG): 1 no RMW, 2 no entry loop, 4 no flush
   float* dplanes;
   long long sb;
   int sq, st;
-  int K, N, HW, R, T;
-  float sr;
+  int R;
+  TileGrid tg;
 };
 
-__device__ __forceinline__ void tile_rmw(float* __restrict__ img, int key, int dxl, int cl, float a0, float a1) {
-  // key = ly << 16 | lx << 8 | flags(ox | oy << 1); dx=1 lanes of an edge cell (ox = 0) would
-  // alias the dx=0 texel inside one instruction: send them (weight 0) to the trash texel
-  const int lx = (key >> 8) & 0xFF, ly = key >> 16, ox = key & 1, oy = (key >> 1) & 1;
-  const int t0 = (dxl && !ox) ? TT * TT : ly * TT + lx + dxl;
-  const int t1 = (dxl && !ox) ? TT * TT : (ly + oy) * TT + lx + dxl;
-  float* p0 = img + t0 * NC + cl;
-  *p0 = *p0 + a0;
-  float* p1 = img + t1 * NC + cl;
-  *p1 = *p1 + a1;
-}
+typedef float img32 __attribute__((ext_vector_type(32)));
+typedef int iv4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) iv4* cint4_p;
+
+// gradient-row stage: row u's float4 k lives at slot k ^ (u & 7) (conflict-free b128 stores)
+__device__ __forceinline__ int stage_at(int u, int c) { return u * NC + ((((c >> 2) ^ (u & 7))) << 2) + (c & 3); }
 
 __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
-  __shared__ __attribute__((aligned(16))) float acc[4 * TILE_F];
-  __shared__ __attribute__((aligned(16))) float stage[4 * 64 * NC];
-  const int tid = threadIdx.x, wv = tid >> 6, l = lane_id();
-  const int dxl = l >> 5, cl = l & 31;
-  float* img = acc + wv * TILE_F;
-  float* G = stage + wv * 64 * NC;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 64 * NC];   // per-wave row stage, then images
+  const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = lane_id();
+  const int h = l >> 5, cl = l & 31;
+  float* G = lds + wv * 64 * NC;
+  // half 0 weights row ly by (1 - n), half 1 row ly + 1 by n
+  const float wsgn = h ? 1.f : -1.f, woff = h ? 0.f : 1.f;
+  const cint4_p L = (cint4_p)A.list;
   const int total = A.meta[0];
+  const int tpp = A.tg.nx * A.tg.ny;
   for (int c = blockIdx.x; c < total; c += gridDim.x) {
-    const int tile = A.chunk_tile[c];
-    const int first = A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK;
-    const int last = min(A.offsets[tile] + A.counts[tile], first + CHUNK);
-    const int bq = tile / (A.T * A.T);
+    // (wave-uniform scalars: readfirstlane keeps the entry loop's control and the register-image
+    // index in SGPRs)
+    const int tile = __builtin_amdgcn_readfirstlane(A.chunk_tile[c]);
+    const int first = __builtin_amdgcn_readfirstlane(A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK);
+    const int last = __builtin_amdgcn_readfirstlane(min(A.offsets[tile] + A.counts[tile], first + CHUNK));
+    const int bq = tile / tpp, rem = tile % tpp;
     const int q = bq % 3, b = bq / 3;
-    const int tx = tile % A.T, ty = (tile / A.T) % A.T;
-    for (int k = tid; k < 4 * TILE_F; k += 256) acc[k] = 0.f;
-    __syncthreads();
-    int cur = -1;
-    float a0 = 0.f, a1 = 0.f;
-    // software pipeline: records + gradient rows of batch k+1 load while batch k is summed
-    int base = first + wv * 64;
-    // (indices clamped to the chunk's last entry: every lane always loads a valid record)
-    int4 rec = A.list[min(base + l, last - 1)];
-    float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
+    const int ty = rem / A.tg.nx, tx = rem % A.tg.nx;
+    // each wave sums a contiguous quarter of the chunk (runs of one ray stay together)
+    const int per = (((last - first) + 3) / 4 + 7) & ~7;
+    const int b0 = first + wv * per, b1 = min(last, b0 + per);
+    img32 img = 0.f;
+    if (b0 < b1) {
+      int4 vrec = A.list[min(b0 + l, b1 - 1)];
+      float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
 #define NFI_LOAD_ROW(REC)                                                                       \
   {                                                                                              \
     const float4* src_ = reinterpret_cast<const float4*>(A.gfeat + (long long)(REC).x * NC);     \
     r0 = src_[0]; r1 = src_[1]; r2 = src_[2]; r3 = src_[3];                                      \
     r4 = src_[4]; r5 = src_[5]; r6 = src_[6]; r7 = src_[7];                                      \
   }
-    NFI_LOAD_ROW(rec)
-    while (base < last) {
-      const int n = min(64, last - base);
-      float4* dst = reinterpret_cast<float4*>(G + l * NC);
-      dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
-      dst[4] = r4; dst[5] = r5; dst[6] = r6; dst[7] = r7;
-      const int key = rec.y;
-      const float pw = __int_as_float(rec.z), pn = __int_as_float(rec.w);
-      const int nb = base + 256;
-      rec = A.list[min(nb + l, last - 1)];
-      NFI_LOAD_ROW(rec)
-      wave_lds_sync();
-      if (A.dbg & 2) { base = nb; continue; }
-      for (int j = 0; j < n; ++j) {
-        const int kj = readlane(key, j);
-        const float w = readlane(pw, j), nn = readlane(pn, j);
-        const float gv = G[j * NC + cl];
-        const float wx = dxl ? w : 1.f - w;
-        const float c0 = gv * ((1.f - nn) * wx), c1 = gv * (nn * wx);
-        if (kj == cur) {
-          a0 += c0;
-          a1 += c1;
-        } else {
-          if (cur >= 0 && !(A.dbg & 1)) tile_rmw(img, cur, dxl, cl, a0, a1);
-          cur = kj;
-          a0 = c0;
-          a1 = c1;
+      NFI_LOAD_ROW(vrec)
+      for (int base = b0; base < b1; base += 64) {
+        const int n = min(64, b1 - base);
+        {
+          float4* dst = reinterpret_cast<float4*>(G + l * NC);
+          const int sw = l & 7;
+          dst[0 ^ sw] = r0; dst[1 ^ sw] = r1; dst[2 ^ sw] = r2; dst[3 ^ sw] = r3;
+          dst[4 ^ sw] = r4; dst[5 ^ sw] = r5; dst[6 ^ sw] = r6; dst[7 ^ sw] = r7;
         }
+        // next 64 rows load while these are summed
+        vrec = A.list[min(base + 64 + l, b1 - 1)];
+        NFI_LOAD_ROW(vrec)
+        wave_lds_sync();
+        // 8 entries per step; records past the chunk end read the list's padding / the next
+        // tile's entries (in bounds) and contribute exactly nothing
+        for (int u = 0; u < n; u += 8) {
+          iv4 rc[8];
+          float gv[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            rc[k] = L[base + u + k];
+            gv[k] = G[stage_at((u + k) & 63, cl)];
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const bool ok = u + k < n;
+            const int slot = ok ? (__builtin_amdgcn_readfirstlane(rc[k].y) & 31) : 0;
+            const float w = __int_as_float(rc[k].z), nn = __int_as_float(rc[k].w);
+            const float gw = ok ? gv[k] * fmaf(nn, wsgn, woff) : 0.f;
+            img[slot] += gw * (1.f - w);
+            img[slot + 1] += gw * w;
+          }
+        }
+        wave_lds_sync();
       }
-      wave_lds_sync();
-      base = nb;
-    }
 #undef NFI_LOAD_ROW
-    if (cur >= 0) tile_rmw(img, cur, dxl, cl, a0, a1);
+    }
+    __syncthreads();   // every wave is done with its row stage
+    // wave images -> LDS [wave][half][slot][channel]
+#pragma unroll
+    for (int r = 0; r < 32; ++r) G[(h * 32 + r) * NC + cl] = img[r];
     __syncthreads();
     float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
-    for (int k = tid; k < TT * TT * NC; k += 256) {
-      const float v = (acc[k] + acc[TILE_F + k]) + (acc[2 * TILE_F + k] + acc[3 * TILE_F + k]);
+    for (int k = tid; k < TTX * TTY * NC; k += 256) {
       const int texel = k / NC, ch = k % NC;
-      const int gy = ty * TS + texel / TT, gx = tx * TS + texel % TT;
-      if (v != 0.f && gy < A.R && gx < A.R && !(A.dbg & 4)) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
+      const int yl = texel / TTX, xl = texel % TTX;
+      float v = 0.f;
+#pragma unroll
+      for (int w4 = 0; w4 < 4; ++w4) {
+        const float* im = lds + w4 * 64 * NC;
+        if (yl < TSY) v += im[(yl * TTX + xl) * NC + ch];
+        if (yl >= 1) v += im[(32 + (yl - 1) * TTX + xl) * NC + ch];
+      }
+      const int gy = ty * TSY + yl, gx = tx * TSX + xl;
+      if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
     }
     __syncthreads();
-  }
-  if (A.dbg) {   // keep the ablated values observable
-    if (threadIdx.x == 0 && blockIdx.x == 0) A.dplanes[0] += 0.f * acc[0];
   }
 }
 
@@ -1299,8 +1318,8 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   const long long nrays = (long long)a->B * a->HW;
   const int N = a->fine ? 2 * a->S : a->S;
   const long long nsamp = nrays * N;
-  const int T = (a->field.R - 1 + TS - 1) / TS;
-  const long long K = (long long)a->B * 3 * T * T;
+  const TileGrid tg = tile_grid(a->field.R);
+  const long long K = (long long)a->B * 3 * tg.nx * tg.ny;
   char* p = static_cast<char*>(base);
   Workspace w;
   auto take = [&](long long bytes) {
@@ -1318,7 +1337,7 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.meta = reinterpret_cast<int*>(take(16));
   // chunks <= ceil(entries / CHUNK) + K  (each tile wastes at most one partial chunk)
   w.chunk_tile = reinterpret_cast<int*>(take((3 * nsamp / CHUNK + K + 1) * 4));
-  w.list = reinterpret_cast<int4*>(take(3 * nsamp * 16));
+  w.list = reinterpret_cast<int4*>(take((3 * nsamp + 64) * 16));   // + padding read by tile_accum
   w.bytes = p - static_cast<char*>(base);
   return w;
 }
@@ -1327,8 +1346,8 @@ template <int SPL, int NPL, bool FINE>
 static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
   const long long nrays = (long long)a->B * a->HW;
   if (a->tile_counts) {
-    const int T = tiles_per_side(a->field.R);
-    NFI_REQUIRE(hipMemsetAsync(a->tile_counts, 0, (size_t)a->B * 3 * T * T * 4, s) == hipSuccess,
+    const TileGrid tg = tile_grid(a->field.R);
+    NFI_REQUIRE(hipMemsetAsync(a->tile_counts, 0, (size_t)a->B * 3 * tg.nx * tg.ny * 4, s) == hipSuccess,
                 "render_forward: memset failed");
   }
   render_fwd_kernel<SPL, NPL, FINE><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
@@ -1340,8 +1359,8 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   const long long nrays = (long long)a->B * a->HW;
   const int N = a->fine ? 2 * a->S : a->S;
   const long long nsamp = nrays * N;
-  const int T = (a->field.R - 1 + TS - 1) / TS;
-  const int K = a->B * 3 * T * T;
+  const TileGrid tg = tile_grid(a->field.R);
+  const int K = a->B * 3 * tg.nx * tg.ny;
   Workspace w = carve(a, g->workspace);
   NFI_REQUIRE(w.bytes <= g->workspace_bytes, "render_backward: workspace too small (%lld < %lld)",
               (long long)g->workspace_bytes, w.bytes);
@@ -1352,7 +1371,7 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   const bool do_bins = stage < 0 || stage == 0, do_field = stage < 0 || stage == 1, do_tiles = stage < 0 || stage == 2;
   const bool fwd_counts = g->tile_counts != nullptr;
   const int* counts = fwd_counts ? g->tile_counts : w.counts;
-  BinArgs B{a->ro, a->rd, a->t_saved, nsamp, N, a->HW, a->field.R, T, a->field.scene_range,
+  BinArgs B{a->ro, a->rd, a->t_saved, nsamp, N, a->HW, a->field.R, tg, a->field.scene_range,
             w.counts, w.cursor, w.list};
   const unsigned sb = (unsigned)((nsamp + 255) / 256);
   if (do_bins) {
@@ -1373,7 +1392,7 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   // 2) per-ray compositing backward, then per-(ray, 64-sample chunk) field backward
   const int NPL = (N + 63) / 64;
   BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat, w.gsig, w.wts, NPL,
-             fwd_counts ? w.cursor : nullptr, w.list, T};
+             fwd_counts ? w.cursor : nullptr, w.list, tg};
   const unsigned rb = (unsigned)((nrays + 3) / 4);
   if (do_field) {
     if (NPL <= 1) composite_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
@@ -1383,13 +1402,11 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
-  // 3) per-tile LDS accumulation of d planes
-  TileArgs TA{a->ro, a->rd, a->t_saved, w.gfeat, counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list,
-              0, g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st, K, N, a->HW, a->field.R, T,
-              a->field.scene_range};
-  if (const char* dbg = getenv("NFI_TILE_DEBUG")) TA.dbg = atoi(dbg);
+  // 3) per-tile register accumulation of d planes
+  TileArgs TA{w.gfeat, counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list, g->d_planes, a->field.sb,
+              (int)a->field.sq, (int)a->field.st, a->field.R, tg};
   if (do_tiles) {
-    tile_accum_kernel<<<2048, 256, 0, s>>>(TA);
+    tile_accum_kernel<<<4096, 256, 0, s>>>(TA);
     NFI_CHECK_LAUNCH("tile_accum_kernel");
   }
   return NFI_OK;
@@ -1445,8 +1462,8 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
 
 int64_t nfi_tile_count_size(const nfi_render_args* a) {
   if (nfi::validate(a)) return -1;
-  const int T = nfi::tiles_per_side(a->field.R);
-  return (int64_t)a->B * 3 * T * T;
+  const nfi::TileGrid tg = nfi::tile_grid(a->field.R);
+  return (int64_t)a->B * 3 * tg.nx * tg.ny;
 }
 
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {
