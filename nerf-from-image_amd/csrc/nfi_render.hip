@@ -966,10 +966,17 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     }
   }
   wave_lds_sync();
-  if (l < NA * 3) {
-    float s = 0.f;
-    for (int j = 0; j < npts; ++j) s += X[j * XS + l];
-    g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = s;
+  {
+    // column sums over the 64 rows (rows of lanes >= npts are zero): lanes (half, column) sum 32
+    // rows each with all reads in flight, then the halves are added
+    const int col = l & 31, r0 = (l >> 5) * 32;
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (col < NA * 3) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) s4[j & 3] += X[(r0 + j) * XS + col];
+    }
+    const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
+    if (l < NA * 3) g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = sh;
   }
   NFI_STAMP(18)
   float gx[NC];
@@ -1016,7 +1023,7 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     point_params(R.o, R.d, te, sr, pv.R, P);
     const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
     const int ngrp = (npts + 3) >> 2;
-    constexpr int GB = GATHER_GB;
+    constexpr int GB = 4;   // (field_bwd has the VGPRs for 4 groups in flight)
 #pragma unroll 1
     for (int gb = 0; gb < ngrp; gb += GB) {
       if (((live >> (4 * gb)) & ((1ull << (4 * GB)) - 1ull)) == 0ull) continue;
@@ -1232,6 +1239,10 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
     const int b0 = first + wv * per, b1 = min(last, b0 + per);
     img32 img = 0.f;
     if (b0 < b1) {
+      // consecutive entries of one cell (a ray's samples) are merged in a0/a1 before the
+      // indexed update (cur starts at slot 0 with nothing pending)
+      int cur = 0;
+      float a0 = 0.f, a1 = 0.f;
       int4 vrec = A.list[min(b0 + l, b1 - 1)];
       float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
 #define NFI_LOAD_ROW(REC)                                                                       \
@@ -1269,13 +1280,22 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
             const int slot = ok ? (__builtin_amdgcn_readfirstlane(rc[k].y) & 31) : 0;
             const float w = __int_as_float(rc[k].z), nn = __int_as_float(rc[k].w);
             const float gw = ok ? gv[k] * fmaf(nn, wsgn, woff) : 0.f;
-            img[slot] += gw * (1.f - w);
-            img[slot + 1] += gw * w;
+            if (slot != cur) {
+              img[cur] += a0;
+              img[cur + 1] += a1;
+              a0 = 0.f;
+              a1 = 0.f;
+              cur = slot;
+            }
+            a0 = fmaf(gw, 1.f - w, a0);
+            a1 = fmaf(gw, w, a1);
           }
         }
         wave_lds_sync();
       }
 #undef NFI_LOAD_ROW
+      img[cur] += a0;
+      img[cur + 1] += a1;
     }
     __syncthreads();   // every wave is done with its row stage
     // wave images -> LDS [wave][half][slot][channel]
