@@ -260,21 +260,18 @@ __device__ __forceinline__ void store_row(float* __restrict__ X, int row, const 
   for (int k = 0; k < NC / 4; ++k) r[k] = make_float4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
 }
 
-// Softplus(beta=1, threshold=20) (generator.py:297) and its derivative (ATen softplus_backward).
-// The correction factor u/(u+1-1) of the accurate log1p and u/(u+1) use the hardware
-// reciprocal (<= 2 ulp) instead of the IEEE division sequence.
+// Softplus(beta=1, threshold=20) (generator.py:297) and its derivative (ATen softplus_backward)
+// on the transcendental units: log(1 + e^z) = log2(1 + 2^(z log2 e)) ln 2.  Rounding 1 + e^z
+// costs at most 2^-24 ABSOLUTE in the result (log' <= 1 near 1), the size of an fp32 rounding
+// of the O(1) hidden activations it feeds, so the log1p correction is not carried.
+// sigmoid(z) = 1 / (1 + e^-z) is exactly 1 in fp32 beyond the threshold and 0 far below it.
 __device__ __forceinline__ float softplus(float z) {
-  const float u = __expf(z);
-  const float up = 1.f + u;
-  const float dd = up - 1.f;
-  // accurate log1p(u) = log(1+u) * u / ((1+u) - 1), on v_log_f32 / v_rcp_f32 (up >= 1: no denormals)
-  const float lg = __builtin_amdgcn_logf(up) * 0.69314718f;
-  const float l1p = (dd == 0.f) ? u : lg * (u * __builtin_amdgcn_rcpf(dd));
-  return (z > 20.f) ? z : l1p;
+  const float u = __builtin_amdgcn_exp2f(z * 1.44269504f);
+  const float h = __builtin_amdgcn_logf(1.f + u) * 0.69314718f;
+  return (z > 20.f) ? z : h;
 }
 __device__ __forceinline__ float softplus_grad(float z) {
-  const float u = __expf(z);
-  return (z > 20.f) ? 1.f : u * __builtin_amdgcn_rcpf(u + 1.f);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z * -1.44269504f));
 }
 
 // The packed decoder is read through the constant address space (AS 4): wave-uniform,
@@ -289,9 +286,9 @@ __device__ __forceinline__ cfloat_p as_const(const float* p) { return (cfloat_p)
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
 
-// W1 row o . x  (x as 16 channel pairs)
-__device__ __forceinline__ float dot32(const f2 x[NC / 2], cf2_p w) {
-  f2 z0 = splat(0.f), z1 = splat(0.f);
+// W1 row o . x + bias  (x as 16 channel pairs)
+__device__ __forceinline__ float dot32(const f2 x[NC / 2], cf2_p w, float bias) {
+  f2 z0 = f2{bias, 0.f}, z1 = splat(0.f);
 #pragma unroll
   for (int c = 0; c < NC / 2; c += 2) {
     z0 = pfma(x[c], w[c], z0);
@@ -320,7 +317,7 @@ __device__ __forceinline__ void mlp_forward(const float* __restrict__ dec_, cons
   for (int o = 0; o < NH; ++o) {
     const cfloat_p u = dec + o * DEC_UNIT;
     const cf2_p u2 = (cf2_p)u;
-    const float h = softplus(dot32(xv, u2) + u[DEC_B1]);
+    const float h = softplus(dot32(xv, u2, u[DEC_B1]));
     const f2 hh = splat(h);
 #pragma unroll
     for (int k = 0; k < NO / 2; ++k) acc[k] = pfma(hh, u2[DEC_W2T / 2 + k], acc[k]);
@@ -348,7 +345,7 @@ __device__ __forceinline__ void mlp_backward(const float* __restrict__ dec_, con
   for (int o = 0; o < NH; ++o) {
     const cfloat_p u = dec + o * DEC_UNIT;
     const cf2_p u2 = (cf2_p)u;
-    const float z = dot32(xv, u2) + u[DEC_B1];
+    const float z = dot32(xv, u2, u[DEC_B1]);
     f2 gh2 = splat(0.f);
 #pragma unroll
     for (int k = 0; k < NO / 2; ++k) gh2 = pfma(gyv[k], u2[DEC_W2T / 2 + k], gh2);
@@ -439,6 +436,38 @@ __device__ __forceinline__ void excl_prod(const float (&a)[E], float (&T)[E]) {
     if (lane_id() == 0) ex = 1.0;
     T[e] = (float)(carry * ex);
     carry = carry * __shfl(inc, 63);
+  }
+}
+
+// Ascending bitonic sort of the 64*E values v[e] (element e*64 + lane) across the wave.
+template <int E>
+__device__ __forceinline__ void bitonic_sort(float (&v)[E]) {
+  const int l = lane_id();
+  constexpr int NN = 64 * E;
+#pragma unroll
+  for (int k = 2; k <= NN; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int pe = e ^ (j >> 6);
+          if (pe > e) {
+            const bool up = ((e * 64 + l) & k) == 0;
+            const float a = v[e], b = v[pe];
+            v[e] = up ? fminf(a, b) : fmaxf(a, b);
+            v[pe] = up ? fmaxf(a, b) : fminf(a, b);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = e * 64 + l;
+          const float o = __shfl_xor(v[e], j);
+          v[e] = (((i & k) == 0) == ((i & j) == 0)) ? fminf(v[e], o) : fmaxf(v[e], o);
+        }
+      }
+    }
   }
 }
 
@@ -645,7 +674,15 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       const float tt = fdiv(fsub(u, c0), denom);
       tf[e] = fadd(b0, fmul(tt, fsub(b1, b0)));
       if (i < S && a.z_fine) a.z_fine[r * S + i] = tf[e];
+      if (i >= S) tf[e] = INFINITY;
     }
+    // fine depths in ascending order (each depends on its own u only, and samples at equal
+    // depths have equal fields, so the order of equal values cannot change any output): the
+    // merge below then needs ranks in two sorted lists instead of an O(N^2) count
+    bitonic_sort<SPL>(tf);
+#pragma unroll
+    for (int e = 0; e < SPL; ++e)
+      if (e * 64 + l >= S) tf[e] = R.near_;   // (padding back to a finite, in-box-safe depth)
     wave_lds_sync();
     NFI_STAMP(4)
     // ---- fine field evaluation (run.py:283-291) ----
@@ -666,16 +703,44 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
       }
     }
     wave_lds_sync();
+    // stratified coarse depths are ascending up to a rounding tie-break; verify, and fall back
+    // to direct counting (stable: cat order breaks ties) if not
+    bool unsorted = false;
+#pragma unroll
+    for (int e = 0; e < SPL; ++e) {
+      const int i = e * 64 + l;
+      if (i + 1 < S) unsorted |= T2[i] > T2[i + 1];
+    }
+    const bool direct = __ballot(unsorted) != 0ull;
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
       const int i = e * 64 + l;
       if (i < S) {
         int rc = 0, rf = 0;
         const float vc = tc[e], vf = tf[e];
-        for (int j = 0; j < 2 * S; ++j) {
-          const float v = T2[j];
-          rc += (v < vc || (v == vc && j < i)) ? 1 : 0;
-          rf += (v < vf || (v == vf && j < S + i)) ? 1 : 0;
+        if (direct) {
+          for (int j = 0; j < 2 * S; ++j) {
+            const float v = T2[j];
+            rc += (v < vc || (v == vc && j < i)) ? 1 : 0;
+            rf += (v < vf || (v == vf && j < S + i)) ? 1 : 0;
+          }
+        } else {
+          // coarse i: i + #fine < vc;  fine i: i + #coarse <= vf  (coarse first on ties)
+          int lo = 0, hi = S;
+          while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (T2[S + m] < vc) lo = m + 1;
+            else hi = m;
+          }
+          rc = i + lo;
+          lo = 0;
+          hi = S;
+          while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (T2[m] <= vf) lo = m + 1;
+            else hi = m;
+          }
+          rf = i + lo;
         }
         Mt[rc] = vc;
         Ms[rc] = sc[e];
