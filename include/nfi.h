@@ -33,8 +33,8 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 5
-#define NFI_DEC_SIZE 3088 /* floats in the packed decoder buffer */
+#define NFI_ABI_VERSION 6
+#define NFI_DEC_SIZE 7184 /* floats in the packed decoder buffer */
 
 enum {
   NFI_OK = 0,

@@ -14,11 +14,22 @@ constexpr int NA = 10;     // attention values (palette rows)
 
 // Packed decoder: per hidden unit o a 48-float record {W1s[o][0..31], W2s^T[o][0..10], b1[o], pad}
 // so that one unit is three s_load_dwordx16 from a wave-uniform address; b2 follows.
-constexpr int DEC_UNIT = 48;
-constexpr int DEC_W2T = 32;
-constexpr int DEC_B1 = 43;
-constexpr int DEC_B2 = NH * DEC_UNIT;          // 11 floats
-constexpr int DEC_SIZE = DEC_B2 + 16;          // 3088 floats
+// Packed decoder = per-lane MFMA operand tables for v_mfma_f32_16x16x4_f32 (lane l: A[l&15][l>>4],
+// B[l>>4][l&15]; C/D: row 4(l>>4)+reg, col l&15), built by nfi_decoder_pack from the
+// gain-scaled EqualizedLinear weights W1s [64,32], b1s [64], W2s [11,64], b2s [11]:
+//   DT1 [hb][l][t]     W1s[16hb + (l&15)][8(l>>4) + t]          layer 1 A (t = 0..7)
+//   DB1 [hb][l][r]     b1s[16hb + 4(l>>4) + r]                  layer 1 C init
+//   DT2 [hb][l][r]     W2s[l&15][16hb + 4(l>>4) + r]            layer 2 A (rows >= 11 zero)
+//   DT3 [hb][l][t]     W2s[4t + (l>>4)][16hb + (l&15)]          d hidden = W2s^T gy, A (t = 0..2)
+//   DT4 [cb][hb][l][r] W1s[16hb + 4(l>>4) + r][16cb + (l&15)]   d x = W1s^T d z, A
+//   DB2 [16]           b2s (zero padded)
+constexpr int DT1 = 0;
+constexpr int DB1 = DT1 + 4 * 64 * 8;
+constexpr int DT2 = DB1 + 4 * 64 * 4;
+constexpr int DT3 = DT2 + 4 * 64 * 4;
+constexpr int DT4 = DT3 + 4 * 64 * 4;
+constexpr int DB2 = DT4 + 2 * 4 * 64 * 4;
+constexpr int DEC_SIZE = DB2 + 16;             // 7184 floats
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

@@ -285,17 +285,31 @@ __global__ void decoder_pack_kernel(const float* __restrict__ w1, const float* _
                                     const float* __restrict__ w2, const float* __restrict__ b2, float g1,
                                     float g2, float gb, float* __restrict__ dec) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < NH * DEC_UNIT) {
-    const int o = t / DEC_UNIT, j = t % DEC_UNIT;
-    float v = 0.f;
-    if (j < NC) v = w1[o * NC + j] * g1;
-    else if (j < DEC_W2T + NO) v = w2[(j - DEC_W2T) * NH + o] * g2;
-    else if (j == DEC_B1) v = b1[o] * gb;
-    dec[t] = v;
-  } else if (t < DEC_SIZE) {
-    const int k = t - DEC_B2;
-    dec[t] = (k < NO) ? b2[k] * gb : 0.f;
+  if (t >= DEC_SIZE) return;
+  // (w1 [64,32], w2 [11,64] row-major; scaled as EqualizedLinear does, stylegan.py:173-176)
+  auto W1 = [&](int h, int c) { return w1[h * NC + c] * g1; };
+  auto W2 = [&](int o, int h) { return (o < NO) ? w2[o * NH + h] * g2 : 0.f; };
+  float v = 0.f;
+  if (t < DB1) {
+    const int hb = t / 512, l = (t / 8) % 64, k = t % 8;
+    v = W1(16 * hb + (l & 15), 8 * (l >> 4) + k);
+  } else if (t < DT2) {
+    const int u = t - DB1, hb = u / 256, l = (u / 4) % 64, r = u % 4;
+    v = b1[16 * hb + 4 * (l >> 4) + r] * gb;
+  } else if (t < DT3) {
+    const int u = t - DT2, hb = u / 256, l = (u / 4) % 64, r = u % 4;
+    v = W2(l & 15, 16 * hb + 4 * (l >> 4) + r);
+  } else if (t < DT4) {
+    const int u = t - DT3, hb = u / 256, l = (u / 4) % 64, k = u % 4;
+    v = (k < 3) ? W2(4 * k + (l >> 4), 16 * hb + (l & 15)) : 0.f;
+  } else if (t < DB2) {
+    const int u = t - DT4, cb = u / 1024, hb = (u / 256) % 4, l = (u / 4) % 64, r = u % 4;
+    v = W1(16 * hb + 4 * (l >> 4) + r, 16 * cb + (l & 15));
+  } else {
+    const int k = t - DB2;
+    v = (k < NO) ? b2[k] * gb : 0.f;
   }
+  dec[t] = v;
 }
 
 // ---------------------------------------------------------------------------------------

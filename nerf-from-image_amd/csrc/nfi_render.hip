@@ -274,90 +274,105 @@ __device__ __forceinline__ float softplus_grad(float z) {
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z * -1.44269504f));
 }
 
-// The packed decoder is read through the constant address space (AS 4): wave-uniform,
-// read-only loads there become s_load into SGPRs even after global stores in the kernel
-// (a plain global pointer would fall back to vector loads into VGPRs once a store may alias).
-// The decoder runs on packed fp32 FMAs (v_pk_fma_f32, two lanes of work per instruction with
-// an SGPR-pair weight operand: the f32 VALU peak, 2x the scalar v_fma_f32 rate).
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef const __attribute__((address_space(4))) float* cfloat_p;
-typedef const __attribute__((address_space(4))) f2* cf2_p;
-__device__ __forceinline__ cfloat_p as_const(const float* p) { return (cfloat_p)(p); }
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+// ---------------------------------------------------------------------------------------
+// Decoder on the matrix cores: v_mfma_f32_16x16x4_f32 (exact f32: a k-ordered fmaf chain per
+// output) for the 64 points of a wave, in the orientation that lets each product's result feed
+// the next one straight from its accumulator registers (operand tables: nfi_common.h DT*).
+// Points are columns: block sb holds points 16sb..16sb+15; lane l = (j = l&15, q = l>>4).
+//   Z^T  [64 hid x 64 pts] = W1s X^T + b1        A = DT1, B = X^T (lane: point j, channels 8q+t)
+//   Y^T  [11 out x 64 pts] = W2s softplus(Z)^T   B = softplus(Z) accumulator registers
+//   dH^T [64 x 64]         = W2s^T dY^T          A = DT3, B = dY^T (through LDS)
+//   dX^T [32 x 64]         = W1s^T (dH o sigmoid(Z))^T   B = accumulator registers
+// The VALU is left with softplus / sigmoid and the surrounding per-point work.
+// ---------------------------------------------------------------------------------------
+typedef float f4v __attribute__((ext_vector_type(4)));
 
-// W1 row o . x + bias  (x as 16 channel pairs)
-__device__ __forceinline__ float dot32(const f2 x[NC / 2], cf2_p w, float bias) {
-  f2 z0 = f2{bias, 0.f}, z1 = splat(0.f);
-#pragma unroll
-  for (int c = 0; c < NC / 2; c += 2) {
-    z0 = pfma(x[c], w[c], z0);
-    z1 = pfma(x[c + 1], w[c + 1], z1);
-  }
-  const f2 z = z0 + z1;
-  return z.x + z.y;
+__device__ __forceinline__ f4v ld4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ void pack_x(const float x[NC], f2 xv[NC / 2]) {
-#pragma unroll
-  for (int c = 0; c < NC / 2; ++c) xv[c] = f2{x[2 * c], x[2 * c + 1]};
+// Z^T block (hb, sb) = W1s[16hb.., :] X^T[:, 16sb..] + b1: xa/xb = channels 8q..8q+3, 8q+4..8q+7
+// of point 16sb + j; ta/tb = DT1 k-steps 0..3, 4..7; b = DB1
+__device__ __forceinline__ f4v layer1(f4v ta, f4v tb, f4v b, f4v xa, f4v xb) {
+  f4v z = b;
+  z = mfma4(ta[0], xa[0], z);
+  z = mfma4(ta[1], xa[1], z);
+  z = mfma4(ta[2], xa[2], z);
+  z = mfma4(ta[3], xa[3], z);
+  z = mfma4(tb[0], xb[0], z);
+  z = mfma4(tb[1], xb[1], z);
+  z = mfma4(tb[2], xb[2], z);
+  z = mfma4(tb[3], xb[3], z);
+  return z;
 }
 
-// TriplanarDecoder.net (generator.py:295-299): y = W2s softplus(W1s x + b1) + b2.
-// Unit o of the packed decoder: u[0..31] = W1s row, u[32..42] = W2s column, u[43] = b1s.
-__device__ __forceinline__ void mlp_forward(const float* __restrict__ dec_, const float x[NC], float y[NO]) {
-  const cfloat_p dec = as_const(dec_);
-  f2 xv[NC / 2];
-  pack_x(x, xv);
-  f2 acc[NO / 2];
+// Decoder forward for the points of the wave's X tile (LDS, rows of XS floats); returns point
+// l's 11 outputs.  The tile is reused as scratch (callers re-sync before writing it).
+__device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, float* __restrict__ X,
+                                                 float y[NO]) {
+  const int l = lane_id(), j = l & 15, q = l >> 4;
+  f4v xa[4], xb[4];
 #pragma unroll
-  for (int k = 0; k < NO / 2; ++k) acc[k] = splat(0.f);
-  float acc10 = 0.f;
-#pragma unroll 1
-  for (int o = 0; o < NH; ++o) {
-    const cfloat_p u = dec + o * DEC_UNIT;
-    const cf2_p u2 = (cf2_p)u;
-    const float h = softplus(dot32(xv, u2, u[DEC_B1]));
-    const f2 hh = splat(h);
-#pragma unroll
-    for (int k = 0; k < NO / 2; ++k) acc[k] = pfma(hh, u2[DEC_W2T / 2 + k], acc[k]);
-    acc10 = fmaf(h, u[DEC_W2T + NO - 1], acc10);
+  for (int sb = 0; sb < 4; ++sb) {
+    xa[sb] = ld4(X + (16 * sb + j) * XS + 8 * q);
+    xb[sb] = ld4(X + (16 * sb + j) * XS + 8 * q + 4);
   }
+  f4v Y[4];
 #pragma unroll
-  for (int k = 0; k < NO / 2; ++k) {
-    y[2 * k] = acc[k].x + dec[DEC_B2 + 2 * k];
-    y[2 * k + 1] = acc[k].y + dec[DEC_B2 + 2 * k + 1];
+  for (int sb = 0; sb < 4; ++sb) Y[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int hb = 0; hb < 4; ++hb) {
+    const f4v ta = ld4(dec + DT1 + (hb * 64 + l) * 8), tb = ld4(dec + DT1 + (hb * 64 + l) * 8 + 4);
+    const f4v b = ld4(dec + DB1 + (hb * 64 + l) * 4);
+    const f4v t2 = ld4(dec + DT2 + (hb * 64 + l) * 4);
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const f4v z = layer1(ta, tb, b, xa[sb], xb[sb]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Y[sb] = mfma4(t2[r], softplus(z[r]), Y[sb]);
+    }
   }
-  y[NO - 1] = acc10 + dec[DEC_B2 + NO - 1];
+  // lane (j, q) holds outputs 4q..4q+3 of point 16sb + j: transpose through the tile
+  wave_lds_sync();
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 4 * q) = Y[sb];
+  wave_lds_sync();
+#pragma unroll
+  for (int o = 0; o < NO; ++o) y[o] = X[l * XS + o] + dec[DB2 + o];
 }
 
-// Input-gradient of the decoder (its weights are frozen during inversion, run.py:630-632).
-__device__ __forceinline__ void mlp_backward(const float* __restrict__ dec_, const float x[NC],
-                                             const float gy[NO], float gx[NC]) {
-  const cfloat_p dec = as_const(dec_);
-  f2 xv[NC / 2], g2[NC / 2], gyv[NO / 2];
-  pack_x(x, xv);
+// Decoder input-gradient (weights frozen during inversion, run.py:630-632) for 64 points:
+// xa/xb as layer1's operands for blocks sb; dY^T operands gyb[sb][t] = dY[16sb + j][4t + q];
+// returns dX^T accumulators gxo[cb][sb] (lane: channels 16cb + 4q + reg of point 16sb + j).
+__device__ __forceinline__ void mlp_backward_mfma(const float* __restrict__ dec, const f4v xa[4], const f4v xb[4],
+                                                  const float gyb[4][3], f4v gxo[2][4]) {
+  const int l = lane_id();
 #pragma unroll
-  for (int c = 0; c < NC / 2; ++c) g2[c] = splat(0.f);
+  for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-  for (int k = 0; k < NO / 2; ++k) gyv[k] = f2{gy[2 * k], gy[2 * k + 1]};
-#pragma unroll 1
-  for (int o = 0; o < NH; ++o) {
-    const cfloat_p u = dec + o * DEC_UNIT;
-    const cf2_p u2 = (cf2_p)u;
-    const float z = dot32(xv, u2, u[DEC_B1]);
-    f2 gh2 = splat(0.f);
+    for (int sb = 0; sb < 4; ++sb) gxo[cb][sb] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < NO / 2; ++k) gh2 = pfma(gyv[k], u2[DEC_W2T / 2 + k], gh2);
-    const float gh = fmaf(gy[NO - 1], u[DEC_W2T + NO - 1], gh2.x + gh2.y);
-    const f2 gz = splat(gh * softplus_grad(z));
+  for (int hb = 0; hb < 4; ++hb) {
+    const f4v ta = ld4(dec + DT1 + (hb * 64 + l) * 8), tb = ld4(dec + DT1 + (hb * 64 + l) * 8 + 4);
+    const f4v b = ld4(dec + DB1 + (hb * 64 + l) * 4);
+    const f4v t3 = ld4(dec + DT3 + (hb * 64 + l) * 4);
+    const f4v t40 = ld4(dec + DT4 + ((0 * 4 + hb) * 64 + l) * 4);
+    const f4v t41 = ld4(dec + DT4 + ((1 * 4 + hb) * 64 + l) * 4);
 #pragma unroll
-    for (int c = 0; c < NC / 2; ++c) g2[c] = pfma(gz, u2[c], g2[c]);
-  }
+    for (int sb = 0; sb < 4; ++sb) {
+      const f4v z = layer1(ta, tb, b, xa[sb], xb[sb]);
+      f4v gh = f4v{0.f, 0.f, 0.f, 0.f};
+      gh = mfma4(t3[0], gyb[sb][0], gh);
+      gh = mfma4(t3[1], gyb[sb][1], gh);
+      gh = mfma4(t3[2], gyb[sb][2], gh);
 #pragma unroll
-  for (int c = 0; c < NC / 2; ++c) {
-    gx[2 * c] = g2[c].x;
-    gx[2 * c + 1] = g2[c].y;
+      for (int r = 0; r < 4; ++r) {
+        const float gz = gh[r] * softplus_grad(z[r]);
+        gxo[0][sb] = mfma4(t40[r], gz, gxo[0][sb]);
+        gxo[1][sb] = mfma4(t41[r], gz, gxo[1][sb]);
+      }
+    }
   }
 }
 
@@ -511,10 +526,8 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
     }
   }
   NFI_STAMP(1)
-  float x[NC];
-  load_row(X, lane_id(), x);
   float y[NO];
-  mlp_forward(a.field.dec, x, y);
+  mlp_forward_tile(a.field.dec, X, y);
   NFI_STAMP(2)
   if (lane_id() < npts) {
     const int N = a.fine ? 2 * a.S : a.S;
@@ -543,7 +556,7 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 // Forward kernel.  SPL = coarse samples per lane (S <= 64*SPL), NPL = merged per lane.
 // ---------------------------------------------------------------------------------------
 template <int SPL, int NPL, bool FINE>
-__global__ void __launch_bounds__(256) render_fwd_kernel(nfi_render_args a) {
+__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? 3 : 2) render_fwd_kernel(nfi_render_args a) {
   constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
   constexpr int WL = XTILE + 6 * NMAX + 2 * SMAX + 8;
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
@@ -944,7 +957,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 // and decoder, sigma/colour head backward, decoder input-gradient, per-sample feature
 // gradient -> gfeat (d planes is summed per tile afterwards), palette partial, and the
 // grid_sampler_2d d-grid -> d ray origins/directions (re-gather, generator.py:312-326).
-__global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
+__global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -977,17 +990,21 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     point_params(R.o, R.d, te, sr, pv.R, P);
     pmask = P.mask;
   }
-  // decoder inputs saved by the forward (no re-gather here)
-  float x[NC];
+  // decoder inputs saved by the forward (no re-gather here), loaded straight into the MFMA
+  // operand layout: lane (j, q) takes channels 8q..8q+7 of points 16sb + j
+  f4v xa[4], xb[4];
   {
-    const float4* xr = reinterpret_cast<const float4*>(a.x_saved + (r * N + ei) * NC);
+    const int j = l & 15, q = l >> 4;
 #pragma unroll
-    for (int k = 0; k < NC / 4; ++k) {
-      const float4 q = v ? xr[k] : make_float4(0.f, 0.f, 0.f, 0.f);
-      x[4 * k] = q.x;
-      x[4 * k + 1] = q.y;
-      x[4 * k + 2] = q.z;
-      x[4 * k + 3] = q.w;
+    for (int sb = 0; sb < 4; ++sb) {
+      const int ip = e * 64 + 16 * sb + j;
+      xa[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+      xb[sb] = xa[sb];
+      if (ip < N) {
+        const float* xr = a.x_saved + (r * N + (int)a.perm[r * N + ip]) * NC + 8 * q;
+        xa[sb] = ld4(xr);
+        xb[sb] = ld4(xr + 4);
+      }
     }
   }
   NFI_STAMP(17)
@@ -1043,16 +1060,45 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
     const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
     if (l < NA * 3) g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = sh;
   }
+  // dY^T operands through the tile: row = point, 12 columns (11 outputs + zero)
+  wave_lds_sync();
+#pragma unroll
+  for (int o = 0; o < NO; ++o) X[l * XS + o] = gy[o];
+  X[l * XS + NO] = 0.f;
+  bool nz = false;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) nz |= (gy[o] != 0.f);
+  // points with an exactly-zero output gradient have a zero feature gradient (linear): the
+  // coordinate re-gather skips them
+  const unsigned long long live = __ballot(nz && v);
+  wave_lds_sync();
+  float gyb[4][3];
+  {
+    const int j = l & 15, q = l >> 4;
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+  }
   NFI_STAMP(18)
-  float gx[NC];
-  mlp_backward(a.field.dec, x, gy, gx);
+  f4v gxo[2][4];
+  mlp_backward_mfma(a.field.dec, xa, xb, gyb, gxo);
   NFI_STAMP(19)
+  // x = (e1+e2+e3)/3: each plane's tap feature gradient is dX/3.  Lane (j, q) holds channels
+  // 16cb + 4q.. of point 16sb + j: to gfeat and (for the coordinate re-gather) the tile
+  wave_lds_sync();
+  {
+    const int j = l & 15, q = l >> 4;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) gx[c] = gx[c] * (1.f / 3.f);   // x = (e1+e2+e3)/3
-  if (v) {
-    float4* gr = reinterpret_cast<float4*>(g.gfeat + (r * N + i) * NC);
+    for (int sb = 0; sb < 4; ++sb) {
+      const int ip = e * 64 + 16 * sb + j;
 #pragma unroll
-    for (int k = 0; k < NC / 4; ++k) gr[k] = make_float4(gx[4 * k], gx[4 * k + 1], gx[4 * k + 2], gx[4 * k + 3]);
+      for (int cb = 0; cb < 2; ++cb) {
+        const f4v gv = gxo[cb][sb] * (1.f / 3.f);
+        if (ip < N) *reinterpret_cast<f4v*>(g.gfeat + (r * N + ip) * NC + 16 * cb + 4 * q) = gv;
+        *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 16 * cb + 4 * q) = gv;
+      }
+    }
   }
   NFI_STAMP(20)
   if (g.cursor) {
@@ -1070,13 +1116,6 @@ __global__ void __launch_bounds__(256) field_bwd_kernel(nfi_render_args a, BwdAr
   }
   NFI_STAMP(21)
   if (!dcoord) return;
-  bool nz = false;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) nz |= (gx[c] != 0.f);
-  // points with an exactly-zero feature gradient move no coordinate: skip their re-gather
-  const unsigned long long live = __ballot(nz && v);
-  wave_lds_sync();
-  store_row(X, l, gx);
   wave_lds_sync();
   // d ray origin / direction: dL/dp_j = sum_q (d grid_q) * (R-1)/2 * inbound / scene_range and
   // dL/d ro = sum_j dL/dp_j, dL/d rd = sum_j t_j dL/dp_j are linear in the per-lane products,
