@@ -969,7 +969,6 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
   if (e * 64 >= N) return;
   NFI_STAMP_INIT
   float* X = lds + wv * XTILE;
-  const bool dcoord = g.g_ro != nullptr;
   const float sr = a.field.scene_range;
   RayCtx R;
   load_ray(a, r, R);
@@ -979,7 +978,6 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
   const float gr0 = g.g_rgb[r * 3 + 0], gr1 = g.g_rgb[r * 3 + 1], gr2 = g.g_rgb[r * 3 + 2];
   NFI_STAMP(16)
 
-  const int npts = min(64, N - e * 64);
   const int i = e * 64 + l;
   const bool v = i < N;
   const float te = v ? a.t_saved[r * N + i] : R.near_;
@@ -1065,12 +1063,6 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
 #pragma unroll
   for (int o = 0; o < NO; ++o) X[l * XS + o] = gy[o];
   X[l * XS + NO] = 0.f;
-  bool nz = false;
-#pragma unroll
-  for (int o = 0; o < NO; ++o) nz |= (gy[o] != 0.f);
-  // points with an exactly-zero output gradient have a zero feature gradient (linear): the
-  // coordinate re-gather skips them
-  const unsigned long long live = __ballot(nz && v);
   wave_lds_sync();
   float gyb[4][3];
   {
@@ -1085,8 +1077,7 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
   mlp_backward_mfma(a.field.dec, xa, xb, gyb, gxo);
   NFI_STAMP(19)
   // x = (e1+e2+e3)/3: each plane's tap feature gradient is dX/3.  Lane (j, q) holds channels
-  // 16cb + 4q.. of point 16sb + j: to gfeat and (for the coordinate re-gather) the tile
-  wave_lds_sync();
+  // 16cb + 4q.. of point 16sb + j
   {
     const int j = l & 15, q = l >> 4;
 #pragma unroll
@@ -1096,7 +1087,6 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
       for (int cb = 0; cb < 2; ++cb) {
         const f4v gv = gxo[cb][sb] * (1.f / 3.f);
         if (ip < N) *reinterpret_cast<f4v*>(g.gfeat + (r * N + ip) * NC + 16 * cb + 4 * q) = gv;
-        *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 16 * cb + 4 * q) = gv;
       }
     }
   }
@@ -1115,19 +1105,53 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
     }
   }
   NFI_STAMP(21)
-  if (!dcoord) return;
+}
+
+// Ray-coordinate gradient of one chunk of 64 merged samples of one ray (one wave): the
+// grid_sampler_2d d-grid (generator.py:312-326) re-gathers the taps and dots them with the
+// per-sample feature gradients gfeat written by field_bwd.  dL/dp_j = sum_q (d grid_q) * (R-1)/2
+// * inbound / scene_range; dL/d ro = sum_j dL/dp_j and dL/d rd = sum_j t_j dL/dp_j are linear in
+// the per-lane products, so every lane accumulates its share and the wave is reduced once.
+// A separate kernel from field_bwd: it is memory-latency bound and runs at higher occupancy.
+__device__ __forceinline__ void dcoord_job(const nfi_render_args& a, const BwdArgs& g, long long job,
+                                           float* __restrict__ X) {
+  const int l = lane_id();
+  const long long nrays = (long long)a.B * a.HW;
+  const long long r = job / g.npl;
+  const int e = (int)(job % g.npl);
+  if (r >= nrays) return;
+  const int N = a.fine ? 2 * a.S : a.S;
+  if (e * 64 >= N) return;
+  const float sr = a.field.scene_range;
+  RayCtx R;
+  load_ray(a, r, R);
+  const PlaneView pv{a.field.planes + (long long)R.b * a.field.sb, (int)a.field.sq, (int)a.field.st,
+                     a.field.R};
+  const int npts = min(64, N - e * 64);
+  const int i = e * 64 + l;
+  const bool v = i < N;
+  const float te = v ? a.t_saved[r * N + i] : R.near_;
+  PointP P;
+  point_params(R.o, R.d, te, sr, pv.R, P);
+  // samples outside the box have an exactly-zero feature gradient (their sigma and weight are 0)
+  const unsigned long long live = __ballot(v && P.mask == 0.f);
+  // gradient rows of the chunk -> tile (coalesced: 1 KiB per instruction)
+  {
+    const float4* src = reinterpret_cast<const float4*>(g.gfeat + (r * N + e * 64) * NC);
+#pragma unroll
+    for (int k = 0; k < NC / 4; ++k) {
+      const int q = k * 64 + l;
+      const float4 val = (q < npts * (NC / 4)) ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(X + (q >> 3) * XS + 4 * (q & 7)) = val;
+    }
+  }
   wave_lds_sync();
-  // d ray origin / direction: dL/dp_j = sum_q (d grid_q) * (R-1)/2 * inbound / scene_range and
-  // dL/d ro = sum_j dL/dp_j, dL/d rd = sum_j t_j dL/dp_j are linear in the per-lane products,
-  // so every lane accumulates its share over all points and the wave is reduced once.
-  // Re-gather in the quad layout of gather_features (4 points per wave instruction).
+  // re-gather in the quad layout of gather_features (4 points per wave instruction)
   float aro0 = 0.f, aro1 = 0.f, aro2 = 0.f, ard0 = 0.f, ard1 = 0.f, ard2 = 0.f;
   {
-    PointP P;
-    point_params(R.o, R.d, te, sr, pv.R, P);
     const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
     const int ngrp = (npts + 3) >> 2;
-    constexpr int GB = 4;   // (field_bwd has the VGPRs for 4 groups in flight)
+    constexpr int GB = 2;
 #pragma unroll 1
     for (int gb = 0; gb < ngrp; gb += GB) {
       if (((live >> (4 * gb)) & ((1ull << (4 * GB)) - 1ull)) == 0ull) continue;
@@ -1154,11 +1178,11 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
         float GX[3], GY[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
+          const float e_ = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
           const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
           const float gxm = __shfl(P.pl[q].gxm, j), gym = __shfl(P.pl[q].gym, j);
           const float4 v0 = V0[u][q], v1 = V1[u][q];
-          const float wx = dx ? w : e;
+          const float wx = dx ? w : e_;
           // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
           const float ax = (s * v0.x + n * v1.x) * gv.x + (s * v0.y + n * v1.y) * gv.y +
                            (s * v0.z + n * v1.z) * gv.z + (s * v0.w + n * v1.w) * gv.w;
@@ -1178,7 +1202,6 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
       }
     }
   }
-  NFI_STAMP(22)
   const float gro0 = wave_sum(aro0) / sr, gro1 = wave_sum(aro1) / sr, gro2 = wave_sum(aro2) / sr;
   const float grd0 = wave_sum(ard0) / sr, grd1 = wave_sum(ard1) / sr, grd2 = wave_sum(ard2) / sr;
   if (l == 0) {
@@ -1189,7 +1212,6 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
     unsafeAtomicAdd(g.g_rd + r * 3 + 1, grd1);
     unsafeAtomicAdd(g.g_rd + r * 3 + 2, grd2);
   }
-  NFI_STAMP(23)
 }
 
 struct BinArgs {
@@ -1316,20 +1338,50 @@ typedef float img32 __attribute__((ext_vector_type(32)));
 typedef int iv4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(4))) iv4* cint4_p;
 
-// gradient-row stage: row u's float4 k lives at slot k ^ (u & 7) (conflict-free b128 stores)
-__device__ __forceinline__ int stage_at(int u, int c) { return u * NC + ((((c >> 2) ^ (u & 7))) << 2) + (c & 3); }
+// gradient-row stage: rows of XS = 36 floats (the 4-float pad makes both the per-lane b128 row
+// stores and the per-entry row reads conflict-free, with immediate-offset addressing)
+__device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 
-__global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
-  __shared__ __attribute__((aligned(16))) float lds[4 * 64 * NC];   // per-wave row stage, then images
+// img[slot] += a0, img[slot + 1] += a1 for a wave-uniform slot: M0-indexed source AND
+// destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
+// v[40:71] at these points so the asm can name its base register.
+__device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1) {
+  asm volatile(
+      "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
+      "v_add_f32 v40, v40, %2\n\t"
+      "v_add_f32 v41, v41, %3\n\t"
+      "s_set_gpr_idx_off"
+      : "+{v[40:71]}"(img)
+      : "s"(slot), "v"(a0), "v"(a1));
+}
+
+// One entry: run-merge into (a0, a1) while the cell repeats, else flush to the image.
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, const iv4 rc, float g,
+                                           float wsgn, float woff, bool ok) {
+  const int slot = __builtin_amdgcn_readfirstlane(rc.y) & 31;
+  const float w = __int_as_float(rc.z), nn = __int_as_float(rc.w);
+  const float gw = ok ? g * fmaf(nn, wsgn, woff) : 0.f;
+  if (slot != cur) {
+    img_add(img, cur, a0, a1);
+    a0 = 0.f;
+    a1 = 0.f;
+    cur = slot;
+  }
+  a0 = fmaf(gw, 1.f - w, a0);
+  a1 = fmaf(gw, w, a1);
+}
+
+// One workgroup-chunk c (< meta[0]) of a tile's entries; lds: 4 * XTILE floats.
+__device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict__ lds, int c) {
   const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = lane_id();
   const int h = l >> 5, cl = l & 31;
-  float* G = lds + wv * 64 * NC;
+  float* G = lds + wv * XTILE;
   // half 0 weights row ly by (1 - n), half 1 row ly + 1 by n
   const float wsgn = h ? 1.f : -1.f, woff = h ? 0.f : 1.f;
   const cint4_p L = (cint4_p)A.list;
-  const int total = A.meta[0];
   const int tpp = A.tg.nx * A.tg.ny;
-  for (int c = blockIdx.x; c < total; c += gridDim.x) {
+  NFI_STAMP_INIT
+  {
     // (wave-uniform scalars: readfirstlane keeps the entry loop's control and the register-image
     // index in SGPRs)
     const int tile = __builtin_amdgcn_readfirstlane(A.chunk_tile[c]);
@@ -1359,48 +1411,46 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
       for (int base = b0; base < b1; base += 64) {
         const int n = min(64, b1 - base);
         {
-          float4* dst = reinterpret_cast<float4*>(G + l * NC);
-          const int sw = l & 7;
-          dst[0 ^ sw] = r0; dst[1 ^ sw] = r1; dst[2 ^ sw] = r2; dst[3 ^ sw] = r3;
-          dst[4 ^ sw] = r4; dst[5 ^ sw] = r5; dst[6 ^ sw] = r6; dst[7 ^ sw] = r7;
+          float4* dst = reinterpret_cast<float4*>(G + l * XS);
+          dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
+          dst[4] = r4; dst[5] = r5; dst[6] = r6; dst[7] = r7;
         }
         // next 64 rows load while these are summed
         vrec = A.list[min(base + 64 + l, b1 - 1)];
         NFI_LOAD_ROW(vrec)
         wave_lds_sync();
-        // 8 entries per step; records past the chunk end read the list's padding / the next
-        // tile's entries (in bounds) and contribute exactly nothing
+        NFI_STAMP(24)
+        // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed;
+        // records past the chunk end read the next tile's entries or the list padding (in
+        // bounds) and are masked in the last, partial step
+        iv4 rc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rc[k] = L[base + k];
         for (int u = 0; u < n; u += 8) {
-          iv4 rc[8];
           float gv[8];
+          iv4 rn[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            rc[k] = L[base + u + k];
-            gv[k] = G[stage_at((u + k) & 63, cl)];
+            gv[k] = G[stage_at(u + k, cl)];
+            rn[k] = L[base + u + 8 + k];
+          }
+          if (u + 8 <= n) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) tile_entry(img, cur, a0, a1, rc[k], gv[k], wsgn, woff, true);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) tile_entry(img, cur, a0, a1, rc[k], gv[k], wsgn, woff, u + k < n);
           }
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const bool ok = u + k < n;
-            const int slot = ok ? (__builtin_amdgcn_readfirstlane(rc[k].y) & 31) : 0;
-            const float w = __int_as_float(rc[k].z), nn = __int_as_float(rc[k].w);
-            const float gw = ok ? gv[k] * fmaf(nn, wsgn, woff) : 0.f;
-            if (slot != cur) {
-              img[cur] += a0;
-              img[cur + 1] += a1;
-              a0 = 0.f;
-              a1 = 0.f;
-              cur = slot;
-            }
-            a0 = fmaf(gw, 1.f - w, a0);
-            a1 = fmaf(gw, w, a1);
-          }
+          for (int k = 0; k < 8; ++k) rc[k] = rn[k];
         }
         wave_lds_sync();
+        NFI_STAMP(25)
       }
 #undef NFI_LOAD_ROW
-      img[cur] += a0;
-      img[cur + 1] += a1;
+      img_add(img, cur, a0, a1);
     }
+    NFI_STAMP(26)
     __syncthreads();   // every wave is done with its row stage
     // wave images -> LDS [wave][half][slot][channel]
 #pragma unroll
@@ -1413,7 +1463,7 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
       float v = 0.f;
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
-        const float* im = lds + w4 * 64 * NC;
+        const float* im = lds + w4 * XTILE;
         if (yl < TSY) v += im[(yl * TTX + xl) * NC + ch];
         if (yl >= 1) v += im[(32 + (yl - 1) * TTX + xl) * NC + ch];
       }
@@ -1421,6 +1471,30 @@ __global__ void __launch_bounds__(256) tile_accum_kernel(TileArgs A) {
       if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
     }
     __syncthreads();
+    NFI_STAMP(27)
+  }
+}
+
+constexpr int FUSED_LDS = 4 * XTILE;
+
+// d planes (tile chunks) and ray-coordinate gradients (dcoord jobs) in ONE launch, the two roles
+// interleaved over the grid so a CU runs both at once: the register-image tile sums are bound by
+// their VALU/SALU dependency chains, the coordinate re-gather by memory latency, and each fills
+// the other's stalls.  With T = meta[0] chunks, block b < T + DB is a tile block iff
+// floor((b+1) T / (T+DB)) > floor(b T / (T+DB)); the grid is sized for a bound on T and the
+// blocks past T + DB exit at once.
+__global__ void __launch_bounds__(256, 4) tile_dcoord_kernel(TileArgs A, nfi_render_args a, BwdArgs g,
+                                                             long long DB) {
+  __shared__ __attribute__((aligned(16))) float lds[FUSED_LDS];
+  const long long T = A.meta[0];
+  const long long b = blockIdx.x, tot = T + DB;
+  if (b >= tot) return;
+  const long long t0 = b * T / tot, t1 = (b + 1) * T / tot;
+  if (t1 > t0) {
+    tile_chunk(A, lds, (int)t0);
+  } else {
+    const int wv = threadIdx.x >> 6;
+    dcoord_job(a, g, (b - t0) * 4 + wv, lds + wv * XTILE);
   }
 }
 
@@ -1461,7 +1535,7 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.meta = reinterpret_cast<int*>(take(16));
   // chunks <= ceil(entries / CHUNK) + K  (each tile wastes at most one partial chunk)
   w.chunk_tile = reinterpret_cast<int*>(take((3 * nsamp / CHUNK + K + 1) * 4));
-  w.list = reinterpret_cast<int4*>(take((3 * nsamp + 64) * 16));   // + padding read by tile_accum
+  w.list = reinterpret_cast<int4*>(take((3 * nsamp + 128) * 16));   // + padding read by tile_chunk
   w.bytes = p - static_cast<char*>(base);
   return w;
 }
@@ -1526,12 +1600,15 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
-  // 3) per-tile register accumulation of d planes
   TileArgs TA{w.gfeat, counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list, g->d_planes, a->field.sb,
               (int)a->field.sq, (int)a->field.st, a->field.R, tg};
   if (do_tiles) {
-    tile_accum_kernel<<<4096, 256, 0, s>>>(TA);
-    NFI_CHECK_LAUNCH("tile_accum_kernel");
+    // 3) + 4) per-tile register accumulation of d planes || coordinate gradients (one launch)
+    const long long TB = 3 * nsamp / CHUNK + K + 1;
+    const long long DB = g->g_ro ? (nrays * NPL + 3) / 4 : 0;
+    NFI_REQUIRE(TB + DB < (1LL << 31), "render_backward: grid too large");
+    tile_dcoord_kernel<<<(unsigned)(TB + DB), 256, 0, s>>>(TA, *a, bg, DB);
+    NFI_CHECK_LAUNCH("tile_dcoord_kernel");
   }
   return NFI_OK;
 }

@@ -23,6 +23,7 @@ from nfi import _lib  # noqa: E402
 FWD = ['setup', 'gather', 'mlp', 'head+save y', 'weights+pdf', 'merge', 'composite+save', 'tile counts', 'sums']
 BWD = ['setup', 'gather', 'y+head bwd+palette', 'mlp bwd', 'gfeat write', 'bin append', 'd-coord regather',
        'ray atomics']
+TILE = ['row wait + stage', 'entry loop', 'tail (first rows)', 'merge + flush']
 
 
 def main():
@@ -55,6 +56,10 @@ def main():
     print('field_bwd (one wave per 64-sample chunk)')
     for k, n in enumerate(BWD):
         print(f'  {n:22s} {out[16 + k] / bwd_waves:10.0f}  {100 * out[16 + k] / max(tot, 1):5.1f}%')
+    tot = sum(out[24 + k] for k in range(len(TILE)))
+    print('tile chunks (cycles summed over tile waves, per step)')
+    for k, n in enumerate(TILE):
+        print(f'  {n:22s} {out[24 + k] / steps:14.0f}  {100 * out[24 + k] / max(tot, 1):5.1f}%')
 
 
 if __name__ == '__main__':
