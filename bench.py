@@ -163,15 +163,24 @@ def main():
     value = world * samples_per_step * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel (SURVEY §8(d) algorithmic bytes per sample):
-    # forward tap 1,536 B; field backward: coordinate re-gather 1,536 B (pose) / 0; tile
-    # accumulation: d planes scatter-add 1,536 B; binning: 12 B of keys/ids.
-    per_sample = {'render_fwd': TAP_BYTES, 'bwd_field': TAP_BYTES if pose else 4 * 32,
-                  'bwd_tiles': TAP_BYTES, 'bwd_bins': 12}
+    # roofline of the dominant stage (DESIGN.md "Kernels and their rooflines"):
+    # algorithmic tap bytes per sample — forward 1,536 B; backward d-planes scatter 1,536 B plus the
+    # pose re-gather 1,536 B (both in the bwd_tiles launch); the field backward touches no taps
+    # (its streamed per-sample state is ~380 B) — and fp32 FLOPs per sample (forward 6,450,
+    # field backward 5,700 of which 5,504 on MFMA, tiles 768 + 768).  Taps are served largely by
+    # L2 / Infinity Cache, so the tap rate can exceed the HBM peak: 'traffic' (rocprofv3 PMC) is
+    # what actually crossed HBM per launch.
+    model = {
+        'render_fwd': (TAP_BYTES + 194, 6450),
+        'bwd_bins': (12, 0),
+        'bwd_field': (380, 5700),
+        'bwd_tiles': (TAP_BYTES * (2 if pose else 1) + 48 + 3 * 128, 768 * (2 if pose else 1)),
+    }
     kernel_of = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
-                 'bwd_tiles': 'tile_accum_kernel', 'bwd_bins': 'bin_fill_kernel'}
+                 'bwd_tiles': 'tile_dcoord_kernel', 'bwd_bins': 'bin_scan_kernel'}
     dom = max(kern, key=kern.get)
-    achieved = samples_per_step * per_sample[dom] / (kern[dom] * 1e-3) / 1e9
+    sec = kern[dom] * 1e-3
+    achieved = samples_per_step * model[dom][0] / sec / 1e9
     traffic = None
     try:
         with open(os.path.join(ROOT, 'profiles', 'latest_counters.json')) as fh:
@@ -180,11 +189,18 @@ def main():
             traffic = round(ctr['hbm_bytes_corrected'] / 1e9, 3)
     except (OSError, ValueError, KeyError):
         pass
+    stages = {k: {'ms': round(v, 4),
+                  'tap_GBps': round(samples_per_step * model[k][0] / (v * 1e-3) / 1e9, 1),
+                  'fp32_TFLOPs': round(samples_per_step * model[k][1] / (v * 1e-3) / 1e12, 2)}
+              for k, v in kern.items() if k in model}
     roof = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
             'traffic': traffic, 'traffic_unit': 'GB per launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE, '
                                                 'profiles/latest_counters.json)',
-            'bytes_per_sample': per_sample[dom], 'ms_per_launch': {k: round(v, 4) for k, v in kern.items()}}
+            'bytes_per_sample': model[dom][0],
+            'hbm_frac_measured': (round(traffic / sec / HBM_PEAK_GBS, 4) if traffic else None),
+            'fp32_TFLOPs': stages[dom]['fp32_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
+            'stages': stages}
 
     out = {
         'metric': 'Msamples/sec fwd+bwd (128^2, 64+64 samples/ray)' if bwd else 'Msamples/sec fwd (128^2, 64+64)',

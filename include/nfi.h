@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 6
+#define NFI_ABI_VERSION 7
 #define NFI_DEC_SIZE 7184 /* floats in the packed decoder buffer */
 
 enum {
@@ -81,6 +81,9 @@ typedef struct nfi_render_args {
   int32_t fine;        /* args.fine_sampling (run.py:259) */
   int32_t white_bg;    /* dataset_config['white_background'] */
   int32_t randomize;   /* stratified jitter + random u in sample_pdf (else linspace) */
+  int32_t W;           /* image width (HW = H*W): with H, W multiples of 16 the kernels walk rays in
+                          16x16-pixel tiles dealt round-robin over the XCDs (L2 locality); 0 = off */
+  int32_t _pad3;
   uint64_t seed, offset;       /* Philox stream when u_* are NULL */
   const float* u_coarse;       /* optional [B*HW,S] injected jitter (nerf_utils.py:120) */
   const float* u_fine;         /* optional [B*HW,S] injected u (nerf_utils.py:202-205) */

@@ -545,6 +545,27 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   NFI_STAMP(3)
 }
 
+// Ray order for L2 locality: with H, W multiples of 16 (W = a.W), physical block b (RB consecutive
+// rays of one pixel row per block, RB | 16) is mapped so that the 8 XCDs (blocks are dealt
+// round-robin: b and b+8 share one) each walk whole 16x16-pixel tiles, tile T going to XCD
+// T % 8: the rays an XCD has in flight are a compact patch of the image, and all XCDs stay on
+// nearby tiles of one image (Infinity Cache).  Bijective; identity when the shape does not tile.
+__device__ __forceinline__ long long ray_of_block(unsigned b, int RB, const nfi_render_args& a) {
+  const int W = a.W;
+  if (W <= 0 || W % 16 || a.HW % W) return (long long)b * RB;
+  const int H = a.HW / W;
+  const int tx_n = W / 16, ty_n = H / 16;
+  const long long tpi = (long long)tx_n * ty_n, NT = (long long)a.B * tpi;
+  if (H % 16 || NT % 8) return (long long)b * RB;
+  const int TBR = 16 / RB, TB = 16 * TBR;   // blocks per tile row / per tile
+  const unsigned x = b & 7, k = b >> 3;
+  const long long T = (long long)(k / TB) * 8 + x;
+  const int j = (int)(k % TB);
+  const long long img = T / tpi, rem = T % tpi;
+  const int row = (int)(rem / tx_n) * 16 + j / TBR, col = (int)(rem % tx_n) * 16 + (j % TBR) * RB;
+  return (img * H + row) * W + col;
+}
+
 // alpha_i = 1 - exp(-sigma_i * dist_i),  a_i = 1 - alpha_i + 1e-10  (nerf_utils.py:136-146)
 __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, float& aa, float& ex) {
   ex = expf(fmul(-sigma, dist));
@@ -562,7 +583,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? 3 : 2) render_fw
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
-  const long long r = (long long)blockIdx.x * 4 + wv;
+  const long long r = ray_of_block(blockIdx.x, 4, a) + wv;
   if (r >= nrays) return;
   NFI_STAMP_INIT
   const int S = a.S;
@@ -884,7 +905,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
   __shared__ float lds[4 * (NMAX + 8)];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
-  const long long r = (long long)blockIdx.x * 4 + wv;
+  const long long r = ray_of_block(blockIdx.x, 4, a) + wv;
   if (r >= nrays) return;
   const int N = a.fine ? 2 * a.S : a.S;
   float* Lt = lds + wv * (NMAX + 8);
@@ -961,7 +982,10 @@ __global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, Bw
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
-  const long long job = (long long)blockIdx.x * 4 + wv;
+  // (npl chunks per ray, 4 jobs per block: 4 / npl rays per block)
+  const long long job = (g.npl <= 4 && 4 % g.npl == 0)
+                            ? ray_of_block(blockIdx.x, 4 / g.npl, a) * g.npl + wv
+                            : (long long)blockIdx.x * 4 + wv;
   const long long r = job / g.npl;
   const int e = (int)(job % g.npl);
   if (r >= nrays) return;

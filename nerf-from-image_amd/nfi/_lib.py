@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 6
+ABI_VERSION = 7
 DEC_SIZE = 7184
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -37,7 +37,8 @@ class NfiRenderArgs(ctypes.Structure):
     _fields_ = [('field', NfiField), ('ro', c_void_p), ('rd', c_void_p), ('near_', c_void_p),
                 ('far_', c_void_p), ('B', ctypes.c_int32), ('HW', ctypes.c_int32),
                 ('S', ctypes.c_int32), ('fine', ctypes.c_int32), ('white_bg', ctypes.c_int32),
-                ('randomize', ctypes.c_int32), ('seed', ctypes.c_uint64),
+                ('randomize', ctypes.c_int32), ('W', ctypes.c_int32), ('_pad3', ctypes.c_int32),
+                ('seed', ctypes.c_uint64),
                 ('offset', ctypes.c_uint64), ('u_coarse', c_void_p), ('u_fine', c_void_p),
                 ('rgb', c_void_p), ('depth', c_void_p), ('mask', c_void_p),
                 ('t_saved', c_void_p), ('sigma_saved', c_void_p), ('rgb_saved', c_void_p),

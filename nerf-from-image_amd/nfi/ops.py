@@ -257,6 +257,7 @@ class _VolumeRender(torch.autograd.Function):
     @staticmethod
     def _args(planes_tm, dec, pal, ro, rd, near, far, opts, B, HW, uc, uf, seed, rgb, depth, mask,
               t_saved, s_saved, c_saved, y_saved, perm, zc, zf):
+        W = ro.shape[2] if ro.dim() == 4 else 0
         R = planes_tm.shape[2]
         field = _lib.NfiField(planes=_ptr(planes_tm), sb=planes_tm.stride(0), sq=planes_tm.stride(1),
                               st=planes_tm.stride(3), R=R, _pad=0, dec=_ptr(dec), palette=_ptr(pal),
@@ -265,6 +266,7 @@ class _VolumeRender(torch.autograd.Function):
         return _lib.NfiRenderArgs(field=field, ro=_ptr(ro), rd=_ptr(rd), near_=_ptr(near), far_=_ptr(far),
                                   B=B, HW=HW, S=opts.samples, fine=int(opts.fine),
                                   white_bg=int(opts.white_background), randomize=int(opts.randomize),
+                                  W=int(W),
                                   seed=seed & ((1 << 64) - 1), offset=0, u_coarse=_ptr(uc),
                                   u_fine=_ptr(uf), rgb=_ptr(rgb), depth=_ptr(depth), mask=_ptr(mask),
                                   t_saved=_ptr(t_saved), sigma_saved=_ptr(s_saved),
