@@ -577,9 +577,15 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 // Forward kernel.  SPL = coarse samples per lane (S <= 64*SPL), NPL = merged per lane.
 // ---------------------------------------------------------------------------------------
 template <int SPL, int NPL, bool FINE>
-__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? 3 : 2) render_fwd_kernel(nfi_render_args a) {
+#ifndef NFI_FWD_OCC
+#define NFI_FWD_OCC 3
+#endif
+__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? NFI_FWD_OCC : 2) render_fwd_kernel(nfi_render_args a) {
   constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
-  constexpr int WL = XTILE + 6 * NMAX + 2 * SMAX + 8;
+  // per-wave LDS: the X tile; the merge / sample_pdf arrays alias it (they are live only
+  // outside field_eval), which keeps a workgroup at 36 KiB
+  constexpr int WL = XTILE;
+  static_assert(6 * NMAX + 2 * SMAX <= XTILE, "merge arrays must fit in the X tile");
   __shared__ __attribute__((aligned(16))) float lds[4 * WL];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -589,7 +595,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? 3 : 2) render_fw
   const int S = a.S;
   const int N = FINE ? 2 * S : S;
   float* X = lds + wv * WL;
-  float* Mt = X + XTILE;          // merged t     [NMAX]
+  float* Mt = X;                  // merged t     [NMAX]
   float* Ms = Mt + NMAX;          // merged sigma [NMAX]
   float* Mc = Ms + NMAX;          // merged rgb   [3][NMAX]
   int* Mi = reinterpret_cast<int*>(Mc + 3 * NMAX);   // merged -> evaluation index [NMAX]
@@ -978,7 +984,10 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 // and decoder, sigma/colour head backward, decoder input-gradient, per-sample feature
 // gradient -> gfeat (d planes is summed per tile afterwards), palette partial, and the
 // grid_sampler_2d d-grid -> d ray origins/directions (re-gather, generator.py:312-326).
-__global__ void __launch_bounds__(256, 3) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
+#ifndef NFI_FIELD_OCC
+#define NFI_FIELD_OCC 4
+#endif
+__global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -1370,6 +1379,10 @@ __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 // destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
 // v[40:71] at these points so the asm can name its base register.
 __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1) {
+#if defined(NFI_ABLATE) && NFI_ABLATE == 1
+  img[0] += a0 + a1 + (float)slot;   // experiment: no indexed update
+  return;
+#endif
   asm volatile(
       "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
       "v_add_f32 v40, v40, %2\n\t"
@@ -1458,6 +1471,12 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
             gv[k] = G[stage_at(u + k, cl)];
             rn[k] = L[base + u + 8 + k];
           }
+#if defined(NFI_ABLATE) && NFI_ABLATE == 2
+          if (true) {   // experiment: entries only loaded
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a0 += gv[k] + __int_as_float(rc[k].z);
+          } else
+#endif
           if (u + 8 <= n) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) tile_entry(img, cur, a0, a1, rc[k], gv[k], wsgn, woff, true);

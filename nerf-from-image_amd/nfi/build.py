@@ -31,7 +31,9 @@ def build(force: bool = False, verbose: bool = True, variant: str = '') -> str:
     if not force and not variant and not _stale():
         return out
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-    extra = {'': [], 'stamps': ['-DNFI_STAMPS']}[variant]
+    extra = {'': [], 'stamps': ['-DNFI_STAMPS']}.get(variant)
+    if extra is None:   # experiment builds: 'D<NAME>=<value>' -> -D<NAME>=<value>
+        extra = ['-' + variant] if variant.startswith('D') else []
     cmd = [hipcc] + FLAGS + extra + ['-o', out + '.tmp'] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(' '.join(cmd), file=sys.stderr)
@@ -41,4 +43,10 @@ def build(force: bool = False, verbose: bool = True, variant: str = '') -> str:
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv, variant='stamps' if '--stamps' in sys.argv else '')
+    var = ''
+    if '--stamps' in sys.argv:
+        var = 'stamps'
+    for a in sys.argv:
+        if a.startswith('--variant='):
+            var = a.split('=', 1)[1]
+    build(force='--force' in sys.argv, variant=var)
