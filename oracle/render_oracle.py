@@ -21,9 +21,11 @@ reference bit for bit.
 
 from __future__ import annotations
 
+import contextlib
 import math
 from dataclasses import dataclass
 from typing import Optional
+
 
 import torch
 import torch.nn.functional as F
@@ -99,8 +101,9 @@ def compute_query_points_from_rays(ray_origins, ray_directions, near_thresh, far
 
 
 def render_volume_density(sigma_a, rgb, ray_origins, ray_directions, depth_values,
-                          white_background: bool = True):
-    """nerf_utils.py:125-163 (normals/semantics maps omitted: out of scope, §8(f) #3)."""
+                          white_background: bool = True, normals=None, semantics=None):
+    """nerf_utils.py:125-163.  Returns (rgb, depth, mask) or, when normals / semantics are given,
+    (rgb, depth, mask, normal_map, semantic_map) (normals composited with detached weights)."""
     zero_tensor = torch.zeros((1,), dtype=ray_origins.dtype, device=ray_origins.device)
     dists = torch.cat((depth_values[..., 1:] - depth_values[..., :-1],
                        zero_tensor.expand(depth_values[..., :1].shape)), dim=-1)
@@ -109,10 +112,16 @@ def render_volume_density(sigma_a, rgb, ray_origins, ray_directions, depth_value
     weights = alpha * cumprod_exclusive(1. - alpha + 1e-10)
     rgb_map = (weights[..., None] * rgb).sum(dim=-2)
     depth_map = (weights.detach() * depth_values.detach()).sum(dim=-1)
+    normal_map = (weights[..., None].detach() * normals).sum(dim=-2) if normals is not None else None
+    semantic_map = (weights[..., None] * semantics).sum(dim=-2) if semantics is not None else None
     mask = weights.sum(-1)
     if white_background:
         rgb_map = rgb_map + (1. - mask[..., None])
-    return rgb_map, depth_map, mask
+        if normal_map is not None:
+            normal_map = normal_map + (1. - mask[..., None])
+    if normals is None and semantics is None:
+        return rgb_map, depth_map, mask
+    return rgb_map, depth_map, mask, normal_map, semantic_map
 
 
 def render_volume_density_weights_only(sigma_a, ray_origins, ray_directions, depth_values):
@@ -237,22 +246,42 @@ def triplanar_decoder(planes, coords, w1, b1, w2, b2):
     return x[..., 1:], x[..., :1]                          # features, density_or_distance
 
 
-def sampler(field: Field, x_in):
-    """The `sampler` closure generator.py:587-681 for request ['sigma','rgb'] with
-    use_sdf=True, attention_values=10, use_viewdir=False (the inversion configuration)."""
+def sampler(field: Field, x_in, extras=()):
+    """The `sampler` closure generator.py:587-681 with use_sdf=True, attention_values=10,
+    use_viewdir=False (the inversion configuration).  Returns (sigma, rgb), or with `extras` ⊂
+    {'normals','semantics','coords'} (sigma, rgb, dict): normals = normalize(d distance / d x_in)
+    by autograd (create_graph=False; sigma and rgb are then detached, :599-622), semantics = the
+    softmax probabilities (:672-674), coords = x_in (:643-644)."""
+    out = {}
+    if 'normals' in extras:
+        x_in = x_in.detach().requires_grad_()
     bs = x_in.shape[0]
     x = x_in.view(bs, -1, 1, 3) / field.scene_range
     with torch.no_grad():
         mask = (x.abs() > 1).any(dim=-1).float()
         mask = mask.flatten(1, len(mask.shape) - 1)
-    features, density_or_distance = triplanar_decoder(field.planes, x, field.w1, field.b1, field.w2, field.b2)
+    with torch.enable_grad() if 'normals' in extras else contextlib.nullcontext():
+        features, density_or_distance = triplanar_decoder(field.planes, x, field.w1, field.b1, field.w2,
+                                                          field.b2)
+    if 'normals' in extras:
+        x_grad, = torch.autograd.grad(density_or_distance[..., -1].sum(), x_in, create_graph=False)
+        out['normals'] = F.normalize(x_grad, dim=-1)
+        density_or_distance = density_or_distance.detach()
+        features = features.detach()
+        x_in = x_in.detach()
+    if 'coords' in extras:
+        out['coords'] = x_in
     beta = field.beta
     alpha = 1 / field.alpha
     neg_distance = -density_or_distance[..., -1]
     density_prealpha = laplace_cdf(neg_distance, beta) * (1 - mask)
     sigma = alpha * density_prealpha
     attention_probs = F.softmax(features, dim=-1)
+    if 'semantics' in extras:
+        out['semantics'] = attention_probs
     rgb = torch.matmul(attention_probs, field.palette)
+    if extras:
+        return sigma, rgb, out
     return sigma, rgb
 
 
@@ -264,9 +293,14 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
            depth_samples_per_ray: int, randomize: bool = True, white_background: bool = False,
            fine_sampling: bool = True, force_no_cam_grad: bool = False,
            u_coarse: Optional[torch.Tensor] = None, u_fine: Optional[torch.Tensor] = None,
-           return_intermediates: bool = False):
-    """run.py:176-350 with compute_normals/semantics/coords=False, use_viewdir=False.
-    Returns (rgb [b,H,W,3], depth [b,H,W], mask [b,H,W]) (+ intermediates dict)."""
+           return_intermediates: bool = False, compute_normals: bool = False,
+           compute_semantics: bool = False, compute_coords: bool = False):
+    """run.py:176-350 with use_viewdir=False.  Returns (rgb [b,H,W,3], depth [b,H,W],
+    mask [b,H,W]) (+ intermediates dict); with any compute_* flag (run.py:227-257, 293-335)
+    (rgb, depth, mask, normal_map [b,H,W,3] | None, semantic_map [b,H,W,10 | 3] | None) — the
+    coords map replaces the semantic map when compute_coords (run.py:334-335)."""
+    extras = tuple(n for n, f in (('normals', compute_normals), ('semantics', compute_semantics),
+                                  ('coords', compute_coords)) if f)
     ray_origins, ray_directions = get_ray_bundle(height, width, focal_length, tform_cam2world, bbox, center)
     ray_directions = F.normalize(ray_directions, dim=-1)
     with torch.no_grad():
@@ -279,9 +313,14 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
         query_points = query_points.detach()
         depth_values = depth_values.detach()
         ray_directions = ray_directions.detach()
-    sigma, rgb = sampler(field, query_points)
+    ex = {}
+    if extras:
+        sigma, rgb, ex = sampler(field, query_points, extras)
+    else:
+        sigma, rgb = sampler(field, query_points)
     sigma = sigma.view(*query_points.shape[:-1], -1)
     rgb = rgb.view(*query_points.shape[:-1], -1)
+    ex = {k: v.view(*query_points.shape[:-1], -1) for k, v in ex.items()}
     inter = {'near': near_thresh, 'far': far_thresh, 'z_coarse': depth_values,
              'ro': ray_origins.detach(), 'rd': ray_directions.detach()}
     if fine_sampling:
@@ -298,18 +337,35 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
             z_samples = z_samples.view(*z_vals.shape[:3], z_samples.shape[-1])
         z_values_sorted, z_indices_sorted = torch.sort(torch.cat((z_vals, z_samples), dim=-1), dim=-1)
         query_points_fine = ray_origins[..., None, :] + ray_directions[..., None, :] * z_samples[..., :, None]
-        sigma_fine, rgb_fine = sampler(field, query_points_fine)
+        ex_fine = {}
+        if extras:
+            sigma_fine, rgb_fine, ex_fine = sampler(field, query_points_fine, extras)
+        else:
+            sigma_fine, rgb_fine = sampler(field, query_points_fine)
         sigma_fine = sigma_fine.view(*query_points_fine.shape[:-1], -1)
         rgb_fine = rgb_fine.view(*query_points_fine.shape[:-1], -1)
-        sigma = torch.cat((sigma, sigma_fine), dim=-2).gather(
-            -2, z_indices_sorted.unsqueeze(-1).expand(-1, -1, -1, -1, sigma.shape[-1]))
-        rgb = torch.cat((rgb, rgb_fine), dim=-2).gather(
-            -2, z_indices_sorted.unsqueeze(-1).expand(-1, -1, -1, -1, rgb.shape[-1]))
+
+        def merge(a, b):
+            return torch.cat((a, b), dim=-2).gather(
+                -2, z_indices_sorted.unsqueeze(-1).expand(-1, -1, -1, -1, a.shape[-1]))
+        sigma = merge(sigma, sigma_fine)
+        rgb = merge(rgb, rgb_fine)
+        ex = {k: merge(v, ex_fine[k].view(*query_points_fine.shape[:-1], -1)) for k, v in ex.items()}
         depth_values = z_values_sorted
         inter['z_fine'] = z_samples
     inter['z_sorted'] = depth_values
     inter['sigma'] = sigma.squeeze(-1)
     inter['rgb'] = rgb
+    if extras:
+        semantics = ex.get('coords', ex.get('semantics'))
+        outs = render_volume_density(sigma.squeeze(-1), rgb, ray_origins, ray_directions, depth_values,
+                                     white_background=white_background, normals=ex.get('normals'),
+                                     semantics=semantics)
+        if outs[3] is None and outs[4] is None:
+            outs = outs[:3]
+        if len(outs) == 3:
+            outs = (*outs, None, None)
+        return (*outs, inter) if return_intermediates else outs
     rgb_map, depth_map, mask = render_volume_density(sigma.squeeze(-1), rgb, ray_origins, ray_directions,
                                                      depth_values, white_background=white_background)
     if return_intermediates:

@@ -148,6 +148,59 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     print(name, 'mask mean', float(mask.mean()), 'rgb mean', float(rgb.mean()))
 
 
+def extras_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, compute_normals,
+                compute_semantics, compute_coords):
+    """render() eval outputs (run.py:227-257, 293-335; generator.py:599-622, 643-644, 672-674;
+    nerf_utils.py:146-161): normals (autograd d SDF / d point, normalised), semantics (softmax
+    probabilities) and coords maps, composited like rgb.  No backward (eval-only outputs)."""
+    torch.manual_seed(2000 + seed)
+    gen = generator.Generator(512, scene_range, attention_values=10, use_sdf=True,
+                              disable_stylegan_noise=True)
+    gen.eval()
+    with torch.no_grad():
+        gen.decoder.net[2].bias[0] -= 0.97
+        gen.beta.fill_(0.1)
+        gen.alpha.fill_(1.0)
+    planes = 1.87 * torch.randn(b, 3, 32, R, R)
+    gen.synthesis_network = PlanesLeaf(planes)
+    palette = generator.wide_sigmoid_rescaled(torch.randn(b, 10, 3)).detach()
+    cam, focal = make_cameras(b, scene_range, flipped, 100 + seed)
+    ws = torch.zeros(b, 15, 512)
+    args_ns = types.SimpleNamespace(use_viewdir=False, fine_sampling=True, use_sdf=True,
+                                    attention_values=10)
+    dataset_config = {'scene_range': scene_range, 'white_background': white_bg}
+    render = extract_render(args_ns, dataset_config)
+    rseed = 177 + seed
+    torch.manual_seed(rseed)
+    rgb, depth, mask, normals, semantics, _ = render(
+        gen, H, W, cam, focal, None, None, ws, S, randomize=True,
+        extra_model_inputs={'attention_values': palette}, force_no_cam_grad=True,
+        compute_normals=compute_normals, compute_semantics=compute_semantics,
+        compute_coords=compute_coords)
+    torch.manual_seed(rseed)
+    u_coarse = torch.rand(b, H, W, S)
+    u_fine = torch.rand(b * H * W, S)
+    out = {
+        'planes': planes, 'w1': gen.decoder.net[0].weight.detach(),
+        'b1': gen.decoder.net[0].bias.detach(), 'w2': gen.decoder.net[2].weight.detach(),
+        'b2': gen.decoder.net[2].bias.detach(), 'palette': palette,
+        'alpha': gen.alpha.detach(), 'beta': gen.beta.detach(),
+        'cam': cam.detach(), 'focal': focal.detach(), 'u_coarse': u_coarse, 'u_fine': u_fine,
+        'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach(),
+    }
+    if normals is not None:
+        out['normals'] = normals.detach()
+    if semantics is not None:
+        out['semantics'] = semantics.detach()
+    meta = dict(H=H, W=W, S=S, R=R, scene_range=scene_range, white_bg=int(white_bg), randomize=1,
+                force_no_cam_grad=1, ortho=0, compute_normals=int(compute_normals),
+                compute_semantics=int(compute_semantics), compute_coords=int(compute_coords))
+    np.savez_compressed(os.path.join(OUT, f'render_{name}.npz'),
+                        **{k: v.numpy() for k, v in out.items()},
+                        **{f'meta_{k}': np.array(v) for k, v in meta.items()})
+    print(name, 'mask mean', float(mask.mean()))
+
+
 def stage_cases():
     g = torch.Generator().manual_seed(123)
     # near/far: rays from a sphere around the box, some missing it (nerf_utils.py:227-275)
@@ -191,3 +244,10 @@ if __name__ == '__main__':
     # perspective with bbox + center (nerf_utils.py:43-56; eval_*_persp.py callers)
     render_case('persp_center_bbox', 3, b=2, H=8, W=12, S=8, R=8, scene_range=1.4,
                 white_bg=False, flipped=True, randomize=True, with_bbox=True, with_center=True)
+    # eval outputs: normals + semantics; white background; coords
+    extras_case('extras_ns', 4, b=2, H=8, W=8, S=16, R=16, scene_range=1.4, white_bg=False,
+                flipped=True, compute_normals=True, compute_semantics=True, compute_coords=False)
+    extras_case('extras_nw', 5, b=1, H=8, W=8, S=8, R=12, scene_range=0.55, white_bg=True,
+                flipped=False, compute_normals=True, compute_semantics=False, compute_coords=False)
+    extras_case('extras_coords', 6, b=1, H=8, W=8, S=8, R=12, scene_range=1.4, white_bg=False,
+                flipped=True, compute_normals=False, compute_semantics=True, compute_coords=True)

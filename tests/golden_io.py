@@ -7,6 +7,7 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox']
+EXTRAS_CASES = ['extras_ns', 'extras_nw', 'extras_coords']   # eval outputs, no gradients
 
 
 def load(name):

@@ -8,7 +8,7 @@ rounding of identical op graphs (in practice bit-exact).
 import pytest
 import torch
 
-from golden_io import RENDER_CASES, field_from, load
+from golden_io import EXTRAS_CASES, RENDER_CASES, field_from, load
 from oracle import render_oracle as orc
 
 
@@ -61,3 +61,27 @@ def test_oracle_sample_pdf_matches_reference():
     rnd = orc.sample_pdf(d['pdf_bins'], d['pdf_w'], S, deterministic=False, u=d['pdf_u'])
     assert torch.equal(det, d['pdf_det'])
     assert torch.equal(rnd, d['pdf_rnd'])
+
+
+@pytest.mark.parametrize('case', EXTRAS_CASES)
+def test_oracle_eval_outputs_match_reference(case):
+    """compute_normals / compute_semantics / compute_coords (run.py:227-257, 293-335)."""
+    d, meta = load(f'render_{case}')
+    field = field_from(d, meta)
+    rgb, depth, mask, nmap, smap = orc.render(
+        field, meta['H'], meta['W'], d['cam'], d['focal'], None, None, meta['S'], randomize=True,
+        white_background=bool(meta['white_bg']), force_no_cam_grad=True, u_coarse=d['u_coarse'],
+        u_fine=d['u_fine'], compute_normals=bool(meta['compute_normals']),
+        compute_semantics=bool(meta['compute_semantics']), compute_coords=bool(meta['compute_coords']))
+    tol = dict(rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(rgb.detach(), d['rgb'], **tol)
+    torch.testing.assert_close(depth.detach(), d['depth'], **tol)
+    torch.testing.assert_close(mask.detach(), d['mask'], **tol)
+    if 'normals' in d:
+        torch.testing.assert_close(nmap.detach(), d['normals'], **tol)
+    else:
+        assert nmap is None
+    if 'semantics' in d:
+        torch.testing.assert_close(smap.detach(), d['semantics'], **tol)
+    else:
+        assert smap is None
