@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 7
+#define NFI_ABI_VERSION 8
 #define NFI_DEC_SIZE 7184 /* floats in the packed decoder buffer */
 
 enum {
@@ -102,6 +102,13 @@ typedef struct nfi_render_args {
                           in the forward (NULL: not written), required by the backward */
   int32_t* tile_counts; /* optional [nfi_tile_count_size()] per-plane-tile sample counts for the
                            backward's d-planes binning (zeroed and filled by the forward); NULL = skip */
+  int32_t extras;      /* eval outputs (run.py:227-257, 293-335): bit 1 normals, 2 semantics, 4 coords
+                          (the coords map replaces the semantic map, run.py:334-335).  Need y_saved
+                          and perm, normals also x_saved; the maps carry no gradient (their callers
+                          are eval renders, run.py:1250-1264) */
+  int32_t _pad4;
+  float* normal_map;   /* [B*HW,3]  (extras & 1): sum_i w_i normalize(d sdf_i / d p_i) (+1-mask if white) */
+  float* semantic_map; /* [B*HW,10] (extras & 2: sum_i w_i softmax_i) or [B*HW,3] (extras & 4: sum_i w_i p_i) */
   float* z_coarse;     /* optional [B*HW,S] debug: coarse depths */
   float* z_fine;       /* optional [B*HW,S] debug: fine depths, sorted */
 } nfi_render_args;

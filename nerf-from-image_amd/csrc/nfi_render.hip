@@ -1518,6 +1518,205 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Eval outputs of render() (run.py:227-257, 293-335), one wave per ray from the forward's saved
+// state: compositing weights w_i in merged order (the forward's arithmetic), then
+//   semantics  sum_i w_i softmax(logits_i)                    (generator.py:672-674)
+//   coords     sum_i w_i (ro + rd t_i)                        (generator.py:643-644)
+//   normals    sum_i w_i normalize(d sdf_i / d p_i) (+ 1-mask on white) (generator.py:599-622,
+//              nerf_utils.py:146-161): d sdf / d features by the MFMA decoder backward with
+//              dY = e_0, then the tap derivative by a re-gather with a per-point reduction.
+// Forward-only (the reference's callers of these outputs render without gradients).
+// ---------------------------------------------------------------------------------------
+template <int NPL>
+__global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * (XTILE + 256)];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long nrays = (long long)a.B * a.HW;
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= nrays) return;
+  float* X = lds + wv * (XTILE + 256);
+  float* ND = X + XTILE;   // [64][4] per-point d sdf / d p
+  const int N = a.fine ? 2 * a.S : a.S;
+  const float sr = a.field.scene_range;
+  RayCtx R;
+  load_ray(a, r, R);
+  const PlaneView pv{a.field.planes + (long long)R.b * a.field.sb, (int)a.field.sq, (int)a.field.st,
+                     a.field.R};
+  float t[NPL], w[NPL];
+  float sm = 0.f;
+  {
+    float al[NPL], aa[NPL], T[NPL];
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      const int i = e * 64 + l;
+      const bool v = i < N;
+      t[e] = v ? a.t_saved[r * N + i] : 0.f;
+      const float sg = v ? a.sigma_saved[r * N + i] : 0.f;
+      const float dist = (i < N - 1) ? fmul(fsub(a.t_saved[r * N + i + 1], t[e]), R.rdn) : 0.f;
+      float ex;
+      alpha_of(sg, dist, al[e], aa[e], ex);
+      if (!v) {
+        al[e] = 0.f;
+        aa[e] = 1.f;
+      }
+    }
+    excl_prod<NPL>(aa, T);
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      w[e] = (e * 64 + l < N) ? fmul(al[e], T[e]) : 0.f;
+      sm += w[e];
+    }
+  }
+  const float mask = wave_sum(sm);
+  if (a.extras & 4) {
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      if (e * 64 + l < N) {
+        c0 = fmaf(w[e], fadd(R.o[0], fmul(R.d[0], t[e])), c0);
+        c1 = fmaf(w[e], fadd(R.o[1], fmul(R.d[1], t[e])), c1);
+        c2 = fmaf(w[e], fadd(R.o[2], fmul(R.d[2], t[e])), c2);
+      }
+    }
+    c0 = wave_sum(c0);
+    c1 = wave_sum(c1);
+    c2 = wave_sum(c2);
+    if (l == 0) {
+      a.semantic_map[r * 3 + 0] = c0;
+      a.semantic_map[r * 3 + 1] = c1;
+      a.semantic_map[r * 3 + 2] = c2;
+    }
+  } else if (a.extras & 2) {
+    float acc[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int e = 0; e < NPL; ++e) {
+      const int i = e * 64 + l;
+      if (i < N) {
+        const int ei = a.perm[r * N + i];
+        float y[NA];
+#pragma unroll
+        for (int k = 0; k < NA; ++k) y[k] = a.y_saved[r * NO * N + (1 + k) * N + ei];
+        // softmax as head_forward forms it
+        float m = y[0];
+#pragma unroll
+        for (int k = 1; k < NA; ++k) m = fmaxf(m, y[k]);
+        float p[NA], sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NA; ++k) {
+          p[k] = __expf(y[k] - m);
+          sum += p[k];
+        }
+        const float rs = 1.f / sum;
+#pragma unroll
+        for (int k = 0; k < NA; ++k) acc[k] = fmaf(w[e], p[k] * rs, acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const float v = wave_sum(acc[k]);
+      if (l == 0) a.semantic_map[r * NA + k] = v;
+    }
+  }
+  if (a.extras & 1) {
+    float n0 = 0.f, n1 = 0.f, n2 = 0.f;
+    const int j16 = l & 15, q = l >> 4;
+    const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
+#pragma unroll 1
+    for (int e = 0; e < NPL; ++e) {
+      if (e * 64 >= N) break;
+      const int npts = min(64, N - e * 64);
+      // d sdf / d x for the chunk's points: decoder backward with dY = e_0 on the matrix cores
+      f4v xa[4], xb[4];
+      float gyb[4][3];
+#pragma unroll
+      for (int sb = 0; sb < 4; ++sb) {
+        const int ip = e * 64 + 16 * sb + j16;
+        xa[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+        xb[sb] = xa[sb];
+        if (ip < N) {
+          const float* xr = a.x_saved + (r * N + (int)a.perm[r * N + ip]) * NC + 8 * q;
+          xa[sb] = ld4(xr);
+          xb[sb] = ld4(xr + 4);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) gyb[sb][tt] = (tt == 0 && q == 0) ? 1.f : 0.f;
+      }
+      f4v gxo[2][4];
+      mlp_backward_mfma(a.field.dec, xa, xb, gyb, gxo);
+      wave_lds_sync();
+#pragma unroll
+      for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          *reinterpret_cast<f4v*>(X + (16 * sb + j16) * XS + 16 * cb + 4 * q) = gxo[cb][sb] * (1.f / 3.f);
+      wave_lds_sync();
+      // tap derivative per point (quad layout), reduced over the point's 16 lanes
+      PointP P;
+      point_params(R.o, R.d, (e * 64 + l < N) ? t[e] : R.near_, sr, pv.R, P);
+      const int ngrp = (npts + 3) >> 2;
+#pragma unroll 1
+      for (int gi = 0; gi < ngrp; ++gi) {
+        const int j = 4 * gi + sub;
+        const float4 gv = *reinterpret_cast<const float4*>(X + j * XS + 4 * q4);
+        float GX[3], GY[3];
+#pragma unroll
+        for (int pq = 0; pq < 3; ++pq) {
+          const int pk = __shfl(P.pl[pq].tex, j);
+          const float e_ = __shfl(P.pl[pq].e, j), ww = __shfl(P.pl[pq].w, j);
+          const float s = __shfl(P.pl[pq].s, j), n = __shfl(P.pl[pq].n, j);
+          const float gxm = __shfl(P.pl[pq].gxm, j), gym = __shfl(P.pl[pq].gym, j);
+          const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
+          const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
+          const float* b = pv.base + pq * pv.sq + 4 * q4;
+          const float4 v0 = *reinterpret_cast<const float4*>(b + t0 * pv.st);
+          const float4 v1 = *reinterpret_cast<const float4*>(b + t1 * pv.st);
+          const float wx = dx ? ww : e_;
+          const float ax = (s * v0.x + n * v1.x) * gv.x + (s * v0.y + n * v1.y) * gv.y +
+                           (s * v0.z + n * v1.z) * gv.z + (s * v0.w + n * v1.w) * gv.w;
+          const float ay = (v1.x - v0.x) * gv.x + (v1.y - v0.y) * gv.y + (v1.z - v0.z) * gv.z +
+                           (v1.w - v0.w) * gv.w;
+          GX[pq] = (dx ? ax : -ax) * gxm;
+          GY[pq] = wx * ay * gym;
+        }
+        float d0 = GX[0] + GX[1], d1 = GY[0] + GX[2], d2 = GY[1] + GY[2];
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+          d0 += __shfl_xor(d0, m);
+          d1 += __shfl_xor(d1, m);
+          d2 += __shfl_xor(d2, m);
+        }
+        if ((l & 15) == 0) {
+          ND[j * 4 + 0] = d0;
+          ND[j * 4 + 1] = d1;
+          ND[j * 4 + 2] = d2;
+        }
+      }
+      wave_lds_sync();
+      if (e * 64 + l < N) {
+        // x = p / scene_range: d sdf / d p = (d sdf / d x) / scene_range; F.normalize (eps 1e-12)
+        const float g0 = ND[l * 4 + 0] / sr, g1 = ND[l * 4 + 1] / sr, g2 = ND[l * 4 + 2] / sr;
+        const float nr = fmaxf(tnorm3(g0, g1, g2), 1e-12f);
+        n0 = fmaf(w[e], g0 / nr, n0);
+        n1 = fmaf(w[e], g1 / nr, n1);
+        n2 = fmaf(w[e], g2 / nr, n2);
+      }
+      wave_lds_sync();
+    }
+    n0 = wave_sum(n0);
+    n1 = wave_sum(n1);
+    n2 = wave_sum(n2);
+    if (l == 0) {
+      const float bg = a.white_bg ? fsub(1.f, mask) : 0.f;
+      a.normal_map[r * 3 + 0] = n0 + bg;
+      a.normal_map[r * 3 + 1] = n1 + bg;
+      a.normal_map[r * 3 + 2] = n2 + bg;
+    }
+  }
+}
+
 constexpr int FUSED_LDS = 4 * XTILE;
 
 // d planes (tile chunks) and ray-coordinate gradients (dcoord jobs) in ONE launch, the two roles
@@ -1593,6 +1792,14 @@ static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
   }
   render_fwd_kernel<SPL, NPL, FINE><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
   NFI_CHECK_LAUNCH("render_fwd_kernel");
+  if (a->extras) {
+    const int N = FINE ? 2 * a->S : a->S;
+    const unsigned grid = (unsigned)((nrays + 3) / 4);
+    if (N <= 64) extras_kernel<1><<<grid, 256, 0, s>>>(*a);
+    else if (N <= 128) extras_kernel<2><<<grid, 256, 0, s>>>(*a);
+    else extras_kernel<4><<<grid, 256, 0, s>>>(*a);
+    NFI_CHECK_LAUNCH("extras_kernel");
+  }
   return NFI_OK;
 }
 
@@ -1701,6 +1908,10 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
   int e = nfi::validate(a);
   if (e) return e;
   NFI_REQUIRE(a->rgb && a->depth && a->mask, "render_forward: null output");
+  NFI_REQUIRE((a->extras & ~7) == 0, "render_forward: unknown extras bits 0x%x", a->extras);
+  NFI_REQUIRE(!(a->extras & 1) || (a->normal_map && a->x_saved),
+              "render_forward: normals need normal_map and x_saved");
+  NFI_REQUIRE(!(a->extras & 6) || a->semantic_map, "render_forward: semantics/coords need semantic_map");
   return nfi::dispatch_fwd(a, (hipStream_t)stream);
 }
 

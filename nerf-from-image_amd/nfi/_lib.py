@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 7
+ABI_VERSION = 8
 DEC_SIZE = 7184
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -43,7 +43,8 @@ class NfiRenderArgs(ctypes.Structure):
                 ('rgb', c_void_p), ('depth', c_void_p), ('mask', c_void_p),
                 ('t_saved', c_void_p), ('sigma_saved', c_void_p), ('rgb_saved', c_void_p),
                 ('y_saved', c_void_p), ('perm', c_void_p), ('x_saved', c_void_p),
-                ('tile_counts', c_void_p),
+                ('tile_counts', c_void_p), ('extras', ctypes.c_int32), ('_pad4', ctypes.c_int32),
+                ('normal_map', c_void_p), ('semantic_map', c_void_p),
                 ('z_coarse', c_void_p), ('z_fine', c_void_p)]
 
 

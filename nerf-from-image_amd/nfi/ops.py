@@ -183,6 +183,7 @@ class RenderOptions:
     scene_range: float = 1.0
     inv_alpha: float = 1.0       # 1 / Generator.alpha
     beta: float = 0.1            # Generator.beta
+    extras: int = 0              # eval outputs: 1 normals, 2 semantics, 4 coords (nfi_render_args.extras)
 
 
 def pack_decoder(w1, b1, w2, b2, lr_multiplier: float = 1.0) -> torch.Tensor:
@@ -221,8 +222,12 @@ class _VolumeRender(torch.autograd.Function):
         c_saved = torch.empty((n, 3, N), device=dev)
         y_saved = torch.empty((n, 11, N), device=dev)
         perm = torch.empty((n, N), device=dev, dtype=torch.int16)
-        # decoder inputs for the backward (saves it the re-gather), only when a gradient is wanted
-        x_saved = torch.empty((n * N, 32), device=dev) if any(ctx.needs_input_grad) else None
+        # decoder inputs for the backward (saves it the re-gather) and for the normals pass
+        need_x = any(ctx.needs_input_grad) or bool(opts.extras & 1)
+        x_saved = torch.empty((n * N, 32), device=dev) if need_x else None
+        nmap = torch.empty((n, 3), device=dev) if opts.extras & 1 else torch.empty(0, device=dev)
+        smap = (torch.empty((n, 3 if opts.extras & 4 else 10), device=dev) if opts.extras & 6
+                else torch.empty(0, device=dev))
         zc = zf = None
         if debug is not None:
             zc = torch.empty((n, S), device=dev)
@@ -233,6 +238,9 @@ class _VolumeRender(torch.autograd.Function):
                                    uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, y_saved, perm,
                                    zc, zf)
         args.x_saved = _ptr(x_saved)
+        args.extras = int(opts.extras)
+        args.normal_map = _ptr(nmap) if nmap.numel() else None
+        args.semantic_map = _ptr(smap) if smap.numel() else None
         tile_counts = None
         if FORWARD_TILE_COUNTS and ctx.needs_input_grad[0]:
             # the forward counts the backward's d-planes tile bins while it has the samples
@@ -251,8 +259,12 @@ class _VolumeRender(torch.autograd.Function):
                               y_saved, perm, x_saved, tile_counts)
         ctx.opts = opts
         ctx.shape = (B, H, W)
-        ctx.mark_non_differentiable(depth)
-        return rgb.view(B, H, W, 3), depth.view(B, H, W), mask.view(B, H, W)
+        ctx.mark_non_differentiable(depth, nmap, smap)
+        if nmap.numel():
+            nmap = nmap.view(B, H, W, 3)
+        if smap.numel():
+            smap = smap.view(B, H, W, -1)
+        return rgb.view(B, H, W, 3), depth.view(B, H, W), mask.view(B, H, W), nmap, smap
 
     @staticmethod
     def _args(planes_tm, dec, pal, ro, rd, near, far, opts, B, HW, uc, uf, seed, rgb, depth, mask,
@@ -274,7 +286,7 @@ class _VolumeRender(torch.autograd.Function):
                                   z_coarse=_ptr(zc), z_fine=_ptr(zf))
 
     @staticmethod
-    def backward(ctx, g_rgb, g_depth, g_mask):
+    def backward(ctx, g_rgb, g_depth, g_mask, g_nmap=None, g_smap=None):
         lib = _lib.load()
         planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm, x_saved, \
             tile_counts = ctx.saved_tensors
@@ -318,7 +330,9 @@ def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOption
                   u_coarse=None, u_fine=None, seed: Optional[int] = None, debug: Optional[dict] = None):
     """Fused coarse+fine render of rays (run.py:202-348).  planes_tm: texel-major
     [B,3,R,R,32] (see planes_texel_major); palette [B,10,3]; ro, rd [B,H,W,3]; near, far
-    [B,H,W].  Returns rgb [B,H,W,3], depth [B,H,W] (no grad), mask [B,H,W]."""
+    [B,H,W].  Returns rgb [B,H,W,3], depth [B,H,W] (no grad), mask [B,H,W]; with opts.extras
+    also the normal map [B,H,W,3] and the semantic [B,H,W,10] / coords [B,H,W,3] map (no grad;
+    None when not requested)."""
     _require_device(planes_tm, palette, ro, rd, near, far, dec, u_coarse, u_fine)
     if planes_tm.dim() != 5 or planes_tm.shape[-1] != 32 or planes_tm.stride(-1) != 1:
         raise ValueError('planes_tm must be texel-major [B,3,R,R,32] with unit channel stride')
@@ -336,4 +350,8 @@ def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOption
             raise ValueError(f'{name} must have B*H*W*S = {n * opts.samples} elements')
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if opts.randomize else 0
-    return _VolumeRender.apply(planes_tm, palette, ro, rd, near, far, dec, opts, u_coarse, u_fine, seed, debug)
+    rgb, depth, mask, nmap, smap = _VolumeRender.apply(planes_tm, palette, ro, rd, near, far, dec, opts,
+                                                       u_coarse, u_fine, seed, debug)
+    if opts.extras:
+        return rgb, depth, mask, (nmap if nmap.numel() else None), (smap if smap.numel() else None)
+    return rgb, depth, mask

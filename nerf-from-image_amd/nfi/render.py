@@ -146,8 +146,10 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
     draws for parity testing (`u_coarse` [B,H,W,S], `u_fine` [B*H*W,S]) or fix the Philox
     seed; `debug` (a dict) receives intermediate depths."""
     cfg = _CONFIG
-    if compute_normals or compute_semantics or compute_coords:
-        raise NotImplementedError('normals/semantics/coords outputs are SURVEY §8(f) #3 (next), not built')
+    if compute_normals and not cfg.use_sdf:
+        raise ValueError('compute_normals needs an SDF field (run.py:229)')
+    # run.py:334-335: the coords map takes the semantic map's place
+    extras = (1 if compute_normals else 0) | (4 if compute_coords else (2 if compute_semantics else 0))
     if cfg.use_viewdir or not cfg.use_sdf or cfg.attention_values != 10:
         raise NotImplementedError('only the inversion field (use_sdf, attention_values=10, no viewdir)')
     f = _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs)
@@ -165,7 +167,11 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
     opts = ops.RenderOptions(samples=int(depth_samples_per_ray), fine=bool(cfg.fine_sampling),
                              white_background=bool(cfg.white_background), randomize=bool(randomize),
                              scene_range=float(cfg.scene_range), inv_alpha=1.0 / float(f.alpha),
-                             beta=float(f.beta))
-    rgb, depth, mask = ops.volume_render(planes_tm, f.palette, ro, rd, near, far, dec, opts,
-                                         u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug)
+                             beta=float(f.beta), extras=extras)
+    out = ops.volume_render(planes_tm, f.palette, ro, rd, near, far, dec, opts,
+                            u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug)
+    if extras:
+        rgb, depth, mask, normals, semantics = out
+        return rgb, depth, mask, normals, semantics, dict(f.model_outputs)
+    rgb, depth, mask = out
     return rgb, depth, mask, None, None, dict(f.model_outputs)

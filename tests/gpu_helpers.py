@@ -128,3 +128,47 @@ def synthetic_inputs(B, H, W, S, R, scene_range, seed, ortho=False, flipped=True
     meta = dict(H=H, W=W, S=S, R=R, scene_range=scene_range, white_bg=int(white_bg),
                 randomize=int(randomize), force_no_cam_grad=0)
     return inp, meta
+
+
+def run_hip_extras(inp, meta, dev):
+    """nfi.render with compute_normals / compute_semantics / compute_coords (eval outputs)."""
+    nfi.configure(scene_range=float(meta['scene_range']), white_background=bool(meta['white_bg']),
+                  fine_sampling=True)
+    f = nfi.TriplaneField(planes=inp['planes'].to(dev), palette=inp['palette'].to(dev),
+                          w1=inp['w1'].to(dev), b1=inp['b1'].to(dev), w2=inp['w2'].to(dev),
+                          b2=inp['b2'].to(dev), alpha=float(inp['alpha']), beta=float(inp['beta']))
+    with torch.no_grad():
+        rgb, depth, mask, nmap, smap, _ = nfi.render(
+            f, int(meta['H']), int(meta['W']), inp['cam'].to(dev), inp['focal'].to(dev), None, None, None,
+            int(meta['S']), randomize=True, compute_normals=bool(meta['compute_normals']),
+            compute_semantics=bool(meta['compute_semantics']), compute_coords=bool(meta['compute_coords']),
+            force_no_cam_grad=True, u_coarse=inp['u_coarse'].to(dev), u_fine=inp['u_fine'].to(dev))
+    out = {'rgb': rgb.cpu(), 'depth': depth.cpu(), 'mask': mask.cpu()}
+    if nmap is not None:
+        out['normals'] = nmap.cpu()
+    if smap is not None:
+        out['semantics'] = smap.cpu()
+    return out
+
+
+def run_oracle_extras(inp, meta, dtype=torch.float32):
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        cast = {k: (v.to(dtype) if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in inp.items()}
+        field = orc.Field(planes=cast['planes'], w1=cast['w1'], b1=cast['b1'], w2=cast['w2'], b2=cast['b2'],
+                          palette=cast['palette'], alpha=cast['alpha'], beta=cast['beta'],
+                          scene_range=float(meta['scene_range']))
+        rgb, depth, mask, nmap, smap = orc.render(
+            field, int(meta['H']), int(meta['W']), cast['cam'], cast['focal'], None, None, int(meta['S']),
+            randomize=True, white_background=bool(meta['white_bg']), force_no_cam_grad=True,
+            u_coarse=cast['u_coarse'], u_fine=cast['u_fine'], compute_normals=bool(meta['compute_normals']),
+            compute_semantics=bool(meta['compute_semantics']), compute_coords=bool(meta['compute_coords']))
+    finally:
+        torch.set_default_dtype(prev)
+    out = {'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach()}
+    if nmap is not None:
+        out['normals'] = nmap.detach()
+    if smap is not None:
+        out['semantics'] = smap.detach()
+    return out

@@ -15,8 +15,9 @@ rel-L2 1e-4, d planes rel-L2 1e-3.
 import pytest
 import torch
 
-from golden_io import RENDER_CASES, load
-from gpu_helpers import rel_l2, run_hip, run_oracle, run_oracle64, synthetic_inputs
+from golden_io import EXTRAS_CASES, RENDER_CASES, load
+from gpu_helpers import (rel_l2, run_hip, run_hip_extras, run_oracle, run_oracle64, run_oracle_extras,
+                         synthetic_inputs)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device('cuda:0')
@@ -109,3 +110,36 @@ def test_backward_binning_paths_agree():
         assert torch.equal(a[key], b[key]), key
     for key in ('d_planes', 'd_cam', 'd_focal'):   # float atomics: order differs run to run
         assert rel_l2(a[key], b[key]) < 1e-5, key
+
+
+@pytest.mark.parametrize('case', EXTRAS_CASES)
+def test_eval_outputs(case):
+    """compute_normals / compute_semantics / compute_coords maps (run.py:227-257, 293-335) against
+    the reference's own fp32 maps (golden) measured from the fp64 oracle.  Floors (max |d|):
+    semantics / coords 2e-5, normals 1e-4 (a normalised gradient of the SDF)."""
+    d, meta = load(f'render_{case}')
+    hip = run_hip_extras(d, meta, DEV)
+    ref64 = run_oracle_extras(d, meta, torch.float64)
+    floors = {'rgb': 2e-5, 'mask': 2e-5, 'depth': 1e-4, 'normals': 1e-4, 'semantics': 2e-5}
+    for key, floor in floors.items():
+        if key not in d:
+            assert key not in hip
+            continue
+        e_hip = float((hip[key].double() - ref64[key]).abs().max())
+        e_ref = float((d[key].double() - ref64[key]).abs().max())
+        print(f'  {key:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
+        assert e_hip <= max(floor, K * e_ref), f'{key}: hip err {e_hip:.3g} vs ref fp32 err {e_ref:.3g}'
+
+
+def test_eval_outputs_full_size():
+    """Normals and semantics at the real plane size and 64+64 samples (oracle fp64 as truth)."""
+    inp, meta = synthetic_inputs(B=1, H=16, W=16, S=64, R=256, scene_range=1.4, seed=31)
+    meta.update(compute_normals=1, compute_semantics=1, compute_coords=0)
+    hip = run_hip_extras(inp, meta, DEV)
+    ref32 = run_oracle_extras(inp, meta, torch.float32)
+    ref64 = run_oracle_extras(inp, meta, torch.float64)
+    for key, floor in (('normals', 1e-4), ('semantics', 2e-5)):
+        e_hip = float((hip[key].double() - ref64[key]).abs().max())
+        e_ref = float((ref32[key].double() - ref64[key]).abs().max())
+        print(f'  {key:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
+        assert e_hip <= max(floor, K * e_ref), key

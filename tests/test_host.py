@@ -31,10 +31,14 @@ def test_cpu_tensors_fail_loudly():
         nfi.render(_field(), 8, 8, cam, torch.ones(1), None, None, None, 32)
 
 
-def test_unsupported_outputs_raise():
-    with pytest.raises(NotImplementedError):
-        nfi.render(_field(), 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32,
-                   compute_normals=True)
+def test_normals_need_sdf_field():
+    nfi.configure(use_sdf=False)
+    try:
+        with pytest.raises(ValueError, match='SDF'):
+            nfi.render(_field(), 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32,
+                       compute_normals=True)
+    finally:
+        nfi.configure(use_sdf=True)
 
 
 def test_viewdir_variant_raises():
