@@ -1304,41 +1304,83 @@ __global__ void __launch_bounds__(256) bin_fill_kernel(BinArgs A) {
 
 // Exclusive scans over the K tile counts: offsets (entry starts; cursor := offsets) and
 // chunk starts (ceil(count / CHUNK) workgroup chunks per tile); total chunks -> meta[0].
-__global__ void __launch_bounds__(1024) bin_scan_kernel(const int* __restrict__ counts, int K,
-                                                        int* __restrict__ offsets, int* __restrict__ cursor,
-                                                        int* __restrict__ chunk_start, int* __restrict__ meta) {
-  __shared__ int s_off[1024], s_chk[1024];
-  const int tid = threadIdx.x;
-  const int per = (K + 1023) / 1024;
-  const int k0 = tid * per, k1 = min(K, k0 + per);
-  int so = 0, sc = 0;
-  for (int k = k0; k < k1; ++k) {
-    so += counts[k];
-    sc += (counts[k] + CHUNK - 1) / CHUNK;
+// Two passes over 1024-tile blocks: block partial sums, then each block scans its tiles after
+// summing the partials of the blocks before it (K/1024 of them).
+__device__ __forceinline__ int wave_incl_scan_i(int v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(v, d);
+    if (l >= d) v += t;
   }
-  s_off[tid] = so;
-  s_chk[tid] = sc;
+  return v;
+}
+
+// inclusive block scan of (a, b) pairs over 1024 threads; returns block totals via tot
+__device__ __forceinline__ void block_scan2(int& a, int& b, int& ta, int& tb) {
+  __shared__ int sa[16], sbx[16];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  a = wave_incl_scan_i(a);
+  b = wave_incl_scan_i(b);
+  if (l == 63) {
+    sa[wv] = a;
+    sbx[wv] = b;
+  }
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    const int a = (tid >= d) ? s_off[tid - d] : 0;
-    const int c = (tid >= d) ? s_chk[tid - d] : 0;
-    __syncthreads();
-    s_off[tid] += a;
-    s_chk[tid] += c;
-    __syncthreads();
+  int pa = 0, pb = 0;
+  ta = 0;
+  tb = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (k < wv) {
+      pa += sa[k];
+      pb += sbx[k];
+    }
+    ta += sa[k];
+    tb += sbx[k];
   }
-  int o = s_off[tid] - so, c = s_chk[tid] - sc;
-  for (int k = k0; k < k1; ++k) {
-    offsets[k] = o;
-    cursor[k] = o;
-    chunk_start[k] = c;
-    o += counts[k];
-    c += (counts[k] + CHUNK - 1) / CHUNK;
+  a += pa;
+  b += pb;
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(1024) scan_partials_kernel(const int* __restrict__ counts, int K,
+                                                             int* __restrict__ part) {
+  const int k = blockIdx.x * 1024 + threadIdx.x;
+  const int c = (k < K) ? counts[k] : 0;
+  int a = c, b = (c + CHUNK - 1) / CHUNK, ta, tb;
+  block_scan2(a, b, ta, tb);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = ta;
+    part[2 * blockIdx.x + 1] = tb;
   }
-  if (tid == 1023) {
-    offsets[K] = s_off[1023];
-    chunk_start[K] = s_chk[1023];
-    meta[0] = s_chk[1023];
+}
+
+__global__ void __launch_bounds__(1024) scan_blocks_kernel(const int* __restrict__ counts, int K,
+                                                           const int* __restrict__ part,
+                                                           int* __restrict__ offsets, int* __restrict__ cursor,
+                                                           int* __restrict__ chunk_start, int* __restrict__ meta) {
+  // prefix of the blocks before this one
+  int pa = 0, pb = 0;
+  for (int q = threadIdx.x; q < (int)blockIdx.x; q += 1024) {
+    pa += part[2 * q];
+    pb += part[2 * q + 1];
+  }
+  int ta, tb;
+  block_scan2(pa, pb, ta, tb);   // (only the totals are used)
+  const int k = blockIdx.x * 1024 + threadIdx.x;
+  const int c = (k < K) ? counts[k] : 0;
+  const int cc = (c + CHUNK - 1) / CHUNK;
+  int a = c, b = cc, ua, ub;
+  block_scan2(a, b, ua, ub);
+  if (k < K) {
+    offsets[k] = ta + a - c;
+    cursor[k] = ta + a - c;
+    chunk_start[k] = tb + b - cc;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 1023) {
+    offsets[K] = ta + a;
+    chunk_start[K] = tb + b;
+    meta[0] = tb + b;
   }
 }
 
@@ -1750,6 +1792,7 @@ struct Workspace {
   int* chunk_start;
   int* chunk_tile;
   int* meta;
+  int* part;
   int4* list;
   long long bytes;
 };
@@ -1775,6 +1818,7 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.offsets = reinterpret_cast<int*>(take((K + 1) * 4));
   w.chunk_start = reinterpret_cast<int*>(take((K + 1) * 4));
   w.meta = reinterpret_cast<int*>(take(16));
+  w.part = reinterpret_cast<int*>(take((K / 1024 + 1) * 8));
   // chunks <= ceil(entries / CHUNK) + K  (each tile wastes at most one partial chunk)
   w.chunk_tile = reinterpret_cast<int*>(take((3 * nsamp / CHUNK + K + 1) * 4));
   w.list = reinterpret_cast<int4*>(take((3 * nsamp + 128) * 16));   // + padding read by tile_chunk
@@ -1828,8 +1872,11 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
       bin_count_kernel<<<sb, 256, 0, s>>>(B);
       NFI_CHECK_LAUNCH("bin_count_kernel");
     }
-    bin_scan_kernel<<<1, 1024, 0, s>>>(counts, K, w.offsets, w.cursor, w.chunk_start, w.meta);
-    NFI_CHECK_LAUNCH("bin_scan_kernel");
+    const unsigned nb = (unsigned)((K + 1023) / 1024);
+    scan_partials_kernel<<<nb, 1024, 0, s>>>(counts, K, w.part);
+    NFI_CHECK_LAUNCH("scan_partials_kernel");
+    scan_blocks_kernel<<<nb, 1024, 0, s>>>(counts, K, w.part, w.offsets, w.cursor, w.chunk_start, w.meta);
+    NFI_CHECK_LAUNCH("scan_blocks_kernel");
     chunk_map_kernel<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(counts, w.chunk_start, K, w.chunk_tile);
     NFI_CHECK_LAUNCH("chunk_map_kernel");
     if (!fwd_counts) {
