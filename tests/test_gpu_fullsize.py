@@ -1,0 +1,76 @@
+"""Size-independent properties at BASELINE's full p3d size (128², 64+64 samples, R=256 planes),
+where the fp64 oracle is too slow to run: determinism, output bounds, linearity of the backward
+in the upstream gradient, and exact linearity of the loss in the palette (rgb = sum_i w_i p_i·palette
+is linear in it, so a directional difference equals <dL/dpalette, delta> up to fp32 rounding)."""
+
+import pytest
+import torch
+
+import nfi
+from gpu_helpers import rel_l2, synthetic_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+def _render(inp, meta, seed, palette=None, g_scale=1.0, grads=True):
+    nfi.configure(scene_range=float(meta['scene_range']), white_background=False, fine_sampling=True)
+    planes = inp['planes'].to(DEV).requires_grad_(grads)
+    pal = (inp['palette'] if palette is None else palette).to(DEV).requires_grad_(grads)
+    cam = inp['cam'].to(DEV).requires_grad_(grads)
+    focal = inp['focal'].to(DEV).requires_grad_(grads)
+    f = nfi.TriplaneField(planes=planes, palette=pal, w1=inp['w1'].to(DEV), b1=inp['b1'].to(DEV),
+                          w2=inp['w2'].to(DEV), b2=inp['b2'].to(DEV), alpha=1.0, beta=0.1)
+    rgb, depth, mask, _, _, _ = nfi.render(f, int(meta['H']), int(meta['W']), cam, focal, None, None, None,
+                                           int(meta['S']), randomize=True, seed=seed)
+    out = {'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach()}
+    if grads:
+        g = torch.Generator(device='cpu').manual_seed(3)
+        g_rgb = torch.randn(rgb.shape, generator=g).to(DEV) * g_scale
+        g_mask = torch.randn(mask.shape, generator=g).to(DEV) * g_scale
+        loss = (rgb * g_rgb).sum() + (mask * g_mask).sum()
+        loss.backward()
+        out.update(loss=loss.detach(), d_planes=planes.grad, d_palette=pal.grad, d_cam=cam.grad,
+                   d_focal=focal.grad)
+    return out
+
+
+@pytest.fixture(scope='module')
+def full():
+    inp, meta = synthetic_inputs(B=2, H=128, W=128, S=64, R=256, scene_range=1.4, seed=77)
+    return inp, meta
+
+
+def test_forward_deterministic_and_bounded(full):
+    inp, meta = full
+    a = _render(inp, meta, seed=11, grads=False)
+    b = _render(inp, meta, seed=11, grads=False)
+    for k in ('rgb', 'depth', 'mask'):
+        assert torch.equal(a[k], b[k]), k
+    assert float(a['mask'].min()) >= 0.0 and float(a['mask'].max()) <= 1.0 + 1e-6
+    assert float(a['depth'].min()) >= 0.0
+    pal_max = float(inp['palette'].abs().max())
+    assert float(a['rgb'].abs().max()) <= pal_max * (1 + 1e-6)
+    assert float(a['mask'].mean()) > 0.05        # the field is not empty
+    c = _render(inp, meta, seed=12, grads=False)
+    assert not torch.equal(a['rgb'], c['rgb'])   # another Philox stream moves the samples
+
+
+def test_backward_linear_in_upstream_gradient(full):
+    inp, meta = full
+    a = _render(inp, meta, seed=5)
+    b = _render(inp, meta, seed=5, g_scale=2.0)
+    assert torch.equal(b['d_palette'], 2 * a['d_palette'])    # deterministic reduction, exact in fp32
+    for k in ('d_planes', 'd_cam', 'd_focal'):                # float atomics: order varies
+        assert rel_l2(b[k], 2 * a[k]) < 1e-5, k
+
+
+def test_loss_linear_in_palette(full):
+    inp, meta = full
+    base = _render(inp, meta, seed=9)
+    delta = torch.randn(inp['palette'].shape, generator=torch.Generator().manual_seed(4))
+    eps = 1e-2
+    moved = _render(inp, meta, seed=9, palette=inp['palette'] + eps * delta, grads=True)
+    lhs = float(moved['loss'] - base['loss'])
+    rhs = eps * float((base['d_palette'].cpu() * delta).sum())
+    assert abs(lhs - rhs) <= 1e-3 * abs(rhs) + 1e-2, (lhs, rhs)
