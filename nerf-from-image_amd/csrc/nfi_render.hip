@@ -186,6 +186,29 @@ struct TileGrid {
 };
 __host__ __device__ __forceinline__ TileGrid tile_grid(int R) { return {(R - 2) / TSX + 1, (R - 2) / TSY + 1}; }
 
+// Tile keys order the accumulation chunks.  Planes xy and xz share their x tile column, so per
+// image the key runs over x-slabs tx with the xy tiles (tx, y) and the xz tiles (tx, z) of a slab
+// next to each other — the same samples' gradient rows are read twice within a short window
+// (L2 / Infinity Cache) — followed by the yz tiles.
+__host__ __device__ __forceinline__ int tile_key(int b, int q, int tx, int ty, TileGrid G) {
+  const int T = G.nx * G.ny;
+  return b * 3 * T + (q == 2 ? 2 * T + ty * G.nx + tx : (tx * 2 + q) * G.ny + ty);
+}
+__device__ __forceinline__ void tile_decode(int key, TileGrid G, int& b, int& q, int& tx, int& ty) {
+  const int T = G.nx * G.ny;
+  b = key / (3 * T);
+  const int r = key % (3 * T);
+  if (r >= 2 * T) {
+    q = 2;
+    ty = (r - 2 * T) / G.nx;
+    tx = (r - 2 * T) % G.nx;
+  } else {
+    tx = r / (2 * G.ny);
+    q = (r / G.ny) & 1;
+    ty = r % G.ny;
+  }
+}
+
 // Tile key of plane q for point P of image b, and the entry record {s, slot | flags, w, n}:
 // slot = ly*8 + lx inside the tile, flags bit 8/9 = grid-gradient multiplier gxm/gym nonzero.
 __device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int R, TileGrid G, long long s,
@@ -205,7 +228,7 @@ __device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int
   const int slot = (y0 - ty * TSY) * TTX + (x0 - tx * TSX);
   rec = make_int4((int)s, slot | (P.pl[q].gxm != 0.f ? 0x100 : 0) | (P.pl[q].gym != 0.f ? 0x200 : 0),
                   __float_as_int(w), __float_as_int(n));
-  return ((b * 3 + q) * G.ny + ty) * G.nx + tx;
+  return tile_key(b, q, tx, ty, G);
 }
 
 // Run-aggregated atomicAdd of 1 per valid lane on base[key]: each run of equal keys in
@@ -1458,7 +1481,6 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
   // half 0 weights row ly by (1 - n), half 1 row ly + 1 by n
   const float wsgn = h ? 1.f : -1.f, woff = h ? 0.f : 1.f;
   const cint4_p L = (cint4_p)A.list;
-  const int tpp = A.tg.nx * A.tg.ny;
   NFI_STAMP_INIT
   {
     // (wave-uniform scalars: readfirstlane keeps the entry loop's control and the register-image
@@ -1466,9 +1488,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int tile = __builtin_amdgcn_readfirstlane(A.chunk_tile[c]);
     const int first = __builtin_amdgcn_readfirstlane(A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK);
     const int last = __builtin_amdgcn_readfirstlane(min(A.offsets[tile] + A.counts[tile], first + CHUNK));
-    const int bq = tile / tpp, rem = tile % tpp;
-    const int q = bq % 3, b = bq / 3;
-    const int ty = rem / A.tg.nx, tx = rem % A.tg.nx;
+    int b, q, tx, ty;
+    tile_decode(tile, A.tg, b, q, tx, ty);
     // each wave sums a contiguous quarter of the chunk (runs of one ray stay together)
     const int per = (((last - first) + 3) / 4 + 7) & ~7;
     const int b0 = first + wv * per, b1 = min(last, b0 + per);
@@ -1775,8 +1796,14 @@ __global__ void __launch_bounds__(256, 4) tile_dcoord_kernel(TileArgs A, nfi_ren
   if (b >= tot) return;
   const long long t0 = b * T / tot, t1 = (b + 1) * T / tot;
   if (t1 > t0) {
+#if defined(NFI_ABLATE) && NFI_ABLATE == 4
+    return;   // experiment: coordinate role only
+#endif
     tile_chunk(A, lds, (int)t0);
   } else {
+#if defined(NFI_ABLATE) && NFI_ABLATE == 3
+    return;   // experiment: tile role only
+#endif
     const int wv = threadIdx.x >> 6;
     dcoord_job(a, g, (b - t0) * 4 + wv, lds + wv * XTILE);
   }
