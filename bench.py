@@ -203,7 +203,8 @@ def main():
             'stages': stages}
 
     out = {
-        'metric': 'Msamples/sec fwd+bwd (128^2, 64+64 samples/ray)' if bwd else 'Msamples/sec fwd (128^2, 64+64)',
+        'metric': (f'Msamples/sec fwd+bwd ({H}^2, {S}+{S} samples/ray)' if bwd
+                   else f'Msamples/sec fwd ({H}^2, {S}+{S} samples/ray)'),
         'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
