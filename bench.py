@@ -111,6 +111,56 @@ def cpu_baseline(args):
             'seconds_per_image_step': t}
 
 
+def inversion_leg(args, dev, cfg, batch, world):
+    """BASELINE.json's second number: seconds per image of the 30-step inversion (run.py:1960-2310,
+    --inv_loss l1, pose optimised): per step the producer (synthesis network + AttentionMapper,
+    PyTorch-ROCm / MIOpen, fp32) forward, the HIP render fwd+bwd, the producer backward to the
+    latent and Adam.  Random-init generator (no checkpoint offline), z_avg from the mapping
+    network, the same cameras as the renderer leg, a synthetic target image.  Timed like the
+    renderer leg (barrier + synchronize around exactly --inv-steps steps, max over ranks)."""
+    import nfi
+    from nfi import inversion, ops, producer
+    sr, wbg, flipped, B, H, S, pose, bwd = cfg
+    torch.manual_seed(4321)
+    gen = producer.InversionGenerator(scene_range=sr).to(dev)
+    with torch.no_grad():
+        gen.decoder.net[2].bias[0] -= 0.97        # the synthetic field's SDF shift (nfi/synthetic.py)
+    gen.requires_grad_(False)
+    w_avg = gen.mapping_network.get_average_w(generator=torch.Generator().manual_seed(7))
+    g = torch.Generator(device=dev).manual_seed(99)
+    target = torch.tanh(torch.randn((B, H, H, 3), generator=g, device=dev))
+    icfg = inversion.InversionConfig(steps=2, resolution=H, samples=S, loss='l1',
+                                     camera_flipped=flipped)
+    cam, focal = batch['cam'].detach(), batch['focal'].detach()
+    inversion.invert(gen, target, cam, focal, w_avg, icfg)           # warm-up (MIOpen kernel search)
+    torch.cuda.synchronize()
+    icfg.steps = args.inv_steps
+    ops.KERNEL_TIMERS = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = inversion.invert(gen, target, cam, focal, w_avg, icfg)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
+    render_ms = sum(a.elapsed_time(b) for v in timers.values() for a, b in v) / icfg.steps
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    step_ms = elapsed / icfg.steps * 1e3
+    return {'s_per_image': round(elapsed / (B * world), 5), 'steps': icfg.steps,
+            'images': B * world, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
+            'render_ms_per_step': round(render_ms, 3),
+            'producer_adam_ms_per_step': round(step_ms - render_ms, 3),
+            'loss': 'l1', 'loss_first_last': [round(res.losses[0], 5), round(res.losses[-1], 5)],
+            'producer': 'StyleGAN2 synthesis 256^2x96 + AttentionMapper, fp32, PyTorch-ROCm (MIOpen)',
+            'renderer': 'nfi HIP fwd+bwd'}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -120,6 +170,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-reps', type=int, default=2)
     ap.add_argument('--cpu-res', type=int, default=128)
+    ap.add_argument('--no-inversion', action='store_true')
+    ap.add_argument('--inv-steps', type=int, default=30)
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -214,6 +266,9 @@ def main():
         'renderer_s_per_image_30step': round(30 * ms_per_step / 1e3 / B, 5),
         'roofline': roof,
     }
+    if bwd and not args.no_inversion:
+        out['inversion'] = inversion_leg(args, dev, cfg, batch, world)
+        out['inversion_s_per_image'] = out['inversion']['s_per_image']
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(args)
         out['cpu_baseline'] = cb

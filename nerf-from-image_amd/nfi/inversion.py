@@ -1,0 +1,217 @@
+"""The inversion loop around the renderer: run.py:1960-2310 for one batch of
+target images — latent + pose optimised by Adam against an image loss, with the volume render
+on the HIP path (nfi.render) and the producer (synthesis network + AttentionMapper) in
+PyTorch-ROCm.
+
+Pose representation (lib/pose_utils.py:48-128): `(z0, t2, s, q)` with focal f = 1 + exp(z0),
+translation t3 = (t2/s, f/s) in camera space, rotation from the unit quaternion q;
+`pose_to_matrix` / `matrix_to_pose` restate it in torch (the quaternion extraction is
+Shepperd's method, as in the reference's `matrix_to_quaternion`).
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .render import render as _nfi_render
+
+
+# ---------------------------------------------------------------------------------------------
+# pose parameterisation (lib/pose_utils.py)
+
+def quaternion_to_matrix(q: torch.Tensor) -> torch.Tensor:
+    """pose_utils.py:41-45: the matrix whose rows are the unit vectors rotated by q, i.e. the
+    transpose of the rotation matrix of q = (w, x, y, z)."""
+    w, x, y, z = q.unbind(-1)
+    r = torch.stack([
+        1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=-1)
+    return r.view(q.shape[:-1] + (3, 3)).transpose(-2, -1)
+
+
+def _flip(mat: torch.Tensor, camera_flipped: bool) -> torch.Tensor:
+    if not camera_flipped:
+        return mat
+    sign = mat.new_tensor([1.0, -1.0, -1.0, -1.0])     # pose_utils.py:61: columns 1..3
+    return torch.cat([mat[:, :3] * sign, mat[:, 3:]], dim=1)
+
+
+def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
+    """pose_utils.py:48-78 -> (cam2world [b,4,4], focal or None)."""
+    rot = quaternion_to_matrix(q)
+    b = q.shape[0]
+    if z0 is not None:
+        f = 1 + z0.exp()
+        t3 = torch.cat([t2 / s[:, None], (f / s)[:, None]], dim=-1)
+        focal = f / 2
+    else:
+        t3 = torch.cat([t2, torch.ones_like(t2[:, :1])], dim=-1) / s[:, None]
+        focal = None
+    top = torch.cat([rot, (rot * t3[:, None, :]).sum(-1, keepdim=True)], dim=-1)
+    bottom = torch.zeros(b, 1, 4, dtype=top.dtype, device=top.device)
+    bottom[:, 0, 3] = 1
+    return _flip(torch.cat([top, bottom], dim=1), camera_flipped), focal
+
+
+def invert_space(mat: torch.Tensor) -> torch.Tensor:
+    """pose_utils.py:20-27: cam2world <-> world2cam of a scaled rigid transform."""
+    scale = mat[:, 3:4, 3:4]
+    rot = mat[:, :3, :3] / scale
+    out = torch.zeros_like(mat)
+    out[:, :3, :3] = rot.transpose(-2, -1)
+    out[:, :3, 3] = -(rot * mat[:, :3, None, 3]).sum(-2)
+    out[:, 3, 3] = 1
+    return out
+
+
+def rotation_to_quaternion(m: torch.Tensor) -> torch.Tensor:
+    """Shepperd's method on the 3x3 block of [b,4,4] matrices (pose_utils.py:81-100), float64;
+    q = (w, x, y, z) with the sign fixed by the dominant component being positive."""
+    m = m.double()
+    hom = m[:, 3, 3]
+    tr = m[:, 0, 0] + m[:, 1, 1] + m[:, 2, 2] + hom
+    out = torch.empty(m.shape[0], 4, dtype=torch.float64, device=m.device)
+    for n in range(m.shape[0]):
+        M = m[n]
+        t = float(tr[n])
+        if t > float(hom[n]):
+            q = [t, float(M[2, 1] - M[1, 2]), float(M[0, 2] - M[2, 0]), float(M[1, 0] - M[0, 1])]
+        else:
+            d = [float(M[0, 0]), float(M[1, 1]), float(M[2, 2])]
+            i = 0
+            if d[1] > d[0]:
+                i = 1
+            if d[2] > d[i]:
+                i = 2
+            j, k = (i + 1) % 3, (i + 2) % 3
+            t = d[i] - (d[j] + d[k]) + float(hom[n])
+            v = [0.0, 0.0, 0.0]
+            v[i] = t
+            v[j] = float(M[i, j] + M[j, i])
+            v[k] = float(M[k, i] + M[i, k])
+            q = [float(M[k, j] - M[j, k])] + v
+        scale = 0.5 / math.sqrt(t * float(hom[n]))
+        out[n] = torch.tensor(q, dtype=torch.float64) * scale
+    return out
+
+
+def matrix_to_pose(cam2world: torch.Tensor, focal: Optional[torch.Tensor], camera_flipped: bool):
+    """pose_utils.py:103-128 -> (z0 or None, t2, s, q) (all detached, float32)."""
+    mat = _flip(cam2world.detach(), camera_flipped)
+    inv = invert_space(mat)
+    t3 = -inv[:, :3, 3]
+    if focal is not None:
+        focal = focal.detach()
+        z0 = torch.log(2 * focal - 1)
+        s = 2 * focal / t3[:, 2]
+    else:
+        z0 = None
+        s = 1 / t3[:, 2]
+    t2 = t3[:, :2] * s[:, None]
+    q = rotation_to_quaternion(inv.cpu()).float().to(t3.device)
+    return z0, t2, s, q
+
+
+# ---------------------------------------------------------------------------------------------
+# the loop (run.py:1960-2310)
+
+@dataclass
+class InversionConfig:
+    steps: int = 30                      # max(checkpoint_steps)
+    lr: float = 2e-3                     # run.py:2007
+    betas: tuple = (0.9, 0.95)
+    gain_z: float = 5.0                  # --inv_gain_z (lr_gain_z, run.py:1749)
+    loss: str = 'l1'                     # --inv_loss: 'l1' | 'mse' ('vgg'/'mixed' need LPIPS weights)
+    samples: int = 64                    # depth_samples_per_ray (fine sampling doubles it)
+    resolution: int = 128
+    optimize_pose: bool = True           # not --inv_no_optimize_pose
+    no_split: bool = False               # --inv_no_split: one w shared by the 15 slots
+    camera_flipped: bool = True          # dataset_config['camera_flipped']
+
+
+@dataclass
+class InversionResult:
+    ws: torch.Tensor                     # [b,15,512] (z_ * gain)
+    z0: Optional[torch.Tensor]
+    t2: torch.Tensor
+    s: torch.Tensor
+    q: torch.Tensor
+    losses: list = field(default_factory=list)
+    seconds: float = 0.0
+
+
+def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """optimize_iter (run.py:2205-2252): per-batch-summed image loss."""
+    b = rgb.shape[0]
+    if kind == 'l1':
+        return F.l1_loss(rgb, target) * b
+    if kind == 'mse':
+        return F.mse_loss(rgb, target) * b
+    raise NotImplementedError(f'inversion loss {kind!r}: LPIPS/VGG weights are not available offline')
+
+
+def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: Optional[torch.Tensor],
+           w_init: torch.Tensor, cfg: InversionConfig = InversionConfig(), center=None, bbox=None,
+           uniforms: Optional[Callable[[int], tuple]] = None, render_fn: Optional[Callable] = None,
+           on_step: Optional[Callable] = None) -> InversionResult:
+    """Fit latent + pose of `generator` (frozen) to `target_img` [b,H,W,3 or 4] in [-1,1].
+
+    `w_init` [1 or b, 15, 512] is the starting latent (z_avg or a regressor output);
+    `cam2world`/`focal` the initial pose.  `uniforms(it) -> (u_coarse, u_fine)` fixes the
+    renderer's random draws per iteration (parity tests); `render_fn` replaces nfi.render with
+    a callable of the same signature (tests only)."""
+    b = target_img.shape[0]
+    res = cfg.resolution
+    rfn = render_fn or _nfi_render
+    z_ = w_init.detach().clone().expand(b, -1, -1).contiguous()
+    if cfg.no_split:
+        z_ = z_.mean(dim=1, keepdim=True)
+    z_ = (z_ / cfg.gain_z).requires_grad_()
+    z0_, t2_, s_, q_ = matrix_to_pose(cam2world, focal, cfg.camera_flipped)
+    params = [z_]
+    if cfg.optimize_pose:
+        pose = [p for p in (z0_, q_, s_, t2_) if p is not None]
+        for p in pose:
+            p.requires_grad_()
+        params += pose
+    opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas)
+    target = target_img[..., :3]
+    losses = []
+    t0 = time.perf_counter()
+    for it in range(cfg.steps):
+        cam, foc = pose_to_matrix(z0_, t2_, s_, F.normalize(q_, dim=-1), cfg.camera_flipped)
+        kw = {}
+        if uniforms is not None:
+            kw['u_coarse'], kw['u_fine'] = uniforms(it)
+        ws = z_ * cfg.gain_z
+        if cfg.no_split:
+            ws = ws.expand(-1, 15, -1)
+        rgb = rfn(generator, res, res, cam, foc, center, bbox, ws, cfg.samples,
+                  force_no_cam_grad=not cfg.optimize_pose, **kw)[0]
+        loss = image_loss(cfg.loss, rgb, target)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        with torch.no_grad():
+            q_.copy_(F.normalize(q_, dim=-1))
+            if z0_ is not None:
+                z0_.clamp_(-4, 4)
+            s_.abs_()
+        losses.append(loss.detach())
+        if on_step is not None:
+            on_step(it, loss)
+    if torch.cuda.is_available() and target_img.is_cuda:
+        torch.cuda.synchronize(target_img.device)
+    secs = time.perf_counter() - t0
+    ws = (z_.detach() * cfg.gain_z)
+    if cfg.no_split:
+        ws = ws.expand(-1, 15, -1)
+    return InversionResult(ws=ws, z0=None if z0_ is None else z0_.detach(), t2=t2_.detach(),
+                           s=s_.detach(), q=q_.detach(), losses=[float(x) for x in losses], seconds=secs)

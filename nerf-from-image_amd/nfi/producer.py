@@ -1,0 +1,281 @@
+"""The tri-plane producer of the inversion step, caller side: the parts of the
+reference Generator that turn a latent ws [b,15,512] into the renderer's inputs —
+StyleGAN2 synthesis network -> tri-planes [b,3,32,256,256] (stylegan.py:293-490,
+generator.py:475-477), AttentionMapper -> palette [b,10,3] (generator.py:132-186,
+455-462) — plus the mapping network used for the average latent (stylegan.py:228-290,
+generator.py:263-282) and the frozen SDF decoder weights.
+
+Plain PyTorch-ROCm (convolutions on MIOpen), written from the reference's published behaviour;
+parameter and buffer names equal the reference Generator's state_dict keys, so a G_ema checkpoint
+loads with `load_state_dict(sd, strict=False)`.  Pinned against the reference by
+tests/golden/producer.npz (tests/test_producer.py).  The HIP renderer consumes it through
+`nfi.render(generator, ...)` exactly as it consumes the reference Generator.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+SQRT2 = math.sqrt(2.0)
+
+
+def blur_kernel() -> torch.Tensor:
+    """[1,3,3,1] x [1,3,3,1] / 64 (stylegan.py `bilinear_filter`)."""
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k = k[:, None] * k[None, :]
+    return k / k.sum()
+
+
+def _depthwise(x: torch.Tensor, k: torch.Tensor, stride: int, transpose: bool) -> torch.Tensor:
+    """Per-channel 4x4 FIR with padding 1 (`EfficientResample`): channels folded into the batch."""
+    b, c, h, w = x.shape
+    xf = x.reshape(b * c, 1, h, w)
+    kk = k[None, None].to(x.dtype)
+    y = (F.conv_transpose2d(xf, kk, padding=1, stride=stride) if transpose
+         else F.conv2d(xf, kk, padding=1, stride=stride))
+    return y.reshape(b, c, y.shape[-2], y.shape[-1])
+
+
+def upsample2x(x: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
+    """2x FIR upsampling of the skip image (`upsample2d`: transposed conv, gain 4)."""
+    return _depthwise(x, k * 4, stride=2, transpose=True)
+
+
+class EqualizedLinear(nn.Module):
+    """y = x (W * lr/sqrt(in))^T + b * lr (stylegan.py:148-180)."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, activate: bool = False,
+                 lr_multiplier: float = 1.0, bias_init: float = 0.0):
+        super().__init__()
+        self.weight = nn.Parameter(torch.randn(out_features, in_features) / lr_multiplier)
+        self.bias = nn.Parameter(torch.full((out_features,), float(bias_init))) if bias else None
+        self.weight_gain = lr_multiplier / math.sqrt(in_features)
+        self.bias_gain = lr_multiplier
+        self.activate = activate
+
+    def forward(self, x):
+        y = F.linear(x, self.weight * self.weight_gain,
+                     None if self.bias is None else self.bias * self.bias_gain)
+        if self.activate:
+            y = F.leaky_relu(y * SQRT2, 0.2)
+        return y
+
+
+class ModulatedConv(nn.Module):
+    """SynthesisLayer (stylegan.py:293-360): style-modulated 3x3 conv with demodulation, optional
+    2x upsampling (transposed conv + FIR), bias, sqrt(2) gain, leaky ReLU.  The modulation scales
+    the input channels and demodulation the output channels, so the convolution itself uses the
+    shared weight (one conv for the whole batch)."""
+
+    def __init__(self, in_ch: int, out_ch: int, w_dim: int, resolution: int, up: bool = False):
+        super().__init__()
+        self.up = up
+        self.affine = EqualizedLinear(w_dim, in_ch, bias_init=1.0)
+        self.weight = nn.Parameter(torch.randn(out_ch, in_ch, 3, 3))
+        self.bias = nn.Parameter(torch.zeros(out_ch))
+        # noise inputs (disabled in the inversion generator: disable_stylegan_noise=True)
+        self.noise_strength = nn.Parameter(torch.zeros([]))
+        self.register_buffer('noise_const', torch.randn(resolution, resolution))
+        self.register_buffer('resample_filter', blur_kernel())
+
+    def forward(self, x, w):
+        styles = self.affine(w)                                           # [b, in]
+        wmod = self.weight[None] * styles[:, None, :, None, None]         # [b, out, in, 3, 3]
+        dcoefs = (wmod.square().sum(dim=(2, 3, 4)) + 1e-8).rsqrt()        # [b, out]
+        x = x * styles[:, :, None, None]
+        if self.up:
+            x = F.conv_transpose2d(x, self.weight.transpose(0, 1), stride=2)
+            x = _depthwise(x, self.resample_filter * 4, stride=1, transpose=False)
+        else:
+            x = F.conv2d(x, self.weight, padding=1)
+        x = x * dcoefs[:, :, None, None]
+        x = (x + self.bias[None, :, None, None]) * SQRT2
+        return F.leaky_relu(x, 0.2)
+
+
+class ToPlanes(nn.Module):
+    """OutputLayer (stylegan.py:363-384): modulated 1x1 conv without demodulation, plus bias."""
+
+    def __init__(self, in_ch: int, out_ch: int, w_dim: int):
+        super().__init__()
+        self.affine = EqualizedLinear(w_dim, in_ch, bias_init=1.0)
+        self.weight = nn.Parameter(torch.randn(out_ch, in_ch, 1, 1))
+        self.bias = nn.Parameter(torch.zeros(out_ch))
+        self.weight_gain = 1.0 / math.sqrt(in_ch)
+
+    def forward(self, x, w):
+        styles = self.affine(w) * self.weight_gain
+        x = F.conv2d(x * styles[:, :, None, None], self.weight)
+        return x + self.bias[None, :, None, None]
+
+
+class SynthesisBlock(nn.Module):
+    """One resolution of the synthesis network (stylegan.py:387-446)."""
+
+    def __init__(self, in_ch: int, out_ch: int, w_dim: int, resolution: int, img_ch: int):
+        super().__init__()
+        self.in_ch = in_ch
+        if in_ch == 0:
+            self.const = nn.Parameter(torch.randn(out_ch, resolution, resolution))
+        else:
+            self.conv0 = ModulatedConv(in_ch, out_ch, w_dim, resolution, up=True)
+        self.conv1 = ModulatedConv(out_ch, out_ch, w_dim, resolution)
+        self.torgb = ToPlanes(out_ch, img_ch, w_dim)
+        self.register_buffer('resample_filter', blur_kernel())
+        self.num_conv = 1 if in_ch == 0 else 2
+
+    def forward(self, x, img, ws):
+        k = 0
+        if self.in_ch == 0:
+            x = self.const[None].expand(ws.shape[0], -1, -1, -1)
+        else:
+            x = self.conv0(x, ws[:, k])
+            k += 1
+        x = self.conv1(x, ws[:, k])
+        y = self.torgb(x, ws[:, k + 1])
+        img = y if img is None else upsample2x(img, self.resample_filter) + y
+        return x, img
+
+
+class SynthesisNetwork(nn.Module):
+    """ws [b, num_ws, w_dim] -> image [b, img_ch, res, res] (stylegan.py:449-490); blocks at
+    4, 8, ..., res with min(channel_base/r, channel_max) channels."""
+
+    def __init__(self, w_dim: int = 512, img_resolution: int = 256, img_channels: int = 96,
+                 channel_base: int = 32768, channel_max: int = 512):
+        super().__init__()
+        self.resolutions = [2 ** i for i in range(2, int(math.log2(img_resolution)) + 1)]
+        ch = {r: min(channel_base // r, channel_max) for r in self.resolutions}
+        self.num_ws = 0
+        for r in self.resolutions:
+            blk = SynthesisBlock(ch[r // 2] if r > 4 else 0, ch[r], w_dim, r, img_channels)
+            setattr(self, f'b{r}', blk)
+            self.num_ws += blk.num_conv
+        self.num_ws += 1   # the last block's toRGB
+
+    def forward(self, ws, noise_mode: str = 'const'):
+        x = img = None
+        k = 0
+        for r in self.resolutions:
+            blk = getattr(self, f'b{r}')
+            x, img = blk(x, img, ws[:, k:k + blk.num_conv + 1])
+            k += blk.num_conv
+        return img
+
+
+class MappingNetwork(nn.Module):
+    """z -> w (stylegan.py:228-290) with normalize_latent, 2 layers, lr multiplier 0.01."""
+
+    def __init__(self, z_dim: int = 512, w_dim: int = 512, num_ws: int = 15, num_layers: int = 2,
+                 lr_multiplier: float = 0.01):
+        super().__init__()
+        self.z_dim, self.w_dim, self.num_ws, self.num_layers = z_dim, w_dim, num_ws, num_layers
+        dims = [z_dim] + [w_dim] * num_layers
+        for i in range(num_layers):
+            setattr(self, f'fc{i}', EqualizedLinear(dims[i], dims[i + 1], activate=True,
+                                                    lr_multiplier=lr_multiplier))
+
+    def forward(self, z, c=None):
+        x = z * (z.square().mean(dim=1, keepdim=True) + 1e-8).rsqrt()
+        for i in range(self.num_layers):
+            x = getattr(self, f'fc{i}')(x)
+        return x.unsqueeze(1).repeat(1, self.num_ws, 1)
+
+
+class MappingWrapper(nn.Module):
+    def __init__(self, backbone: MappingNetwork):
+        super().__init__()
+        self.backbone = backbone
+
+    def forward(self, z, c=None):
+        return self.backbone(z, c)
+
+    @torch.no_grad()
+    def get_average_w(self, n_samples: int = 10000, generator=None):
+        """Mean w over n_samples z ~ N(0, I) (generator.py:263-271)."""
+        dev = self.backbone.fc0.weight.device
+        z = torch.randn((n_samples, self.backbone.z_dim), generator=generator).to(dev)
+        return self(z).mean(dim=0, keepdim=True)
+
+
+class ConditionalLayerNorm(nn.Module):
+    """LayerNorm (no affine) with (1 + gamma(z)) scale and beta(z) shift (generator.py:42-60)."""
+
+    def __init__(self, ch: int, emb_dim: int):
+        super().__init__()
+        self.ch = ch
+        self.fc_gamma = EqualizedLinear(emb_dim, ch)
+        self.fc_beta = EqualizedLinear(emb_dim, ch)
+
+    def forward(self, x, z):
+        x = F.layer_norm(x, (self.ch,))
+        return torch.addcmul(self.fc_beta(z), 1 + self.fc_gamma(z), x)
+
+
+def wide_sigmoid_rescaled(x):
+    """MipNeRF wide sigmoid rescaled to [-1.002, 1.002] (generator.py:37-39)."""
+    return torch.sigmoid(x) * 2.004 - 1.002
+
+
+class PaletteMapper(nn.Module):
+    """AttentionMapper (generator.py:132-186): w_tex -> 10 RGB attention values."""
+
+    def __init__(self, latent_dim: int = 512, num_values: int = 10, hidden: int = 512):
+        super().__init__()
+        self.num_values = num_values
+        self.const = nn.Parameter(torch.randn(1, hidden))
+        for i in range(1, 5):
+            setattr(self, f'fc{i}', EqualizedLinear(hidden, hidden, bias=False))
+            setattr(self, f'norm{i}', ConditionalLayerNorm(hidden, latent_dim))
+        self.fc5 = EqualizedLinear(hidden, hidden)
+        self.fc_values = EqualizedLinear(hidden, num_values * 3)
+
+    def forward(self, c):
+        scale = SQRT2 / 2
+        x = self.const.expand(c.shape[0], -1)
+        for pair in ((1, 2), (3, 4)):
+            shortcut = x
+            for i in pair:
+                x = F.leaky_relu(getattr(self, f'norm{i}')(getattr(self, f'fc{i}')(x), c), 0.2)
+            x = (x + shortcut) * scale
+        x = F.leaky_relu(self.fc5(x), 0.2)
+        return wide_sigmoid_rescaled(self.fc_values(x).view(-1, self.num_values, 3))
+
+
+class Decoder(nn.Module):
+    """TriplanarDecoder.net weights (generator.py:288-299); evaluated by the HIP renderer."""
+
+    def __init__(self, num_in: int = 32, num_out: int = 10, hidden: int = 64):
+        super().__init__()
+        self.net = nn.Sequential(EqualizedLinear(num_in, hidden), nn.Softplus(),
+                                 EqualizedLinear(hidden, 1 + num_out))
+
+
+class InversionGenerator(nn.Module):
+    """The inversion configuration of the reference Generator (generator.py:334-405:
+    latent 512, attention_values=10, use_sdf, no viewdir / encoder / classes, StyleGAN noise
+    disabled).  `nfi.render(gen, ...)` renders it; `planes_and_palette(ws)` exposes the producer."""
+
+    def __init__(self, scene_range: float, img_resolution: int = 256):
+        super().__init__()
+        self.scene_range = scene_range
+        self.attention_values = 10
+        self.use_sdf = True
+        self.use_viewdir = False
+        self.use_encoder = False
+        self.num_classes = None
+        self.mapping_network = MappingWrapper(MappingNetwork(num_ws=15))
+        self.synthesis_network = SynthesisNetwork(512, img_resolution, 96)
+        self.decoder = Decoder(32, 10)
+        self.texture_mapper = PaletteMapper(512, 10)
+        self.beta = nn.Parameter(torch.tensor([0.1]))
+        self.alpha = nn.Parameter(torch.tensor([1.0]))
+
+    def planes_and_palette(self, ws):
+        palette = self.texture_mapper(ws[:, 14])
+        planes = self.synthesis_network(ws[:, :14])
+        return planes.view(ws.shape[0], 3, 32, planes.shape[-2], planes.shape[-1]), palette

@@ -12,36 +12,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from .inversion import pose_to_matrix
 from .render import TriplaneField
-
-
-def quaternion_to_matrix(q):
-    """pose_utils.py:30-45 (caller-side camera math)."""
-    v = torch.eye(3, device=q.device).unsqueeze(0).expand(q.shape[0], -1, -1)
-    qvec = q[:, 1:].unsqueeze(1).expand(-1, 3, -1)
-    uv = torch.cross(qvec, v, dim=2)
-    uuv = torch.cross(qvec, uv, dim=2)
-    return v + 2 * (q[:, :1].unsqueeze(1) * uv + uuv)
-
-
-def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
-    """pose_utils.py:48-75: (z0, t2, s, q) -> cam2world [B,4,4], focal (perspective) or None."""
-    R = quaternion_to_matrix(q)
-    mat = torch.zeros((q.shape[0], 4, 4), device=R.device)
-    mat[:, 3, 3] = 1
-    mat[:, :3, :3] = R
-    if z0 is not None:
-        f = 1 + z0.exp()
-        t3 = torch.cat((t2 / s.unsqueeze(-1), (f / s).unsqueeze(-1)), dim=-1)
-        mat[:, :3, 3] = (t3[:, None, :] * R).sum(dim=-1)
-        if camera_flipped:
-            mat[:, :3, 1:] *= -1
-        return mat, f / 2
-    t3 = torch.cat((t2, torch.ones_like(t2[:, :1])), dim=-1) / s
-    mat[:, :3, 3] = (t3[:, None, :] * R).sum(dim=-1)
-    if camera_flipped:
-        mat[:, :3, 1:] *= -1
-    return mat, None
 
 
 def inversion_batch(B, H, W, S, R, scene_range, seed, flipped=True, device='cuda'):

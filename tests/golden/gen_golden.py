@@ -10,11 +10,18 @@ and expected outputs/gradients of
                 nerf_utils ray bundle / near-far / stratified sampling / sample_pdf /
                 compositing are all the reference's code;
   * per-stage nerf_utils functions (compute_near_far_planes, sample_pdf, get_ray_bundle).
+  * the producer: the reference Generator (mapping network, StyleGAN2
+    synthesis network, AttentionMapper) at full size with seeded weights (golden_io.load_seeded,
+    so no weights are stored), sampled planes + checksums, palette, and the latent gradient;
+  * pose_utils pose_to_matrix / matrix_to_pose on a few cameras;
+  * an inversion trajectory: the loop of run.py:1960-2310 restated around
+    the reference's Generator, render() and pose_utils, L1 loss, 3 Adam steps.
 Random draws of the reference (torch.rand_like / torch.rand) are recovered by re-seeding and
 drawing the same shapes in the same order, and stored as `u_coarse` / `u_fine`.
 """
 
 import ast
+import json
 import os
 import sys
 import types
@@ -30,6 +37,9 @@ sys.path.insert(0, REF)
 
 from lib import nerf_utils, pose_utils  # noqa: E402  (reference modules)
 from models import generator  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(OUT))
+from golden_io import load_seeded  # noqa: E402  (the seeded-weights recipe the tests share)
 
 
 def extract_render(args_ns, dataset_config):
@@ -229,8 +239,131 @@ def stage_cases():
     print('stages written')
 
 
+def seeded_generator(seed, scene_range=1.4):
+    gen = generator.Generator(512, scene_range, attention_values=10, use_sdf=True,
+                              disable_stylegan_noise=True)
+    gen.eval()
+    load_seeded(gen, seed)
+    gen.requires_grad_(False)
+    return gen
+
+
+def producer_case(seed=21, b=2, nsample=8192):
+    gen = seeded_generator(seed)
+    sd = gen.state_dict()
+    g = torch.Generator().manual_seed(seed)
+    z = torch.randn(b, 512, generator=g)
+    ws = (0.6 * torch.randn(b, 15, 512, generator=g)).requires_grad_()
+    with torch.no_grad():
+        w_map = gen.mapping_network(z)
+    palette = gen.texture_mapper(ws[:, 14])                       # generator.py:455-462
+    planes = gen.synthesis_network(ws[:, :14])                    # generator.py:475-477
+    gp = torch.randn(planes.shape, generator=torch.Generator().manual_seed(seed + 1))
+    gq = torch.randn(palette.shape, generator=torch.Generator().manual_seed(seed + 2))
+    ((planes * gp).sum() + (palette * gq).sum()).backward()
+    idx = torch.randint(0, planes.numel(), (nsample,), generator=g)
+    keys = list(sd.keys())
+    shapes = json.dumps({k: list(v.shape) for k, v in sd.items()})
+    np.savez_compressed(os.path.join(OUT, 'producer.npz'),
+                        z=z.numpy(), ws=ws.detach().numpy(), w_map=w_map.numpy(),
+                        palette=palette.detach().numpy(), idx=idx.numpy(),
+                        planes_sample=planes.detach().reshape(-1)[idx].numpy(),
+                        planes_chsum=planes.detach().double().sum(dim=(2, 3)).numpy(),
+                        planes_chabs=planes.detach().double().abs().sum(dim=(2, 3)).numpy(),
+                        d_ws=ws.grad.numpy(), sd_keys=np.array(keys), sd_shapes=np.array(shapes),
+                        meta_seed=np.array(seed))
+    print('producer planes std', float(planes.std()), 'palette mean', float(palette.mean()))
+
+
+def ref_matrix_to_pose(mat, focal, flipped):
+    """pose_utils.matrix_to_pose on float64 copies of the inputs: its matrix_to_quaternion
+    (pose_utils.py:79, np.array(..., copy=False)) raises under numpy 2 unless handed float64;
+    the outputs are cast back to float32 as the reference's float32 path returns them."""
+    r = pose_utils.matrix_to_pose(mat.double(), None if focal is None else focal.double(), flipped)
+    return tuple(None if v is None else v.float() for v in r)
+
+
+def pose_cases():
+    g = torch.Generator().manual_seed(31)
+    out = {}
+    for name, flipped, persp in (('pf', True, True), ('pu', False, True), ('of', True, False)):
+        b = 4 if persp else 1      # pose_utils.py:69 divides [b,3] by s [b]: b=1 only
+        q = F.normalize(torch.randn(b, 4, generator=g), dim=-1)
+        t2 = 0.1 * torch.randn(b, 2, generator=g)
+        s = 0.5 + torch.rand(b, generator=g)
+        z0 = torch.randn(b, generator=g) if persp else None
+        mat, focal = pose_utils.pose_to_matrix(z0, t2, s, q, flipped)
+        rz0, rt2, rs, rq = ref_matrix_to_pose(mat, focal, flipped)
+        out.update({f'{name}_q': q, f'{name}_t2': t2, f'{name}_s': s, f'{name}_mat': mat,
+                    f'{name}_rt2': rt2, f'{name}_rs': rs, f'{name}_rq': rq})
+        if persp:
+            out.update({f'{name}_z0': z0, f'{name}_focal': focal, f'{name}_rz0': rz0})
+    np.savez_compressed(os.path.join(OUT, 'pose.npz'), **{k: v.numpy() for k, v in out.items()})
+    print('pose written')
+
+
+def inversion_case(seed=41, b=2, H=16, S=8, steps=3, scene_range=1.4, flipped=True):
+    """run.py:1960-2310 with --inv_loss l1, fine sampling, pose optimised; the loop skeleton
+    is restated here, every op inside it is the reference's (Generator, render, pose_utils)."""
+    gen = seeded_generator(seed, scene_range)
+    with torch.no_grad():
+        gen.decoder.net[2].bias[0] += SDF_SHIFT         # a partly-covered image (mask ~0.3-0.7)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        w_init = gen.mapping_network(torch.randn(64, 512, generator=g)).mean(dim=0, keepdim=True)
+    cam0, focal0 = make_cameras(b, scene_range, flipped, seed)
+    target = torch.tanh(torch.randn(b, H, H, 3, generator=g))
+    args_ns = types.SimpleNamespace(use_viewdir=False, fine_sampling=True, use_sdf=True,
+                                    attention_values=10)
+    render = extract_render(args_ns, {'scene_range': scene_range, 'white_background': False})
+    gain = 5.0
+    z_ = (w_init.clone().expand(b, -1, -1).contiguous() / gain).requires_grad_()
+    z0_, t2_, s_, R_ = ref_matrix_to_pose(cam0.detach(), focal0.detach(), flipped)
+    for p in (t2_, s_, R_, z0_):
+        p.requires_grad_()
+    opt = torch.optim.Adam([z_, z0_, R_, s_, t2_], lr=2e-3, betas=(0.9, 0.95))
+    u_c, u_f, losses, masks = [], [], [], []
+    for it in range(steps):
+        cam, focal = pose_utils.pose_to_matrix(z0_, t2_, s_, F.normalize(R_, dim=-1), flipped)
+        rseed = 900 + it
+        torch.manual_seed(rseed)
+        rgb, _, mask, _, _, _ = render(gen, H, H, cam, focal, None, None, z_ * gain, S)
+        torch.manual_seed(rseed)
+        u_c.append(torch.rand(b, H, H, S))
+        u_f.append(torch.rand(b * H * H, S))
+        loss = F.l1_loss(rgb, target) * b
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        R_.data[:] = F.normalize(R_.data, dim=-1)
+        z0_.data.clamp_(-4, 4)
+        s_.data.abs_()
+        losses.append(float(loss))
+        masks.append(float(mask.mean()))
+    np.savez_compressed(os.path.join(OUT, 'inversion.npz'),
+                        w_init=w_init.numpy(), cam0=cam0.numpy(), focal0=focal0.numpy(),
+                        target=target.numpy(), u_coarse=torch.stack(u_c).numpy(),
+                        u_fine=torch.stack(u_f).numpy(), losses=np.array(losses),
+                        ws=(z_.detach() * gain).numpy(), z0=z0_.detach().numpy(),
+                        t2=t2_.detach().numpy(), s=s_.detach().numpy(), q=R_.detach().numpy(),
+                        meta_seed=np.array(seed), meta_H=np.array(H), meta_S=np.array(S),
+                        meta_steps=np.array(steps), meta_scene_range=np.array(scene_range),
+                        meta_sdf_shift=np.array(SDF_SHIFT), meta_flipped=np.array(int(flipped)))
+    print('inversion losses', losses, 'mask', masks)
+
+
+SDF_SHIFT = 0.0
+
+
 if __name__ == '__main__':
     torch.set_num_threads(4)
+    if len(sys.argv) > 1:              # regenerate selected groups only
+        for a in sys.argv[1:]:
+            globals()[a]()
+        sys.exit(0)
+    producer_case()
+    pose_cases()
+    inversion_case()
     stage_cases()
     # p3d_car-like: perspective, flipped, black bg, pose grads, random sampling
     render_case('p3d', 0, b=2, H=16, W=16, S=16, R=16, scene_range=1.4, white_bg=False,

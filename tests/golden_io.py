@@ -17,6 +17,8 @@ def load(name):
     for k in z.files:
         if k.startswith('meta_'):
             meta[k[5:]] = z[k].item()
+        elif z[k].dtype.kind == 'U':
+            d[k] = z[k]                            # text (state_dict key/shape lists)
         else:
             d[k] = torch.from_numpy(z[k].copy())
     return d, meta
@@ -27,3 +29,41 @@ def field_from(d, meta):
     return Field(planes=d['planes'], w1=d['w1'], b1=d['b1'], w2=d['w2'], b2=d['b2'],
                  palette=d['palette'], alpha=d['alpha'], beta=d['beta'],
                  scene_range=float(meta['scene_range']))
+
+
+PRODUCER_SKIP = ('resample_filter', 'noise_const')
+
+
+def seeded_parameters(named_shapes, seed):
+    """Deterministic weights for a generator's parameters, shared by gen_golden.py (applied to
+    the reference Generator) and the tests (applied to nfi.producer): each tensor drawn by numpy
+    from (seed, crc32(name)), so the fixture stores no weights.  Modulation-affine biases sit
+    around 1 (their init), other biases around 0, alpha/beta keep the reference's init."""
+    import zlib
+    out = {}
+    for name, shape in named_shapes:
+        if name.endswith(PRODUCER_SKIP):
+            continue
+        if name == 'alpha':
+            v = np.ones(shape, np.float32)
+        elif name == 'beta':
+            v = np.full(shape, 0.1, np.float32)
+        else:
+            rng = np.random.default_rng([seed, zlib.crc32(name.encode())])
+            v = rng.standard_normal(shape, dtype=np.float32)
+            if name.endswith('affine.bias'):
+                v = 1 + 0.1 * v
+            elif name.endswith('bias'):
+                v = 0.1 * v
+        out[name] = torch.from_numpy(v)
+    return out
+
+
+def load_seeded(module, seed):
+    """Overwrite `module`'s parameters with seeded_parameters(...) (buffers untouched)."""
+    shapes = [(k, tuple(p.shape)) for k, p in module.named_parameters()]
+    vals = seeded_parameters(shapes, seed)
+    with torch.no_grad():
+        for k, p in module.named_parameters():
+            p.copy_(vals[k])
+    return module
