@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 8
+#define NFI_ABI_VERSION 9
 #define NFI_DEC_SIZE 7184 /* floats in the packed decoder buffer */
 
 enum {

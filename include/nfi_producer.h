@@ -1,0 +1,68 @@
+/*
+ * nfi producer C-ABI: the memory-bound operators of the tri-plane producer (the StyleGAN2
+ * synthesis network of yuliangguo/nerf-from-image, models/stylegan.py:293-490) around its
+ * convolutions, fused for MI355X (gfx950).  The convolutions themselves stay library calls
+ * (MIOpen through PyTorch-ROCm); everything between them is here:
+ *
+ *   modulated-conv epilogue  stylegan.py:140-145, 345-356   x*dcoefs + bias, *sqrt(2), leaky ReLU
+ *   up-sampling FIR epilogue stylegan.py:99-103 (filter2d gain 4, pad 1) + the epilogue above
+ *   skip-image upsample+add  stylegan.py:69-73, 428-433     upsample2d(img) + (toRGB conv + bias)
+ *   channel-scale backward   stylegan.py:130                d(x*styles): g*styles and sum(g*x)
+ *
+ * Tensors are NCHW float32, contiguous; "planes" P = B*C images of one channel; per-plane
+ * scales `d` have P entries ([B,C] row-major), per-channel biases C entries.  `stream` is a
+ * hipStream_t.  Return NFI_OK (0) or a negative code (nfi_last_error() explains).  The
+ * python-side mirror is nerf-from-image_amd/nfi/producer_ops.py.
+ */
+#ifndef NFI_PRODUCER_H
+#define NFI_PRODUCER_H
+
+#include <stdint.h>
+
+#include "nfi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* y = lrelu(gain * (o * d[p] + bias[c]), 0.2) over P planes of HW (HW % 4 == 0).
+ * Replaces stylegan.py:145 (x * dcoefs) + 348-356 (bias, act_gain, leaky_relu). */
+int32_t nfi_syn_act_forward(const float* o, const float* d, const float* bias, float* y,
+                            int32_t P, int32_t C, int32_t HW, float gain, void* stream);
+
+/* Backward of nfi_syn_act_forward: gz = g * gain * slope(pre); go = gz * d[p];
+ * dd[p] = sum_hw gz * o (dd is overwritten). */
+int32_t nfi_syn_act_backward(const float* g, const float* o, const float* d, const float* bias,
+                             float* go, float* dd, int32_t P, int32_t C, int32_t HW, float gain,
+                             void* stream);
+
+/* Up-sampling layer tail (stylegan.py:99-103 then the epilogue): t [P, 2n+1, 2n+1] (the stride-2
+ * transposed-conv output) -> o = FIR_4x4(t) * 4 with pad 1 ([1,3,3,1] outer / 64), [P, 2n, 2n];
+ * y = lrelu(gain * (o * d[p] + bias[c])).  o is written for the backward. */
+int32_t nfi_syn_fir_up_act_forward(const float* t, const float* d, const float* bias, float* o,
+                                   float* y, int32_t P, int32_t C, int32_t n, float gain,
+                                   void* stream);
+
+/* Adjoint of the 4x4 FIR (stylegan.py:36-46 EfficientResample backward): go [P,2n,2n] ->
+ * gt [P,2n+1,2n+1]. */
+int32_t nfi_syn_fir_up_backward(const float* go, float* gt, int32_t P, int32_t n, void* stream);
+
+/* Skip path (stylegan.py:428-433 + 380-381): out [P,2n,2n] = upsample2d(img [P,n,n]) + c +
+ * bias[c]; img may be NULL (first block: out = c + bias). */
+int32_t nfi_syn_up_add_forward(const float* img, const float* c, const float* bias, float* out,
+                               int32_t P, int32_t C, int32_t n, void* stream);
+
+/* Adjoint of upsample2d: g [P,2n,2n] -> gimg [P,n,n] (conv2d with the gain-4 FIR, stride 2,
+ * pad 1; stylegan.py:79-83). */
+int32_t nfi_syn_up_backward(const float* g, float* gimg, int32_t P, int32_t n, void* stream);
+
+/* Backward of x * s[p] (stylegan.py:130 modulation): gx = g * s[p] (gx may be NULL),
+ * ds[p] = sum_hw g * x (overwritten).  HW % 4 == 0. */
+int32_t nfi_syn_scale_backward(const float* g, const float* x, const float* s, float* gx,
+                               float* ds, int32_t P, int32_t HW, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NFI_PRODUCER_H */

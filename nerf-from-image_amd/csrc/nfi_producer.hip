@@ -1,0 +1,338 @@
+// Memory-bound operators of the tri-plane producer (StyleGAN2 synthesis network,
+// models/stylegan.py:293-490) fused for gfx950: everything between the convolutions.
+// One pass over HBM per fused operator, float4 accesses on the contiguous NCHW planes, per-plane
+// reductions folded into the same pass (wave shuffles + one atomic per 4096-element chunk).
+// See include/nfi_producer.h for the contract and DESIGN.md ("Producer") for the traffic model.
+#include "nfi_host.h"
+#include "../../include/nfi_producer.h"
+
+namespace nfi {
+namespace syn {
+
+constexpr int RED_CHUNK4 = 1024;   // float4 per reduction block (4 per thread, 256 threads)
+constexpr float SLOPE = 0.2f;      // F.leaky_relu(x, 0.2) (stylegan.py:356)
+
+__device__ __forceinline__ float act(float o, float d, float b, float gain) {
+  // stylegan.py:145 (x * dcoefs), :350 (+ bias), :352 (mul_(act_gain)), :356 (leaky_relu)
+  float z = __fmul_rn(__fadd_rn(__fmul_rn(o, d), b), gain);
+  return z > 0.f ? z : __fmul_rn(z, SLOPE);
+}
+
+__device__ __forceinline__ float act_slope(float o, float d, float b) {
+  return __fadd_rn(__fmul_rn(o, d), b) > 0.f ? 1.f : SLOPE;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+// block (256) sum -> one atomic per block into *dst
+__device__ __forceinline__ void block_sum_atomic(float v, float* dst) {
+  __shared__ float part[4];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) part[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(dst, (part[0] + part[1]) + (part[2] + part[3]));
+}
+
+__global__ void __launch_bounds__(256) act_fwd_kernel(const float4* __restrict__ o,
+                                                      const float* __restrict__ d,
+                                                      const float* __restrict__ bias,
+                                                      float4* __restrict__ y, int64_t n4, int C,
+                                                      int HW4, float gain) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int p = (int)(i / HW4);
+  const float dp = d[p], b = bias[p % C];
+  const float4 v = o[i];
+  y[i] = make_float4(act(v.x, dp, b, gain), act(v.y, dp, b, gain), act(v.z, dp, b, gain),
+                     act(v.w, dp, b, gain));
+}
+
+// grid (chunks, P): gz = g*gain*slope, go = gz*d, dd[p] += sum gz*o
+__global__ void __launch_bounds__(256) act_bwd_kernel(const float4* __restrict__ g,
+                                                      const float4* __restrict__ o,
+                                                      const float* __restrict__ d,
+                                                      const float* __restrict__ bias,
+                                                      float4* go, float* __restrict__ dd, int C,
+                                                      int HW4, float gain) {
+  const int p = blockIdx.y;
+  const float dp = d[p], b = bias[p % C];
+  const int64_t base = (int64_t)p * HW4;
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = blockIdx.x * RED_CHUNK4 + k * 256 + threadIdx.x;
+    if (j < HW4) {
+      const float4 gv = g[base + j], ov = o[base + j];
+      float4 gz;
+      gz.x = gv.x * gain * act_slope(ov.x, dp, b);
+      gz.y = gv.y * gain * act_slope(ov.y, dp, b);
+      gz.z = gv.z * gain * act_slope(ov.z, dp, b);
+      gz.w = gv.w * gain * act_slope(ov.w, dp, b);
+      acc += (gz.x * ov.x + gz.y * ov.y) + (gz.z * ov.z + gz.w * ov.w);
+      go[base + j] = make_float4(gz.x * dp, gz.y * dp, gz.z * dp, gz.w * dp);
+    }
+  }
+  block_sum_atomic(acc, dd + p);
+}
+
+// grid (chunks, P): gx = g*s[p] (optional), ds[p] += sum g*x
+__global__ void __launch_bounds__(256) scale_bwd_kernel(const float4* __restrict__ g,
+                                                        const float4* __restrict__ x,
+                                                        const float* __restrict__ s,
+                                                        float4* __restrict__ gx,
+                                                        float* __restrict__ ds, int HW4) {
+  const int p = blockIdx.y;
+  const float sp = s[p];
+  const int64_t base = (int64_t)p * HW4;
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = blockIdx.x * RED_CHUNK4 + k * 256 + threadIdx.x;
+    if (j < HW4) {
+      const float4 gv = g[base + j], xv = x[base + j];
+      acc += (gv.x * xv.x + gv.y * xv.y) + (gv.z * xv.z + gv.w * xv.w);
+      if (gx) gx[base + j] = make_float4(gv.x * sp, gv.y * sp, gv.z * sp, gv.w * sp);
+    }
+  }
+  block_sum_atomic(acc, ds + p);
+}
+
+// [1,3,3,1] taps
+__device__ __forceinline__ float k4(int i) { return (i == 0 || i == 3) ? 1.f : 3.f; }
+
+// FIR (gain 4, pad 1) of the (2n+1)^2 transposed-conv output + epilogue; 4 outputs per thread
+__global__ void __launch_bounds__(256) fir_up_act_kernel(const float* __restrict__ t,
+                                                         const float* __restrict__ d,
+                                                         const float* __restrict__ bias,
+                                                         float4* __restrict__ o,
+                                                         float4* __restrict__ y, int64_t n4,
+                                                         int C, int n, float gain) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int W2 = 2 * n, T = 2 * n + 1, q4 = W2 >> 2;
+  const int per = W2 * q4;
+  const int p = (int)(i / per);
+  const int rem = (int)(i - (int64_t)p * per);
+  const int yy = rem / q4, x0 = (rem - yy * q4) * 4;
+  const float* tp = t + (int64_t)p * T * T;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = yy - 1 + r;
+    if (row < 0 || row >= T) continue;
+    float v[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int col = x0 - 1 + j;
+      v[j] = (col >= 0 && col < T) ? tp[row * T + col] : 0.f;
+    }
+    const float kr = k4(r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      acc[k] += kr * ((v[k] + v[k + 3]) + 3.f * (v[k + 1] + v[k + 2]));
+  }
+  const float dp = d[p], b = bias[p % C];
+  const float inv = 1.f / 16.f;
+  const float4 ov = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+  o[i] = ov;
+  y[i] = make_float4(act(ov.x, dp, b, gain), act(ov.y, dp, b, gain), act(ov.z, dp, b, gain),
+                     act(ov.w, dp, b, gain));
+}
+
+// adjoint FIR: gt[r][c] = sum_ij k_i k_j / 16 * go[r+1-i][c+1-j]
+__global__ void __launch_bounds__(256) fir_up_bwd_kernel(const float* __restrict__ go,
+                                                         float* __restrict__ gt, int64_t total,
+                                                         int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int W2 = 2 * n, T = 2 * n + 1;
+  const int p = (int)(i / (T * T));
+  const int rem = (int)(i - (int64_t)p * T * T);
+  const int r = rem / T, c = rem - r * T;
+  const float* gp = go + (int64_t)p * W2 * W2;
+  float acc = 0.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = r + 1 - a;
+    if (row < 0 || row >= W2) continue;
+    float h = 0.f;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int col = c + 1 - bb;
+      if (col >= 0 && col < W2) h += k4(bb) * gp[row * W2 + col];
+    }
+    acc += k4(a) * h;
+  }
+  gt[i] = acc * (1.f / 16.f);
+}
+
+// out[2n x 2n] = upsample2d(img[n x n]) + c + bias; 4 outputs per thread
+__global__ void __launch_bounds__(256) up_add_kernel(const float* __restrict__ img,
+                                                     const float4* __restrict__ cc,
+                                                     const float* __restrict__ bias,
+                                                     float4* __restrict__ out, int64_t n4, int C,
+                                                     int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int W2 = 2 * n, q4 = W2 >> 2;
+  const int per = W2 * q4;
+  const int p = (int)(i / per);
+  const int rem = (int)(i - (int64_t)p * per);
+  const int yy = rem / q4, x0 = (rem - yy * q4) * 4;
+  const float b = bias[p % C];
+  float4 cv = cc[i];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (img) {
+    const float* ip = img + (int64_t)p * n * n;
+    const int q = yy >> 1;
+    // rows: even yy=2q -> img[q-1]*1 + img[q]*3 ; odd yy=2q+1 -> img[q]*3 + img[q+1]*1
+    const int r0 = (yy & 1) ? q : q - 1;
+    const float w0 = (yy & 1) ? 3.f : 1.f, w1 = (yy & 1) ? 1.f : 3.f;
+    const int m = x0 >> 1;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int row = r0 + rr;
+      if (row < 0 || row >= n) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = m - 1 + j;
+        v[j] = (col >= 0 && col < n) ? ip[row * n + col] : 0.f;
+      }
+      const float wr = rr == 0 ? w0 : w1;
+      acc[0] += wr * (v[0] + 3.f * v[1]);
+      acc[1] += wr * (3.f * v[1] + v[2]);
+      acc[2] += wr * (v[1] + 3.f * v[2]);
+      acc[3] += wr * (3.f * v[2] + v[3]);
+    }
+  }
+  const float inv = 1.f / 16.f;
+  out[i] = make_float4(acc[0] * inv + (cv.x + b), acc[1] * inv + (cv.y + b),
+                       acc[2] * inv + (cv.z + b), acc[3] * inv + (cv.w + b));
+}
+
+// gimg[q][m] = sum over rows {2q-1:1, 2q:3, 2q+1:3, 2q+2:1} x cols (same) / 16
+__global__ void __launch_bounds__(256) up_bwd_kernel(const float* __restrict__ g,
+                                                     float* __restrict__ gimg, int64_t total,
+                                                     int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int W2 = 2 * n;
+  const int p = (int)(i / (n * n));
+  const int rem = (int)(i - (int64_t)p * n * n);
+  const int q = rem / n, m = rem - q * n;
+  const float* gp = g + (int64_t)p * W2 * W2;
+  float acc = 0.f;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = 2 * q - 1 + a;
+    if (row < 0 || row >= W2) continue;
+    float h = 0.f;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int col = 2 * m - 1 + bb;
+      if (col >= 0 && col < W2) h += k4(bb) * gp[row * W2 + col];
+    }
+    acc += k4(a) * h;
+  }
+  gimg[i] = acc * (1.f / 16.f);
+}
+
+inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace syn
+}  // namespace nfi
+
+using namespace nfi::syn;
+
+extern "C" {
+
+int32_t nfi_syn_act_forward(const float* o, const float* d, const float* bias, float* y, int32_t P,
+                            int32_t C, int32_t HW, float gain, void* stream) {
+  NFI_REQUIRE(o && d && bias && y, "syn_act_forward: null pointer");
+  NFI_REQUIRE(P > 0 && C > 0 && P % C == 0 && HW > 0 && HW % 4 == 0, "syn_act_forward: bad shape");
+  const int64_t n4 = (int64_t)P * (HW / 4);
+  act_fwd_kernel<<<blocks(n4), 256, 0, (hipStream_t)stream>>>((const float4*)o, d, bias, (float4*)y,
+                                                               n4, C, HW / 4, gain);
+  NFI_CHECK_LAUNCH("act_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_act_backward(const float* g, const float* o, const float* d, const float* bias,
+                             float* go, float* dd, int32_t P, int32_t C, int32_t HW, float gain,
+                             void* stream) {
+  NFI_REQUIRE(g && o && d && bias && go && dd, "syn_act_backward: null pointer");
+  NFI_REQUIRE(P > 0 && C > 0 && P % C == 0 && HW > 0 && HW % 4 == 0, "syn_act_backward: bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(dd, 0, sizeof(float) * P, s) != hipSuccess) {
+    nfi::set_error("syn_act_backward: memset failed");
+    return NFI_ELAUNCH;
+  }
+  const int HW4 = HW / 4;
+  act_bwd_kernel<<<dim3((HW4 + RED_CHUNK4 - 1) / RED_CHUNK4, P), 256, 0, s>>>(
+      (const float4*)g, (const float4*)o, d, bias, (float4*)go, dd, C, HW4, gain);
+  NFI_CHECK_LAUNCH("act_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_fir_up_act_forward(const float* t, const float* d, const float* bias, float* o,
+                                   float* y, int32_t P, int32_t C, int32_t n, float gain,
+                                   void* stream) {
+  NFI_REQUIRE(t && d && bias && o && y, "syn_fir_up_act_forward: null pointer");
+  NFI_REQUIRE(P > 0 && C > 0 && P % C == 0 && n >= 2 && n % 2 == 0, "syn_fir_up_act_forward: bad shape");
+  const int64_t n4 = (int64_t)P * (2 * n) * (2 * n) / 4;
+  fir_up_act_kernel<<<blocks(n4), 256, 0, (hipStream_t)stream>>>(t, d, bias, (float4*)o, (float4*)y,
+                                                                  n4, C, n, gain);
+  NFI_CHECK_LAUNCH("fir_up_act_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_fir_up_backward(const float* go, float* gt, int32_t P, int32_t n, void* stream) {
+  NFI_REQUIRE(go && gt && P > 0 && n >= 1, "syn_fir_up_backward: bad args");
+  const int64_t total = (int64_t)P * (2 * n + 1) * (2 * n + 1);
+  fir_up_bwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(go, gt, total, n);
+  NFI_CHECK_LAUNCH("fir_up_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_add_forward(const float* img, const float* c, const float* bias, float* out,
+                               int32_t P, int32_t C, int32_t n, void* stream) {
+  NFI_REQUIRE(c && bias && out, "syn_up_add_forward: null pointer");
+  NFI_REQUIRE(P > 0 && C > 0 && P % C == 0 && n >= 2 && n % 2 == 0, "syn_up_add_forward: bad shape");
+  const int64_t n4 = (int64_t)P * (2 * n) * (2 * n) / 4;
+  up_add_kernel<<<blocks(n4), 256, 0, (hipStream_t)stream>>>(img, (const float4*)c, bias,
+                                                              (float4*)out, n4, C, n);
+  NFI_CHECK_LAUNCH("up_add_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_backward(const float* g, float* gimg, int32_t P, int32_t n, void* stream) {
+  NFI_REQUIRE(g && gimg && P > 0 && n >= 1, "syn_up_backward: bad args");
+  const int64_t total = (int64_t)P * n * n;
+  up_bwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(g, gimg, total, n);
+  NFI_CHECK_LAUNCH("up_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_scale_backward(const float* g, const float* x, const float* s, float* gx, float* ds,
+                               int32_t P, int32_t HW, void* stream) {
+  NFI_REQUIRE(g && x && s && ds, "syn_scale_backward: null pointer");
+  NFI_REQUIRE(P > 0 && HW > 0 && HW % 4 == 0, "syn_scale_backward: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(ds, 0, sizeof(float) * P, st) != hipSuccess) {
+    nfi::set_error("syn_scale_backward: memset failed");
+    return NFI_ELAUNCH;
+  }
+  const int HW4 = HW / 4;
+  scale_bwd_kernel<<<dim3((HW4 + RED_CHUNK4 - 1) / RED_CHUNK4, P), 256, 0, st>>>(
+      (const float4*)g, (const float4*)x, s, (float4*)gx, ds, HW4);
+  NFI_CHECK_LAUNCH("scale_bwd_kernel");
+  return NFI_OK;
+}
+
+}  // extern "C"

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 8
+ABI_VERSION = 9
 DEC_SIZE = 7184
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -78,6 +78,23 @@ SIGNATURES = {
     'nfi_render_backward_stage': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
                                                    ctypes.POINTER(NfiRenderGradArgs), ctypes.c_int32,
                                                    c_void_p]),
+    # include/nfi_producer.h
+    'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),
+    'nfi_syn_act_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                              ctypes.c_float, c_void_p]),
+    'nfi_syn_fir_up_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                    ctypes.c_float, c_void_p]),
+    'nfi_syn_fir_up_backward': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                 c_void_p]),
+    'nfi_syn_up_add_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
+                                                ctypes.c_int32, ctypes.c_int32, c_void_p]),
+    'nfi_syn_up_backward': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                             c_void_p]),
+    'nfi_syn_scale_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                ctypes.c_int32, ctypes.c_int32, c_void_p]),
 }
 
 _lib = None

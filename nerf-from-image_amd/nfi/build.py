@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), 'csrc')
 OUT = os.path.join(HERE, 'libnfi_hip.so')
-SOURCES = ['nfi_rays.hip', 'nfi_render.hip']
+SOURCES = ['nfi_rays.hip', 'nfi_render.hip', 'nfi_producer.hip']
 HEADERS = ['nfi_common.h', 'nfi_host.h']
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-munsafe-fp-atomics',
          '-Wall', '-Wno-unused-result']
@@ -20,7 +20,8 @@ def _stale() -> bool:
         return True
     t = os.path.getmtime(OUT)
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps.append(os.path.join(os.path.dirname(os.path.dirname(HERE)), 'include', 'nfi.h'))
+    inc = os.path.join(os.path.dirname(os.path.dirname(HERE)), 'include')
+    deps += [os.path.join(inc, h) for h in ('nfi.h', 'nfi_producer.h')]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

@@ -5,11 +5,19 @@ generator.py:475-477), AttentionMapper -> palette [b,10,3] (generator.py:132-186
 455-462) — plus the mapping network used for the average latent (stylegan.py:228-290,
 generator.py:263-282) and the frozen SDF decoder weights.
 
-Plain PyTorch-ROCm (convolutions on MIOpen), written from the reference's published behaviour;
-parameter and buffer names equal the reference Generator's state_dict keys, so a G_ema checkpoint
-loads with `load_state_dict(sd, strict=False)`.  Pinned against the reference by
-tests/golden/producer.npz (tests/test_producer.py).  The HIP renderer consumes it through
-`nfi.render(generator, ...)` exactly as it consumes the reference Generator.
+Two backends, chosen explicitly (never a silent fallback):
+  'hip'   (default) the convolutions are library calls (MIOpen via PyTorch-ROCm) and everything
+          between them runs in the fused HIP kernels of csrc/nfi_producer.hip (producer_ops.py):
+          modulation backward, demodulation + bias + gain + leaky-ReLU epilogue, the up-sampling
+          FIR fused with that epilogue, the skip-image upsample + add; the demodulation
+          coefficients as one [b,in]x[in,out] product (sum_k W^2 precomputed per forward);
+          device tensors only;
+  'torch' the reference's op sequence restated in plain PyTorch (any device) — the CPU-pinned
+          restatement the tests check against the reference's fixtures.
+Parameter and buffer names equal the reference Generator's state_dict keys, so a G_ema
+checkpoint loads with `load_state_dict(sd)`.  Pinned by tests/golden/producer.npz
+(tests/test_producer.py on CPU, tests/test_gpu_inversion.py for 'hip').  The HIP renderer
+consumes it through `nfi.render(generator, ...)` exactly as it consumes the reference Generator.
 """
 
 from __future__ import annotations
@@ -21,6 +29,12 @@ import torch.nn.functional as F
 from torch import nn
 
 SQRT2 = math.sqrt(2.0)
+BACKENDS = ('hip', 'torch')
+
+
+def _hip():
+    from . import producer_ops
+    return producer_ops
 
 
 def blur_kernel() -> torch.Tensor:
@@ -82,7 +96,11 @@ class ModulatedConv(nn.Module):
         self.register_buffer('noise_const', torch.randn(resolution, resolution))
         self.register_buffer('resample_filter', blur_kernel())
 
+    backend = 'hip'
+
     def forward(self, x, w):
+        if self.backend == 'hip':
+            return self._forward_hip(x, w)
         styles = self.affine(w)                                           # [b, in]
         wmod = self.weight[None] * styles[:, None, :, None, None]         # [b, out, in, 3, 3]
         dcoefs = (wmod.square().sum(dim=(2, 3, 4)) + 1e-8).rsqrt()        # [b, out]
@@ -96,6 +114,17 @@ class ModulatedConv(nn.Module):
         x = (x + self.bias[None, :, None, None]) * SQRT2
         return F.leaky_relu(x, 0.2)
 
+    def _forward_hip(self, x, w):
+        ops = _hip()
+        styles = self.affine(w)
+        w2 = self.weight.square().sum(dim=(2, 3))                         # [out, in]
+        dcoefs = (styles.square() @ w2.t() + 1e-8).rsqrt()                # [b, out]
+        xs = ops.scale(x, styles)
+        if self.up:
+            t = F.conv_transpose2d(xs, self.weight.transpose(0, 1), stride=2)
+            return ops.fir_up_act(t, dcoefs, self.bias, SQRT2)
+        return ops.act(F.conv2d(xs, self.weight, padding=1), dcoefs, self.bias, SQRT2)
+
 
 class ToPlanes(nn.Module):
     """OutputLayer (stylegan.py:363-384): modulated 1x1 conv without demodulation, plus bias."""
@@ -107,8 +136,12 @@ class ToPlanes(nn.Module):
         self.bias = nn.Parameter(torch.zeros(out_ch))
         self.weight_gain = 1.0 / math.sqrt(in_ch)
 
+    backend = 'hip'
+
     def forward(self, x, w):
         styles = self.affine(w) * self.weight_gain
+        if self.backend == 'hip':
+            return F.conv2d(_hip().scale(x, styles), self.weight)          # bias added in up_add
         x = F.conv2d(x * styles[:, :, None, None], self.weight)
         return x + self.bias[None, :, None, None]
 
@@ -128,6 +161,8 @@ class SynthesisBlock(nn.Module):
         self.register_buffer('resample_filter', blur_kernel())
         self.num_conv = 1 if in_ch == 0 else 2
 
+    backend = 'hip'
+
     def forward(self, x, img, ws):
         k = 0
         if self.in_ch == 0:
@@ -137,6 +172,8 @@ class SynthesisBlock(nn.Module):
             k += 1
         x = self.conv1(x, ws[:, k])
         y = self.torgb(x, ws[:, k + 1])
+        if self.backend == 'hip':
+            return x, _hip().up_add(img, y, self.torgb.bias)
         img = y if img is None else upsample2x(img, self.resample_filter) + y
         return x, img
 
@@ -260,7 +297,7 @@ class InversionGenerator(nn.Module):
     latent 512, attention_values=10, use_sdf, no viewdir / encoder / classes, StyleGAN noise
     disabled).  `nfi.render(gen, ...)` renders it; `planes_and_palette(ws)` exposes the producer."""
 
-    def __init__(self, scene_range: float, img_resolution: int = 256):
+    def __init__(self, scene_range: float, img_resolution: int = 256, backend: str = 'hip'):
         super().__init__()
         self.scene_range = scene_range
         self.attention_values = 10
@@ -274,6 +311,18 @@ class InversionGenerator(nn.Module):
         self.texture_mapper = PaletteMapper(512, 10)
         self.beta = nn.Parameter(torch.tensor([0.1]))
         self.alpha = nn.Parameter(torch.tensor([1.0]))
+        self.set_backend(backend)
+
+    def set_backend(self, backend: str):
+        """'hip' (fused HIP kernels between the convolutions, device tensors only) or 'torch'
+        (the reference's op sequence in plain PyTorch)."""
+        if backend not in BACKENDS:
+            raise ValueError(f'backend must be one of {BACKENDS}')
+        self.backend = backend
+        for m in self.synthesis_network.modules():
+            if isinstance(m, (ModulatedConv, ToPlanes, SynthesisBlock)):
+                m.backend = backend
+        return self
 
     def planes_and_palette(self, ws):
         palette = self.texture_mapper(ws[:, 14])

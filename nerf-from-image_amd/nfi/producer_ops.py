@@ -1,0 +1,160 @@
+"""Autograd operators over the producer C-ABI (include/nfi_producer.h): the fused HIP kernels
+between the synthesis network's convolutions.  Device tensors only; the generator is frozen in
+the inversion (run.py:630-632), so biases never receive gradients (asking for one raises).
+
+  scale      x * s[b,c]                         stylegan.py:130 (modulation)
+  act        lrelu(gain*(o*d[b,c] + bias[c]))   stylegan.py:145, 348-356 (demodulation epilogue)
+  fir_up_act FIR(t) then act                    stylegan.py:99-103 + the epilogue (up layers)
+  up_add     upsample2d(img) + c + bias[c]      stylegan.py:69-73, 380-381, 428-433 (skip image)
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .ops import _require_device, _stream
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _call(name, *args):
+    lib = _lib.load()
+    _lib.check(getattr(lib, name)(*args), name)
+
+
+def _frozen(bias):
+    if torch.is_grad_enabled() and bias.requires_grad:
+        raise NotImplementedError('producer biases are frozen in the inversion path '
+                                  '(call requires_grad_(False) on the generator)')
+
+
+class _Scale(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        _require_device(x, s)
+        x = x.contiguous()
+        s = s.contiguous()
+        ctx.save_for_backward(x, s)
+        return x * s[:, :, None, None]
+
+    @staticmethod
+    def backward(ctx, g):
+        x, s = ctx.saved_tensors
+        g = g.contiguous()
+        B, C, H, W = x.shape
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
+        _call('nfi_syn_scale_backward', _p(g), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W,
+              _stream(x.device))
+        return gx, ds
+
+
+class _Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, o, d, bias, gain: float):
+        _require_device(o, d, bias)
+        _frozen(bias)
+        o = o.contiguous()
+        d = d.contiguous()
+        B, C, H, W = o.shape
+        y = torch.empty_like(o)
+        _call('nfi_syn_act_forward', _p(o), _p(d), _p(bias), _p(y), B * C, C, H * W,
+              ctypes.c_float(gain), _stream(o.device))
+        ctx.save_for_backward(o, d, bias)
+        ctx.gain = gain
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        o, d, bias = ctx.saved_tensors
+        g = g.contiguous()
+        B, C, H, W = o.shape
+        go = torch.empty_like(o)
+        dd = torch.empty_like(d)
+        _call('nfi_syn_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(go), _p(dd), B * C, C,
+              H * W, ctypes.c_float(ctx.gain), _stream(o.device))
+        return go, dd, None, None
+
+
+class _FirUpAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t, d, bias, gain: float):
+        _require_device(t, d, bias)
+        _frozen(bias)
+        t = t.contiguous()
+        d = d.contiguous()
+        B, C, T, T2 = t.shape
+        assert T == T2 and T % 2 == 1
+        n = (T - 1) // 2
+        o = torch.empty((B, C, 2 * n, 2 * n), device=t.device, dtype=t.dtype)
+        y = torch.empty_like(o)
+        _call('nfi_syn_fir_up_act_forward', _p(t), _p(d), _p(bias), _p(o), _p(y), B * C, C, n,
+              ctypes.c_float(gain), _stream(t.device))
+        ctx.save_for_backward(o, d, bias)
+        ctx.gain = gain
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        o, d, bias = ctx.saved_tensors
+        g = g.contiguous()
+        B, C, H, W = o.shape
+        n = H // 2
+        go = torch.empty_like(o)
+        dd = torch.empty_like(d)
+        dev = _stream(o.device)
+        _call('nfi_syn_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(go), _p(dd), B * C, C,
+              H * W, ctypes.c_float(ctx.gain), dev)
+        gt = torch.empty((B, C, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
+        _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * C, n, dev)
+        return gt, dd, None, None
+
+
+class _UpAdd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, c, bias):
+        _require_device(img, c, bias)
+        _frozen(bias)
+        c = c.contiguous()
+        B, C, H, W = c.shape
+        n = H // 2
+        if img is not None:
+            img = img.contiguous()
+            assert img.shape == (B, C, n, n), (img.shape, c.shape)
+        out = torch.empty_like(c)
+        _call('nfi_syn_up_add_forward', _p(img), _p(c), _p(bias), _p(out), B * C, C, n,
+              _stream(c.device))
+        ctx.has_img = img is not None
+        ctx.shape = (B, C, n)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gimg = None
+        if ctx.has_img and ctx.needs_input_grad[0]:
+            g = g.contiguous()
+            B, C, n = ctx.shape
+            gimg = torch.empty((B, C, n, n), device=g.device, dtype=g.dtype)
+            _call('nfi_syn_up_backward', _p(g), _p(gimg), B * C, n, _stream(g.device))
+        return gimg, g, None
+
+
+def scale(x, s):
+    return _Scale.apply(x, s)
+
+
+def act(o, d, bias, gain: float):
+    return _Act.apply(o, d, bias, gain)
+
+
+def fir_up_act(t, d, bias, gain: float):
+    return _FirUpAct.apply(t, d, bias, gain)
+
+
+def up_add(img, c, bias):
+    return _UpAdd.apply(img, c, bias)

@@ -1,5 +1,5 @@
 """CPU-side checks of the C-ABI boundary: the in-tree HIP library loads, exports every entry
-point declared in include/nfi.h, and the ctypes structs match the C layout (gcc-compiled
+point declared in include/*.h (nfi.h, nfi_producer.h), and the ctypes structs match the C layout (gcc-compiled
 probe).  No compute calls (no GPU here)."""
 
 import os
@@ -13,10 +13,12 @@ from nfi import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, 'include', 'nfi.h')
+HEADERS = [os.path.join(ROOT, 'include', h) for h in sorted(os.listdir(os.path.join(ROOT, 'include')))
+           if h.endswith('.h')]
 
 
 def declared_functions():
-    src = open(HEADER).read()
+    src = '\n'.join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r'^\s*(?:int32_t|int64_t|const char\*)\s+(nfi_\w+)\s*\(', src, re.M)))
 
 

@@ -4,8 +4,11 @@ and pose_utils; 3 Adam steps, L1 loss, pose optimised, injected random draws).
 
 The producer runs in PyTorch-ROCm on the GPU; the volume render (forward + backward to planes,
 palette and the camera) is the HIP path.  Tolerances: losses to 1e-4 relative (the HIP render
-matches the reference to fp32 rounding, tests/test_gpu_parity.py); latent and pose as in
-tests/test_producer.py::check_trajectory.
+matches the reference to fp32 rounding, tests/test_gpu_parity.py); latent and pose within 3%
+of the distance the reference moved them (tests/test_producer.py::check_trajectory): the fp32
+differences of the GPU producer (MIOpen; d_ws 4e-4 relative L2) and renderer in the gradient
+feed Adam's normalised steps, where small gradient coordinates count as much as large ones
+(measured 1.1-1.25%; the CPU oracle in the same loop stays below 0.1%).
 """
 
 import pytest
@@ -50,7 +53,7 @@ def test_producer_on_gpu():
     """The producer on the GPU (MIOpen convolutions) against the reference's CPU outputs."""
     dev = torch.device('cuda:0')
     d, meta = load('producer')
-    gen = producer.InversionGenerator(scene_range=1.4)
+    gen = producer.InversionGenerator(scene_range=1.4)           # backend 'hip'
     load_seeded(gen, int(meta['seed']))
     gen.requires_grad_(False).to(dev)
     ws = d['ws'].to(dev).requires_grad_()

@@ -1,0 +1,119 @@
+"""The producer's fused HIP operators (csrc/nfi_producer.hip via nfi/producer_ops.py) against
+plain PyTorch fp32 formulations of the same ops — forward values and gradients (autograd of
+the torch formulation) at the resolutions the synthesis network uses and odd channel counts."""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from nfi import producer, producer_ops
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+GAIN = math.sqrt(2.0)
+
+
+def _rand(*shape, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randn(shape, generator=g, device=DEV)
+
+
+def _close(a, b, rel=2e-6):
+    scale = float(b.abs().max()) + 1e-30
+    err = float((a - b).abs().max())
+    assert err <= rel * scale * 8, (err, scale)
+
+
+def _act_ref(o, d, bias):
+    x = o * d[:, :, None, None]
+    x = (x + bias[None, :, None, None]) * GAIN
+    return F.leaky_relu(x, 0.2)
+
+
+@pytest.mark.parametrize('B,C,H', [(2, 3, 4), (2, 5, 8), (3, 7, 32), (2, 4, 128)])
+def test_scale(B, C, H):
+    x = _rand(B, C, H, H, seed=1).requires_grad_()
+    s = _rand(B, C, seed=2).requires_grad_()
+    g = _rand(B, C, H, H, seed=3)
+    y = producer_ops.scale(x, s)
+    y.backward(g)
+    xr, sr = x.detach().clone().requires_grad_(), s.detach().clone().requires_grad_()
+    (xr * sr[:, :, None, None]).backward(g)
+    _close(y.detach(), (xr * sr[:, :, None, None]).detach())
+    _close(x.grad, xr.grad)
+    _close(s.grad, sr.grad, rel=1e-5)
+
+
+@pytest.mark.parametrize('B,C,H', [(2, 3, 4), (2, 5, 8), (3, 7, 32), (2, 4, 128)])
+def test_act(B, C, H):
+    o = _rand(B, C, H, H, seed=4).requires_grad_()
+    d = (_rand(B, C, seed=5).abs() + 0.1).requires_grad_()
+    bias = 0.3 * _rand(C, seed=6)
+    g = _rand(B, C, H, H, seed=7)
+    y = producer_ops.act(o, d, bias, GAIN)
+    y.backward(g)
+    orf, drf = o.detach().clone().requires_grad_(), d.detach().clone().requires_grad_()
+    yr = _act_ref(orf, drf, bias)
+    yr.backward(g)
+    _close(y.detach(), yr.detach())
+    _close(o.grad, orf.grad)
+    _close(d.grad, drf.grad, rel=1e-5)
+
+
+@pytest.mark.parametrize('B,C,n', [(2, 3, 2), (2, 5, 4), (3, 6, 16), (2, 4, 64)])
+def test_fir_up_act(B, C, n):
+    t = _rand(B, C, 2 * n + 1, 2 * n + 1, seed=8).requires_grad_()
+    d = (_rand(B, C, seed=9).abs() + 0.1).requires_grad_()
+    bias = 0.3 * _rand(C, seed=10)
+    g = _rand(B, C, 2 * n, 2 * n, seed=11)
+    y = producer_ops.fir_up_act(t, d, bias, GAIN)
+    y.backward(g)
+    trf, drf = t.detach().clone().requires_grad_(), d.detach().clone().requires_grad_()
+    o = producer._depthwise(trf, producer.blur_kernel().to(DEV) * 4, stride=1, transpose=False)
+    yr = _act_ref(o, drf, bias)
+    yr.backward(g)
+    _close(y.detach(), yr.detach())
+    _close(t.grad, trf.grad)
+    _close(d.grad, drf.grad, rel=1e-5)
+
+
+@pytest.mark.parametrize('B,C,n', [(2, 3, 2), (2, 5, 4), (1, 96, 16), (2, 96, 128)])
+@pytest.mark.parametrize('with_img', [True, False])
+def test_up_add(B, C, n, with_img):
+    img = _rand(B, C, n, n, seed=12).requires_grad_() if with_img else None
+    c = _rand(B, C, 2 * n, 2 * n, seed=13).requires_grad_()
+    bias = 0.3 * _rand(C, seed=14)
+    g = _rand(B, C, 2 * n, 2 * n, seed=15)
+    out = producer_ops.up_add(img, c, bias)
+    out.backward(g)
+    crf = c.detach().clone().requires_grad_()
+    yr = crf + bias[None, :, None, None]
+    if with_img:
+        irf = img.detach().clone().requires_grad_()
+        yr = producer.upsample2x(irf, producer.blur_kernel().to(DEV)) + yr
+    yr.backward(g)
+    _close(out.detach(), yr.detach())
+    _close(c.grad, crf.grad)
+    if with_img:
+        _close(img.grad, irf.grad)
+
+
+def test_backends_agree_on_gpu():
+    """Full producer: 'hip' against 'torch' (the reference's op sequence) on the same device."""
+    torch.manual_seed(3)
+    gen = producer.InversionGenerator(1.4).to(DEV).requires_grad_(False)
+    ws = (0.6 * _rand(2, 15, 512, seed=16)).requires_grad_()
+    g = _rand(2, 3, 32, 256, 256, seed=17)
+    out = {}
+    for be in ('hip', 'torch'):
+        gen.set_backend(be)
+        w = ws.detach().clone().requires_grad_()
+        planes, pal = gen.planes_and_palette(w)
+        ((planes * g).sum() + pal.sum()).backward()
+        out[be] = (planes.detach(), w.grad)
+    scale = float(out['torch'][0].abs().max())
+    assert float((out['hip'][0] - out['torch'][0]).abs().max()) < 1e-4 * scale
+    gerr = float((out['hip'][1] - out['torch'][1]).norm() / out['torch'][1].norm())
+    assert gerr < 1e-3, gerr

@@ -21,7 +21,7 @@ from nfi import inversion, producer
 @pytest.fixture(scope='module')
 def prod():
     d, meta = load('producer')
-    gen = producer.InversionGenerator(scene_range=1.4)
+    gen = producer.InversionGenerator(scene_range=1.4, backend='torch')
     load_seeded(gen, int(meta['seed']))
     gen.requires_grad_(False)
     return gen, d
@@ -101,7 +101,8 @@ def oracle_render_fn(scene_range):
 
 def inversion_setup(device='cpu'):
     d, meta = load('inversion')
-    gen = producer.InversionGenerator(scene_range=float(meta['scene_range']))
+    gen = producer.InversionGenerator(scene_range=float(meta['scene_range']),
+                                      backend='torch' if str(device) == 'cpu' else 'hip')
     load_seeded(gen, int(meta['seed']))
     with torch.no_grad():
         gen.decoder.net[2].bias[0] += float(meta['sdf_shift'])
@@ -158,3 +159,13 @@ def test_inversion_default_renderer_is_hip_only():
     with pytest.raises(RuntimeError, match='HIP devices only'):
         inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg,
                          uniforms=lambda it: (d['u_coarse'][it], d['u_fine'][it]))
+
+
+def test_hip_backend_refuses_cpu_tensors():
+    gen = producer.InversionGenerator(scene_range=1.4)          # default backend: hip
+    assert gen.backend == 'hip'
+    gen.requires_grad_(False)
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        gen.planes_and_palette(torch.zeros(1, 15, 512))
+    with pytest.raises(ValueError):
+        gen.set_backend('cpu')
