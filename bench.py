@@ -105,21 +105,66 @@ def cpu_baseline(args):
                     break
     except OSError:
         pass
-    return {'value': samples / t / 1e6, 'unit': 'Msamples/s', 'cores': cores, 'kind': 'port',
-            'sample': f'1 image {H}x{H}, 64+64 samples/ray, fwd+bwd (planes, palette, pose grads), '
-                      f'median of {args.cpu_reps} after 1 warm-up; {model or platform.processor()}',
-            'seconds_per_image_step': t}
+    out = {'value': samples / t / 1e6, 'unit': 'Msamples/s', 'cores': cores, 'kind': 'port',
+           'sample': f'1 image {H}x{H}, 64+64 samples/ray, fwd+bwd (planes, palette, pose grads), '
+                     f'median of {args.cpu_reps} after 1 warm-up; {model or platform.processor()}',
+           'seconds_per_image_step': t}
+    if not args.no_inversion:
+        inv = cpu_inversion_step(inp, H, args.inv_loss.split(','))
+        first = args.inv_loss.split(',')[0]
+        out['inversion'] = inv[first]
+        for k, v in inv.items():
+            if k != first:
+                out[f'inversion_{k}'] = v
+    return out
 
 
-def inversion_leg(args, dev, cfg, batch, world):
+def cpu_inversion_step(inp, H, loss_kinds):
+    """One step of the inversion loop on the CPU, the reference's way: producer in PyTorch (the
+    'torch' backend, the reference's op sequence) + the oracle renderer, L1 loss, Adam; 1 image at
+    HxH, 64+64 samples; s/image for 30 steps = 30 x the step (timed after one warm-up step)."""
+    from nfi import inversion, lpips, producer
+    from oracle import render_oracle as orc
+    torch.manual_seed(4321)
+    gen = producer.InversionGenerator(scene_range=1.4, backend='torch')
+    with torch.no_grad():
+        gen.decoder.net[2].bias[0] -= 0.97
+    gen.requires_grad_(False)
+    w_avg = gen.mapping_network.get_average_w(n_samples=1000, generator=torch.Generator().manual_seed(7))
+    target = torch.tanh(torch.randn((1, H, H, 3), generator=torch.Generator().manual_seed(99)))
+
+    def render_fn(g, Hh, Ww, cam, focal, center, bbox, ws, S, force_no_cam_grad=False, **kw):
+        planes, palette = g.planes_and_palette(ws)
+        net = g.decoder.net
+        field = orc.Field(planes=planes, w1=net[0].weight, b1=net[0].bias, w2=net[2].weight,
+                          b2=net[2].bias, palette=palette, alpha=g.alpha, beta=g.beta, scene_range=1.4)
+        return orc.render(field, Hh, Ww, cam, focal, center, bbox, S, randomize=True,
+                          force_no_cam_grad=force_no_cam_grad)
+
+    res = {}
+    for loss in loss_kinds:
+        cfg = inversion.InversionConfig(steps=1, resolution=H, samples=64, loss=loss, camera_flipped=True)
+        net = lpips.LPIPS(backend='torch') if loss in inversion.VGG_LOSSES else None
+        inversion.invert(gen, target, inp['cam'], inp['focal'], w_avg, cfg, render_fn=render_fn, lpips_net=net)
+        t0 = time.perf_counter()
+        inversion.invert(gen, target, inp['cam'], inp['focal'], w_avg, cfg, render_fn=render_fn, lpips_net=net)
+        step = time.perf_counter() - t0
+        res[loss] = {'s_per_image': round(30 * step, 3), 'step_seconds': round(step, 3),
+                     'sample': f'1 image {H}x{H}, 64+64 samples, producer (torch backend) + oracle render '
+                               f'fwd+bwd, loss {loss}, Adam; one timed step after one warm-up, x30'}
+    return res
+
+
+def inversion_leg(args, dev, cfg, batch, world, loss):
     """BASELINE.json's second number: seconds per image of the 30-step inversion (run.py:1960-2310,
-    --inv_loss l1, pose optimised): per step the producer (synthesis network + AttentionMapper,
-    PyTorch-ROCm / MIOpen, fp32) forward, the HIP render fwd+bwd, the producer backward to the
-    latent and Adam.  Random-init generator (no checkpoint offline), z_avg from the mapping
-    network, the same cameras as the renderer leg, a synthetic target image.  Timed like the
-    renderer leg (barrier + synchronize around exactly --inv-steps steps, max over ranks)."""
-    import nfi
-    from nfi import inversion, ops, producer
+    pose optimised): per step the producer (synthesis network + AttentionMapper: convolutions on
+    MIOpen, the rest in the fused HIP kernels, fp32) forward, the HIP render fwd+bwd, the loss
+    ('vgg' = the reference default --inv_loss: LPIPS-VGG over the image + 15 augmented copies,
+    random weights since none ship offline; or 'l1'), the backward to the latent and pose, Adam.
+    Random-init generator (no checkpoint offline), z_avg from the mapping network, the same
+    cameras as the renderer leg, a synthetic target image.  Timed like the renderer leg (barrier +
+    synchronize around exactly --inv-steps steps, max over ranks)."""
+    from nfi import inversion, lpips, ops, producer
     sr, wbg, flipped, B, H, S, pose, bwd = cfg
     torch.manual_seed(4321)
     gen = producer.InversionGenerator(scene_range=sr).to(dev)
@@ -129,10 +174,11 @@ def inversion_leg(args, dev, cfg, batch, world):
     w_avg = gen.mapping_network.get_average_w(generator=torch.Generator().manual_seed(7))
     g = torch.Generator(device=dev).manual_seed(99)
     target = torch.tanh(torch.randn((B, H, H, 3), generator=g, device=dev))
-    icfg = inversion.InversionConfig(steps=2, resolution=H, samples=S, loss='l1',
-                                     camera_flipped=flipped)
+    icfg = inversion.InversionConfig(steps=2, resolution=H, samples=S, loss=loss,
+                                     camera_flipped=flipped, white_background=wbg)
+    net = lpips.LPIPS().to(dev) if loss in inversion.VGG_LOSSES else None
     cam, focal = batch['cam'].detach(), batch['focal'].detach()
-    inversion.invert(gen, target, cam, focal, w_avg, icfg)           # warm-up (MIOpen kernel search)
+    inversion.invert(gen, target, cam, focal, w_avg, icfg, lpips_net=net)   # warm-up (MIOpen search)
     torch.cuda.synchronize()
     icfg.steps = args.inv_steps
     ops.KERNEL_TIMERS = {}
@@ -140,7 +186,7 @@ def inversion_leg(args, dev, cfg, batch, world):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = inversion.invert(gen, target, cam, focal, w_avg, icfg)
+    res = inversion.invert(gen, target, cam, focal, w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -155,9 +201,11 @@ def inversion_leg(args, dev, cfg, batch, world):
     return {'s_per_image': round(elapsed / (B * world), 5), 'steps': icfg.steps,
             'images': B * world, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
             'render_ms_per_step': round(render_ms, 3),
-            'producer_adam_ms_per_step': round(step_ms - render_ms, 3),
-            'loss': 'l1', 'loss_first_last': [round(res.losses[0], 5), round(res.losses[-1], 5)],
-            'producer': 'StyleGAN2 synthesis 256^2x96 + AttentionMapper, fp32, PyTorch-ROCm (MIOpen)',
+            'rest_ms_per_step': round(step_ms - render_ms, 3),
+            'loss': loss + (' (LPIPS-VGG, random weights, 16 copies)' if net is not None else ''),
+            'loss_first_last': [round(res.losses[0], 5), round(res.losses[-1], 5)],
+            'producer': 'StyleGAN2 synthesis 256^2x96 + AttentionMapper, fp32: convs MIOpen, '
+                        'epilogues/FIR/skip/modulation-backward nfi HIP',
             'renderer': 'nfi HIP fwd+bwd'}
 
 
@@ -172,6 +220,8 @@ def main():
     ap.add_argument('--cpu-res', type=int, default=128)
     ap.add_argument('--no-inversion', action='store_true')
     ap.add_argument('--inv-steps', type=int, default=30)
+    ap.add_argument('--inv-loss', default='vgg,l1',
+                    help="comma list; the first is reported as inversion_s_per_image")
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -267,8 +317,11 @@ def main():
         'roofline': roof,
     }
     if bwd and not args.no_inversion:
-        out['inversion'] = inversion_leg(args, dev, cfg, batch, world)
-        out['inversion_s_per_image'] = out['inversion']['s_per_image']
+        for k, loss in enumerate(args.inv_loss.split(',')):
+            leg = inversion_leg(args, dev, cfg, batch, world, loss)
+            out['inversion' if k == 0 else f'inversion_{loss}'] = leg
+            if k == 0:
+                out['inversion_s_per_image'] = leg['s_per_image']
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(args)
         out['cpu_baseline'] = cb

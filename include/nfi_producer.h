@@ -8,6 +8,7 @@
  *   up-sampling FIR epilogue stylegan.py:99-103 (filter2d gain 4, pad 1) + the epilogue above
  *   skip-image upsample+add  stylegan.py:69-73, 428-433     upsample2d(img) + (toRGB conv + bias)
  *   channel-scale backward   stylegan.py:130                d(x*styles): g*styles and sum(g*x)
+ *   LPIPS distance head      metrics.py:130-146 (lpips 0.1) normalise, difference, lin, mean
  *
  * Tensors are NCHW float32, contiguous; "planes" P = B*C images of one channel; per-plane
  * scales `d` have P entries ([B,C] row-major), per-channel biases C entries.  `stream` is a
@@ -60,6 +61,20 @@ int32_t nfi_syn_up_backward(const float* g, float* gimg, int32_t P, int32_t n, v
  * ds[p] = sum_hw g * x (overwritten).  HW % 4 == 0. */
 int32_t nfi_syn_scale_backward(const float* g, const float* x, const float* s, float* gx,
                                float* ds, int32_t P, int32_t HW, void* stream);
+
+/* LPIPS distance head for one feature layer (lpips 0.1 `LPIPS.forward` as wrapped by
+ * lib/metrics.py:130-146): per pixel n(f) = f / (||f||_C + 1e-10), d = sum_c w[c] (n(f0)-n(f1))_c^2;
+ * out[i] = mean_hw d (out [N] overwritten).  f0, f1 [N,C,HW]; inv0/inv1 [N*HW] receive
+ * 1/(||f||+1e-10) for the backward. */
+int32_t nfi_lpips_head_forward(const float* f0, const float* f1, const float* w, float* out,
+                               float* inv0, float* inv1, int32_t N, int32_t C, int32_t HW,
+                               void* stream);
+
+/* d out / d f0 scaled by g[N]: gf0 [N,C,HW] (overwritten).  At a pixel whose f0 vector is all
+ * zero the gradient is 0 (torch's autograd of normalize_tensor gives NaN there). */
+int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1, const float* w,
+                                const float* inv0, const float* inv1, float* gf0, int32_t N,
+                                int32_t C, int32_t HW, void* stream);
 
 #ifdef __cplusplus
 }

@@ -243,6 +243,90 @@ __global__ void __launch_bounds__(256) up_bwd_kernel(const float* __restrict__ g
   gimg[i] = acc * (1.f / 16.f);
 }
 
+// LPIPS head: one thread per pixel, channels strided by HW (coalesced across the wave)
+constexpr float LP_EPS = 1e-10f;
+
+__global__ void __launch_bounds__(256) lpips_fwd_kernel(const float* __restrict__ f0,
+                                                        const float* __restrict__ f1,
+                                                        const float* __restrict__ w,
+                                                        float* __restrict__ out,
+                                                        float* __restrict__ inv0,
+                                                        float* __restrict__ inv1, int N, int C,
+                                                        int HW) {
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = pix < (int64_t)N * HW;
+  const int n = live ? (int)(pix / HW) : 0;
+  const int hw = live ? (int)(pix - (int64_t)n * HW) : 0;
+  float d = 0.f;
+  if (live) {
+    const float* a = f0 + (int64_t)n * C * HW + hw;
+    const float* b = f1 + (int64_t)n * C * HW + hw;
+    float ra = 0.f, rb = 0.f;
+#pragma unroll 4
+    for (int c = 0; c < C; ++c) {
+      const float x = a[(int64_t)c * HW], y = b[(int64_t)c * HW];
+      ra += x * x;
+      rb += y * y;
+    }
+    const float ia = 1.f / (sqrtf(ra) + LP_EPS), ib = 1.f / (sqrtf(rb) + LP_EPS);
+#pragma unroll 4
+    for (int c = 0; c < C; ++c) {
+      const float t = a[(int64_t)c * HW] * ia - b[(int64_t)c * HW] * ib;
+      d += w[c] * t * t;
+    }
+    inv0[pix] = ia;
+    inv1[pix] = ib;
+    d *= 1.f / (float)HW;
+  }
+  if (HW % 64 == 0) {               // the whole wave is one image
+    d = wave_sum(d);
+    if ((threadIdx.x & 63) == 0 && live) atomicAdd(out + n, d);
+  } else if (live) {
+    atomicAdd(out + n, d);
+  }
+}
+
+__global__ void __launch_bounds__(256) lpips_bwd_kernel(const float* __restrict__ g,
+                                                        const float* __restrict__ f0,
+                                                        const float* __restrict__ f1,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ inv0,
+                                                        const float* __restrict__ inv1,
+                                                        float* __restrict__ gf0, int N, int C,
+                                                        int HW) {
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (int64_t)N * HW) return;
+  const int n = (int)(pix / HW);
+  const int hw = (int)(pix - (int64_t)n * HW);
+  const int64_t off = (int64_t)n * C * HW + hw;
+  const float* a = f0 + off;
+  const float* b = f1 + off;
+  const float ia = inv0[pix], ib = inv1[pix];
+  const float s = 2.f * g[n] / (float)HW;
+  // u_c = s w_c (a_c ia - b_c ib); grad_k = ia u_k - ia^2 (a_k / r) sum_c u_c a_c, r = ||a||
+  float ua = 0.f, r2 = 0.f;
+#pragma unroll 4
+  for (int c = 0; c < C; ++c) {
+    const float x = a[(int64_t)c * HW];
+    const float u = s * w[c] * (x * ia - b[(int64_t)c * HW] * ib);
+    ua += u * x;
+    r2 += x * x;
+  }
+  const float r = sqrtf(r2);
+  float* o = gf0 + off;
+  if (r == 0.f) {   // all-zero feature vector: torch's sqrt backward gives 0*inf = NaN here; we give 0
+    for (int c = 0; c < C; ++c) o[(int64_t)c * HW] = 0.f;
+    return;
+  }
+  const float k2 = ia * ia * ua / r;
+#pragma unroll 4
+  for (int c = 0; c < C; ++c) {
+    const float x = a[(int64_t)c * HW];
+    const float u = s * w[c] * (x * ia - b[(int64_t)c * HW] * ib);
+    o[(int64_t)c * HW] = ia * u - k2 * x;
+  }
+}
+
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace syn
@@ -332,6 +416,32 @@ int32_t nfi_syn_scale_backward(const float* g, const float* x, const float* s, f
   scale_bwd_kernel<<<dim3((HW4 + RED_CHUNK4 - 1) / RED_CHUNK4, P), 256, 0, st>>>(
       (const float4*)g, (const float4*)x, s, (float4*)gx, ds, HW4);
   NFI_CHECK_LAUNCH("scale_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_lpips_head_forward(const float* f0, const float* f1, const float* w, float* out,
+                               float* inv0, float* inv1, int32_t N, int32_t C, int32_t HW,
+                               void* stream) {
+  NFI_REQUIRE(f0 && f1 && w && out && inv0 && inv1, "lpips_head_forward: null pointer");
+  NFI_REQUIRE(N > 0 && C > 0 && HW > 0, "lpips_head_forward: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(out, 0, sizeof(float) * N, st) != hipSuccess) {
+    nfi::set_error("lpips_head_forward: memset failed");
+    return NFI_ELAUNCH;
+  }
+  lpips_fwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(f0, f1, w, out, inv0, inv1, N, C, HW);
+  NFI_CHECK_LAUNCH("lpips_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1, const float* w,
+                                const float* inv0, const float* inv1, float* gf0, int32_t N,
+                                int32_t C, int32_t HW, void* stream) {
+  NFI_REQUIRE(g && f0 && f1 && w && inv0 && inv1 && gf0, "lpips_head_backward: null pointer");
+  NFI_REQUIRE(N > 0 && C > 0 && HW > 0, "lpips_head_backward: bad shape");
+  lpips_bwd_kernel<<<blocks((int64_t)N * HW), 256, 0, (hipStream_t)stream>>>(g, f0, f1, w, inv0,
+                                                                              inv1, gf0, N, C, HW);
+  NFI_CHECK_LAUNCH("lpips_bwd_kernel");
   return NFI_OK;
 }
 

@@ -95,6 +95,12 @@ SIGNATURES = {
                                              c_void_p]),
     'nfi_syn_scale_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                                 ctypes.c_int32, ctypes.c_int32, c_void_p]),
+    'nfi_lpips_head_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                ctypes.c_int32, c_void_p]),
+    'nfi_lpips_head_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.c_int32, c_void_p]),
 }
 
 _lib = None

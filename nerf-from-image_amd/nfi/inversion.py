@@ -128,7 +128,8 @@ class InversionConfig:
     lr: float = 2e-3                     # run.py:2007
     betas: tuple = (0.9, 0.95)
     gain_z: float = 5.0                  # --inv_gain_z (lr_gain_z, run.py:1749)
-    loss: str = 'l1'                     # --inv_loss: 'l1' | 'mse' ('vgg'/'mixed' need LPIPS weights)
+    loss: str = 'l1'                     # --inv_loss: 'vgg' (reference default) | 'vgg_nocrop' | 'mixed' | 'l1' | 'mse'
+    white_background: bool = False       # dataset_config['white_background'] (augmentation fill)
     samples: int = 64                    # depth_samples_per_ray (fine sampling doubles it)
     resolution: int = 128
     optimize_pose: bool = True           # not --inv_no_optimize_pose
@@ -147,24 +148,84 @@ class InversionResult:
     seconds: float = 0.0
 
 
-def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-    """optimize_iter (run.py:2205-2252): per-batch-summed image loss."""
+def augment_images(img: torch.Tensor, p: float, white_background: bool = False,
+                   disable_scale: bool = False, generator: Optional[torch.Generator] = None):
+    """augment_impl (run.py:720-767) for images only (pose None, as the loss calls it): random
+    rotation, scale and translation per image with probability p, applied by affine_grid +
+    bilinear grid_sample (zero padding, or white for white-background datasets).  Random draws in
+    the reference's order, on img.device (or from `generator`)."""
+    bs, dev = img.shape[0], img.device
+
+    def rand(*shape):
+        return torch.rand(shape, device=dev, generator=generator)
+
+    def randn(*shape):
+        return torch.randn(shape, device=dev, generator=generator)
+
+    rot = (rand(bs) - 0.5) * 2 * math.pi
+    rot = rot * (rand(bs) < p).float()
+    if disable_scale:
+        scale = torch.ones((bs,), device=dev)
+    else:
+        scale = torch.exp2(randn(bs) * 0.2)
+        scale = torch.lerp(torch.ones_like(scale), scale, (rand(bs) < p).float())
+    translation = randn(bs, 2) * 0.1
+    translation = torch.lerp(torch.zeros_like(translation), translation, (rand(bs, 1) < p).float())
+    c, s = torch.cos(rot), torch.sin(rot)
+    rotm = torch.stack([torch.stack([c, -s], -1), torch.stack([s, c], -1)], 1)   # [bs,2,2]
+    t = torch.stack([translation[:, 0], -translation[:, 1]], -1) * scale[:, None]
+    theta = torch.cat([rotm * scale[:, None, None], (rotm * t[:, None, :]).sum(-1, keepdim=True)], -1)
+    grid = F.affine_grid(theta, list(img.shape), align_corners=False)
+    if white_background:
+        img = img - 1
+    out = F.grid_sample(img, grid, mode='bilinear', padding_mode='zeros', align_corners=False)
+    return out + 1 if white_background else out
+
+
+VGG_LOSSES = ('vgg', 'vgg_nocrop', 'mixed')
+
+
+def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor, lpips_net=None,
+               white_background: bool = False, augment_generator=None) -> torch.Tensor:
+    """optimize_iter (run.py:2205-2252): per-batch-summed image loss.  'vgg' = LPIPS over the
+    image plus 15 augmented copies of (prediction, target) pairs; 'vgg_nocrop' without the
+    copies; 'mixed' = ('vgg' + 'l1') / 2; 'l1'; 'mse'."""
     b = rgb.shape[0]
-    if kind == 'l1':
-        return F.l1_loss(rgb, target) * b
+    if kind not in VGG_LOSSES + ('l1', 'mse'):
+        raise NotImplementedError(f'inversion loss {kind!r}')
     if kind == 'mse':
         return F.mse_loss(rgb, target) * b
-    raise NotImplementedError(f'inversion loss {kind!r}: LPIPS/VGG weights are not available offline')
+    loss = 0.
+    if kind in VGG_LOSSES:
+        if lpips_net is None:
+            raise ValueError(f'inversion loss {kind!r} needs an LPIPS network (nfi.lpips.LPIPS with '
+                             f'weights loaded via load_weights; none ship offline)')
+        pred, tgt = rgb.permute(0, 3, 1, 2), target.permute(0, 3, 1, 2)
+        if kind != 'vgg_nocrop':
+            cat = torch.cat((pred, tgt), dim=1).unsqueeze(1).expand(-1, 15, -1, -1, -1)
+            cat = augment_images(cat.contiguous().flatten(0, 1), 1.0, white_background,
+                                 generator=augment_generator)
+            pred = torch.cat((pred, cat[:, :3]), dim=0)
+            # the target copies carry no gradient to any parameter (the reference backpropagates
+            # into them and drops the result at the target leaf)
+            tgt = torch.cat((tgt, cat[:, 3:].detach()), dim=0)
+        loss = loss + lpips_net(pred, tgt).mean() * b
+    if kind in ('l1', 'mixed'):
+        loss = loss + F.l1_loss(rgb, target) * b
+    if kind == 'mixed':
+        loss = loss / 2
+    return loss
 
 
 def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: Optional[torch.Tensor],
            w_init: torch.Tensor, cfg: InversionConfig = InversionConfig(), center=None, bbox=None,
            uniforms: Optional[Callable[[int], tuple]] = None, render_fn: Optional[Callable] = None,
-           on_step: Optional[Callable] = None) -> InversionResult:
+           on_step: Optional[Callable] = None, lpips_net=None) -> InversionResult:
     """Fit latent + pose of `generator` (frozen) to `target_img` [b,H,W,3 or 4] in [-1,1].
 
     `w_init` [1 or b, 15, 512] is the starting latent (z_avg or a regressor output);
-    `cam2world`/`focal` the initial pose.  `uniforms(it) -> (u_coarse, u_fine)` fixes the
+    `cam2world`/`focal` the initial pose.  `lpips_net` (nfi.lpips.LPIPS) is needed by the
+    'vgg' losses.  `uniforms(it) -> (u_coarse, u_fine)` fixes the
     renderer's random draws per iteration (parity tests); `render_fn` replaces nfi.render with
     a callable of the same signature (tests only)."""
     b = target_img.shape[0]
@@ -195,7 +256,7 @@ def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: 
             ws = ws.expand(-1, 15, -1)
         rgb = rfn(generator, res, res, cam, foc, center, bbox, ws, cfg.samples,
                   force_no_cam_grad=not cfg.optimize_pose, **kw)[0]
-        loss = image_loss(cfg.loss, rgb, target)
+        loss = image_loss(cfg.loss, rgb, target, lpips_net, cfg.white_background)
         loss.backward()
         opt.step()
         opt.zero_grad()

@@ -1,0 +1,110 @@
+"""LPIPS-VGG perceptual loss of the inversion step: lib/metrics.py:104-146
+(`LPIPSLoss`, the reference's wrapper) around the third-party `lpips` package, version 0.1
+(`lpips.LPIPS(net='vgg')`, its published algorithm restated here — the package and its weights
+are not in this image, so PARITY IS UNPINNED for this module: no fixture exists to check it
+against, and random weights stand in unless `load_weights` is given the two state_dicts).
+
+  features  ScalingLayer ((x - shift) / scale) then torchvision VGG16 `features` cut after
+            relu1_2, relu2_2, relu3_3, relu4_3, relu5_3 (lpips/pretrained_networks.py `vgg16`)
+  distance  sum_l mean_hw( lin_l( (n(f0_l) - n(f1_l))^2 ) ), n(x) = x / (||x||_channels + 1e-10),
+            lin_l a bias-free 1x1 conv to one channel (lpips/lpips.py NetLinLayer; dropout is
+            inactive in eval)
+
+Backends: 'hip' (the VGG convolutions are MIOpen calls; the distance head — normalisation,
+difference, lin, spatial mean — is one fused HIP kernel per layer, forward and backward,
+csrc/nfi_producer.hip) and 'torch' (the op sequence above in PyTorch).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+VGG_CFG = [64, 64, 'M', 128, 128, 'M', 256, 256, 256, 'M', 512, 512, 512, 'M', 512, 512, 512]
+TAPS = (3, 8, 15, 22, 29)          # torchvision vgg16.features indices of relu1_2 .. relu5_3
+CHANNELS = (64, 128, 256, 512, 512)
+SHIFT = (-.030, -.088, -.188)      # lpips ScalingLayer
+SCALE = (.458, .448, .450)
+EPS = 1e-10
+
+
+class VGG16Features(nn.Module):
+    """torchvision.models.vgg16().features[:30] with the same module indices (state_dict keys
+    'features.<i>.weight'/'bias' load directly)."""
+
+    def __init__(self):
+        super().__init__()
+        layers, c = [], 3
+        for v in VGG_CFG:
+            if v == 'M':
+                layers.append(nn.MaxPool2d(2, 2))
+            else:
+                layers += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=False)]
+                c = v
+        self.features = nn.Sequential(*layers)
+
+    def forward(self, x):
+        out = []
+        for i, layer in enumerate(self.features):
+            x = layer(x)
+            if i in TAPS:
+                out.append(x)
+        return out
+
+
+class LPIPS(nn.Module):
+    """`LPIPSLoss` (metrics.py:104-146): forward(in0, in1) -> [N, 1] distances (reduction
+    'none'), in0/in1 in [-1, 1] (normalize=False, as run.py:2231 calls it)."""
+
+    def __init__(self, backend: str = 'hip'):
+        super().__init__()
+        self.net = VGG16Features()
+        self.lins = nn.ModuleList([nn.Conv2d(c, 1, 1, bias=False) for c in CHANNELS])
+        self.register_buffer('shift', torch.tensor(SHIFT).view(1, 3, 1, 1))
+        self.register_buffer('scale', torch.tensor(SCALE).view(1, 3, 1, 1))
+        with torch.no_grad():                  # lpips lin weights are non-negative
+            for lin in self.lins:
+                lin.weight.abs_().mul_(0.1)
+        self.backend = backend
+        self.eval()
+        self.requires_grad_(False)
+
+    def load_weights(self, vgg_state_dict: dict, lin_state_dict: dict):
+        """vgg_state_dict: torchvision vgg16 keys ('features.0.weight', ...); lin_state_dict:
+        lpips weights/v0.1/vgg.pth keys ('lin0.model.1.weight', ...).  Load both with
+        torch.load(..., weights_only=True)."""
+        feats = {k: v for k, v in vgg_state_dict.items() if k.startswith('features.')}
+        self.net.load_state_dict(feats, strict=False)
+        for i, lin in enumerate(self.lins):
+            lin.weight.data.copy_(lin_state_dict[f'lin{i}.model.1.weight'])
+        return self
+
+    def features(self, im):
+        return self.net((im - self.shift) / self.scale)
+
+    def forward(self, in0, in1):
+        f0 = self.features(in0)
+        with torch.no_grad() if not in1.requires_grad else _null():
+            f1 = self.features(in1)
+        if self.backend == 'hip':
+            from . import producer_ops
+            return sum(producer_ops.lpips_head(a, b, lin.weight.view(-1))
+                       for a, b, lin in zip(f0, f1, self.lins))[:, None]
+        return sum(lin((normalize(a) - normalize(b)).square()).mean(dim=[2, 3])
+                   for a, b, lin in zip(f0, f1, self.lins))
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def normalize(x):
+    """lpips.normalize_tensor (eps 1e-10)."""
+    return x / (x.square().sum(dim=1, keepdim=True).sqrt() + EPS)

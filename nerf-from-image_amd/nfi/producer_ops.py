@@ -144,6 +144,40 @@ class _UpAdd(torch.autograd.Function):
         return gimg, g, None
 
 
+class _LpipsHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f0, f1, w):
+        _require_device(f0, f1, w)
+        f0 = f0.contiguous()
+        f1 = f1.detach().contiguous()
+        w = w.detach().contiguous()
+        N, C, H, W = f0.shape
+        out = torch.empty(N, device=f0.device, dtype=f0.dtype)
+        inv0 = torch.empty(N * H * W, device=f0.device, dtype=f0.dtype)
+        inv1 = torch.empty_like(inv0)
+        _call('nfi_lpips_head_forward', _p(f0), _p(f1), _p(w), _p(out), _p(inv0), _p(inv1), N, C,
+              H * W, _stream(f0.device))
+        ctx.save_for_backward(f0, f1, w, inv0, inv1)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        f0, f1, w, inv0, inv1 = ctx.saved_tensors
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            raise NotImplementedError('lpips_head differentiates the first input only')
+        g = g.contiguous()
+        N, C, H, W = f0.shape
+        gf0 = torch.empty_like(f0)
+        _call('nfi_lpips_head_backward', _p(g), _p(f0), _p(f1), _p(w), _p(inv0), _p(inv1), _p(gf0),
+              N, C, H * W, _stream(f0.device))
+        return gf0, None, None
+
+
+def lpips_head(f0, f1, w):
+    """[N] = mean_hw sum_c w_c (n(f0) - n(f1))_c^2 (lpips distance of one layer)."""
+    return _LpipsHead.apply(f0, f1, w)
+
+
 def scale(x, s):
     return _Scale.apply(x, s)
 

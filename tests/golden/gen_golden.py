@@ -14,6 +14,7 @@ and expected outputs/gradients of
     synthesis network, AttentionMapper) at full size with seeded weights (golden_io.load_seeded,
     so no weights are stored), sampled planes + checksums, palette, and the latent gradient;
   * pose_utils pose_to_matrix / matrix_to_pose on a few cameras;
+  * augment_impl (run.py:720-797) on images, the inversion loss's augmentation;
   * an inversion trajectory: the loop of run.py:1960-2310 restated around
     the reference's Generator, render() and pose_utils, L1 loss, 3 Adam steps.
 Random draws of the reference (torch.rand_like / torch.rand) are recovered by re-seeding and
@@ -239,6 +240,35 @@ def stage_cases():
     print('stages written')
 
 
+def extract_function(name, ns):
+    """AST-extract a top-level function of run.py and exec it with the given globals."""
+    src = open(os.path.join(REF, 'run.py')).read()
+    fn = [n for n in ast.parse(src).body if isinstance(n, ast.FunctionDef) and n.name == name][0]
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), os.path.join(REF, 'run.py'), 'exec'), ns)
+    return ns[name]
+
+
+def augment_cases():
+    """augment_impl (run.py:720-797) on images only, p=1 (the inversion loss's call)."""
+    out = {}
+    for wbg in (False, True):
+        ns = {'torch': torch, 'F': F, 'np': np, 'pose_utils': pose_utils,
+              'dataset_config': {'white_background': wbg},
+              'args': types.SimpleNamespace(supervise_alpha=False)}
+        augment_impl = extract_function('augment_impl', ns)
+        g = torch.Generator().manual_seed(51 + wbg)
+        img = torch.tanh(torch.randn(7, 6, 16, 12, generator=g))
+        torch.manual_seed(61 + wbg)
+        res, _, _, tform = augment_impl(img, None, None, 1.0)
+        key = 'w' if wbg else 'b'
+        out[f'{key}_img'] = img
+        out[f'{key}_out'] = res
+        out[f'{key}_rot'], out[f'{key}_scale'], out[f'{key}_translation'] = tform
+    np.savez_compressed(os.path.join(OUT, 'augment.npz'), **{k: v.numpy() for k, v in out.items()},
+                        meta_seed_b=np.array(61), meta_seed_w=np.array(62))
+    print('augment written')
+
+
 def seeded_generator(seed, scene_range=1.4):
     gen = generator.Generator(512, scene_range, attention_values=10, use_sdf=True,
                               disable_stylegan_noise=True)
@@ -364,6 +394,7 @@ if __name__ == '__main__':
     producer_case()
     pose_cases()
     inversion_case()
+    augment_cases()
     stage_cases()
     # p3d_car-like: perspective, flipped, black bg, pose grads, random sampling
     render_case('p3d', 0, b=2, H=16, W=16, S=16, R=16, scene_range=1.4, white_bg=False,

@@ -1,0 +1,56 @@
+"""The fused LPIPS distance head (HIP) against the torch formulation of the same op, and the
+'vgg' inversion loss (LPIPS over 16 augmented copies, run.py:2211-2235) running through the HIP
+path.  Parity against the reference is UNPINNED (no lpips package / weights offline; see
+tests/test_lpips.py)."""
+
+import pytest
+import torch
+
+from nfi import inversion, lpips, producer_ops
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+@pytest.mark.parametrize('N,C,H', [(3, 64, 32), (2, 512, 8), (5, 7, 3)])
+def test_lpips_head_matches_torch(N, C, H):
+    g = torch.Generator(device=DEV).manual_seed(C)
+    f0 = torch.randn((N, C, H, H), device=DEV, generator=g).relu().requires_grad_()
+    f1 = torch.randn((N, C, H, H), device=DEV, generator=g).relu()
+    f0.data[0, :, 0, 0] = 0          # an all-zero feature vector (the a == 0 branch)
+    w = torch.rand((C,), device=DEV, generator=g)
+    gout = torch.randn((N,), device=DEV, generator=g)
+    out = producer_ops.lpips_head(f0, f1, w)
+    out.backward(gout)
+    r0 = f0.detach().clone().requires_grad_()
+    ref = (lpips.normalize(r0) - lpips.normalize(f1)).square().mul(w[None, :, None, None]).sum(1).mean((1, 2))
+    ref.backward(gout)
+    torch.testing.assert_close(out.detach(), ref.detach(), rtol=1e-5, atol=1e-7)
+    gref = torch.nan_to_num(r0.grad, nan=0.0)     # torch: 0/0 at the all-zero vector
+    torch.testing.assert_close(f0.grad, gref, rtol=1e-4, atol=1e-6 * float(gref.abs().max()))
+
+
+def test_lpips_backends_agree():
+    torch.manual_seed(0)
+    net = lpips.LPIPS(backend='torch').to(DEV)
+    a = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV)).requires_grad_()
+    b = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV))
+    ref = net(a, b)
+    ref.sum().backward()
+    ga = a.grad.clone()
+    a.grad = None
+    net.backend = 'hip'
+    out = net(a, b)
+    out.sum().backward()
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-6)
+    assert float((a.grad - ga).norm() / ga.norm()) < 1e-4
+
+
+def test_vgg_inversion_loss_runs():
+    from test_producer import inversion_setup
+    gen, d, meta, cfg = inversion_setup(DEV)
+    cfg.steps, cfg.loss = 2, 'vgg'
+    net = lpips.LPIPS().to(DEV)
+    res = inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg, lpips_net=net)
+    assert len(res.losses) == 2 and all(torch.isfinite(torch.tensor(res.losses)))
+    assert torch.isfinite(res.ws).all()

@@ -1,0 +1,52 @@
+"""LPIPS-VGG (nfi/lpips.py).  PARITY UNPINNED: the reference calls the
+third-party `lpips` 0.1 package with pretrained VGG16 + lin weights (lib/metrics.py:104-146);
+neither the package nor the weights exist offline, so no reference output can be produced.
+These CPU tests check the restated structure: state_dict layout of the two weight files it
+loads, the metric's identities (d(x, x) = 0, symmetry, non-negativity), and the distance head
+against a direct per-pixel evaluation.  The HIP head is checked against the torch backend in
+tests/test_gpu_lpips.py."""
+
+import torch
+
+from nfi import lpips
+
+
+def test_weight_layout_matches_torchvision_and_lpips_files():
+    net = lpips.LPIPS(backend='torch')
+    keys = set(net.net.state_dict())
+    # torchvision vgg16().features conv indices
+    convs = [0, 2, 5, 7, 10, 12, 14, 17, 19, 21, 24, 26, 28]
+    assert keys == {f'features.{i}.{p}' for i in convs for p in ('weight', 'bias')}
+    vgg_sd = {k: torch.randn_like(v) for k, v in net.net.state_dict().items()}
+    vgg_sd['classifier.0.weight'] = torch.zeros(1)       # ignored
+    lin_sd = {f'lin{i}.model.1.weight': torch.rand(1, c, 1, 1) for i, c in enumerate(lpips.CHANNELS)}
+    net.load_weights(vgg_sd, lin_sd)
+    assert torch.equal(net.net.features[28].weight, vgg_sd['features.28.weight'])
+    assert torch.equal(net.lins[3].weight, lin_sd['lin3.model.1.weight'])
+
+
+def test_metric_identities():
+    torch.manual_seed(0)
+    net = lpips.LPIPS(backend='torch')
+    a = torch.tanh(torch.randn(3, 3, 64, 64))
+    b = torch.tanh(torch.randn(3, 3, 64, 64))
+    dab, dba, daa = net(a, b), net(b, a), net(a, a)
+    assert dab.shape == (3, 1)
+    assert torch.all(dab > 0)
+    torch.testing.assert_close(dab, dba, rtol=1e-5, atol=1e-7)
+    assert float(daa.abs().max()) == 0.0
+
+
+def test_distance_head_per_pixel():
+    torch.manual_seed(1)
+    f0, f1 = torch.randn(2, 5, 3, 4).relu(), torch.randn(2, 5, 3, 4).relu()
+    w = torch.rand(5)
+    got = (lpips.normalize(f0) - lpips.normalize(f1)).square().mul(w[None, :, None, None]).sum(1).mean((1, 2))
+    want = torch.zeros(2)
+    for n in range(2):
+        for y in range(3):
+            for x in range(4):
+                a, b = f0[n, :, y, x], f1[n, :, y, x]
+                na, nb = a / (a.norm() + 1e-10), b / (b.norm() + 1e-10)
+                want[n] += (w * (na - nb) ** 2).sum() / 12
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-7)

@@ -147,9 +147,19 @@ def test_inversion_loop_with_oracle_renderer():
     check_trajectory(res, d, loss_rtol=1e-5, w_rel=1e-3)
 
 
-def test_inversion_rejects_lpips_without_weights():
-    with pytest.raises(NotImplementedError):
+def test_inversion_vgg_loss_needs_lpips_network():
+    with pytest.raises(ValueError, match='LPIPS'):
         inversion.image_loss('vgg', torch.zeros(1, 2, 2, 3), torch.zeros(1, 2, 2, 3))
+    with pytest.raises(NotImplementedError):
+        inversion.image_loss('ssim', torch.zeros(1, 2, 2, 3), torch.zeros(1, 2, 2, 3))
+
+
+@pytest.mark.parametrize('key', ['b', 'w'])
+def test_augment_matches_reference(key):
+    d, meta = load('augment')
+    g = torch.Generator().manual_seed(int(meta[f'seed_{key}']))
+    out = inversion.augment_images(d[f'{key}_img'], 1.0, white_background=key == 'w', generator=g)
+    torch.testing.assert_close(out, d[f'{key}_out'], rtol=1e-6, atol=1e-6)
 
 
 def test_inversion_default_renderer_is_hip_only():
