@@ -220,14 +220,17 @@ def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor, lpips_net=Non
 def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: Optional[torch.Tensor],
            w_init: torch.Tensor, cfg: InversionConfig = InversionConfig(), center=None, bbox=None,
            uniforms: Optional[Callable[[int], tuple]] = None, render_fn: Optional[Callable] = None,
-           on_step: Optional[Callable] = None, lpips_net=None) -> InversionResult:
+           on_step: Optional[Callable] = None, lpips_net=None, checkpoints=(),
+           on_checkpoint: Optional[Callable] = None) -> InversionResult:
     """Fit latent + pose of `generator` (frozen) to `target_img` [b,H,W,3 or 4] in [-1,1].
 
     `w_init` [1 or b, 15, 512] is the starting latent (z_avg or a regressor output);
     `cam2world`/`focal` the initial pose.  `lpips_net` (nfi.lpips.LPIPS) is needed by the
     'vgg' losses.  `uniforms(it) -> (u_coarse, u_fine)` fixes the
     renderer's random draws per iteration (parity tests); `render_fn` replaces nfi.render with
-    a callable of the same signature (tests only)."""
+    a callable of the same signature (tests only).  `on_checkpoint(it, (z_, z0_, t2_, s_, q_))`
+    runs before the first step if 0 is in `checkpoints` and after step it if it is
+    (evaluate_inversion, run.py:2020-2110 and 2302-2305; see nfi.report.evaluate)."""
     b = target_img.shape[0]
     res = cfg.resolution
     rfn = render_fn or _nfi_render
@@ -245,6 +248,8 @@ def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: 
     opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas)
     target = target_img[..., :3]
     losses = []
+    if on_checkpoint is not None and 0 in checkpoints:
+        on_checkpoint(0, (z_, z0_, t2_, s_, q_))
     t0 = time.perf_counter()
     for it in range(cfg.steps):
         cam, foc = pose_to_matrix(z0_, t2_, s_, F.normalize(q_, dim=-1), cfg.camera_flipped)
@@ -268,6 +273,8 @@ def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: 
         losses.append(loss.detach())
         if on_step is not None:
             on_step(it, loss)
+        if on_checkpoint is not None and it + 1 in checkpoints:
+            on_checkpoint(it + 1, (z_, z0_, t2_, s_, q_))
     if torch.cuda.is_available() and target_img.is_cuda:
         torch.cuda.synchronize(target_img.device)
     secs = time.perf_counter() - t0

@@ -15,6 +15,7 @@ and expected outputs/gradients of
     so no weights are stored), sampled planes + checksums, palette, and the latent gradient;
   * pose_utils pose_to_matrix / matrix_to_pose on a few cameras;
   * augment_impl (run.py:720-797) on images, the inversion loss's augmentation;
+  * metrics.psnr / iou and pose_utils.rotation_matrix_distance (inversion report metrics);
   * an inversion trajectory: the loop of run.py:1960-2310 restated around
     the reference's Generator, render() and pose_utils, L1 loss, 3 Adam steps.
 Random draws of the reference (torch.rand_like / torch.rand) are recovered by re-seeding and
@@ -248,6 +249,32 @@ def extract_function(name, ns):
     return ns[name]
 
 
+def metrics_cases():
+    """metrics.psnr / iou (metrics.py:22-103, AST-extracted: the module imports lpips and
+    scikit-image, absent here) and pose_utils.rotation_matrix_distance."""
+    src = open(os.path.join(REF, 'lib', 'metrics.py')).read()
+    ns = {'torch': torch}
+    fns = [n for n in ast.parse(src).body if isinstance(n, ast.FunctionDef)
+           and n.name in ('range_check', 'psnr', 'iou')]
+    exec(compile(ast.Module(body=fns, type_ignores=[]), os.path.join(REF, 'lib', 'metrics.py'), 'exec'), ns)
+    g = torch.Generator().manual_seed(71)
+    pred = torch.rand(4, 3, 16, 16, generator=g)
+    tgt = (pred + 0.1 * torch.randn(4, 3, 16, 16, generator=g)).clamp(0, 1)
+    tgt[3] = pred[3]                                        # the 60 dB clamp
+    a0 = torch.rand(4, 16, 16, generator=g)
+    a1 = torch.rand(4, 16, 16, generator=g)
+    q = F.normalize(torch.randn(6, 4, generator=g), dim=-1)
+    m0, _ = pose_utils.pose_to_matrix(None, torch.zeros(6, 2), torch.ones(1), q, False)
+    q2 = F.normalize(q + 0.2 * torch.randn(6, 4, generator=g), dim=-1)
+    m1, _ = pose_utils.pose_to_matrix(None, torch.zeros(6, 2), torch.ones(1), q2, False)
+    np.savez_compressed(os.path.join(OUT, 'metrics.npz'), pred=pred.numpy(), tgt=tgt.numpy(),
+                        psnr=ns['psnr'](pred, tgt, reduction='none').numpy(),
+                        psnr_mean=ns['psnr'](pred, tgt).numpy(), a0=a0.numpy(), a1=a1.numpy(),
+                        iou=ns['iou'](a0, a1, reduction='none').numpy(), m0=m0.numpy(),
+                        m1=m1.numpy(), rot=pose_utils.rotation_matrix_distance(m0, m1).numpy())
+    print('metrics written')
+
+
 def augment_cases():
     """augment_impl (run.py:720-797) on images only, p=1 (the inversion loss's call)."""
     out = {}
@@ -395,6 +422,7 @@ if __name__ == '__main__':
     pose_cases()
     inversion_case()
     augment_cases()
+    metrics_cases()
     stage_cases()
     # p3d_car-like: perspective, flipped, black bg, pose grads, random sampling
     render_case('p3d', 0, b=2, H=16, W=16, S=16, R=16, scene_range=1.4, white_bg=False,

@@ -72,3 +72,20 @@ def test_producer_on_gpu():
     assert err < 1e-4
     torch.testing.assert_close(palette.detach().cpu(), d['palette'], rtol=1e-4, atol=1e-5)
     assert gerr < 1e-3
+
+
+def test_report_batch_loop_hip(tmp_path):
+    """nfi.report.run with the HIP renderer and producer: report layout and s/img lines."""
+    from nfi import lpips, report
+    dev = torch.device('cuda:0')
+    gen, d, meta, cfg = inversion_setup(dev)
+    nfi.configure(scene_range=float(meta['scene_range']), white_background=False)
+    cfg.steps = 3
+    lines = []
+    rep = report.run(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg, test_bs=2,
+                     report_path=str(tmp_path / 'ck.pth'), lpips_net=lpips.LPIPS().to(dev),
+                     gt_cams=d['cam0'], log=lines.append)
+    assert sorted(rep) == [0, 3] and len(lines) == 1
+    for k in ('ws', 'psnr', 'ssim', 'lpips', 'rot_error'):
+        assert rep[3][k].shape[0] == 2, k
+    assert torch.isfinite(rep[3]['psnr']).all()
