@@ -161,11 +161,13 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
     MIOpen, the rest in the fused HIP kernels, fp32) forward, the HIP render fwd+bwd, the loss
     ('vgg' = the reference default --inv_loss: LPIPS-VGG over the image + 15 augmented copies,
     random weights since none ship offline; or 'l1'), the backward to the latent and pose, Adam.
-    Random-init generator (no checkpoint offline), z_avg from the mapping network, the same
-    cameras as the renderer leg, a synthetic target image.  Timed like the renderer leg (barrier +
+    Random-init generator (no checkpoint offline), z_avg from the mapping network, the first
+    --inv-batch (default 4 = BASELINE configs[3]'s 32 images over 8 GPUs) cameras of the
+    renderer leg, a synthetic target image.  Timed like the renderer leg (barrier +
     synchronize around exactly --inv-steps steps, max over ranks)."""
     from nfi import inversion, lpips, ops, producer
-    sr, wbg, flipped, B, H, S, pose, bwd = cfg
+    sr, wbg, flipped, _, H, S, pose, bwd = cfg
+    B = args.inv_batch              # BASELINE configs[3]: batch 32 over 8 GPUs = 4 per GPU
     torch.manual_seed(4321)
     gen = producer.InversionGenerator(scene_range=sr).to(dev)
     with torch.no_grad():
@@ -177,7 +179,7 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
     icfg = inversion.InversionConfig(steps=2, resolution=H, samples=S, loss=loss,
                                      camera_flipped=flipped, white_background=wbg)
     net = lpips.LPIPS().to(dev) if loss in inversion.VGG_LOSSES else None
-    cam, focal = batch['cam'].detach(), batch['focal'].detach()
+    cam, focal = batch['cam'][:B].detach(), batch['focal'][:B].detach()
     inversion.invert(gen, target, cam, focal, w_avg, icfg, lpips_net=net)   # warm-up (MIOpen search)
     torch.cuda.synchronize()
     icfg.steps = args.inv_steps
@@ -199,7 +201,7 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
         elapsed = float(t.item())
     step_ms = elapsed / icfg.steps * 1e3
     return {'s_per_image': round(elapsed / (B * world), 5), 'steps': icfg.steps,
-            'images': B * world, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
+            'images': B * world, 'images_per_gpu': B, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
             'render_ms_per_step': round(render_ms, 3),
             'rest_ms_per_step': round(step_ms - render_ms, 3),
             'loss': loss + (' (LPIPS-VGG, random weights, 16 copies)' if net is not None else ''),
@@ -220,6 +222,7 @@ def main():
     ap.add_argument('--cpu-res', type=int, default=128)
     ap.add_argument('--no-inversion', action='store_true')
     ap.add_argument('--inv-steps', type=int, default=30)
+    ap.add_argument('--inv-batch', type=int, default=4, help='images per GPU in the inversion leg')
     ap.add_argument('--inv-loss', default='vgg,l1',
                     help="comma list; the first is reported as inversion_s_per_image")
     args = ap.parse_args()

@@ -76,6 +76,24 @@ def _as_float(x) -> float:
     return float(x.detach().reshape(-1)[0].item()) if torch.is_tensor(x) else float(x)
 
 
+def _sdf_params(gen):
+    """(alpha, beta) of a generator as floats, read from the device once per value: a cache keyed
+    on the parameters' storage and in-place version counters, so the inversion loop does not
+    synchronise the host on every render (the generator is frozen there)."""
+    a, b = gen.alpha, gen.beta
+    if not (torch.is_tensor(a) and torch.is_tensor(b)):
+        return _as_float(a), _as_float(b)
+    key = (a.data_ptr(), a._version, b.data_ptr(), b._version)
+    cached = getattr(gen, '_nfi_sdf_params', None)
+    if cached is None or cached[0] != key:
+        cached = (key, (_as_float(a), _as_float(b)))
+        try:
+            object.__setattr__(gen, '_nfi_sdf_params', cached)
+        except AttributeError:
+            pass
+    return cached[1]
+
+
 def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
                          extra_model_inputs: Optional[dict] = None) -> TriplaneField:
     """Runs the parts of Generator.forward (generator.py:423-503) that produce the path's
@@ -113,9 +131,10 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
         if k not in ('attention_values',):
             raise NotImplementedError(f'model output {k!r} (training regulariser) is outside the path')
     dec = gen.decoder.net
+    alpha, beta = _sdf_params(gen)
     return TriplaneField(planes=planes, palette=palette, w1=dec[0].weight, b1=dec[0].bias,
-                         w2=dec[2].weight, b2=dec[2].bias, alpha=_as_float(gen.alpha),
-                         beta=_as_float(gen.beta), model_outputs=outs)
+                         w2=dec[2].weight, b2=dec[2].bias, alpha=alpha, beta=beta,
+                         model_outputs=outs)
 
 
 def _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs) -> TriplaneField:
