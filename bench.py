@@ -282,7 +282,7 @@ def main():
         'bwd_tiles': (TAP_BYTES * (2 if pose else 1) + 48 + 3 * 128, 768 * (2 if pose else 1)),
     }
     kernel_of = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
-                 'bwd_tiles': 'tile_dcoord_kernel', 'bwd_bins': 'scan_blocks_kernel'}
+                 'bwd_tiles': 'tile_kernel', 'bwd_bins': 'scan_blocks_kernel'}
     dom = max(kern, key=kern.get)
     sec = kern[dom] * 1e-3
     achieved = samples_per_step * model[dom][0] / sec / 1e9

@@ -1163,113 +1163,6 @@ __global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_rende
   NFI_STAMP(21)
 }
 
-// Ray-coordinate gradient of one chunk of 64 merged samples of one ray (one wave): the
-// grid_sampler_2d d-grid (generator.py:312-326) re-gathers the taps and dots them with the
-// per-sample feature gradients gfeat written by field_bwd.  dL/dp_j = sum_q (d grid_q) * (R-1)/2
-// * inbound / scene_range; dL/d ro = sum_j dL/dp_j and dL/d rd = sum_j t_j dL/dp_j are linear in
-// the per-lane products, so every lane accumulates its share and the wave is reduced once.
-// A separate kernel from field_bwd: it is memory-latency bound and runs at higher occupancy.
-__device__ __forceinline__ void dcoord_job(const nfi_render_args& a, const BwdArgs& g, long long job,
-                                           float* __restrict__ X) {
-  const int l = lane_id();
-  const long long nrays = (long long)a.B * a.HW;
-  const long long r = job / g.npl;
-  const int e = (int)(job % g.npl);
-  if (r >= nrays) return;
-  const int N = a.fine ? 2 * a.S : a.S;
-  if (e * 64 >= N) return;
-  const float sr = a.field.scene_range;
-  RayCtx R;
-  load_ray(a, r, R);
-  const PlaneView pv{a.field.planes + (long long)R.b * a.field.sb, (int)a.field.sq, (int)a.field.st,
-                     a.field.R};
-  const int npts = min(64, N - e * 64);
-  const int i = e * 64 + l;
-  const bool v = i < N;
-  const float te = v ? a.t_saved[r * N + i] : R.near_;
-  PointP P;
-  point_params(R.o, R.d, te, sr, pv.R, P);
-  // samples outside the box have an exactly-zero feature gradient (their sigma and weight are 0)
-  const unsigned long long live = __ballot(v && P.mask == 0.f);
-  // gradient rows of the chunk -> tile (coalesced: 1 KiB per instruction)
-  {
-    const float4* src = reinterpret_cast<const float4*>(g.gfeat + (r * N + e * 64) * NC);
-#pragma unroll
-    for (int k = 0; k < NC / 4; ++k) {
-      const int q = k * 64 + l;
-      const float4 val = (q < npts * (NC / 4)) ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(X + (q >> 3) * XS + 4 * (q & 7)) = val;
-    }
-  }
-  wave_lds_sync();
-  // re-gather in the quad layout of gather_features (4 points per wave instruction)
-  float aro0 = 0.f, aro1 = 0.f, aro2 = 0.f, ard0 = 0.f, ard1 = 0.f, ard2 = 0.f;
-  {
-    const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
-    const int ngrp = (npts + 3) >> 2;
-    constexpr int GB = 2;
-#pragma unroll 1
-    for (int gb = 0; gb < ngrp; gb += GB) {
-      if (((live >> (4 * gb)) & ((1ull << (4 * GB)) - 1ull)) == 0ull) continue;
-      float4 V0[GB][3], V1[GB][3];
-#pragma unroll
-      for (int u = 0; u < GB; ++u) {
-        const int j = min(4 * (gb + u) + sub, WAVE - 1);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const int pk = __shfl(P.pl[q].tex, j);
-          const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
-          const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-          const float* b = pv.base + q * pv.sq + 4 * q4;
-          V0[u][q] = *reinterpret_cast<const float4*>(b + t0 * pv.st);
-          V1[u][q] = *reinterpret_cast<const float4*>(b + t1 * pv.st);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < GB; ++u) {
-        const int jr = 4 * (gb + u) + sub, j = min(jr, WAVE - 1);
-        const bool lj = jr < WAVE && ((live >> j) & 1ull);
-        const float tj = __shfl(te, j);
-        const float4 gv = *reinterpret_cast<const float4*>(X + j * XS + 4 * q4);
-        float GX[3], GY[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          const float e_ = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
-          const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
-          const float gxm = __shfl(P.pl[q].gxm, j), gym = __shfl(P.pl[q].gym, j);
-          const float4 v0 = V0[u][q], v1 = V1[u][q];
-          const float wx = dx ? w : e_;
-          // grid_sampler_2d_backward: gx += ((ne-nw) s + (se-sw) n) g, gy += ((sw-nw) e + (se-ne) w) g
-          const float ax = (s * v0.x + n * v1.x) * gv.x + (s * v0.y + n * v1.y) * gv.y +
-                           (s * v0.z + n * v1.z) * gv.z + (s * v0.w + n * v1.w) * gv.w;
-          const float ay = (v1.x - v0.x) * gv.x + (v1.y - v0.y) * gv.y + (v1.z - v0.z) * gv.z +
-                           (v1.w - v0.w) * gv.w;
-          GX[q] = lj ? (dx ? ax : -ax) * gxm : 0.f;
-          GY[q] = lj ? wx * ay * gym : 0.f;
-        }
-        // coords (x, y, z) of planes xy, xz, yz
-        const float d0 = GX[0] + GX[1], d1 = GY[0] + GX[2], d2 = GY[1] + GY[2];
-        aro0 += d0;
-        aro1 += d1;
-        aro2 += d2;
-        ard0 = fmaf(d0, tj, ard0);
-        ard1 = fmaf(d1, tj, ard1);
-        ard2 = fmaf(d2, tj, ard2);
-      }
-    }
-  }
-  const float gro0 = wave_sum(aro0) / sr, gro1 = wave_sum(aro1) / sr, gro2 = wave_sum(aro2) / sr;
-  const float grd0 = wave_sum(ard0) / sr, grd1 = wave_sum(ard1) / sr, grd2 = wave_sum(ard2) / sr;
-  if (l == 0) {
-    unsafeAtomicAdd(g.g_ro + r * 3 + 0, gro0);
-    unsafeAtomicAdd(g.g_ro + r * 3 + 1, gro1);
-    unsafeAtomicAdd(g.g_ro + r * 3 + 2, gro2);
-    unsafeAtomicAdd(g.g_rd + r * 3 + 0, grd0);
-    unsafeAtomicAdd(g.g_rd + r * 3 + 1, grd1);
-    unsafeAtomicAdd(g.g_rd + r * 3 + 2, grd2);
-  }
-}
-
 struct BinArgs {
   const float* ro;
   const float* rd;
@@ -1418,6 +1311,8 @@ __global__ void __launch_bounds__(256) chunk_map_kernel(const int* __restrict__ 
 }
 
 struct TileArgs {
+  const float* planes;    // texel-major, strides sb / sq / st as dplanes
+  float* dpc;             // [nsamp][3 planes][2] grid gradients (NULL: no pose gradients)
   const float* gfeat;     // [nsamp][32]
   const int* counts;
   const int* offsets;
@@ -1434,11 +1329,17 @@ struct TileArgs {
 
 typedef float img32 __attribute__((ext_vector_type(32)));
 typedef int iv4 __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(4))) iv4* cint4_p;
 
-// gradient-row stage: rows of XS = 36 floats (the 4-float pad makes both the per-lane b128 row
-// stores and the per-entry row reads conflict-free, with immediate-offset addressing)
+// gradient-row stage: BATCH rows of XS = 36 floats per wave (the 4-float pad makes both the
+// per-lane b128 row stores / reads and the per-entry row reads conflict-free, with
+// immediate-offset addressing).  60 rows, not 64, so that the stages, the tile texels and 4
+// workgroups fit one CU's LDS; the stage (2,160 floats) still holds a wave's 2,048-float image.
+constexpr int BATCH = 60;
+constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
+__device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
+constexpr int TEXF = TTX * TTY * NC;            // 1,280 floats
+constexpr int TILE_LDS = 4 * TROWS + TEXF;      // 39,680 B: 4 workgroups per CU
 
 // img[slot] += a0, img[slot + 1] += a1 for a wave-uniform slot: M0-indexed source AND
 // destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
@@ -1458,10 +1359,8 @@ __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1
 }
 
 // One entry: run-merge into (a0, a1) while the cell repeats, else flush to the image.
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, const iv4 rc, float g,
-                                           float wsgn, float woff, bool ok) {
-  const int slot = __builtin_amdgcn_readfirstlane(rc.y) & 31;
-  const float w = __int_as_float(rc.z), nn = __int_as_float(rc.w);
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
+                                           float nn, float g, float wsgn, float woff, bool ok) {
   const float gw = ok ? g * fmaf(nn, wsgn, woff) : 0.f;
   if (slot != cur) {
     img_add(img, cur, a0, a1);
@@ -1473,14 +1372,44 @@ __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, floa
   a1 = fmaf(gw, w, a1);
 }
 
-// One workgroup-chunk c (< meta[0]) of a tile's entries; lds: 4 * XTILE floats.
+// Grid gradient of one (sample, plane) entry from its gradient row g (stage row l of G) and the
+// tile texels: grid_sampler_2d_backward (generator.py:312-326 through ATen, border padding,
+// align_corners) in the normalized cell,
+//   gx = gxm sum_c g_c (s (T01 - T00) + n (T11 - T10)),  gy = gym sum_c g_c (e (T10 - T00) + w (T11 - T01))
+// with T_yx the cell's texels (row y0 + y, column x0 + x), e = 1 - w, s = 1 - n, and the
+// multipliers gxm / gym = (R-1)/2 strictly inside, else 0 (record flags).  A border-clipped
+// point (x0 = R-1, w = 0, gxm = 0) normalized to (R-2, w = 1) gives the same gy, and likewise in y.
+__device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, const float* __restrict__ Tex,
+                                                int l, int4 rec, int q, float half, float* __restrict__ dpc) {
+  const int slot = rec.y & 31;
+  const float w = __int_as_float(rec.z), n = __int_as_float(rec.w);
+  const float e = 1.f - w, s = 1.f - n;
+  float gx = 0.f, gy = 0.f;
+#pragma unroll 1
+  for (int k = 0; k < NC / 4; ++k) {
+    const float4 g4 = *reinterpret_cast<const float4*>(G + stage_q(l, k));
+    const float4 t00 = *reinterpret_cast<const float4*>(Tex + slot * NC + 4 * (k ^ (slot & 7)));
+    const float4 t01 = *reinterpret_cast<const float4*>(Tex + (slot + 1) * NC + 4 * (k ^ ((slot + 1) & 7)));
+    const float4 t10 = *reinterpret_cast<const float4*>(Tex + (slot + TTX) * NC + 4 * (k ^ ((slot + TTX) & 7)));
+    const float4 t11 = *reinterpret_cast<const float4*>(Tex + (slot + TTX + 1) * NC + 4 * (k ^ ((slot + TTX + 1) & 7)));
+#define NFI_GG(C)                                                     \
+  gx = fmaf(g4.C, fmaf(s, t01.C - t00.C, n * (t11.C - t10.C)), gx);   \
+  gy = fmaf(g4.C, fmaf(e, t10.C - t00.C, w * (t11.C - t01.C)), gy);
+    NFI_GG(x) NFI_GG(y) NFI_GG(z) NFI_GG(w)
+#undef NFI_GG
+  }
+  const float2 out = make_float2((rec.y & 0x100) ? gx * half : 0.f, (rec.y & 0x200) ? gy * half : 0.f);
+  *reinterpret_cast<float2*>(dpc + ((long long)rec.x * 3 + q) * 2) = out;
+}
+
+// One workgroup-chunk c (< meta[0]) of a tile's entries; lds: TILE_LDS floats.
 __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict__ lds, int c) {
   const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = lane_id();
   const int h = l >> 5, cl = l & 31;
-  float* G = lds + wv * XTILE;
+  float* G = lds + wv * TROWS;
+  float* Tex = lds + 4 * TROWS;
   // half 0 weights row ly by (1 - n), half 1 row ly + 1 by n
   const float wsgn = h ? 1.f : -1.f, woff = h ? 0.f : 1.f;
-  const cint4_p L = (cint4_p)A.list;
   NFI_STAMP_INIT
   {
     // (wave-uniform scalars: readfirstlane keeps the entry loop's control and the register-image
@@ -1490,6 +1419,20 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int last = __builtin_amdgcn_readfirstlane(min(A.offsets[tile] + A.counts[tile], first + CHUNK));
     int b, q, tx, ty;
     tile_decode(tile, A.tg, b, q, tx, ty);
+    if (A.dpc) {
+      // the tile's texels of plane q (texels past the plane edge are never referenced: cells
+      // are normalized to x0, y0 <= R-2)
+      const float* src = A.planes + (long long)b * A.sb + (long long)q * A.sq;
+      for (int k = tid; k < TTX * TTY * (NC / 4); k += 256) {
+        const int texel = k / (NC / 4), c4 = k % (NC / 4);
+        const int gy = ty * TSY + texel / TTX, gx = tx * TSX + texel % TTX;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gy < A.R && gx < A.R) v = *reinterpret_cast<const float4*>(src + (long long)(gy * A.R + gx) * A.st + 4 * c4);
+        *reinterpret_cast<float4*>(Tex + texel * NC + 4 * (c4 ^ (texel & 7))) = v;
+      }
+      __syncthreads();
+    }
+    const float half = (float)(A.R - 1) / 2.f;
     // each wave sums a contiguous quarter of the chunk (runs of one ray stay together)
     const int per = (((last - first) + 3) / 4 + 7) & ~7;
     const int b0 = first + wv * per, b1 = min(last, b0 + per);
@@ -1508,47 +1451,43 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     r4 = src_[4]; r5 = src_[5]; r6 = src_[6]; r7 = src_[7];                                      \
   }
       NFI_LOAD_ROW(vrec)
-      for (int base = b0; base < b1; base += 64) {
-        const int n = min(64, b1 - base);
-        {
+      for (int base = b0; base < b1; base += BATCH) {
+        const int n = min(BATCH, b1 - base);
+        if (l < BATCH) {
           float4* dst = reinterpret_cast<float4*>(G + l * XS);
           dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
           dst[4] = r4; dst[5] = r5; dst[6] = r6; dst[7] = r7;
         }
-        // next 64 rows load while these are summed
-        vrec = A.list[min(base + 64 + l, b1 - 1)];
-        NFI_LOAD_ROW(vrec)
         wave_lds_sync();
+        // pose: each lane's own entry against the staged texels (one lane per entry; before the
+        // next rows are in flight, which keeps the register count at occupancy 4)
+        if (A.dpc && l < n) entry_grid_grad(G, Tex, l, vrec, q, half, A.dpc);
+        // this batch's records stay in VGPRs (lane j = entry base + j; lanes past the chunk end
+        // hold the clamped last record and are masked); the entry loop reads them with
+        // v_readlane.  (Scalar loads of the records shared the lgkm counter with the LDS row
+        // reads, so every 8-entry step waited for a full K$-miss round trip.)
+        const int cslot = vrec.y & 31;
+        const int cw = vrec.z, cn = vrec.w;
+        // next 64 rows load while these are summed
+        vrec = A.list[min(base + BATCH + l, b1 - 1)];
+        NFI_LOAD_ROW(vrec)
         NFI_STAMP(24)
-        // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed;
-        // records past the chunk end read the next tile's entries or the list padding (in
-        // bounds) and are masked in the last, partial step
-        iv4 rc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) rc[k] = L[base + k];
         for (int u = 0; u < n; u += 8) {
           float gv[8];
-          iv4 rn[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            gv[k] = G[stage_at(u + k, cl)];
-            rn[k] = L[base + u + 8 + k];
-          }
-#if defined(NFI_ABLATE) && NFI_ABLATE == 2
-          if (true) {   // experiment: entries only loaded
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a0 += gv[k] + __int_as_float(rc[k].z);
-          } else
-#endif
+          for (int k = 0; k < 8; ++k) gv[k] = G[stage_at(u + k, cl)];
+#define NFI_ENTRY(K, OK)                                                                            \
+  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readlane(cslot, u + (K)),                           \
+             __int_as_float(__builtin_amdgcn_readlane(cw, u + (K))),                                 \
+             __int_as_float(__builtin_amdgcn_readlane(cn, u + (K))), gv[K], wsgn, woff, OK)
           if (u + 8 <= n) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) tile_entry(img, cur, a0, a1, rc[k], gv[k], wsgn, woff, true);
+            for (int k = 0; k < 8; ++k) NFI_ENTRY(k, true);
           } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) tile_entry(img, cur, a0, a1, rc[k], gv[k], wsgn, woff, u + k < n);
+            for (int k = 0; k < 8; ++k) NFI_ENTRY(k, u + k < n);
           }
-#pragma unroll
-          for (int k = 0; k < 8; ++k) rc[k] = rn[k];
+#undef NFI_ENTRY
         }
         wave_lds_sync();
         NFI_STAMP(25)
@@ -1569,7 +1508,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       float v = 0.f;
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
-        const float* im = lds + w4 * XTILE;
+        const float* im = lds + w4 * TROWS;
         if (yl < TSY) v += im[(yl * TTX + xl) * NC + ch];
         if (yl >= 1) v += im[(32 + (yl - 1) * TTX + xl) * NC + ch];
       }
@@ -1780,32 +1719,56 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
   }
 }
 
-constexpr int FUSED_LDS = 4 * XTILE;
+// d planes and the per-(sample, plane) grid gradients of the pose path, one workgroup per tile
+// chunk (the grid is sized for a bound on the chunk count; blocks past meta[0] exit at once).
+__global__ void __launch_bounds__(256, 4) tile_kernel(TileArgs A) {
+  __shared__ __attribute__((aligned(16))) float lds[TILE_LDS];
+  if ((long long)blockIdx.x >= A.meta[0]) return;
+  tile_chunk(A, lds, (int)blockIdx.x);
+}
 
-// d planes (tile chunks) and ray-coordinate gradients (dcoord jobs) in ONE launch, the two roles
-// interleaved over the grid so a CU runs both at once: the register-image tile sums are bound by
-// their VALU/SALU dependency chains, the coordinate re-gather by memory latency, and each fills
-// the other's stalls.  With T = meta[0] chunks, block b < T + DB is a tile block iff
-// floor((b+1) T / (T+DB)) > floor(b T / (T+DB)); the grid is sized for a bound on T and the
-// blocks past T + DB exit at once.
-__global__ void __launch_bounds__(256, 4) tile_dcoord_kernel(TileArgs A, nfi_render_args a, BwdArgs g,
-                                                             long long DB) {
-  __shared__ __attribute__((aligned(16))) float lds[FUSED_LDS];
-  const long long T = A.meta[0];
-  const long long b = blockIdx.x, tot = T + DB;
-  if (b >= tot) return;
-  const long long t0 = b * T / tot, t1 = (b + 1) * T / tot;
-  if (t1 > t0) {
-#if defined(NFI_ABLATE) && NFI_ABLATE == 4
-    return;   // experiment: coordinate role only
-#endif
-    tile_chunk(A, lds, (int)t0);
-  } else {
-#if defined(NFI_ABLATE) && NFI_ABLATE == 3
-    return;   // experiment: tile role only
-#endif
-    const int wv = threadIdx.x >> 6;
-    dcoord_job(a, g, (b - t0) * 4 + wv, lds + wv * XTILE);
+// Ray-coordinate gradients from the tile pass's grid gradients, one wave per 64 merged samples:
+// dL/dp_j = (gx_xy + gx_xz, gy_xy + gx_yz, gy_xz + gy_yz)_j / scene_range (planes xy, xz, yz take
+// coordinates (x, y), (x, z), (y, z); generator.py:312-326, 604), dL/d ro = sum_j dL/dp_j and
+// dL/d rd = sum_j t_j dL/dp_j (p = ro + rd t, run.py:283-288).  Samples outside the box have no
+// entries (their sigma and weight are 0, so their feature gradient is exactly zero).
+__global__ void __launch_bounds__(256) dcoord_reduce_kernel(nfi_render_args a, BwdArgs g, const float* __restrict__ dpc) {
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long nrays = (long long)a.B * a.HW;
+  const long long job = (long long)blockIdx.x * 4 + wv;
+  const long long r = job / g.npl;
+  const int e = (int)(job % g.npl);
+  if (r >= nrays) return;
+  const int N = a.fine ? 2 * a.S : a.S;
+  if (e * 64 >= N) return;
+  const float sr = a.field.scene_range;
+  RayCtx R;
+  load_ray(a, r, R);
+  const int i = e * 64 + l;
+  const bool v = i < N;
+  const float te = v ? a.t_saved[r * N + i] : R.near_;
+  // the in-box test of point_params (the tile entries were made with the same arithmetic)
+  float cx[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(R.o[k], fmul(R.d[k], te)), sr);
+  const bool live = v && !(fabsf(cx[0]) > 1.f || fabsf(cx[1]) > 1.f || fabsf(cx[2]) > 1.f);
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+  if (live) {
+    const float2* p = reinterpret_cast<const float2*>(dpc + (r * N + i) * 6);
+    const float2 xy = p[0], xz = p[1], yz = p[2];
+    d0 = xy.x + xz.x;
+    d1 = xy.y + yz.x;
+    d2 = xz.y + yz.y;
+  }
+  const float gro0 = wave_sum(d0) / sr, gro1 = wave_sum(d1) / sr, gro2 = wave_sum(d2) / sr;
+  const float grd0 = wave_sum(d0 * te) / sr, grd1 = wave_sum(d1 * te) / sr, grd2 = wave_sum(d2 * te) / sr;
+  if (l == 0) {
+    unsafeAtomicAdd(g.g_ro + r * 3 + 0, gro0);
+    unsafeAtomicAdd(g.g_ro + r * 3 + 1, gro1);
+    unsafeAtomicAdd(g.g_ro + r * 3 + 2, gro2);
+    unsafeAtomicAdd(g.g_rd + r * 3 + 0, grd0);
+    unsafeAtomicAdd(g.g_rd + r * 3 + 1, grd1);
+    unsafeAtomicAdd(g.g_rd + r * 3 + 2, grd2);
   }
 }
 
@@ -1821,6 +1784,7 @@ struct Workspace {
   int* meta;
   int* part;
   int4* list;
+  float* dpc;
   long long bytes;
 };
 
@@ -1849,6 +1813,7 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   // chunks <= ceil(entries / CHUNK) + K  (each tile wastes at most one partial chunk)
   w.chunk_tile = reinterpret_cast<int*>(take((3 * nsamp / CHUNK + K + 1) * 4));
   w.list = reinterpret_cast<int4*>(take((3 * nsamp + 128) * 16));   // + padding read by tile_chunk
+  w.dpc = reinterpret_cast<float*>(take(nsamp * 6 * 4));
   w.bytes = p - static_cast<char*>(base);
   return w;
 }
@@ -1924,15 +1889,29 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
-  TileArgs TA{w.gfeat, counts, w.offsets, w.chunk_start, w.chunk_tile, w.meta, w.list, g->d_planes, a->field.sb,
-              (int)a->field.sq, (int)a->field.st, a->field.R, tg};
+#if defined(NFI_ABLATE) && NFI_ABLATE == 5
+  float* const dpc_used = nullptr;   // experiment: no pose path in the tile pass
+#else
+  float* const dpc_used = g->g_ro ? w.dpc : nullptr;
+#endif
+  TileArgs TA{a->field.planes, dpc_used, w.gfeat, counts, w.offsets, w.chunk_start,
+              w.chunk_tile, w.meta, w.list, g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st,
+              a->field.R, tg};
   if (do_tiles) {
-    // 3) + 4) per-tile register accumulation of d planes || coordinate gradients (one launch)
+    // 3) per-tile register accumulation of d planes (+ per-entry grid gradients for the pose)
     const long long TB = 3 * nsamp / CHUNK + K + 1;
-    const long long DB = g->g_ro ? (nrays * NPL + 3) / 4 : 0;
-    NFI_REQUIRE(TB + DB < (1LL << 31), "render_backward: grid too large");
-    tile_dcoord_kernel<<<(unsigned)(TB + DB), 256, 0, s>>>(TA, *a, bg, DB);
-    NFI_CHECK_LAUNCH("tile_dcoord_kernel");
+    NFI_REQUIRE(TB < (1LL << 31), "render_backward: grid too large");
+    tile_kernel<<<(unsigned)TB, 256, 0, s>>>(TA);
+    NFI_CHECK_LAUNCH("tile_kernel");
+    // 4) ray-coordinate gradients
+#if defined(NFI_ABLATE) && (NFI_ABLATE == 5 || NFI_ABLATE == 6)
+    if (false) {   // experiment: no reduce launch
+#else
+    if (g->g_ro) {
+#endif
+      dcoord_reduce_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg, w.dpc);
+      NFI_CHECK_LAUNCH("dcoord_reduce_kernel");
+    }
   }
   return NFI_OK;
 }

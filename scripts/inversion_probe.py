@@ -43,6 +43,9 @@ def run(B, loss, steps=10, cl=False):
 
 
 if __name__ == '__main__':
+    if len(sys.argv) > 1:          # python scripts/inversion_probe.py B loss steps
+        run(int(sys.argv[1]), sys.argv[2], steps=int(sys.argv[3]))
+        sys.exit(0)
     for B in (4, 8, 16):
         run(B, 'l1')
     for B in (4, 8):
