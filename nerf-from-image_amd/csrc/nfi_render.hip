@@ -1329,6 +1329,7 @@ struct TileArgs {
 
 typedef float img32 __attribute__((ext_vector_type(32)));
 typedef int iv4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) iv4* cint4_p;
 
 // gradient-row stage: BATCH rows of XS = 36 floats per wave (the 4-float pad makes both the
 // per-lane b128 row stores / reads and the per-entry row reads conflict-free, with
@@ -1338,8 +1339,10 @@ constexpr int BATCH = 60;
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 __device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
-constexpr int TEXF = TTX * TTY * NC;            // 1,280 floats
-constexpr int TILE_LDS = 4 * TROWS + TEXF;      // 39,680 B: 4 workgroups per CU
+// the tile's 8x5 plane texels x 32 channels (pose gradients), texel rows of XS floats (per-lane
+// b128 reads of different texels conflict only for texels 16 slots apart)
+constexpr int TEXF = TTX * TTY * XS;            // 1,440 floats
+constexpr int TILE_LDS = 4 * TROWS + TEXF;      // 40,320 B: 4 workgroups per CU
 
 // img[slot] += a0, img[slot + 1] += a1 for a wave-uniform slot: M0-indexed source AND
 // destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
@@ -1347,6 +1350,11 @@ constexpr int TILE_LDS = 4 * TROWS + TEXF;      // 39,680 B: 4 workgroups per CU
 __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1) {
 #if defined(NFI_ABLATE) && NFI_ABLATE == 1
   img[0] += a0 + a1 + (float)slot;   // experiment: no indexed update
+  return;
+#endif
+#ifdef NFI_IMG_NATIVE
+  img[slot] += a0;       // experiment: the compiler's indirect register addressing
+  img[slot + 1] += a1;
   return;
 #endif
   asm volatile(
@@ -1385,13 +1393,14 @@ __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, con
   const float w = __int_as_float(rec.z), n = __int_as_float(rec.w);
   const float e = 1.f - w, s = 1.f - n;
   float gx = 0.f, gy = 0.f;
-#pragma unroll 1
+#pragma unroll 2
   for (int k = 0; k < NC / 4; ++k) {
     const float4 g4 = *reinterpret_cast<const float4*>(G + stage_q(l, k));
-    const float4 t00 = *reinterpret_cast<const float4*>(Tex + slot * NC + 4 * (k ^ (slot & 7)));
-    const float4 t01 = *reinterpret_cast<const float4*>(Tex + (slot + 1) * NC + 4 * (k ^ ((slot + 1) & 7)));
-    const float4 t10 = *reinterpret_cast<const float4*>(Tex + (slot + TTX) * NC + 4 * (k ^ ((slot + TTX) & 7)));
-    const float4 t11 = *reinterpret_cast<const float4*>(Tex + (slot + TTX + 1) * NC + 4 * (k ^ ((slot + TTX + 1) & 7)));
+    const float* t = Tex + slot * XS + 4 * k;
+    const float4 t00 = *reinterpret_cast<const float4*>(t);
+    const float4 t01 = *reinterpret_cast<const float4*>(t + XS);
+    const float4 t10 = *reinterpret_cast<const float4*>(t + TTX * XS);
+    const float4 t11 = *reinterpret_cast<const float4*>(t + (TTX + 1) * XS);
 #define NFI_GG(C)                                                     \
   gx = fmaf(g4.C, fmaf(s, t01.C - t00.C, n * (t11.C - t10.C)), gx);   \
   gy = fmaf(g4.C, fmaf(e, t10.C - t00.C, w * (t11.C - t01.C)), gy);
@@ -1428,7 +1437,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         const int gy = ty * TSY + texel / TTX, gx = tx * TSX + texel % TTX;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gy < A.R && gx < A.R) v = *reinterpret_cast<const float4*>(src + (long long)(gy * A.R + gx) * A.st + 4 * c4);
-        *reinterpret_cast<float4*>(Tex + texel * NC + 4 * (c4 ^ (texel & 7))) = v;
+        *reinterpret_cast<float4*>(Tex + texel * XS + 4 * c4) = v;
       }
       __syncthreads();
     }
@@ -1462,32 +1471,35 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         // pose: each lane's own entry against the staged texels (one lane per entry; before the
         // next rows are in flight, which keeps the register count at occupancy 4)
         if (A.dpc && l < n) entry_grid_grad(G, Tex, l, vrec, q, half, A.dpc);
-        // this batch's records stay in VGPRs (lane j = entry base + j; lanes past the chunk end
-        // hold the clamped last record and are masked); the entry loop reads them with
-        // v_readlane.  (Scalar loads of the records shared the lgkm counter with the LDS row
-        // reads, so every 8-entry step waited for a full K$-miss round trip.)
-        const int cslot = vrec.y & 31;
-        const int cw = vrec.z, cn = vrec.w;
-        // next 64 rows load while these are summed
+        // the next batch of rows loads while this one is summed
         vrec = A.list[min(base + BATCH + l, b1 - 1)];
         NFI_LOAD_ROW(vrec)
         NFI_STAMP(24)
+        // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed;
+        // records past the chunk end read the next tile's entries or the list padding (in
+        // bounds) and are masked in the last, partial step
+        const cint4_p L = (cint4_p)A.list;
+        iv4 rc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rc[k] = L[base + k];
         for (int u = 0; u < n; u += 8) {
           float gv[8];
+          iv4 rn[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) gv[k] = G[stage_at(u + k, cl)];
-#define NFI_ENTRY(K, OK)                                                                            \
-  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readlane(cslot, u + (K)),                           \
-             __int_as_float(__builtin_amdgcn_readlane(cw, u + (K))),                                 \
-             __int_as_float(__builtin_amdgcn_readlane(cn, u + (K))), gv[K], wsgn, woff, OK)
-          if (u + 8 <= n) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) NFI_ENTRY(k, true);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) NFI_ENTRY(k, u + k < n);
+          for (int k = 0; k < 8; ++k) {
+            gv[k] = G[stage_at(u + k, cl)];
+            rn[k] = L[base + u + 8 + k];
           }
+#define NFI_ENTRY(K, OK)                                                                             \
+  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(rc[K].y) & 31, __int_as_float(rc[K].z), \
+             __int_as_float(rc[K].w), gv[K], wsgn, woff, OK)
+          // one body for full and partial steps: a second copy of the body made the register
+          // allocator move the whole image at every step
+#pragma unroll
+          for (int k = 0; k < 8; ++k) NFI_ENTRY(k, u + k < n);
 #undef NFI_ENTRY
+#pragma unroll
+          for (int k = 0; k < 8; ++k) rc[k] = rn[k];
         }
         wave_lds_sync();
         NFI_STAMP(25)
