@@ -127,8 +127,10 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int pk = __shfl(P.pl[q].tex, j);
-        const float e = __shfl(P.pl[q].e, j), w = __shfl(P.pl[q].w, j);
-        const float s = __shfl(P.pl[q].s, j), n = __shfl(P.pl[q].n, j);
+        // (e = 1 - w and s = 1 - n recomputed here, as plane_params rounds them: 3 ds_bpermute per
+        // plane instead of 5)
+        const float w = __shfl(P.pl[q].w, j), n = __shfl(P.pl[q].n, j);
+        const float e = 1.f - w, s = 1.f - n;
         const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
         const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
         const float* b = pv.base + q * pv.sq + 4 * q4;
@@ -1300,11 +1302,15 @@ __global__ void __launch_bounds__(1024) scan_blocks_kernel(const int* __restrict
   }
 }
 
-// chunk -> tile map (one dependent load per chunk in tile_accum instead of a binary search)
+// chunk -> tile map (one dependent load per chunk in tile_accum instead of a binary search); block
+// 0 also zeroes the 64 list records after the last entry, which the tile pass's record prefetch
+// reads past the end (a zero record: slot 0, weights 0)
 __global__ void __launch_bounds__(256) chunk_map_kernel(const int* __restrict__ counts,
                                                         const int* __restrict__ chunk_start, int K,
-                                                        int* __restrict__ chunk_tile) {
+                                                        int* __restrict__ chunk_tile,
+                                                        const int* __restrict__ offsets, int4* __restrict__ list) {
   const int k = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 64) list[offsets[K] + threadIdx.x] = make_int4(0, 0, 0, 0);
   if (k >= K) return;
   const int c0 = chunk_start[k], nc = (counts[k] + CHUNK - 1) / CHUNK;
   for (int j = 0; j < nc; ++j) chunk_tile[c0 + j] = k;
@@ -1335,7 +1341,7 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 // per-lane b128 row stores / reads and the per-entry row reads conflict-free, with
 // immediate-offset addressing).  60 rows, not 64, so that the stages, the tile texels and 4
 // workgroups fit one CU's LDS; the stage (2,160 floats) still holds a wave's 2,048-float image.
-constexpr int BATCH = 60;
+constexpr int BATCH = 56;
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 __device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
@@ -1348,6 +1354,7 @@ constexpr int TILE_LDS = 4 * TROWS + TEXF;      // 40,320 B: 4 workgroups per CU
 // destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
 // v[40:71] at these points so the asm can name its base register.
 __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1) {
+  slot = min(slot, 30);   // (cells are slots 0..30; never index past v71, whatever the record)
 #if defined(NFI_ABLATE) && NFI_ABLATE == 1
   img[0] += a0 + a1 + (float)slot;   // experiment: no indexed update
   return;
@@ -1363,13 +1370,14 @@ __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1
       "v_add_f32 v41, v41, %3\n\t"
       "s_set_gpr_idx_off"
       : "+{v[40:71]}"(img)
-      : "s"(slot), "v"(a0), "v"(a1));
+      : "s"(slot), "v"(a0), "v"(a1));   // (M0, which the index goes through, is reserved:
+                                         //  the compiler re-initializes it before any use)
 }
 
 // One entry: run-merge into (a0, a1) while the cell repeats, else flush to the image.
 __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff, bool ok) {
-  const float gw = ok ? g * fmaf(nn, wsgn, woff) : 0.f;
+                                           float nn, float g, float wsgn, float woff) {
+  const float gw = g * fmaf(nn, wsgn, woff);
   if (slot != cur) {
     img_add(img, cur, a0, a1);
     a0 = 0.f;
@@ -1462,6 +1470,9 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       NFI_LOAD_ROW(vrec)
       for (int base = b0; base < b1; base += BATCH) {
         const int n = min(BATCH, b1 - base);
+        // rows past the chunk end are zeroed: the last step's surplus entries then add 0 (their
+        // records, from the next tile or the list padding, only move the run cursor)
+        if (l >= n) r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (l < BATCH) {
           float4* dst = reinterpret_cast<float4*>(G + l * XS);
           dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
@@ -1475,9 +1486,9 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         vrec = A.list[min(base + BATCH + l, b1 - 1)];
         NFI_LOAD_ROW(vrec)
         NFI_STAMP(24)
-        // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed;
-        // records past the chunk end read the next tile's entries or the list padding (in
-        // bounds) and are masked in the last, partial step
+        // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed.
+        // The surplus entries of the last step read the next tile's records or the zeroed list
+        // padding (chunk_map_kernel): valid cells, and their zeroed rows add 0.
         const cint4_p L = (cint4_p)A.list;
         iv4 rc[8];
 #pragma unroll
@@ -1490,13 +1501,13 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
             gv[k] = G[stage_at(u + k, cl)];
             rn[k] = L[base + u + 8 + k];
           }
-#define NFI_ENTRY(K, OK)                                                                             \
+#define NFI_ENTRY(K)                                                                                 \
   tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(rc[K].y) & 31, __int_as_float(rc[K].z), \
-             __int_as_float(rc[K].w), gv[K], wsgn, woff, OK)
-          // one body for full and partial steps: a second copy of the body made the register
-          // allocator move the whole image at every step
+             __int_as_float(rc[K].w), gv[K], wsgn, woff)
+          // one body for full and partial steps (a second copy of the body made the register
+          // allocator move the whole image at every step)
 #pragma unroll
-          for (int k = 0; k < 8; ++k) NFI_ENTRY(k, u + k < n);
+          for (int k = 0; k < 8; ++k) NFI_ENTRY(k);
 #undef NFI_ENTRY
 #pragma unroll
           for (int k = 0; k < 8; ++k) rc[k] = rn[k];
@@ -1511,7 +1522,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     __syncthreads();   // every wave is done with its row stage
     // wave images -> LDS [wave][half][slot][channel]
 #pragma unroll
-    for (int r = 0; r < 32; ++r) G[(h * 32 + r) * NC + cl] = img[r];
+    for (int r = 0; r < 32; ++r) lds[wv * 2048 + (h * 32 + r) * NC + cl] = img[r];
     __syncthreads();
     float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
     for (int k = tid; k < TTX * TTY * NC; k += 256) {
@@ -1520,7 +1531,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       float v = 0.f;
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
-        const float* im = lds + w4 * TROWS;
+        const float* im = lds + w4 * 2048;
         if (yl < TSY) v += im[(yl * TTX + xl) * NC + ch];
         if (yl >= 1) v += im[(32 + (yl - 1) * TTX + xl) * NC + ch];
       }
@@ -1881,7 +1892,8 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     NFI_CHECK_LAUNCH("scan_partials_kernel");
     scan_blocks_kernel<<<nb, 1024, 0, s>>>(counts, K, w.part, w.offsets, w.cursor, w.chunk_start, w.meta);
     NFI_CHECK_LAUNCH("scan_blocks_kernel");
-    chunk_map_kernel<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(counts, w.chunk_start, K, w.chunk_tile);
+    chunk_map_kernel<<<(unsigned)((K + 255) / 256), 256, 0, s>>>(counts, w.chunk_start, K, w.chunk_tile, w.offsets,
+                                                               w.list);
     NFI_CHECK_LAUNCH("chunk_map_kernel");
     if (!fwd_counts) {
       bin_fill_kernel<<<sb, 256, 0, s>>>(B);

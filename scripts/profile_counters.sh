@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/ctr_${TAG:-r01}
 mkdir -p $OUT
-BENCH="bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_EXTRA:-}"
+BENCH="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-inversion ${BENCH_EXTRA:-}"
 i=0
 run() {
   i=$((i+1))
