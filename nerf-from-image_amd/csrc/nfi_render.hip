@@ -110,7 +110,10 @@ __device__ __forceinline__ float4 ror8_add(float4 v) {
 
 // Loads of GB groups (4*GB points) are issued before any is consumed: the gather is bound by
 // load latency (texels mostly come from MALL/HBM), so the wave keeps 6*GB KiB in flight.
-constexpr int GATHER_GB = 2;
+#ifndef NFI_GATHER_GB
+#define NFI_GATHER_GB 2
+#endif
+constexpr int GATHER_GB = NFI_GATHER_GB;
 
 __device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
                                                 float* __restrict__ X) {
