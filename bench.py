@@ -155,6 +155,13 @@ def cpu_inversion_step(inp, H, loss_kinds):
     return res
 
 
+def max_over_ranks(x: float, dev) -> float:
+    """MAX of a host float over the ranks (on the device for RCCL, on the host for gloo)."""
+    t = torch.tensor([x], device=dev if dist.get_backend() == 'nccl' else 'cpu', dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def inversion_leg(args, dev, cfg, batch, world, loss):
     """BASELINE.json's second number: seconds per image of the 30-step inversion (run.py:1960-2310,
     pose optimised): per step the producer (synthesis network + AttentionMapper: convolutions on
@@ -196,11 +203,11 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
     timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
     render_ms = sum(a.elapsed_time(b) for v in timers.values() for a, b in v) / icfg.steps
     if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dev)
     step_ms = elapsed / icfg.steps * 1e3
-    return {'s_per_image': round(elapsed / (B * world), 5), 'steps': icfg.steps,
+    # s/image of a 30-step inversion (run.py:1762 --inv_steps default 30): all ranks together
+    # finish B * world images per `elapsed` for icfg.steps steps
+    return {'s_per_image': round(elapsed * 30 / icfg.steps / (B * world), 5), 'steps': icfg.steps,
             'images': B * world, 'images_per_gpu': B, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
             'render_ms_per_step': round(render_ms, 3),
             'rest_ms_per_step': round(step_ms - render_ms, 3),
@@ -230,11 +237,15 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    # NFI_BENCH_DIST=gloo rehearses the N-rank path on a box with fewer GPUs than ranks (ranks
+    # share devices round-robin); the driver's multi-GPU runs use RCCL ('nccl'), one GPU per rank.
+    backend = os.environ.get('NFI_BENCH_DIST', 'nccl')
+    if backend != 'nccl':
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group(backend, **({'device_id': dev} if backend == 'nccl' else {}))
 
     import nfi
     from nfi import ops
@@ -260,9 +271,7 @@ def main():
     timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
     kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}  # ms/launch
     if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, dev)
 
     samples_per_step = B * H * H * 2 * S
     value = world * samples_per_step * args.steps / elapsed / 1e6
