@@ -205,7 +205,7 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
     step_ms = elapsed / icfg.steps * 1e3
-    # s/image of a 30-step inversion (arguments.py:174 --inv_steps default 30): all ranks together
+    # s/image of a 30-step inversion (run.py:1829-1830: checkpoint_steps [0, 30] by default): all ranks together
     # finish B * world images per `elapsed` for icfg.steps steps
     return {'s_per_image': round(elapsed * 30 / icfg.steps / (B * world), 5), 'steps': icfg.steps,
             'images': B * world, 'images_per_gpu': B, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
