@@ -9,6 +9,7 @@
  *   skip-image upsample+add  stylegan.py:69-73, 428-433     upsample2d(img) + (toRGB conv + bias)
  *   channel-scale backward   stylegan.py:130                d(x*styles): g*styles and sum(g*x)
  *   LPIPS distance head      metrics.py:130-146 (lpips 0.1) normalise, difference, lin, mean
+ *   LPIPS VGG16 epilogue     bias + ReLU (+ 2x2 max pool) after each trunk convolution
  *
  * Tensors are NCHW float32, contiguous; "planes" P = B*C images of one channel; per-plane
  * scales `d` have P entries ([B,C] row-major), per-channel biases C entries.  `stream` is a
@@ -75,6 +76,18 @@ int32_t nfi_lpips_head_forward(const float* f0, const float* f1, const float* w,
 int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1, const float* w,
                                 const float* inv0, const float* inv1, float* gf0, int32_t N,
                                 int32_t C, int32_t HW, void* stream);
+
+/* LPIPS VGG16 block epilogue (torchvision vgg16.features[:30] as lpips 0.1 runs it, metrics.py:107):
+ * x [P, H, W] = a bias-free 3x3 convolution's output (P = N*C planes) -> y = relu(x + bias[c]);
+ * when `pooled` is not NULL also pooled [P, H/2, W/2] = MaxPool2d(2, 2)(y).  Replaces the bias
+ * add, nn.ReLU and nn.MaxPool2d passes of the conv blocks.  W % 4 == 0 (H even when pooling). */
+int32_t nfi_vgg_bias_relu_forward(const float* x, const float* bias, float* y, float* pooled,
+                                  int32_t P, int32_t C, int32_t H, int32_t W, void* stream);
+
+/* Its backward: gx = (y > 0) * (gy + route(gpooled)), route = max_pool2d's backward (gradient to
+ * the first maximum of each 2x2 window, row-major).  gy or gpooled may be NULL (not both). */
+int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float* y, float* gx,
+                              int32_t P, int32_t H, int32_t W, void* stream);
 
 #ifdef __cplusplus
 }

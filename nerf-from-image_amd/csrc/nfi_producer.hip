@@ -327,6 +327,107 @@ __global__ void __launch_bounds__(256) lpips_bwd_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// VGG16 block epilogue of the LPIPS trunk (torchvision vgg16.features as lpips 0.1 runs it):
+// conv output x (MIOpen, no bias) -> y = ReLU(x + bias[c]) and, before a MaxPool2d(2, 2), the
+// pooled map m = max over each 2x2 window of y, in one pass (torch: bias add, relu, max_pool2d =
+// three passes).  One thread per 2x4 patch of y (two float4 rows, two pooled outputs).
+// Backward: gx = (y > 0) * (gy + route(gm)), route = gm to the FIRST maximum of its window in
+// row-major order (ATen max_pool2d's `val > maxval` scan), i.e. threshold_backward of the sum of
+// the tap gradient and max_pool2d_backward — the three backward kernels in one.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) vgg_bias_relu_kernel(const float4* __restrict__ x,
+                                                            const float* __restrict__ bias,
+                                                            float4* __restrict__ y, int64_t n4, int C,
+                                                            int HW4) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float b = bias[(int)((i / HW4) % C)];
+  const float4 v = x[i];
+  y[i] = make_float4(fmaxf(v.x + b, 0.f), fmaxf(v.y + b, 0.f), fmaxf(v.z + b, 0.f), fmaxf(v.w + b, 0.f));
+}
+
+__device__ __forceinline__ int first_max4(float a, float b, float c, float d, float& m) {
+  int k = 0;
+  m = a;
+  if (b > m) { m = b; k = 1; }
+  if (c > m) { m = c; k = 2; }
+  if (d > m) { m = d; k = 3; }
+  return k;
+}
+
+// patches: P planes x (H/2) row pairs x (W/4) column quads
+__global__ void __launch_bounds__(256) vgg_bias_relu_pool_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ y,
+                                                                 float* __restrict__ m, int64_t npatch,
+                                                                 int C, int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npatch) return;
+  const int W4 = W >> 2, H2 = H >> 1;
+  const int qx = (int)(i % W4);
+  const int64_t t = i / W4;
+  const int ry = (int)(t % H2);
+  const int64_t p = t / H2;
+  const float b = bias[(int)(p % C)];
+  const int64_t o0 = (p * H + 2 * ry) * W + 4 * qx;
+  const float4 u = *reinterpret_cast<const float4*>(x + o0);
+  const float4 v = *reinterpret_cast<const float4*>(x + o0 + W);
+  const float4 yu = make_float4(fmaxf(u.x + b, 0.f), fmaxf(u.y + b, 0.f), fmaxf(u.z + b, 0.f), fmaxf(u.w + b, 0.f));
+  const float4 yv = make_float4(fmaxf(v.x + b, 0.f), fmaxf(v.y + b, 0.f), fmaxf(v.z + b, 0.f), fmaxf(v.w + b, 0.f));
+  *reinterpret_cast<float4*>(y + o0) = yu;
+  *reinterpret_cast<float4*>(y + o0 + W) = yv;
+  float m0, m1;
+  first_max4(yu.x, yu.y, yv.x, yv.y, m0);
+  first_max4(yu.z, yu.w, yv.z, yv.w, m1);
+  *reinterpret_cast<float2*>(m + (p * H2 + ry) * (W >> 1) + 2 * qx) = make_float2(m0, m1);
+}
+
+__global__ void __launch_bounds__(256) vgg_relu_bwd_kernel(const float4* __restrict__ gy,
+                                                           const float4* __restrict__ y,
+                                                           float4* __restrict__ gx, int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4 g = gy[i], v = y[i];
+  gx[i] = make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f,
+                      v.w > 0.f ? g.w : 0.f);
+}
+
+__global__ void __launch_bounds__(256) vgg_relu_pool_bwd_kernel(const float* __restrict__ gy,
+                                                                const float* __restrict__ gm,
+                                                                const float* __restrict__ y,
+                                                                float* __restrict__ gx, int64_t npatch,
+                                                                int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npatch) return;
+  const int W4 = W >> 2, H2 = H >> 1;
+  const int qx = (int)(i % W4);
+  const int64_t t = i / W4;
+  const int ry = (int)(t % H2);
+  const int64_t p = t / H2;
+  const int64_t o0 = (p * H + 2 * ry) * W + 4 * qx;
+  const float4 yu = *reinterpret_cast<const float4*>(y + o0);
+  const float4 yv = *reinterpret_cast<const float4*>(y + o0 + W);
+  float4 gu = make_float4(0.f, 0.f, 0.f, 0.f), gv = gu;
+  if (gy) {
+    gu = *reinterpret_cast<const float4*>(gy + o0);
+    gv = *reinterpret_cast<const float4*>(gy + o0 + W);
+  }
+  if (gm) {
+    const float2 g2 = *reinterpret_cast<const float2*>(gm + (p * H2 + ry) * (W >> 1) + 2 * qx);
+    float mm;
+    const int k0 = first_max4(yu.x, yu.y, yv.x, yv.y, mm);
+    const int k1 = first_max4(yu.z, yu.w, yv.z, yv.w, mm);
+    // (g + 0 == g exactly: the unrouted entries keep the tap gradient unchanged)
+    if (k0 == 0) gu.x += g2.x; else if (k0 == 1) gu.y += g2.x; else if (k0 == 2) gv.x += g2.x; else gv.y += g2.x;
+    if (k1 == 0) gu.z += g2.y; else if (k1 == 1) gu.w += g2.y; else if (k1 == 2) gv.z += g2.y; else gv.w += g2.y;
+  }
+  *reinterpret_cast<float4*>(gx + o0) = make_float4(yu.x > 0.f ? gu.x : 0.f, yu.y > 0.f ? gu.y : 0.f,
+                                                    yu.z > 0.f ? gu.z : 0.f, yu.w > 0.f ? gu.w : 0.f);
+  *reinterpret_cast<float4*>(gx + o0 + W) = make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f,
+                                                        yv.z > 0.f ? gv.z : 0.f, yv.w > 0.f ? gv.w : 0.f);
+}
+
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace syn
@@ -442,6 +543,43 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
   lpips_bwd_kernel<<<blocks((int64_t)N * HW), 256, 0, (hipStream_t)stream>>>(g, f0, f1, w, inv0,
                                                                               inv1, gf0, N, C, HW);
   NFI_CHECK_LAUNCH("lpips_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_vgg_bias_relu_forward(const float* x, const float* bias, float* y, float* pooled,
+                                  int32_t P, int32_t C, int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(x && bias && y, "vgg_bias_relu_forward: null pointer");
+  NFI_REQUIRE(P > 0 && C > 0 && P % C == 0 && H > 0 && W > 0 && W % 4 == 0,
+              "vgg_bias_relu_forward: bad shape (W % 4 == 0 required)");
+  NFI_REQUIRE(!pooled || H % 2 == 0, "vgg_bias_relu_forward: pooling needs an even height");
+  hipStream_t st = (hipStream_t)stream;
+  if (pooled) {
+    const int64_t np = (int64_t)P * (H / 2) * (W / 4);
+    vgg_bias_relu_pool_kernel<<<blocks(np), 256, 0, st>>>(x, bias, y, pooled, np, C, H, W);
+    NFI_CHECK_LAUNCH("vgg_bias_relu_pool_kernel");
+  } else {
+    const int64_t n4 = (int64_t)P * H * W / 4;
+    vgg_bias_relu_kernel<<<blocks(n4), 256, 0, st>>>((const float4*)x, bias, (float4*)y, n4, C, H * W / 4);
+    NFI_CHECK_LAUNCH("vgg_bias_relu_kernel");
+  }
+  return NFI_OK;
+}
+
+int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float* y, float* gx,
+                              int32_t P, int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(y && gx && (gy || gpooled), "vgg_relu_backward: null pointer");
+  NFI_REQUIRE(P > 0 && H > 0 && W > 0 && W % 4 == 0, "vgg_relu_backward: bad shape (W % 4 == 0 required)");
+  NFI_REQUIRE(!gpooled || H % 2 == 0, "vgg_relu_backward: pooling needs an even height");
+  hipStream_t st = (hipStream_t)stream;
+  if (gpooled) {
+    const int64_t np = (int64_t)P * (H / 2) * (W / 4);
+    vgg_relu_pool_bwd_kernel<<<blocks(np), 256, 0, st>>>(gy, gpooled, y, gx, np, H, W);
+    NFI_CHECK_LAUNCH("vgg_relu_pool_bwd_kernel");
+  } else {
+    const int64_t n4 = (int64_t)P * H * W / 4;
+    vgg_relu_bwd_kernel<<<blocks(n4), 256, 0, st>>>((const float4*)gy, (const float4*)y, (float4*)gx, n4);
+    NFI_CHECK_LAUNCH("vgg_relu_bwd_kernel");
+  }
   return NFI_OK;
 }
 

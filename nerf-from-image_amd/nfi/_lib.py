@@ -101,6 +101,11 @@ SIGNATURES = {
     'nfi_lpips_head_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                                  c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_int32, c_void_p]),
+    'nfi_vgg_bias_relu_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p,
+                                                   ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_int32, c_void_p]),
+    'nfi_vgg_relu_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_int32, c_void_p]),
 }
 
 _lib = None

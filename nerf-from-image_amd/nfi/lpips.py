@@ -10,7 +10,8 @@ against, and random weights stand in unless `load_weights` is given the two stat
             lin_l a bias-free 1x1 conv to one channel (lpips/lpips.py NetLinLayer; dropout is
             inactive in eval)
 
-Backends: 'hip' (the VGG convolutions are MIOpen calls; the distance head — normalisation,
+Backends: 'hip' (the VGG convolutions are bias-free MIOpen calls, each followed by one fused HIP
+epilogue — bias, ReLU and the 2x2 max pool where one follows; the distance head — normalisation,
 difference, lin, spatial mean — is one fused HIP kernel per layer, forward and backward,
 csrc/nfi_producer.hip) and 'torch' (the op sequence above in PyTorch).
 """
@@ -46,12 +47,32 @@ class VGG16Features(nn.Module):
                 c = v
         self.features = nn.Sequential(*layers)
 
-    def forward(self, x):
+    def forward(self, x, fused: bool = False):
         out = []
-        for i, layer in enumerate(self.features):
-            x = layer(x)
-            if i in TAPS:
-                out.append(x)
+        if not fused:
+            for i, layer in enumerate(self.features):
+                x = layer(x)
+                if i in TAPS:
+                    out.append(x)
+            return out
+        # each conv block as MIOpen's bias-free convolution + one HIP epilogue pass (bias, ReLU and
+        # the following MaxPool2d when there is one; producer_ops.vgg_epilogue)
+        from . import producer_ops
+        f, i = self.features, 0
+        while i < len(f):
+            conv = f[i]
+            pool = i + 2 < len(f) and isinstance(f[i + 2], nn.MaxPool2d)
+            z = F.conv2d(x, conv.weight, None, 1, 1)
+            if z.shape[-1] % 4 == 0 and not (pool and z.shape[-2] % 2):
+                r = producer_ops.vgg_epilogue(z, conv.bias, pool)
+                y, x = r if pool else (r, r)
+            else:                      # (maps narrower than 4 columns: the unfused ops)
+                y = x = F.relu(z + conv.bias[None, :, None, None])
+                if pool:
+                    x = F.max_pool2d(y, 2, 2)
+            if i + 1 in TAPS:
+                out.append(y)
+            i += 3 if pool else 2
         return out
 
 
@@ -83,7 +104,7 @@ class LPIPS(nn.Module):
         return self
 
     def features(self, im):
-        return self.net((im - self.shift) / self.scale)
+        return self.net((im - self.shift) / self.scale, fused=self.backend == 'hip')
 
     def forward(self, in0, in1):
         f0 = self.features(in0)

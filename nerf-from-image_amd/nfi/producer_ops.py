@@ -6,6 +6,7 @@ the inversion (run.py:630-632), so biases never receive gradients (asking for on
   act        lrelu(gain*(o*d[b,c] + bias[c]))   stylegan.py:145, 348-356 (demodulation epilogue)
   fir_up_act FIR(t) then act                    stylegan.py:99-103 + the epilogue (up layers)
   up_add     upsample2d(img) + c + bias[c]      stylegan.py:69-73, 380-381, 428-433 (skip image)
+  vgg_epilogue relu(x + bias[c]) (+ 2x2 max pool) LPIPS VGG16 trunk (lpips 0.1 via metrics.py:107)
 """
 
 from __future__ import annotations
@@ -171,6 +172,40 @@ class _LpipsHead(torch.autograd.Function):
         _call('nfi_lpips_head_backward', _p(g), _p(f0), _p(f1), _p(w), _p(inv0), _p(inv1), _p(gf0),
               N, C, H * W, _stream(f0.device))
         return gf0, None, None
+
+
+class _VggEpilogue(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, pool: bool):
+        _require_device(x, bias)
+        _frozen(bias)
+        x = x.contiguous()
+        N, C, H, W = x.shape
+        y = torch.empty_like(x)
+        m = torch.empty((N, C, H // 2, W // 2), device=x.device, dtype=x.dtype) if pool else None
+        _call('nfi_vgg_bias_relu_forward', _p(x), _p(bias.detach().contiguous()), _p(y), _p(m),
+              N * C, C, H, W, _stream(x.device))
+        ctx.save_for_backward(y)
+        ctx.set_materialize_grads(False)       # an unused output's gradient arrives as None
+        return (y, m) if pool else y
+
+    @staticmethod
+    def backward(ctx, gy, gm=None):
+        y, = ctx.saved_tensors
+        if gy is None and gm is None:
+            return None, None, None
+        N, C, H, W = y.shape
+        gx = torch.empty_like(y)
+        gy = None if gy is None else gy.contiguous()
+        gm = None if gm is None else gm.contiguous()
+        _call('nfi_vgg_relu_backward', _p(gy), _p(gm), _p(y), _p(gx), N * C, H, W, _stream(y.device))
+        return gx, None, None
+
+
+def vgg_epilogue(x, bias, pool: bool = False):
+    """relu(x + bias[c]) of a bias-free conv output x; with pool=True also returns MaxPool2d(2, 2)
+    of it: (y, pooled).  One HIP pass each way (nfi_vgg_bias_relu_forward / nfi_vgg_relu_backward)."""
+    return _VggEpilogue.apply(x, bias, pool)
 
 
 def lpips_head(f0, f1, w):

@@ -30,6 +30,37 @@ def test_lpips_head_matches_torch(N, C, H):
     torch.testing.assert_close(f0.grad, gref, rtol=1e-4, atol=1e-6 * float(gref.abs().max()))
 
 
+@pytest.mark.parametrize('pool', [False, True])
+@pytest.mark.parametrize('N,C,H,W', [(2, 64, 16, 16), (3, 5, 6, 12), (1, 512, 8, 8)])
+def test_vgg_epilogue_matches_torch(N, C, H, W, pool):
+    """bias + ReLU (+ MaxPool2d(2, 2)) of the VGG trunk: forward bit-exact against the torch ops,
+    backward (tap gradient + pooled gradient) against autograd, including tied windows (all-zero
+    after the ReLU, and equal positive values: the gradient goes to the first maximum)."""
+    g = torch.Generator(device=DEV).manual_seed(N * C + H)
+    x = torch.randn((N, C, H, W), device=DEV, generator=g)
+    x[:, :, :2, :2] = 0.25                  # a window of equal positive values
+    x[:, :, 2:4, :2] = -3.0                 # an all-zero window after the ReLU
+    bias = torch.randn((C,), device=DEV, generator=g) * 0.1
+    bias[0] = 0.0
+    gy = torch.randn((N, C, H, W), device=DEV, generator=g)
+    xa = x.clone().requires_grad_()
+    out = producer_ops.vgg_epilogue(xa, bias, pool)
+    xr = x.clone().requires_grad_()
+    yr = torch.relu(xr + bias[None, :, None, None])
+    if pool:
+        gm = torch.randn((N, C, H // 2, W // 2), device=DEV, generator=g)
+        mr = torch.nn.functional.max_pool2d(yr, 2, 2)
+        y, m = out
+        assert torch.equal(y, yr) and torch.equal(m, mr)
+        torch.autograd.backward([y, m], [gy, gm])
+        torch.autograd.backward([yr, mr], [gy, gm])
+    else:
+        assert torch.equal(out, yr)
+        out.backward(gy)
+        yr.backward(gy)
+    assert torch.equal(xa.grad, xr.grad)
+
+
 def test_lpips_backends_agree():
     torch.manual_seed(0)
     net = lpips.LPIPS(backend='torch').to(DEV)
