@@ -148,19 +148,18 @@ class InversionResult:
     seconds: float = 0.0
 
 
-def augment_images(img: torch.Tensor, p: float, white_background: bool = False,
-                   disable_scale: bool = False, generator: Optional[torch.Generator] = None):
-    """augment_impl (run.py:720-767) for images only (pose None, as the loss calls it): random
-    rotation, scale and translation per image with probability p, applied by affine_grid +
-    bilinear grid_sample (zero padding, or white for white-background datasets).  Random draws in
-    the reference's order, on img.device (or from `generator`)."""
-    bs, dev = img.shape[0], img.device
+def augment_grid(shape, p: float, dev, disable_scale: bool = False,
+                 generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """The sampling grid of augment_impl (run.py:720-767) for images of `shape` [bs,C,H,W]: random
+    rotation, scale and translation per image with probability p, as affine_grid(align_corners=
+    False).  Random draws in the reference's order, on `dev` (or from `generator`)."""
+    bs = shape[0]
 
-    def rand(*shape):
-        return torch.rand(shape, device=dev, generator=generator)
+    def rand(*sh):
+        return torch.rand(sh, device=dev, generator=generator)
 
-    def randn(*shape):
-        return torch.randn(shape, device=dev, generator=generator)
+    def randn(*sh):
+        return torch.randn(sh, device=dev, generator=generator)
 
     rot = (rand(bs) - 0.5) * 2 * math.pi
     rot = rot * (rand(bs) < p).float()
@@ -175,11 +174,22 @@ def augment_images(img: torch.Tensor, p: float, white_background: bool = False,
     rotm = torch.stack([torch.stack([c, -s], -1), torch.stack([s, c], -1)], 1)   # [bs,2,2]
     t = torch.stack([translation[:, 0], -translation[:, 1]], -1) * scale[:, None]
     theta = torch.cat([rotm * scale[:, None, None], (rotm * t[:, None, :]).sum(-1, keepdim=True)], -1)
-    grid = F.affine_grid(theta, list(img.shape), align_corners=False)
+    return F.affine_grid(theta, list(shape), align_corners=False)
+
+
+def apply_grid(img: torch.Tensor, grid: torch.Tensor, white_background: bool = False) -> torch.Tensor:
+    """Bilinear grid_sample with zero padding (white for white-background datasets), run.py:754-764."""
     if white_background:
         img = img - 1
     out = F.grid_sample(img, grid, mode='bilinear', padding_mode='zeros', align_corners=False)
     return out + 1 if white_background else out
+
+
+def augment_images(img: torch.Tensor, p: float, white_background: bool = False,
+                   disable_scale: bool = False, generator: Optional[torch.Generator] = None):
+    """augment_impl (run.py:720-767) for images only (pose None, as the loss calls it)."""
+    grid = augment_grid(img.shape, p, img.device, disable_scale, generator)
+    return apply_grid(img, grid, white_background)
 
 
 VGG_LOSSES = ('vgg', 'vgg_nocrop', 'mixed')
@@ -202,13 +212,20 @@ def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor, lpips_net=Non
                              f'weights loaded via load_weights; none ship offline)')
         pred, tgt = rgb.permute(0, 3, 1, 2), target.permute(0, 3, 1, 2)
         if kind != 'vgg_nocrop':
-            cat = torch.cat((pred, tgt), dim=1).unsqueeze(1).expand(-1, 15, -1, -1, -1)
-            cat = augment_images(cat.contiguous().flatten(0, 1), 1.0, white_background,
-                                 generator=augment_generator)
-            pred = torch.cat((pred, cat[:, :3]), dim=0)
-            # the target copies carry no gradient to any parameter (the reference backpropagates
-            # into them and drops the result at the target leaf)
-            tgt = torch.cat((tgt, cat[:, 3:].detach()), dim=0)
+            # the reference augments cat((pred, target), channels) expanded to 15 copies; grid_sample
+            # treats channels independently, so the prediction and target copies are sampled with
+            # the same grid separately (identical values), and only the prediction's copies
+            # carry a gradient (the reference backpropagates into the target copies and drops the
+            # result at the target leaf)
+            def copies(x):
+                return x.unsqueeze(1).expand(-1, 15, -1, -1, -1).contiguous().flatten(0, 1)
+            shape = (15 * b, 6) + tuple(pred.shape[2:])
+            grid = augment_grid(shape, 1.0, pred.device, generator=augment_generator)
+            aug_pred = apply_grid(copies(pred), grid, white_background)
+            with torch.no_grad():
+                aug_tgt = apply_grid(copies(tgt), grid, white_background)
+            pred = torch.cat((pred, aug_pred), dim=0)
+            tgt = torch.cat((tgt, aug_tgt), dim=0)
         loss = loss + lpips_net(pred, tgt).mean() * b
     if kind in ('l1', 'mixed'):
         loss = loss + F.l1_loss(rgb, target) * b

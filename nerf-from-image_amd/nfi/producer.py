@@ -59,6 +59,25 @@ def upsample2x(x: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
     return _depthwise(x, k * 4, stride=2, transpose=True)
 
 
+def frozen_value(mod: nn.Module, key: str, fn, *params):
+    """fn() cached on `mod` while `params` are frozen and unmodified: the gain-scaled weights and
+    the demodulation sums of squares are functions of the generator's parameters only, which the
+    inversion does not train (run.py:630-632), so they are computed once instead of every step.
+    Invalidated by any in-place update of a parameter (tensor version counter) or a new tensor;
+    a parameter that requires grad is never cached."""
+    tag = tuple((None if p is None else (p.data_ptr(), p._version, p.requires_grad, p.device))
+                for p in params)
+    if any(p is not None and p.requires_grad for p in params) and torch.is_grad_enabled():
+        return fn()
+    cache = mod.__dict__.setdefault('_frozen_cache', {})
+    hit = cache.get(key)
+    if hit is None or hit[0] != tag:
+        with torch.no_grad():
+            hit = (tag, fn())
+        cache[key] = hit
+    return hit[1]
+
+
 class EqualizedLinear(nn.Module):
     """y = x (W * lr/sqrt(in))^T + b * lr (stylegan.py:148-180)."""
 
@@ -72,8 +91,10 @@ class EqualizedLinear(nn.Module):
         self.activate = activate
 
     def forward(self, x):
-        y = F.linear(x, self.weight * self.weight_gain,
-                     None if self.bias is None else self.bias * self.bias_gain)
+        w, b = frozen_value(self, 'scaled', lambda: (
+            self.weight * self.weight_gain, None if self.bias is None else self.bias * self.bias_gain),
+            self.weight, self.bias)
+        y = F.linear(x, w, b)
         if self.activate:
             y = F.leaky_relu(y * SQRT2, 0.2)
         return y
@@ -117,7 +138,7 @@ class ModulatedConv(nn.Module):
     def _forward_hip(self, x, w):
         ops = _hip()
         styles = self.affine(w)
-        w2 = self.weight.square().sum(dim=(2, 3))                         # [out, in]
+        w2 = frozen_value(self, 'w2', lambda: self.weight.square().sum(dim=(2, 3)), self.weight)  # [out, in]
         dcoefs = (styles.square() @ w2.t() + 1e-8).rsqrt()                # [b, out]
         xs = ops.scale(x, styles)
         if self.up:

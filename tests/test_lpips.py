@@ -6,6 +6,7 @@ loads, the metric's identities (d(x, x) = 0, symmetry, non-negativity), and the 
 against a direct per-pixel evaluation.  The HIP head is checked against the torch backend in
 tests/test_gpu_lpips.py."""
 
+import pytest
 import torch
 
 from nfi import lpips
@@ -50,3 +51,26 @@ def test_distance_head_per_pixel():
                 na, nb = a / (a.norm() + 1e-10), b / (b.norm() + 1e-10)
                 want[n] += (w * (na - nb) ** 2).sum() / 12
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize('white', [False, True])
+def test_vgg_loss_matches_reference_augmentation_order(white):
+    """image_loss('vgg') samples the prediction and target copies separately with one grid; the
+    reference (run.py:2214-2235) augments cat((pred, target), channels) — same loss, and the same
+    gradient to the prediction."""
+    from nfi import inversion
+    torch.manual_seed(3)
+    net = lpips.LPIPS(backend='torch')
+    rgb = torch.tanh(torch.randn(2, 32, 32, 3)).requires_grad_()
+    target = torch.tanh(torch.randn(2, 32, 32, 3))
+    got = inversion.image_loss('vgg', rgb, target, net, white, torch.Generator().manual_seed(5))
+    got.backward()
+    g_got = rgb.grad.clone()
+    rgb.grad = None
+    pred, tgt = rgb.permute(0, 3, 1, 2), target.permute(0, 3, 1, 2)
+    cat = torch.cat((pred, tgt), dim=1).unsqueeze(1).expand(-1, 15, -1, -1, -1).contiguous().flatten(0, 1)
+    cat = inversion.augment_images(cat, 1.0, white, generator=torch.Generator().manual_seed(5))
+    want = net(torch.cat((pred, cat[:, :3])), torch.cat((tgt, cat[:, 3:]))).mean() * 2
+    want.backward()
+    assert torch.equal(got.detach(), want.detach())
+    torch.testing.assert_close(g_got, rgb.grad, rtol=1e-6, atol=1e-9)
