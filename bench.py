@@ -290,6 +290,10 @@ def main():
         'bwd_field': (380, 5700),
         'bwd_tiles': (TAP_BYTES * (2 if pose else 1) + 48 + 3 * 128, 768 * (2 if pose else 1)),
     }
+    plane_bytes = 3 * 32 * 256 * 256 * 4 / (H * H * 2 * S)       # per sample, one pass over the planes
+    compulsory = {'render_fwd': plane_bytes, 'bwd_bins': 0.0, 'bwd_field': 0.0,
+                  'bwd_tiles': plane_bytes * (2 if pose else 1)}
+    compulsory = {k: round(v, 3) for k, v in compulsory.items()}
     kernel_of = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
                  'bwd_tiles': 'tile_kernel', 'bwd_bins': 'scan_blocks_kernel'}
     dom = max(kern, key=kern.get)
@@ -313,6 +317,11 @@ def main():
                                                 'profiles/latest_counters.json)',
             'bytes_per_sample': model[dom][0],
             'hbm_frac_measured': (round(traffic / sec / HBM_PEAK_GBS, 4) if traffic else None),
+            # SURVEY §8(d)'s compulsory bytes: the planes once per image and pass (25.17 MB = 12 B per
+            # sample at 128^2 x 128) — read by render_fwd; the tile pass writes d planes (and, with
+            # pose gradients, reads each tile's texels): 12 or 24 B per sample
+            'compulsory_bytes_per_sample': compulsory[dom],
+            'compulsory_frac': round(samples_per_step * compulsory[dom] / sec / 1e9 / HBM_PEAK_GBS, 4),
             'fp32_TFLOPs': stages[dom]['fp32_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
             'stages': stages}
 
