@@ -220,16 +220,20 @@ class Field:
     planes [b,3,32,R,R] (synthesis output viewed at generator.py:476-477), the
     TriplanarDecoder's two EqualizedLinear layers (raw parameters, generator.py:295-299),
     the per-image attention palette [b,10,3] (AttentionMapper output, generator.py:455-462),
-    and the SDF parameters alpha, beta (generator.py:397-399)."""
+    and the SDF parameters alpha, beta (generator.py:397-399).  attention_values = 0 (no
+    palette; decoder [4, 64]: distance + 3 colour features, generator.py:377-384) and
+    use_sdf = False (no alpha / beta) are the reference's other field variants."""
     planes: torch.Tensor
     w1: torch.Tensor       # [64, 32]
     b1: torch.Tensor       # [64]
-    w2: torch.Tensor       # [11, 64]
+    w2: torch.Tensor       # [11, 64] ([4, 64] without attention)
     b2: torch.Tensor       # [11]
-    palette: torch.Tensor  # [b, 10, 3]
-    alpha: torch.Tensor    # [1]
-    beta: torch.Tensor     # [1]
+    palette: Optional[torch.Tensor]  # [b, 10, 3] (None without attention)
+    alpha: Optional[torch.Tensor]    # [1] (None without SDF)
+    beta: Optional[torch.Tensor]     # [1]
     scene_range: float
+    attention_values: int = 10
+    use_sdf: bool = True
 
 
 def triplanar_decoder(planes, coords, w1, b1, w2, b2):
@@ -247,8 +251,9 @@ def triplanar_decoder(planes, coords, w1, b1, w2, b2):
 
 
 def sampler(field: Field, x_in, extras=()):
-    """The `sampler` closure generator.py:587-681 with use_sdf=True, attention_values=10,
-    use_viewdir=False (the inversion configuration).  Returns (sigma, rgb), or with `extras` ⊂
+    """The `sampler` closure generator.py:587-681 with use_viewdir=False; use_sdf=True,
+    attention_values=10 is the inversion configuration (the other density / colour heads follow
+    field.use_sdf / field.attention_values).  Returns (sigma, rgb), or with `extras` ⊂
     {'normals','semantics','coords'} (sigma, rgb, dict): normals = normalize(d distance / d x_in)
     by autograd (create_graph=False; sigma and rgb are then detached, :599-622), semantics = the
     softmax probabilities (:672-674), coords = x_in (:643-644)."""
@@ -271,15 +276,22 @@ def sampler(field: Field, x_in, extras=()):
         x_in = x_in.detach()
     if 'coords' in extras:
         out['coords'] = x_in
-    beta = field.beta
-    alpha = 1 / field.alpha
-    neg_distance = -density_or_distance[..., -1]
-    density_prealpha = laplace_cdf(neg_distance, beta) * (1 - mask)
-    sigma = alpha * density_prealpha
-    attention_probs = F.softmax(features, dim=-1)
-    if 'semantics' in extras:
-        out['semantics'] = attention_probs
-    rgb = torch.matmul(attention_probs, field.palette)
+    if field.use_sdf:                                        # generator.py:628-636
+        beta = field.beta
+        alpha = 1 / field.alpha
+        neg_distance = -density_or_distance[..., -1]
+        density_prealpha = laplace_cdf(neg_distance, beta) * (1 - mask)
+        sigma = alpha * density_prealpha
+    else:                                                    # standard NeRF density, :637-641
+        density_pre = density_or_distance[..., -1] - 1
+        sigma = F.softplus(density_pre) * (1 - mask)
+    if field.attention_values == 0:                          # :665-666
+        rgb = wide_sigmoid_rescaled(features)
+    else:
+        attention_probs = F.softmax(features, dim=-1)
+        if 'semantics' in extras:
+            out['semantics'] = attention_probs
+        rgb = torch.matmul(attention_probs, field.palette)
     if extras:
         return sigma, rgb, out
     return sigma, rgb

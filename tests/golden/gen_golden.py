@@ -84,15 +84,17 @@ def make_cameras(b, scene_range, flipped, seed, ortho=False):
 
 
 def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, randomize,
-                force_no_cam_grad=False, ortho=False, with_bbox=False, with_center=False):
+                force_no_cam_grad=False, ortho=False, with_bbox=False, with_center=False,
+                attention_values=10, use_sdf=True):
     torch.manual_seed(1000 + seed)
-    gen = generator.Generator(512, scene_range, attention_values=10, use_sdf=True,
+    gen = generator.Generator(512, scene_range, attention_values=attention_values, use_sdf=use_sdf,
                               disable_stylegan_noise=True)
     gen.eval()
     with torch.no_grad():
-        gen.decoder.net[2].bias[0] -= 0.97     # mask mean ~0.6 instead of ~5e-4
-        gen.beta.fill_(0.1)
-        gen.alpha.fill_(1.0)
+        if use_sdf:
+            gen.decoder.net[2].bias[0] -= 0.97     # mask mean ~0.6 instead of ~5e-4
+            gen.beta.fill_(0.1)
+            gen.alpha.fill_(1.0)
     planes = (1.87 * torch.randn(b, 3, 32, R, R)).requires_grad_()
     gen.synthesis_network = PlanesLeaf(planes)
     palette = generator.wide_sigmoid_rescaled(torch.randn(b, 10, 3)).detach().requires_grad_()
@@ -108,8 +110,8 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     if with_center:
         center = 0.5 + 0.05 * torch.randn(b, 2)
     ws = torch.zeros(b, 15, 512)
-    args_ns = types.SimpleNamespace(use_viewdir=False, fine_sampling=True, use_sdf=True,
-                                    attention_values=10)
+    args_ns = types.SimpleNamespace(use_viewdir=False, fine_sampling=True, use_sdf=use_sdf,
+                                    attention_values=attention_values)
     dataset_config = {'scene_range': scene_range, 'white_background': white_bg}
     render = extract_render(args_ns, dataset_config)
 
@@ -117,7 +119,8 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     torch.manual_seed(rseed)
     rgb, depth, mask, _, _, _ = render(gen, H, W, cam, focal, center, bbox, ws, S,
                                        randomize=randomize,
-                                       extra_model_inputs={'attention_values': palette},
+                                       extra_model_inputs=({'attention_values': palette}
+                                                           if attention_values else {}),
                                        force_no_cam_grad=force_no_cam_grad)
     torch.manual_seed(rseed)
     if randomize:
@@ -134,13 +137,16 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     out = {
         'planes': planes.detach(), 'w1': gen.decoder.net[0].weight.detach(),
         'b1': gen.decoder.net[0].bias.detach(), 'w2': gen.decoder.net[2].weight.detach(),
-        'b2': gen.decoder.net[2].bias.detach(), 'palette': palette.detach(),
-        'alpha': gen.alpha.detach(), 'beta': gen.beta.detach(),
+        'b2': gen.decoder.net[2].bias.detach(),
         'cam': cam.detach(), 'u_coarse': u_coarse, 'u_fine': u_fine,
         'g_rgb': g_rgb, 'g_mask': g_mask,
         'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach(),
-        'd_planes': planes.grad, 'd_palette': palette.grad,
+        'd_planes': planes.grad,
     }
+    if attention_values:
+        out['palette'], out['d_palette'] = palette.detach(), palette.grad
+    if use_sdf:
+        out['alpha'], out['beta'] = gen.alpha.detach(), gen.beta.detach()
     if focal is not None:
         out['focal'] = focal.detach()
     if bbox is not None:
@@ -153,7 +159,7 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
             out['d_focal'] = focal.grad
     meta = dict(H=H, W=W, S=S, R=R, scene_range=scene_range, white_bg=int(white_bg),
                 randomize=int(randomize), force_no_cam_grad=int(force_no_cam_grad),
-                ortho=int(ortho))
+                ortho=int(ortho), attention_values=attention_values, use_sdf=int(use_sdf))
     np.savez_compressed(os.path.join(OUT, f'render_{name}.npz'),
                         **{k: v.numpy() for k, v in out.items()},
                         **{f'meta_{k}': np.array(v) for k, v in meta.items()})
@@ -409,6 +415,18 @@ def inversion_case(seed=41, b=2, H=16, S=8, steps=3, scene_range=1.4, flipped=Tr
     print('inversion losses', losses, 'mask', masks)
 
 
+def field_variant_cases():
+    """The reference's other field heads (generator.py:637-641, 665-666): colour by
+    wide_sigmoid_rescaled of 3 decoder features (--attention_values 0), standard NeRF density
+    softplus(d - 1) (use_sdf False), and both."""
+    render_case('rgbhead', 7, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=False,
+                flipped=True, randomize=True, attention_values=0)
+    render_case('nerfdensity', 8, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=True,
+                flipped=True, randomize=True, use_sdf=False)
+    render_case('nerf_rgbhead', 9, b=1, H=8, W=8, S=8, R=12, scene_range=0.55, white_bg=False,
+                flipped=False, randomize=False, attention_values=0, use_sdf=False)
+
+
 SDF_SHIFT = 0.0
 
 
@@ -436,6 +454,7 @@ if __name__ == '__main__':
     # perspective with bbox + center (nerf_utils.py:43-56; eval_*_persp.py callers)
     render_case('persp_center_bbox', 3, b=2, H=8, W=12, S=8, R=8, scene_range=1.4,
                 white_bg=False, flipped=True, randomize=True, with_bbox=True, with_center=True)
+    field_variant_cases()
     # eval outputs: normals + semantics; white background; coords
     extras_case('extras_ns', 4, b=2, H=8, W=8, S=16, R=16, scene_range=1.4, white_bg=False,
                 flipped=True, compute_normals=True, compute_semantics=True, compute_coords=False)

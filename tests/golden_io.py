@@ -7,6 +7,7 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox']
+VARIANT_CASES = ['rgbhead', 'nerfdensity', 'nerf_rgbhead']   # attention_values 0 / use_sdf False
 EXTRAS_CASES = ['extras_ns', 'extras_nw', 'extras_coords']   # eval outputs, no gradients
 
 
@@ -27,8 +28,10 @@ def load(name):
 def field_from(d, meta):
     from oracle.render_oracle import Field
     return Field(planes=d['planes'], w1=d['w1'], b1=d['b1'], w2=d['w2'], b2=d['b2'],
-                 palette=d['palette'], alpha=d['alpha'], beta=d['beta'],
-                 scene_range=float(meta['scene_range']))
+                 palette=d.get('palette'), alpha=d.get('alpha'), beta=d.get('beta'),
+                 scene_range=float(meta['scene_range']),
+                 attention_values=int(meta.get('attention_values', 10)),
+                 use_sdf=bool(meta.get('use_sdf', 1)))
 
 
 PRODUCER_SKIP = ('resample_filter', 'noise_const')

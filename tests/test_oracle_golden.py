@@ -8,14 +8,15 @@ rounding of identical op graphs (in practice bit-exact).
 import pytest
 import torch
 
-from golden_io import EXTRAS_CASES, RENDER_CASES, field_from, load
+from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, field_from, load
 from oracle import render_oracle as orc
 
 
 def _run_oracle(d, meta):
     field = field_from(d, meta)
     field.planes = field.planes.clone().requires_grad_()
-    field.palette = field.palette.clone().requires_grad_()
+    if field.palette is not None:
+        field.palette = field.palette.clone().requires_grad_()
     ncg = bool(meta['force_no_cam_grad'])
     cam = d['cam'].clone().requires_grad_(not ncg)
     focal = d.get('focal')
@@ -31,7 +32,7 @@ def _run_oracle(d, meta):
     return rgb, depth, mask, field, cam, focal
 
 
-@pytest.mark.parametrize('case', RENDER_CASES)
+@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES)
 def test_oracle_render_matches_reference(case):
     d, meta = load(f'render_{case}')
     rgb, depth, mask, field, cam, focal = _run_oracle(d, meta)
@@ -40,7 +41,8 @@ def test_oracle_render_matches_reference(case):
     torch.testing.assert_close(depth.detach(), d['depth'], **tol)
     torch.testing.assert_close(mask.detach(), d['mask'], **tol)
     torch.testing.assert_close(field.planes.grad, d['d_planes'], **tol)
-    torch.testing.assert_close(field.palette.grad, d['d_palette'], **tol)
+    if 'd_palette' in d:
+        torch.testing.assert_close(field.palette.grad, d['d_palette'], **tol)
     if 'd_cam' in d:
         torch.testing.assert_close(cam.grad, d['d_cam'], rtol=1e-5, atol=1e-5)
     if 'd_focal' in d:
