@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 9
+#define NFI_ABI_VERSION 10
 #define NFI_DEC_SIZE 7184 /* floats in the packed decoder buffer */
 
 enum {
@@ -58,7 +58,16 @@ typedef struct nfi_camera {
  *   planes[b*sb + q*sq + (y*R + x)*st + c]   (c contiguous; 32 channels; q = xy, xz, yz).
  * dec: packed, gain-scaled decoder from nfi_decoder_pack().
  * palette: attention values [B,10,3] (AttentionMapper output, generator.py:455-462).
- * inv_alpha = 1/Generator.alpha, beta = Generator.beta (generator.py:397-399, 629-636). */
+ * inv_alpha = 1/Generator.alpha, beta = Generator.beta (generator.py:397-399, 629-636).
+ * heads: the reference's field variants (sampler closure, generator.py:628-679), 0 = the
+ *   inversion field (SDF density, attention colour) or an OR of
+ *   NFI_HEAD_RGB_SIGMOID   --attention_values 0: rgb = wide_sigmoid_rescaled(features[0..2])
+ *                          (:665-666, :36-39); decoder [4,64] zero-padded to [11,64]; palette
+ *                          unused (may be NULL); no semantics
+ *   NFI_HEAD_NERF_DENSITY  use_sdf False: sigma = softplus(d - 1) * (1 - mask) (:637-641);
+ *                          inv_alpha / beta unused; no normals */
+#define NFI_HEAD_RGB_SIGMOID 1
+#define NFI_HEAD_NERF_DENSITY 2
 typedef struct nfi_field {
   const float* planes;
   int64_t sb, sq, st;
@@ -67,7 +76,7 @@ typedef struct nfi_field {
   const float* dec;
   const float* palette;
   float inv_alpha, beta, scene_range;
-  int32_t _pad2;
+  int32_t heads;
 } nfi_field;
 
 /* One render call: rays of B images × HW pixels, S coarse samples (+ S fine if fine). */
@@ -130,7 +139,8 @@ int32_t nfi_abi_version(void);
 const char* nfi_last_error(void);
 
 /* EqualizedLinear parameters (stylegan.py:173-176) -> packed, gain-scaled decoder:
- * W1s = w1*g1 [64,32], b1s = b1*gb, W2s = w2*g2 [11,64], b2s = b2*gb. */
+ * W1s = w1*g1 [64,32], b1s = b1*gb, W2s = w2*g2 [11,64], b2s = b2*gb (a [4,64] decoder of
+ * NFI_HEAD_RGB_SIGMOID is passed zero-padded to 11 rows). */
 int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, const float* b2,
                          float g1, float g2, float gb, float* dec, void* stream);
 

@@ -406,18 +406,40 @@ __device__ __forceinline__ void mlp_backward_mfma(const float* __restrict__ dec,
 
 // Head: sigma = (1/alpha) * laplace_cdf(-d, beta) * (1 - mask)  (generator.py:629-636, 30-33)
 //       rgb   = softmax(features) @ palette                    (generator.py:668-679)
+// and the reference's other heads (nfi_field.heads, wave-uniform):
+//   NFI_HEAD_NERF_DENSITY  sigma = softplus(d - 1) * (1 - mask)       (generator.py:637-641)
+//   NFI_HEAD_RGB_SIGMOID   rgb = sigmoid(features[0..2]) * 2.004 - 1.002 (:665-666, :36-39);
+//                          p[0..2] keeps the sigmoids for the backward
 struct Head {
   float sigma;
   float rgb[3];
   float p[NA];
 };
 
+// F.softplus (beta 1, threshold 20) as ATen's CPU kernel forms it
+__device__ __forceinline__ float softplus_ref(float z) { return z > 20.f ? z : log1pf(expf(z)); }
+
 __device__ __forceinline__ void head_forward(const float y[NO], float mask, float inv_alpha, float beta,
-                                             const float* __restrict__ pal, Head& h) {
-  const float xn = -y[0];
-  const float ex = expf(-fabsf(xn) / beta);
-  const float cdf = 0.5f + 0.5f * tsign(xn) * (1.f - ex);
-  h.sigma = inv_alpha * (cdf * (1.f - mask));
+                                             const float* __restrict__ pal, int heads, Head& h) {
+  if (heads & NFI_HEAD_NERF_DENSITY) {
+    h.sigma = fmul(softplus_ref(fsub(y[0], 1.f)), fsub(1.f, mask));
+  } else {
+    const float xn = -y[0];
+    const float ex = expf(-fabsf(xn) / beta);
+    const float cdf = 0.5f + 0.5f * tsign(xn) * (1.f - ex);
+    h.sigma = inv_alpha * (cdf * (1.f - mask));
+  }
+  if (heads & NFI_HEAD_RGB_SIGMOID) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) h.p[k] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float sg = 1.f / (1.f + expf(-y[1 + c]));
+      h.p[c] = sg;
+      h.rgb[c] = fsub(fmul(sg, 2.004f), 1.002f);
+    }
+    return;
+  }
   float m = y[1];
 #pragma unroll
   for (int k = 2; k <= NA; ++k) m = fmaxf(m, y[k]);
@@ -564,7 +586,7 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
     for (int k = 0; k < NO; ++k) ys[k * N] = y[k];
   }
   Head h;
-  head_forward(y, P.mask, a.field.inv_alpha, a.field.beta, a.field.palette + R.b * (NA * 3), h);
+  head_forward(y, P.mask, a.field.inv_alpha, a.field.beta, a.field.palette + R.b * (NA * 3), a.field.heads, h);
   sigma = h.sigma;
   rgb[0] = h.rgb[0];
   rgb[1] = h.rgb[1];
@@ -1015,6 +1037,9 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 #ifndef NFI_FIELD_OCC
 #define NFI_FIELD_OCC 4
 #endif
+// VARIANT = false: the inversion field (heads == 0 at compile time, the register budget of the
+// hot path is not shared with the other heads); true: nfi_field.heads read at run time.
+template <bool VARIANT>
 __global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
@@ -1077,37 +1102,55 @@ __global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_rende
   float gy[NO];
   {
     Head h;
-    head_forward(y, pmask, a.field.inv_alpha, a.field.beta, pal, h);
-    // sigma -> distance  (generator.py:629-636, laplace_cdf generator.py:30-33)
+    const int heads = VARIANT ? a.field.heads : 0;
+    head_forward(y, pmask, a.field.inv_alpha, a.field.beta, pal, heads, h);
     const float gs = v ? g.gsig[r * N + i] : 0.f;
-    const float xn = -y[0];
-    const float sgn = tsign(xn);
-    const float ex2 = expf(-fabsf(xn) / a.field.beta);
-    const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
-    gy[0] = -(((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn);
-    // rgb -> logits (softmax backward) and palette gradient  (generator.py:668-679)
+    if (heads & NFI_HEAD_NERF_DENSITY) {
+      // sigma -> d: softplus_backward of d - 1 (ATen: z > 20 ? g : g * e^z / (e^z + 1)), :637-641
+      const float z = fsub(y[0], 1.f);
+      const float gm = fmul(gs, fsub(1.f, pmask));
+      const float ez = expf(z);
+      gy[0] = z > 20.f ? gm : gm * (ez / (ez + 1.f));
+    } else {
+      // sigma -> distance  (generator.py:629-636, laplace_cdf generator.py:30-33)
+      const float xn = -y[0];
+      const float sgn = tsign(xn);
+      const float ex2 = expf(-fabsf(xn) / a.field.beta);
+      const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
+      gy[0] = -(((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn);
+    }
     const float w = v ? g.wts[r * N + i] : 0.f;
     const float gc0 = w * gr0, gc1 = w * gr1, gc2 = w * gr2;
-    float gp[NA], dot = 0.f;
+    if (heads & NFI_HEAD_RGB_SIGMOID) {
+      // rgb -> features: (g * 2.004) * (1 - s) * s  (sigmoid backward), no palette
+      const float gc[3] = {gc0, gc1, gc2};
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      gp[k] = gc0 * pal[k * 3 + 0] + gc1 * pal[k * 3 + 1] + gc2 * pal[k * 3 + 2];
-      dot = fmaf(gp[k], h.p[k], dot);
-    }
+      for (int k = 0; k < NA; ++k) gy[1 + k] = 0.f;
 #pragma unroll
-    for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
-    // per-point palette contributions p_k * gc, column-summed through the LDS tile
-    wave_lds_sync();
-    float* row = X + l * XS;
+      for (int c = 0; c < 3; ++c) gy[1 + c] = fmul(fmul(gc[c], 2.004f), fsub(1.f, h.p[c])) * h.p[c];
+    } else {
+      // rgb -> logits (softmax backward) and palette gradient  (generator.py:668-679)
+      float gp[NA], dot = 0.f;
 #pragma unroll
-    for (int k = 0; k < NA; ++k) {
-      row[k * 3 + 0] = h.p[k] * gc0;
-      row[k * 3 + 1] = h.p[k] * gc1;
-      row[k * 3 + 2] = h.p[k] * gc2;
+      for (int k = 0; k < NA; ++k) {
+        gp[k] = gc0 * pal[k * 3 + 0] + gc1 * pal[k * 3 + 1] + gc2 * pal[k * 3 + 2];
+        dot = fmaf(gp[k], h.p[k], dot);
+      }
+#pragma unroll
+      for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
+      // per-point palette contributions p_k * gc, column-summed through the LDS tile
+      wave_lds_sync();
+      float* row = X + l * XS;
+#pragma unroll
+      for (int k = 0; k < NA; ++k) {
+        row[k * 3 + 0] = h.p[k] * gc0;
+        row[k * 3 + 1] = h.p[k] * gc1;
+        row[k * 3 + 2] = h.p[k] * gc2;
+      }
     }
   }
   wave_lds_sync();
-  {
+  if (!VARIANT || !(a.field.heads & NFI_HEAD_RGB_SIGMOID)) {
     // column sums over the 64 rows (rows of lanes >= npts are zero): lanes (half, column) sum 32
     // rows each with all reads in flight, then the halves are added
     const int col = l & 31, r0 = (l >> 5) * 32;
@@ -1913,7 +1956,10 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
     else if (NPL <= 2) composite_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
     else composite_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("composite_bwd_kernel");
-    field_bwd_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+    if (a->field.heads)
+      field_bwd_kernel<true><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+    else
+      field_bwd_kernel<false><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
 #if defined(NFI_ABLATE) && NFI_ABLATE == 5
@@ -1966,11 +2012,14 @@ static bool supported_S(const nfi_render_args* a) {
 static int validate(const nfi_render_args* a) {
   NFI_REQUIRE(a != nullptr, "render: null args");
   const nfi_field& f = a->field;
-  NFI_REQUIRE(f.planes && f.dec && f.palette, "render: null field pointer");
+  NFI_REQUIRE((f.heads & ~(NFI_HEAD_RGB_SIGMOID | NFI_HEAD_NERF_DENSITY)) == 0, "render: unknown heads bits 0x%x",
+              f.heads);
+  NFI_REQUIRE(f.planes && f.dec && (f.palette || (f.heads & NFI_HEAD_RGB_SIGMOID)), "render: null field pointer");
   NFI_REQUIRE(f.R >= 2 && f.R <= 1024, "render: plane resolution R=%d out of range [2,1024]", f.R);
   NFI_REQUIRE(f.st >= NC && 3LL * f.sq < (1LL << 31) && (long long)f.R * f.R * f.st < (1LL << 31),
               "render: plane strides out of range (st=%lld sq=%lld)", (long long)f.st, (long long)f.sq);
-  NFI_REQUIRE(f.beta > 0.f && std::isfinite(f.inv_alpha) && f.scene_range > 0.f, "render: bad field scalars");
+  NFI_REQUIRE(((f.heads & NFI_HEAD_NERF_DENSITY) || (f.beta > 0.f && std::isfinite(f.inv_alpha))) &&
+                  f.scene_range > 0.f, "render: bad field scalars");
   NFI_REQUIRE(a->ro && a->rd && a->near_ && a->far_, "render: null ray pointer");
   NFI_REQUIRE(a->B > 0 && a->HW > 0, "render: bad shape B=%d HW=%d", a->B, a->HW);
   NFI_REQUIRE(a->t_saved && a->sigma_saved && a->rgb_saved && a->y_saved && a->perm,
@@ -1992,6 +2041,10 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
   NFI_REQUIRE(!(a->extras & 1) || (a->normal_map && a->x_saved),
               "render_forward: normals need normal_map and x_saved");
   NFI_REQUIRE(!(a->extras & 6) || a->semantic_map, "render_forward: semantics/coords need semantic_map");
+  NFI_REQUIRE(!(a->extras & 1) || !(a->field.heads & NFI_HEAD_NERF_DENSITY),
+              "render_forward: normals need the SDF field (run.py:229)");
+  NFI_REQUIRE((a->extras & 6) != 2 || !(a->field.heads & NFI_HEAD_RGB_SIGMOID),
+              "render_forward: semantics need attention values (run.py:232)");
   return nfi::dispatch_fwd(a, (hipStream_t)stream);
 }
 
@@ -2009,7 +2062,8 @@ int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream) {
   int e = nfi::validate(a);
   if (e) return e;
-  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
+  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->workspace &&
+                  (g->d_palette_ray || (a->field.heads & NFI_HEAD_RGB_SIGMOID)),
               "render_backward: null grad pointer");
   NFI_REQUIRE(a->x_saved, "render_backward: x_saved (decoder inputs saved by the forward) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
@@ -2020,7 +2074,8 @@ int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_gra
                                   void* stream) {
   int e = nfi::validate(a);
   if (e) return e;
-  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->d_palette_ray && g->workspace,
+  NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->workspace &&
+                  (g->d_palette_ray || (a->field.heads & NFI_HEAD_RGB_SIGMOID)),
               "render_backward: null grad pointer");
   NFI_REQUIRE(a->x_saved, "render_backward: x_saved (decoder inputs saved by the forward) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 9
+ABI_VERSION = 10
 DEC_SIZE = 7184
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -30,7 +30,7 @@ class NfiField(ctypes.Structure):
                 ('st', ctypes.c_int64), ('R', ctypes.c_int32), ('_pad', ctypes.c_int32),
                 ('dec', c_void_p), ('palette', c_void_p), ('inv_alpha', ctypes.c_float),
                 ('beta', ctypes.c_float), ('scene_range', ctypes.c_float),
-                ('_pad2', ctypes.c_int32)]
+                ('heads', ctypes.c_int32)]
 
 
 class NfiRenderArgs(ctypes.Structure):

@@ -184,11 +184,22 @@ class RenderOptions:
     inv_alpha: float = 1.0       # 1 / Generator.alpha
     beta: float = 0.1            # Generator.beta
     extras: int = 0              # eval outputs: 1 normals, 2 semantics, 4 coords (nfi_render_args.extras)
+    heads: int = 0               # nfi_field.heads: HEAD_RGB_SIGMOID (attention_values 0) | HEAD_NERF_DENSITY (no SDF)
+
+
+HEAD_RGB_SIGMOID = 1             # include/nfi.h NFI_HEAD_RGB_SIGMOID
+DEBUG_BACKWARD = None            # a dict: the next backward stores its workspace there (diagnostics)
+HEAD_NERF_DENSITY = 2            # include/nfi.h NFI_HEAD_NERF_DENSITY
 
 
 def pack_decoder(w1, b1, w2, b2, lr_multiplier: float = 1.0) -> torch.Tensor:
-    """EqualizedLinear gains (stylegan.py:173-176) folded into the packed decoder buffer."""
+    """EqualizedLinear gains (stylegan.py:173-176) folded into the packed decoder buffer.  A
+    [4, 64] output layer (attention_values 0: distance + 3 colour features) is zero-padded to the
+    kernels' 11 rows."""
     _require_device(w1, b1, w2, b2)
+    if w2.shape[0] < 11:
+        w2 = torch.cat([w2.detach(), w2.new_zeros(11 - w2.shape[0], w2.shape[1])])
+        b2 = torch.cat([b2.detach(), b2.new_zeros(11 - b2.shape[0])])
     lib = _lib.load()
     dec = torch.empty((_lib.DEC_SIZE,), device=w1.device)
     g1 = float(torch.tensor(lr_multiplier / math.sqrt(w1.shape[1]), dtype=torch.float32))
@@ -213,7 +224,7 @@ class _VolumeRender(torch.autograd.Function):
         N = 2 * S if opts.fine else S
         ro_c, rd_c = ro.contiguous(), rd.contiguous()
         near_c, far_c = near.contiguous(), far.contiguous()
-        pal_c = palette.contiguous()
+        pal_c = None if palette is None else palette.contiguous()
         rgb = torch.empty((n, 3), device=dev)
         depth = torch.empty((n,), device=dev)
         mask = torch.empty((n,), device=dev)
@@ -274,7 +285,7 @@ class _VolumeRender(torch.autograd.Function):
         field = _lib.NfiField(planes=_ptr(planes_tm), sb=planes_tm.stride(0), sq=planes_tm.stride(1),
                               st=planes_tm.stride(3), R=R, _pad=0, dec=_ptr(dec), palette=_ptr(pal),
                               inv_alpha=float(opts.inv_alpha), beta=float(opts.beta),
-                              scene_range=float(opts.scene_range), _pad2=0)
+                              scene_range=float(opts.scene_range), heads=int(opts.heads))
         return _lib.NfiRenderArgs(field=field, ro=_ptr(ro), rd=_ptr(rd), near_=_ptr(near), far_=_ptr(far),
                                   B=B, HW=HW, S=opts.samples, fine=int(opts.fine),
                                   white_bg=int(opts.white_background), randomize=int(opts.randomize),
@@ -298,7 +309,7 @@ class _VolumeRender(torch.autograd.Function):
         g_mask = torch.zeros((n,), device=dev) if g_mask is None else g_mask.contiguous()
         d_planes = torch.zeros_like(planes_tm)   # preserves (texel-major) strides
         npl = ((2 * opts.samples if opts.fine else opts.samples) + 63) // 64
-        d_pal_ray = torch.empty((n * npl, 30), device=dev)
+        d_pal_ray = torch.empty((n * npl, 30), device=dev) if pal is not None else None
         need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         g_ro = torch.empty((n, 3), device=dev) if need_coords else None
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
@@ -309,6 +320,8 @@ class _VolumeRender(torch.autograd.Function):
         if nbytes < 0:
             _lib.check(-1, 'nfi_render_backward_workspace_bytes')
         ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
+        if DEBUG_BACKWARD is not None:          # diagnostics: the backward workspace (per-sample state)
+            DEBUG_BACKWARD['workspace'] = ws
         gargs = _lib.NfiRenderGradArgs(g_rgb=_ptr(g_rgb), g_mask=_ptr(g_mask), d_planes=_ptr(d_planes),
                                        d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd),
                                        tile_counts=_ptr(tile_counts), workspace=_ptr(ws), workspace_bytes=nbytes)
@@ -317,19 +330,23 @@ class _VolumeRender(torch.autograd.Function):
             with _timed(name, dev):
                 _lib.check(lib.nfi_render_backward_stage(ctypes.byref(args), ctypes.byref(gargs), stage, st),
                            'nfi_render_backward_stage')
-        d_pal = torch.empty((B, 30), device=dev)
-        ws = torch.empty((B * 64 * 30,), device=dev)
-        _lib.check(lib.nfi_segment_sum(_ptr(d_pal_ray), B, H * W * npl, 30, _ptr(d_pal), _ptr(ws), st),
-                   'nfi_segment_sum')
+        d_pal = None
+        if pal is not None:
+            d_pal = torch.empty((B, 30), device=dev)
+            ws = torch.empty((B * 64 * 30,), device=dev)
+            _lib.check(lib.nfi_segment_sum(_ptr(d_pal_ray), B, H * W * npl, 30, _ptr(d_pal), _ptr(ws), st),
+                       'nfi_segment_sum')
+            d_pal = d_pal.view(B, 10, 3)
         d_ro = g_ro.view(B, H, W, 3) if need_coords else None
         d_rd = g_rd.view(B, H, W, 3) if need_coords else None
-        return (d_planes, d_pal.view(B, 10, 3), d_ro, d_rd, None, None, None, None, None, None, None, None)
+        return (d_planes, d_pal, d_ro, d_rd, None, None, None, None, None, None, None, None)
 
 
 def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOptions,
                   u_coarse=None, u_fine=None, seed: Optional[int] = None, debug: Optional[dict] = None):
     """Fused coarse+fine render of rays (run.py:202-348).  planes_tm: texel-major
-    [B,3,R,R,32] (see planes_texel_major); palette [B,10,3]; ro, rd [B,H,W,3]; near, far
+    [B,3,R,R,32] (see planes_texel_major); palette [B,10,3] (None with opts.heads &
+    HEAD_RGB_SIGMOID); ro, rd [B,H,W,3]; near, far
     [B,H,W].  Returns rgb [B,H,W,3], depth [B,H,W] (no grad), mask [B,H,W]; with opts.extras
     also the normal map [B,H,W,3] and the semantic [B,H,W,10] / coords [B,H,W,3] map (no grad;
     None when not requested)."""
@@ -342,7 +359,9 @@ def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOption
         raise ValueError('planes_tm must be 16-byte aligned with texel/plane/batch strides '
                          'divisible by 4 (the kernels load channel quads as float4)')
     B = planes_tm.shape[0]
-    if ro.shape[0] != B or palette.shape != (B, 10, 3):
+    if (palette is None) != bool(opts.heads & HEAD_RGB_SIGMOID):
+        raise ValueError('a palette is required exactly when the colour head is the attention head')
+    if ro.shape[0] != B or (palette is not None and palette.shape != (B, 10, 3)):
         raise ValueError('batch mismatch between planes, palette and rays')
     n = ro.shape[0] * ro.shape[1] * ro.shape[2]
     for name, u in (('u_coarse', u_coarse), ('u_fine', u_fine)):

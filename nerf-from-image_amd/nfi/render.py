@@ -62,14 +62,16 @@ def get_config() -> RenderConfig:
 class TriplaneField:
     """The inputs the renderer reads from a Generator (generator.py:392-503)."""
     planes: torch.Tensor                 # [B,3,32,R,R] (contiguous or channels_last producer output)
-    palette: torch.Tensor                # [B,10,3] attention values
+    palette: Optional[torch.Tensor]      # [B,10,3] attention values (None: attention_values 0)
     w1: torch.Tensor                     # decoder.net[0].weight [64,32]
     b1: torch.Tensor                     # decoder.net[0].bias   [64]
-    w2: torch.Tensor                     # decoder.net[2].weight [11,64]
+    w2: torch.Tensor                     # decoder.net[2].weight [11,64] ([4,64] without attention)
     b2: torch.Tensor                     # decoder.net[2].bias   [11]
     alpha: float = 1.0                   # Generator.alpha (sigma = laplace_cdf / alpha)
     beta: float = 0.1                    # Generator.beta
     model_outputs: dict = dc_field(default_factory=dict)
+    attention_values: int = 10           # Generator.attention_values (0: wide-sigmoid colour head)
+    use_sdf: bool = True                 # Generator.use_sdf (False: softplus(d - 1) density)
 
 
 def _as_float(x) -> float:
@@ -98,43 +100,47 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
                          extra_model_inputs: Optional[dict] = None) -> TriplaneField:
     """Runs the parts of Generator.forward (generator.py:423-503) that produce the path's
     inputs — ws, AttentionMapper palette, synthesis tri-planes — on the reference's own
-    modules, for the inversion configuration (attention_values=10, use_sdf, no viewdir,
-    no encoder, unconditional)."""
+    modules: unconditional, no encoder, no viewdir; attention_values 10 (the inversion
+    configuration) or 0, use_sdf or not."""
     extra_model_inputs = extra_model_inputs or {}
     for k in extra_model_inputs:
         if k not in ('freeze_noise', 'attention_values', 'attention_values_bias'):
             raise AssertionError(k)
     if getattr(gen, 'use_encoder', False) or getattr(gen, 'num_classes', None):
         raise NotImplementedError('encoder-/class-conditioned generators are outside the inversion path')
-    if getattr(gen, 'attention_values', 0) != 10 or not getattr(gen, 'use_sdf', False) \
-            or getattr(gen, 'use_viewdir', False):
-        raise NotImplementedError('nfi renders the SDF + 10-value attention field of the inversion path')
+    nattn = int(getattr(gen, 'attention_values', 0))
+    use_sdf = bool(getattr(gen, 'use_sdf', False))
+    if nattn not in (0, 10) or getattr(gen, 'use_viewdir', False):
+        raise NotImplementedError('nfi renders fields with 10 or 0 attention values and no viewdir mapper')
     if c.dim() == 3:
         ws = c.expand(-1, gen.mapping_network.backbone.num_ws, -1).contiguous() if c.shape[1] == 1 else c
     else:
         ws = gen.mapping_network(c, None)
-    assert ws.shape[1] == 15
-    w_tex, w_syn = ws[:, 14], ws[:, :14]
-    if 'attention_values' in extra_model_inputs:
-        palette = extra_model_inputs['attention_values']
+    if nattn:                           # generator.py:451-462
+        assert ws.shape[1] == 15
+        w_tex, w_syn = ws[:, 14], ws[:, :14]
+        if 'attention_values' in extra_model_inputs:
+            palette = extra_model_inputs['attention_values']
+        else:
+            palette = gen.texture_mapper(w_tex)
+            if 'attention_values_bias' in extra_model_inputs:
+                palette = palette + extra_model_inputs['attention_values_bias']
     else:
-        palette = gen.texture_mapper(w_tex)
-        if 'attention_values_bias' in extra_model_inputs:
-            palette = palette + extra_model_inputs['attention_values_bias']
+        w_syn, palette = ws, None
     kw = {'noise_mode': 'const'} if extra_model_inputs.get('freeze_noise') else {}
     planes = gen.synthesis_network(w_syn, **kw)
     planes = planes.view(c.shape[0], 3, 32, planes.shape[-2], planes.shape[-1])
     outs = {}
-    if 'attention_values' in extra_model_outputs:
+    if 'attention_values' in extra_model_outputs and palette is not None:
         outs['attention_values'] = palette
     for k in extra_model_outputs:
         if k not in ('attention_values',):
             raise NotImplementedError(f'model output {k!r} (training regulariser) is outside the path')
     dec = gen.decoder.net
-    alpha, beta = _sdf_params(gen)
+    alpha, beta = _sdf_params(gen) if use_sdf else (1.0, 0.1)
     return TriplaneField(planes=planes, palette=palette, w1=dec[0].weight, b1=dec[0].bias,
                          w2=dec[2].weight, b2=dec[2].bias, alpha=alpha, beta=beta,
-                         model_outputs=outs)
+                         model_outputs=outs, attention_values=nattn, use_sdf=use_sdf)
 
 
 def _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs) -> TriplaneField:
@@ -167,12 +173,20 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
     cfg = _CONFIG
     if compute_normals and not cfg.use_sdf:
         raise ValueError('compute_normals needs an SDF field (run.py:229)')
+    if compute_semantics and cfg.attention_values <= 0:
+        raise ValueError('compute_semantics needs attention values (run.py:232)')
     # run.py:334-335: the coords map takes the semantic map's place
     extras = (1 if compute_normals else 0) | (4 if compute_coords else (2 if compute_semantics else 0))
-    if cfg.use_viewdir or not cfg.use_sdf or cfg.attention_values != 10:
-        raise NotImplementedError('only the inversion field (use_sdf, attention_values=10, no viewdir)')
+    if cfg.use_viewdir:
+        raise NotImplementedError('the view-direction mapper (--use_viewdir) is not built')
     f = _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs)
     _check_frozen(f)
+    if compute_normals and not f.use_sdf:
+        raise ValueError('compute_normals needs an SDF field (generator.py:600-601)')
+    if compute_semantics and not f.attention_values:
+        raise ValueError('compute_semantics needs attention values (generator.py:670-671)')
+    heads = ((ops.HEAD_RGB_SIGMOID if f.attention_values == 0 else 0)
+             | (0 if f.use_sdf else ops.HEAD_NERF_DENSITY))
     ro, rd, near, far = ops.rays(tform_cam2world, focal_length, center, bbox, height, width,
                                  cfg.scene_range)
     if debug is not None:
@@ -186,7 +200,7 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
     opts = ops.RenderOptions(samples=int(depth_samples_per_ray), fine=bool(cfg.fine_sampling),
                              white_background=bool(cfg.white_background), randomize=bool(randomize),
                              scene_range=float(cfg.scene_range), inv_alpha=1.0 / float(f.alpha),
-                             beta=float(f.beta), extras=extras)
+                             beta=float(f.beta), extras=extras, heads=heads)
     out = ops.volume_render(planes_tm, f.palette, ro, rd, near, far, dec, opts,
                             u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug)
     if extras:

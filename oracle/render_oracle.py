@@ -306,7 +306,8 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
            fine_sampling: bool = True, force_no_cam_grad: bool = False,
            u_coarse: Optional[torch.Tensor] = None, u_fine: Optional[torch.Tensor] = None,
            return_intermediates: bool = False, compute_normals: bool = False,
-           compute_semantics: bool = False, compute_coords: bool = False):
+           compute_semantics: bool = False, compute_coords: bool = False,
+           z_fine: Optional[torch.Tensor] = None):
     """run.py:176-350 with use_viewdir=False.  Returns (rgb [b,H,W,3], depth [b,H,W],
     mask [b,H,W]) (+ intermediates dict); with any compute_* flag (run.py:227-257, 293-335)
     (rgb, depth, mask, normal_map [b,H,W,3] | None, semantic_map [b,H,W,10 | 3] | None) — the
@@ -346,6 +347,8 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
             z_vals_mid = .5 * (z_vals[..., 1:] + z_vals[..., :-1])
             z_samples = sample_pdf(z_vals_mid.flatten(0, 2), weights[..., 1:-1], depth_samples_per_ray,
                                    deterministic=not randomize, u=u_fine)
+            if z_fine is not None:      # (tests: evaluate at given fine depths [b*H*W, S] instead)
+                z_samples = z_fine.to(z_samples.dtype).reshape(z_samples.shape)
             z_samples = z_samples.view(*z_vals.shape[:3], z_samples.shape[-1])
         z_values_sorted, z_indices_sorted = torch.sort(torch.cat((z_vals, z_samples), dim=-1), dim=-1)
         query_points_fine = ray_origins[..., None, :] + ray_directions[..., None, :] * z_samples[..., :, None]

@@ -21,7 +21,9 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
                   fine_sampling=bool(meta.get('fine', 1)))
     ncg = bool(meta.get('force_no_cam_grad', 0))
     planes = inp['planes'].to(dev).requires_grad_(with_grad)
-    palette = inp['palette'].to(dev).requires_grad_(with_grad)
+    nattn = int(meta.get('attention_values', 10))
+    use_sdf = bool(meta.get('use_sdf', 1))
+    palette = inp['palette'].to(dev).requires_grad_(with_grad) if nattn else None
     cam = inp['cam'].to(dev).requires_grad_(with_grad and not ncg)
     focal = inp.get('focal')
     if focal is not None:
@@ -29,8 +31,10 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
     center = inp.get('center')
     bbox = inp.get('bbox')
     f = nfi.TriplaneField(planes=planes, palette=palette, w1=inp['w1'].to(dev), b1=inp['b1'].to(dev),
-                          w2=inp['w2'].to(dev), b2=inp['b2'].to(dev), alpha=float(inp['alpha']),
-                          beta=float(inp['beta']))
+                          w2=inp['w2'].to(dev), b2=inp['b2'].to(dev),
+                          alpha=float(inp['alpha']) if use_sdf else 1.0,
+                          beta=float(inp['beta']) if use_sdf else 0.1,
+                          attention_values=nattn, use_sdf=use_sdf)
     rnd = bool(meta['randomize'])
     uc = inp['u_coarse'].to(dev) if rnd else None
     uf = inp['u_fine'].to(dev) if rnd else None
@@ -44,7 +48,8 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
         loss.backward()
         torch.cuda.synchronize()
         out['d_planes'] = planes.grad.cpu()
-        out['d_palette'] = palette.grad.cpu()
+        if palette is not None:
+            out['d_palette'] = palette.grad.cpu()
         if cam.requires_grad:
             out['d_cam'] = cam.grad.cpu()
             if focal is not None:
@@ -52,23 +57,25 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
     return out
 
 
-def run_oracle64(inp, meta, with_grad=True, return_intermediates=False):
+def run_oracle64(inp, meta, with_grad=True, return_intermediates=False, z_fine=None):
     """The oracle evaluated in float64 — the 'exact' answer both fp32 paths are measured against."""
     inp64 = {k: (v.double() if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in inp.items()}
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.float64)
     try:
-        return run_oracle(inp64, meta, with_grad, return_intermediates)
+        return run_oracle(inp64, meta, with_grad, return_intermediates, z_fine=z_fine)
     finally:
         torch.set_default_dtype(prev)
 
 
-def run_oracle(inp, meta, with_grad=True, return_intermediates=False):
+def run_oracle(inp, meta, with_grad=True, return_intermediates=False, z_fine=None):
     ncg = bool(meta.get('force_no_cam_grad', 0))
+    nattn = int(meta.get('attention_values', 10))
     field = orc.Field(planes=inp['planes'].clone().requires_grad_(with_grad),
                       w1=inp['w1'], b1=inp['b1'], w2=inp['w2'], b2=inp['b2'],
-                      palette=inp['palette'].clone().requires_grad_(with_grad),
-                      alpha=inp['alpha'], beta=inp['beta'], scene_range=float(meta['scene_range']))
+                      palette=inp['palette'].clone().requires_grad_(with_grad) if nattn else None,
+                      alpha=inp.get('alpha'), beta=inp.get('beta'), scene_range=float(meta['scene_range']),
+                      attention_values=nattn, use_sdf=bool(meta.get('use_sdf', 1)))
     cam = inp['cam'].clone().requires_grad_(with_grad and not ncg)
     focal = inp.get('focal')
     if focal is not None:
@@ -78,7 +85,7 @@ def run_oracle(inp, meta, with_grad=True, return_intermediates=False):
                      int(meta['S']), randomize=rnd, white_background=bool(meta['white_bg']),
                      fine_sampling=bool(meta.get('fine', 1)), force_no_cam_grad=ncg,
                      u_coarse=inp['u_coarse'] if rnd else None, u_fine=inp['u_fine'] if rnd else None,
-                     return_intermediates=return_intermediates)
+                     return_intermediates=return_intermediates, z_fine=z_fine)
     rgb, depth, mask = res[:3]
     out = {'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach()}
     if return_intermediates:
@@ -87,7 +94,8 @@ def run_oracle(inp, meta, with_grad=True, return_intermediates=False):
         loss = (rgb * inp['g_rgb']).sum() + (mask * inp['g_mask']).sum()
         loss.backward()
         out['d_planes'] = field.planes.grad
-        out['d_palette'] = field.palette.grad
+        if field.palette is not None:
+            out['d_palette'] = field.palette.grad
         if cam.requires_grad:
             out['d_cam'] = cam.grad
             if focal is not None:

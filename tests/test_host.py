@@ -41,6 +41,21 @@ def test_normals_need_sdf_field():
         nfi.configure(use_sdf=True)
 
 
+def test_field_heads_follow_the_field():
+    """attention_values 0 / use_sdf False fields: normals need the SDF (generator.py:600-601),
+    semantics the attention values (:670-671); the checks fire before any device work."""
+    f = _field()
+    f.use_sdf = False
+    with pytest.raises(ValueError, match='SDF'):
+        nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32, compute_normals=True)
+    f = _field()
+    f.attention_values, f.palette = 0, None
+    with pytest.raises(ValueError, match='attention'):
+        nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32, compute_semantics=True)
+    with pytest.raises(RuntimeError, match='HIP devices only'):       # and the rest reaches the op
+        nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
+
+
 def test_viewdir_variant_raises():
     nfi.configure(use_viewdir=True)
     try:
