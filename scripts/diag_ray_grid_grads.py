@@ -1,5 +1,9 @@
-"""Diagnostic: one ray of the failing field-head case rendered alone (nfi.ops.volume_render with
-the ray as a leaf) vs the oracle with the same ray; gradient paths split by dL/d rgb / dL/d mask."""
+"""Diagnostic: one ray rendered alone (nfi.ops.volume_render with the ray as a leaf) vs the oracle
+with the same ray: d ray-origin split by dL/d rgb / dL/d mask, then the per-sample grid gradients
+of every (sample, plane) entry (the backward workspace, ops.DEBUG_BACKWARD) against the fp64
+oracle's grid_sample gradients.  It located the texel-boundary kink described in
+tests/test_gpu_parity.py::test_field_heads_seeded (a fine sample 1e-7 of the span from a texel
+column takes the other one-sided x-derivative).  Usage (GPU box): python scripts/diag_ray_grid_grads.py [ray]"""
 import os
 import sys
 
