@@ -1536,6 +1536,38 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         // The surplus entries of the last step read the next tile's records or the zeroed list
         // padding (chunk_map_kernel): valid cells, and their zeroed rows add 0.
         const cint4_p L = (cint4_p)A.list;
+#ifndef NFI_TILE_PINGPONG
+#define NFI_TILE_PINGPONG 1
+#endif
+#if NFI_TILE_PINGPONG
+        // Scalar (record) and LDS (row) loads share lgkmcnt and scalar loads return out of order,
+        // so a step that waits for its LDS rows also waits for every scalar load in flight.  The
+        // next step's records are therefore issued only after this step's rows have been waited
+        // for (nfi_lgkm_consume + a compiler barrier), into the other half of a ping-pong pair: the
+        // one wait per step then covers a scalar load that had a whole step to arrive.
+        iv4 ra[8], rb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ra[k] = L[base + k];
+#define NFI_ENTRY(R, K)                                                                              \
+  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(R[K].y) & 31, __int_as_float(R[K].z), \
+             __int_as_float(R[K].w), gv[K], wsgn, woff)
+#define NFI_STEP(U, RUSE, RNEXT)                                                                     \
+  {                                                                                                  \
+    float gv[8];                                                                                     \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) gv[k] = G[stage_at((U) + k, cl)];                 \
+    asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
+                 "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base + (U) + 8 + k];                 \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
+  }
+        for (int u = 0; u < n; u += 16) {
+          NFI_STEP(u, ra, rb)
+          if (u + 8 >= n) break;
+          NFI_STEP(u + 8, rb, ra)
+        }
+#undef NFI_STEP
+#undef NFI_ENTRY
+#else
         iv4 rc[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) rc[k] = L[base + k];
@@ -1558,6 +1590,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #pragma unroll
           for (int k = 0; k < 8; ++k) rc[k] = rn[k];
         }
+#endif
         wave_lds_sync();
         NFI_STAMP(25)
       }
