@@ -115,58 +115,90 @@ __device__ __forceinline__ float4 ror8_add(float4 v) {
 #endif
 constexpr int GATHER_GB = NFI_GATHER_GB;
 
+// NFI_GATHER_PIPE 1: software pipeline over single groups (measured slower on MI355X: 2.58 vs
+// 2.50 ms forward — the batched form keeps more bytes in flight at the same register count)
+#ifndef NFI_GATHER_PIPE
+#define NFI_GATHER_PIPE 0
+#endif
+
+// One group's loads: the parameters of point 4g + sub arrive by ds_bpermute (e = 1 - w and s = 1 - n
+// recomputed as plane_params rounds them: 3 ds_bpermute per plane instead of 5), then the two
+// texel rows of each plane.
+__device__ __forceinline__ void gather_issue(const PlaneView& pv, const PointP& P, int g, int sub, int dx,
+                                             int q4, float4 (&V0)[3], float4 (&V1)[3], float (&W0)[3],
+                                             float (&W1)[3]) {
+  const int j = min(4 * g + sub, WAVE - 1);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int pk = __shfl(P.pl[q].tex, j);
+    const float w = __shfl(P.pl[q].w, j), n = __shfl(P.pl[q].n, j);
+    const float e = 1.f - w, s = 1.f - n;
+    const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
+    const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
+    const float* b = pv.base + q * pv.sq + 4 * q4;
+    V0[q] = *reinterpret_cast<const float4*>(b + t0 * pv.st);
+    V1[q] = *reinterpret_cast<const float4*>(b + t1 * pv.st);
+    const float wx = dx ? w : e;
+    W0[q] = s * wx;
+    W1[q] = n * wx;
+  }
+}
+
+// Interpolate one group and write its 4 feature vectors (mean of the 3 planes) to the X tile.
+__device__ __forceinline__ void gather_consume(int g, int sub, int dx, int q4, int npts, const float4 (&V0)[3],
+                                               const float4 (&V1)[3], const float (&W0)[3],
+                                               const float (&W1)[3], float* __restrict__ X) {
+  const int j = 4 * g + sub;
+  float4 E[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    float4 pr;
+    pr.x = V0[q].x * W0[q] + V1[q].x * W1[q];
+    pr.y = V0[q].y * W0[q] + V1[q].y * W1[q];
+    pr.z = V0[q].z * W0[q] + V1[q].z * W1[q];
+    pr.w = V0[q].w * W0[q] + V1[q].w * W1[q];
+    E[q] = ror8_add(pr);
+  }
+  if (dx == 0 && j < npts) {
+    float4 f;
+    f.x = ((E[0].x + E[1].x) + E[2].x) * (1.f / 3.f);
+    f.y = ((E[0].y + E[1].y) + E[2].y) * (1.f / 3.f);
+    f.z = ((E[0].z + E[1].z) + E[2].z) * (1.f / 3.f);
+    f.w = ((E[0].w + E[1].w) + E[2].w) * (1.f / 3.f);
+    *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
+  }
+}
+
 __device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
                                                 float* __restrict__ X) {
   const int l = lane_id();
   const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
   const int ngrp = (npts + 3) >> 2;
+#if NFI_GATHER_PIPE
+  // Software pipeline over groups, two register sets: group g + 1's loads are in flight while
+  // group g is interpolated (the batched form below issues GB groups, then waits for all of them).
+  float4 A0[3], A1[3], B0[3], B1[3];
+  float AW0[3], AW1[3], BW0[3], BW1[3];
+  gather_issue(pv, P, 0, sub, dx, q4, A0, A1, AW0, AW1);
+#pragma unroll 1
+  for (int g = 0; g < ngrp; g += 2) {
+    if (g + 1 < ngrp) gather_issue(pv, P, g + 1, sub, dx, q4, B0, B1, BW0, BW1);
+    gather_consume(g, sub, dx, q4, npts, A0, A1, AW0, AW1, X);
+    if (g + 1 >= ngrp) break;
+    if (g + 2 < ngrp) gather_issue(pv, P, g + 2, sub, dx, q4, A0, A1, AW0, AW1);
+    gather_consume(g + 1, sub, dx, q4, npts, B0, B1, BW0, BW1, X);
+  }
+#else
 #pragma unroll 1
   for (int gb = 0; gb < ngrp; gb += GATHER_GB) {
     float4 V0[GATHER_GB][3], V1[GATHER_GB][3];
     float W0[GATHER_GB][3], W1[GATHER_GB][3];
 #pragma unroll
-    for (int u = 0; u < GATHER_GB; ++u) {
-      const int j = min(4 * (gb + u) + sub, WAVE - 1);
+    for (int u = 0; u < GATHER_GB; ++u) gather_issue(pv, P, gb + u, sub, dx, q4, V0[u], V1[u], W0[u], W1[u]);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int pk = __shfl(P.pl[q].tex, j);
-        // (e = 1 - w and s = 1 - n recomputed here, as plane_params rounds them: 3 ds_bpermute per
-        // plane instead of 5)
-        const float w = __shfl(P.pl[q].w, j), n = __shfl(P.pl[q].n, j);
-        const float e = 1.f - w, s = 1.f - n;
-        const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
-        const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-        const float* b = pv.base + q * pv.sq + 4 * q4;
-        V0[u][q] = *reinterpret_cast<const float4*>(b + t0 * pv.st);
-        V1[u][q] = *reinterpret_cast<const float4*>(b + t1 * pv.st);
-        const float wx = dx ? w : e;
-        W0[u][q] = s * wx;
-        W1[u][q] = n * wx;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < GATHER_GB; ++u) {
-      const int j = 4 * (gb + u) + sub;
-      float4 E[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        float4 pr;
-        pr.x = V0[u][q].x * W0[u][q] + V1[u][q].x * W1[u][q];
-        pr.y = V0[u][q].y * W0[u][q] + V1[u][q].y * W1[u][q];
-        pr.z = V0[u][q].z * W0[u][q] + V1[u][q].z * W1[u][q];
-        pr.w = V0[u][q].w * W0[u][q] + V1[u][q].w * W1[u][q];
-        E[q] = ror8_add(pr);
-      }
-      if (dx == 0 && j < npts) {
-        float4 f;
-        f.x = ((E[0].x + E[1].x) + E[2].x) * (1.f / 3.f);
-        f.y = ((E[0].y + E[1].y) + E[2].y) * (1.f / 3.f);
-        f.z = ((E[0].z + E[1].z) + E[2].z) * (1.f / 3.f);
-        f.w = ((E[0].w + E[1].w) + E[2].w) * (1.f / 3.f);
-        *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
-      }
-    }
+    for (int u = 0; u < GATHER_GB; ++u) gather_consume(gb + u, sub, dx, q4, npts, V0[u], V1[u], W0[u], W1[u], X);
   }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
