@@ -1108,16 +1108,21 @@ __global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_rende
   }
   // decoder inputs saved by the forward (no re-gather here), loaded straight into the MFMA
   // operand layout: lane (j, q) takes channels 8q..8q+7 of points 16sb + j
+  // (point 16sb + j's evaluation index is lane 16sb + j's ei: one ds_bpermute each instead of a
+  //  dependent perm load per block, so the 8 row loads issue together)
   f4v xa[4], xb[4];
   {
     const int j = l & 15, q = l >> 4;
+    int eis[4];
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) eis[sb] = __shfl(ei, 16 * sb + j);
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
       const int ip = e * 64 + 16 * sb + j;
       xa[sb] = f4v{0.f, 0.f, 0.f, 0.f};
       xb[sb] = xa[sb];
       if (ip < N) {
-        const float* xr = a.x_saved + (r * N + (int)a.perm[r * N + ip]) * NC + 8 * q;
+        const float* xr = a.x_saved + (r * N + eis[sb]) * NC + 8 * q;
         xa[sb] = ld4(xr);
         xb[sb] = ld4(xr + 4);
       }
