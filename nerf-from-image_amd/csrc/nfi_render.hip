@@ -381,6 +381,37 @@ __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, 
   f4v Y[4];
 #pragma unroll
   for (int sb = 0; sb < 4; ++sb) Y[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+#ifndef NFI_MLP_PREFETCH
+#define NFI_MLP_PREFETCH 1
+#endif
+#if NFI_MLP_PREFETCH
+  // operand tables of hidden block hb + 1 are loaded while block hb runs (L1/L2 round trips
+  // otherwise serialise with the MFMA chains: 16 more VGPRs, within occupancy 3)
+  f4v ta = ld4(dec + DT1 + l * 8), tb = ld4(dec + DT1 + l * 8 + 4);
+  f4v b = ld4(dec + DB1 + l * 4), t2 = ld4(dec + DT2 + l * 4);
+#pragma unroll
+  for (int hb = 0; hb < 4; ++hb) {
+    f4v nta = ta, ntb = tb, nb = b, nt2 = t2;
+    if (hb < 3) {
+      const int hn = hb + 1;
+      nta = ld4(dec + DT1 + (hn * 64 + l) * 8);
+      ntb = ld4(dec + DT1 + (hn * 64 + l) * 8 + 4);
+      nb = ld4(dec + DB1 + (hn * 64 + l) * 4);
+      nt2 = ld4(dec + DT2 + (hn * 64 + l) * 4);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // (keeps the scheduler from sinking the loads to their use)
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const f4v z = layer1(ta, tb, b, xa[sb], xb[sb]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Y[sb] = mfma4(t2[r], softplus(z[r]), Y[sb]);
+    }
+    ta = nta;
+    tb = ntb;
+    b = nb;
+    t2 = nt2;
+  }
+#else
 #pragma unroll
   for (int hb = 0; hb < 4; ++hb) {
     const f4v ta = ld4(dec + DT1 + (hb * 64 + l) * 8), tb = ld4(dec + DT1 + (hb * 64 + l) * 8 + 4);
@@ -393,6 +424,7 @@ __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, 
       for (int r = 0; r < 4; ++r) Y[sb] = mfma4(t2[r], softplus(z[r]), Y[sb]);
     }
   }
+#endif
   // lane (j, q) holds outputs 4q..4q+3 of point 16sb + j: transpose through the tile
   wave_lds_sync();
 #pragma unroll
