@@ -135,6 +135,7 @@ class InversionConfig:
     optimize_pose: bool = True           # not --inv_no_optimize_pose
     no_split: bool = False               # --inv_no_split: one w shared by the 15 slots
     camera_flipped: bool = True          # dataset_config['camera_flipped']
+    overlap_target: bool = True          # 'vgg' losses: target features on a side stream (GPU)
 
 
 @dataclass
@@ -195,11 +196,31 @@ def augment_images(img: torch.Tensor, p: float, white_background: bool = False,
 VGG_LOSSES = ('vgg', 'vgg_nocrop', 'mixed')
 
 
+def _copies(x):
+    return x.unsqueeze(1).expand(-1, 15, -1, -1, -1).contiguous().flatten(0, 1)
+
+
+def vgg_target(kind: str, target: torch.Tensor, lpips_net, white_background: bool = False,
+               augment_generator=None):
+    """The prediction-independent half of the 'vgg' losses: the augmentation grid (run.py:720-767
+    draws, in the reference's order) and the LPIPS features of the target and its 15 augmented
+    copies (no gradient).  Returns (grid or None, target features)."""
+    tgt = target.permute(0, 3, 1, 2)
+    if kind == 'vgg_nocrop':
+        return None, lpips_net.target_features(tgt)
+    b = tgt.shape[0]
+    grid = augment_grid((15 * b, 6) + tuple(tgt.shape[2:]), 1.0, tgt.device, generator=augment_generator)
+    with torch.no_grad():
+        aug_tgt = apply_grid(_copies(tgt), grid, white_background)
+    return grid, lpips_net.target_features(torch.cat((tgt, aug_tgt), dim=0))
+
+
 def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor, lpips_net=None,
-               white_background: bool = False, augment_generator=None) -> torch.Tensor:
+               white_background: bool = False, augment_generator=None, prepared=None) -> torch.Tensor:
     """optimize_iter (run.py:2205-2252): per-batch-summed image loss.  'vgg' = LPIPS over the
     image plus 15 augmented copies of (prediction, target) pairs; 'vgg_nocrop' without the
-    copies; 'mixed' = ('vgg' + 'l1') / 2; 'l1'; 'mse'."""
+    copies; 'mixed' = ('vgg' + 'l1') / 2; 'l1'; 'mse'.  `prepared` = vgg_target(...) computed
+    beforehand (the grid and the target's features; the loss then only runs the prediction)."""
     b = rgb.shape[0]
     if kind not in VGG_LOSSES + ('l1', 'mse'):
         raise NotImplementedError(f'inversion loss {kind!r}')
@@ -210,23 +231,17 @@ def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor, lpips_net=Non
         if lpips_net is None:
             raise ValueError(f'inversion loss {kind!r} needs an LPIPS network (nfi.lpips.LPIPS with '
                              f'weights loaded via load_weights; none ship offline)')
-        pred, tgt = rgb.permute(0, 3, 1, 2), target.permute(0, 3, 1, 2)
+        # the reference augments cat((pred, target), channels) expanded to 15 copies; grid_sample
+        # treats channels independently, so the prediction and target copies are sampled with the
+        # same grid separately (identical values), and only the prediction's copies carry a
+        # gradient (the reference backpropagates into the target copies and drops the result at
+        # the target leaf)
+        grid, f1 = prepared if prepared is not None else vgg_target(kind, target, lpips_net,
+                                                                     white_background, augment_generator)
+        pred = rgb.permute(0, 3, 1, 2)
         if kind != 'vgg_nocrop':
-            # the reference augments cat((pred, target), channels) expanded to 15 copies; grid_sample
-            # treats channels independently, so the prediction and target copies are sampled with
-            # the same grid separately (identical values), and only the prediction's copies
-            # carry a gradient (the reference backpropagates into the target copies and drops the
-            # result at the target leaf)
-            def copies(x):
-                return x.unsqueeze(1).expand(-1, 15, -1, -1, -1).contiguous().flatten(0, 1)
-            shape = (15 * b, 6) + tuple(pred.shape[2:])
-            grid = augment_grid(shape, 1.0, pred.device, generator=augment_generator)
-            aug_pred = apply_grid(copies(pred), grid, white_background)
-            with torch.no_grad():
-                aug_tgt = apply_grid(copies(tgt), grid, white_background)
-            pred = torch.cat((pred, aug_pred), dim=0)
-            tgt = torch.cat((tgt, aug_tgt), dim=0)
-        loss = loss + lpips_net(pred, tgt).mean() * b
+            pred = torch.cat((pred, apply_grid(_copies(pred), grid, white_background)), dim=0)
+        loss = loss + lpips_net(pred, f1=f1).mean() * b
     if kind in ('l1', 'mixed'):
         loss = loss + F.l1_loss(rgb, target) * b
     if kind == 'mixed':
@@ -267,8 +282,19 @@ def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: 
     losses = []
     if on_checkpoint is not None and 0 in checkpoints:
         on_checkpoint(0, (z_, z0_, t2_, s_, q_))
+    # the prediction-independent half of the 'vgg' losses (augmentation grid, LPIPS features of the
+    # target and its copies) runs on a side stream, concurrently with the producer and the render
+    side = None
+    if cfg.loss in VGG_LOSSES and target.is_cuda and cfg.overlap_target:
+        side = torch.cuda.Stream(device=target.device)
     t0 = time.perf_counter()
     for it in range(cfg.steps):
+        prepared = None
+        if side is not None:
+            main = torch.cuda.current_stream(target.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                prepared = vgg_target(cfg.loss, target, lpips_net, cfg.white_background)
         cam, foc = pose_to_matrix(z0_, t2_, s_, F.normalize(q_, dim=-1), cfg.camera_flipped)
         kw = {}
         if uniforms is not None:
@@ -278,7 +304,11 @@ def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: 
             ws = ws.expand(-1, 15, -1)
         rgb = rfn(generator, res, res, cam, foc, center, bbox, ws, cfg.samples,
                   force_no_cam_grad=not cfg.optimize_pose, **kw)[0]
-        loss = image_loss(cfg.loss, rgb, target, lpips_net, cfg.white_background)
+        if side is not None:
+            main.wait_stream(side)
+            for t in ([prepared[0]] if prepared[0] is not None else []) + list(prepared[1]):
+                t.record_stream(main)
+        loss = image_loss(cfg.loss, rgb, target, lpips_net, cfg.white_background, prepared=prepared)
         loss.backward()
         opt.step()
         opt.zero_grad()

@@ -106,10 +106,17 @@ class LPIPS(nn.Module):
     def features(self, im):
         return self.net((im - self.shift) / self.scale, fused=self.backend == 'hip')
 
-    def forward(self, in0, in1):
+    def target_features(self, in1):
+        """The second input's feature taps without gradient (forward(in0, f1=...) consumes them:
+        the inversion computes them for the target on a side stream)."""
+        with torch.no_grad():
+            return self.features(in1)
+
+    def forward(self, in0, in1=None, f1=None):
         f0 = self.features(in0)
-        with torch.no_grad() if not in1.requires_grad else _null():
-            f1 = self.features(in1)
+        if f1 is None:
+            with torch.no_grad() if not in1.requires_grad else _null():
+                f1 = self.features(in1)
         if self.backend == 'hip':
             from . import producer_ops
             return sum(producer_ops.lpips_head(a, b, lin.weight.view(-1))

@@ -85,3 +85,42 @@ def test_vgg_inversion_loss_runs():
     res = inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg, lpips_net=net)
     assert len(res.losses) == 2 and all(torch.isfinite(torch.tensor(res.losses)))
     assert torch.isfinite(res.ws).all()
+
+
+def test_vgg_target_on_side_stream_matches_inline():
+    """The target half of the 'vgg' loss (grid + target features) computed on a side stream gives
+    the inline loss and gradient (same device draws, same kernels); the inversion
+    trajectory with overlap_target on and off agrees in its losses (its latents differ only by
+    the float-atomic order of d planes, amplified by Adam's normalised first steps)."""
+    torch.manual_seed(0)
+    net = lpips.LPIPS().to(DEV)
+    rgb = torch.tanh(torch.randn(2, 64, 64, 3, device=DEV)).requires_grad_()
+    target = torch.tanh(torch.randn(2, 64, 64, 3, device=DEV))
+    torch.manual_seed(5)
+    ref = inversion.image_loss('vgg', rgb, target, net)
+    ref.backward()
+    g_ref = rgb.grad.clone()
+    rgb.grad = None
+    torch.manual_seed(5)
+    side = torch.cuda.Stream(device=DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        prepared = inversion.vgg_target('vgg', target, net)
+    torch.cuda.current_stream(DEV).wait_stream(side)
+    got = inversion.image_loss('vgg', rgb, target, net, prepared=prepared)
+    got.backward()
+    # (the distance head's spatial mean and grid_sample's backward accumulate with float atomics:
+    #  reproducible to accumulation order, not bit for bit)
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=0.0)
+    torch.testing.assert_close(rgb.grad, g_ref, rtol=1e-5, atol=1e-6 * float(g_ref.abs().max()))
+
+    from test_producer import inversion_setup
+    gen, d, meta, cfg = inversion_setup(DEV)
+    cfg.steps, cfg.loss = 3, 'vgg'
+    losses = []
+    for overlap in (True, False):
+        cfg.overlap_target = overlap
+        torch.manual_seed(11)
+        losses.append(inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg,
+                                       lpips_net=net).losses)
+    torch.testing.assert_close(torch.tensor(losses[0]), torch.tensor(losses[1]), rtol=1e-5, atol=1e-7)
