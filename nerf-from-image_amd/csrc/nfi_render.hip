@@ -1575,6 +1575,15 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       int cur = 0;
       float a0 = 0.f, a1 = 0.f;
       int4 vrec = A.list[min(b0 + l, b1 - 1)];
+#ifndef NFI_TILE_REC2
+#define NFI_TILE_REC2 0
+#endif
+#if NFI_TILE_REC2
+      // records two batches ahead: a batch's row loads then depend on a record that arrived a
+      // batch ago (one HBM round trip on the critical path instead of record + row).  Measured
+      // no faster (2.28-2.36 vs 2.21-2.25 ms: the extra registers spill at occupancy 4), kept off.
+      int4 vnext = A.list[min(b0 + BATCH + l, b1 - 1)];
+#endif
       float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
 #define NFI_LOAD_ROW(REC)                                                                       \
   {                                                                                              \
@@ -1598,8 +1607,14 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         // next rows are in flight, which keeps the register count at occupancy 4)
         if (A.dpc && l < n) entry_grid_grad(G, Tex, l, vrec, q, half, A.dpc);
         // the next batch of rows loads while this one is summed
+#if NFI_TILE_REC2
+        vrec = vnext;
+        NFI_LOAD_ROW(vrec)
+        vnext = A.list[min(base + 2 * BATCH + l, b1 - 1)];
+#else
         vrec = A.list[min(base + BATCH + l, b1 - 1)];
         NFI_LOAD_ROW(vrec)
+#endif
         NFI_STAMP(24)
         // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed.
         // The surplus entries of the last step read the next tile's records or the zeroed list
