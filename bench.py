@@ -56,7 +56,9 @@ def run_step(nfi, batch, cfg, backward: bool):
     f.palette.grad = None
     cam = batch['cam'].detach().requires_grad_(pose and backward)
     focal = batch['focal'].detach().requires_grad_(pose and backward)
-    rgb, depth, mask, _, _, _ = nfi.render(f, H, H, cam, focal, None, None, None, S, randomize=True)
+    # a forward-only step renders under no_grad, as the reference's eval renders do (run.py:2036-2051)
+    with torch.enable_grad() if backward else torch.no_grad():
+        rgb, depth, mask, _, _, _ = nfi.render(f, H, H, cam, focal, None, None, None, S, randomize=True)
     if backward:
         loss = (rgb * batch['g_rgb']).sum() + (mask * batch['g_mask']).sum()
         loss.backward()

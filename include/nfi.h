@@ -100,7 +100,8 @@ typedef struct nfi_render_args {
   float* rgb;          /* [B*HW,3] */
   float* depth;        /* [B*HW]   */
   float* mask;         /* [B*HW]   */
-  /* per-ray state kept for backward: merged, sorted samples (N = fine ? 2S : S) */
+  /* per-ray state kept for backward: merged, sorted samples (N = fine ? 2S : S).  t/sigma/rgb/y/perm
+     are all set or all NULL: NULL = a forward-only call (no backward, extras or tile counts) */
   float* t_saved;      /* [B*HW,N]   */
   float* sigma_saved;  /* [B*HW,N]   */
   float* rgb_saved;    /* [B*HW,3,N] */

@@ -643,7 +643,7 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   float y[NO];
   mlp_forward_tile(a.field.dec, X, y);
   NFI_STAMP(2)
-  if (lane_id() < npts) {
+  if (a.y_saved && lane_id() < npts) {     // (no saved state in forward-only calls)
     const int N = a.fine ? 2 * a.S : a.S;
     float* ys = a.y_saved + R.r * NO * N + eval_base + lane_id();
 #pragma unroll
@@ -940,7 +940,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? NFI_FWD_OCC : 2)
       al[e] = 0.f;
       aa[e] = 1.f;
     }
-    if (v) {
+    if (v && a.t_saved) {
       a.t_saved[r * N + i] = t[e];
       a.sigma_saved[r * N + i] = sg;
 #pragma unroll
@@ -2139,8 +2139,11 @@ static int validate(const nfi_render_args* a) {
                   f.scene_range > 0.f, "render: bad field scalars");
   NFI_REQUIRE(a->ro && a->rd && a->near_ && a->far_, "render: null ray pointer");
   NFI_REQUIRE(a->B > 0 && a->HW > 0, "render: bad shape B=%d HW=%d", a->B, a->HW);
-  NFI_REQUIRE(a->t_saved && a->sigma_saved && a->rgb_saved && a->y_saved && a->perm,
-              "render: null saved-state pointer");
+  {
+    const bool all = a->t_saved && a->sigma_saved && a->rgb_saved && a->y_saved && a->perm;
+    const bool none = !a->t_saved && !a->sigma_saved && !a->rgb_saved && !a->y_saved && !a->perm;
+    NFI_REQUIRE(all || none, "render: saved-state pointers must be all set or all null");
+  }
   NFI_REQUIRE(supported_S(a), "render: unsupported samples per ray S=%d (fine=%d): need 3..128 with fine "
               "sampling, 1..256 without", a->S, (int)a->fine);
   return NFI_OK;
@@ -2154,6 +2157,8 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
   int e = nfi::validate(a);
   if (e) return e;
   NFI_REQUIRE(a->rgb && a->depth && a->mask, "render_forward: null output");
+  NFI_REQUIRE(a->t_saved || (!a->extras && !a->tile_counts && !a->x_saved),
+              "render_forward: eval outputs / backward state need the saved-state buffers");
   NFI_REQUIRE((a->extras & ~7) == 0, "render_forward: unknown extras bits 0x%x", a->extras);
   NFI_REQUIRE(!(a->extras & 1) || (a->normal_map && a->x_saved),
               "render_forward: normals need normal_map and x_saved");
@@ -2182,7 +2187,8 @@ int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args
   NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->workspace &&
                   (g->d_palette_ray || (a->field.heads & NFI_HEAD_RGB_SIGMOID)),
               "render_backward: null grad pointer");
-  NFI_REQUIRE(a->x_saved, "render_backward: x_saved (decoder inputs saved by the forward) is required");
+  NFI_REQUIRE(a->x_saved && a->t_saved,
+              "render_backward: the forward's saved state (x_saved, t/sigma/rgb/y/perm) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
   return nfi::launch_bwd(a, g, (hipStream_t)stream, -1);
 }
@@ -2194,7 +2200,8 @@ int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_gra
   NFI_REQUIRE(g && g->g_rgb && g->g_mask && g->d_planes && g->workspace &&
                   (g->d_palette_ray || (a->field.heads & NFI_HEAD_RGB_SIGMOID)),
               "render_backward: null grad pointer");
-  NFI_REQUIRE(a->x_saved, "render_backward: x_saved (decoder inputs saved by the forward) is required");
+  NFI_REQUIRE(a->x_saved && a->t_saved,
+              "render_backward: the forward's saved state (x_saved, t/sigma/rgb/y/perm) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
   NFI_REQUIRE(stage >= 0 && stage <= 2, "render_backward_stage: stage %d not in 0..2", stage);
   return nfi::launch_bwd(a, g, (hipStream_t)stream, stage);

@@ -228,11 +228,13 @@ class _VolumeRender(torch.autograd.Function):
         rgb = torch.empty((n, 3), device=dev)
         depth = torch.empty((n,), device=dev)
         mask = torch.empty((n,), device=dev)
-        t_saved = torch.empty((n, N), device=dev)
-        s_saved = torch.empty((n, N), device=dev)
-        c_saved = torch.empty((n, 3, N), device=dev)
-        y_saved = torch.empty((n, 11, N), device=dev)
-        perm = torch.empty((n, N), device=dev, dtype=torch.int16)
+        # per-sample state for the backward / eval outputs / debug; a forward-only call skips it
+        keep = any(ctx.needs_input_grad) or bool(opts.extras) or debug is not None
+        t_saved = torch.empty((n, N), device=dev) if keep else None
+        s_saved = torch.empty((n, N), device=dev) if keep else None
+        c_saved = torch.empty((n, 3, N), device=dev) if keep else None
+        y_saved = torch.empty((n, 11, N), device=dev) if keep else None
+        perm = torch.empty((n, N), device=dev, dtype=torch.int16) if keep else None
         # decoder inputs for the backward (saves it the re-gather) and for the normals pass
         need_x = any(ctx.needs_input_grad) or bool(opts.extras & 1)
         x_saved = torch.empty((n * N, 32), device=dev) if need_x else None
