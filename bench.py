@@ -287,7 +287,7 @@ def main():
     # L2 / Infinity Cache, so the tap rate can exceed the HBM peak: 'traffic' (rocprofv3 PMC) is
     # what actually crossed HBM per launch.
     model = {
-        'render_fwd': (TAP_BYTES + 194, 6450),
+        'render_fwd': (TAP_BYTES + (194 if bwd else 0), 6450),   # + saved state when a backward follows
         'bwd_bins': (12, 0),
         'bwd_field': (380, 5700),
         'bwd_tiles': (TAP_BYTES * (2 if pose else 1) + 48 + 3 * 128, 768 * (2 if pose else 1)),
