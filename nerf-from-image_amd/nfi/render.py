@@ -166,10 +166,15 @@ def _check_frozen(f: TriplaneField):
 def render(target_model, height, width, tform_cam2world, focal_length, center, bbox, model_input,
            depth_samples_per_ray, randomize=True, compute_normals=False, compute_semantics=False,
            compute_coords=False, extra_model_outputs=[], extra_model_inputs={},
-           force_no_cam_grad=False, *, u_coarse=None, u_fine=None, seed=None, debug=None):
+           force_no_cam_grad=False, *, u_coarse=None, u_fine=None, seed=None, debug=None,
+           depth_mode: str = 'ray'):
     """run.py:176-350.  Extra keyword-only arguments (not in the reference) inject the random
     draws for parity testing (`u_coarse` [B,H,W,S], `u_fine` [B*H*W,S]) or fix the Philox
-    seed; `debug` (a dict) receives intermediate depths."""
+    seed; `debug` (a dict) receives intermediate depths.  depth_mode 'zbuffer' returns the
+    camera-space z depth of the perspective eval scripts' render copies instead of the ray
+    distance (eval_nusc_persp.py:221-228; see render_zbuffer)."""
+    if depth_mode not in ('ray', 'zbuffer'):
+        raise ValueError("depth_mode must be 'ray' or 'zbuffer'")
     cfg = _CONFIG
     if compute_normals and not cfg.use_sdf:
         raise ValueError('compute_normals needs an SDF field (run.py:229)')
@@ -205,6 +210,27 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
                             u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug)
     if extras:
         rgb, depth, mask, normals, semantics = out
-        return rgb, depth, mask, normals, semantics, dict(f.model_outputs)
-    rgb, depth, mask = out
-    return rgb, depth, mask, None, None, dict(f.model_outputs)
+    else:
+        (rgb, depth, mask), normals, semantics = out, None, None
+    if depth_mode == 'zbuffer':
+        depth = zbuffer_depth(depth, rd, tform_cam2world)
+    return rgb, depth, mask, normals, semantics, dict(f.model_outputs)
+
+
+def zbuffer_depth(depth, ray_directions, tform_cam2world):
+    """eval_{nusc,kitti,waymo}_persp.py:221-228: the compositing depth (a
+    distance along the unit ray) -> camera-space z of the flipped camera,
+    -(R_world2cam · rd)_z · depth.  No gradient: the depth map carries none (nerf_utils.py:151)
+    and the eval scripts' losses never read it."""
+    from .inversion import invert_space
+    with torch.no_grad():
+        w2c = invert_space(tform_cam2world.detach())
+        view = torch.sum(ray_directions.detach()[..., None, :] * w2c[:, None, None, :3, :3], dim=-1)
+        return (view * depth.unsqueeze(-1))[..., -1] * (-1)
+
+
+def render_zbuffer(*args, **kwargs):
+    """The render() copy of the perspective eval scripts (eval_nusc_persp.py:43-231,
+    eval_kitti_persp.py, eval_waymo_persp.py): run.py's render with the depth map converted to
+    camera-space z (zbuffer_depth).  Same signature as render."""
+    return render(*args, depth_mode='zbuffer', **kwargs)

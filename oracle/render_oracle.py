@@ -307,7 +307,7 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
            u_coarse: Optional[torch.Tensor] = None, u_fine: Optional[torch.Tensor] = None,
            return_intermediates: bool = False, compute_normals: bool = False,
            compute_semantics: bool = False, compute_coords: bool = False,
-           z_fine: Optional[torch.Tensor] = None):
+           z_fine: Optional[torch.Tensor] = None, zbuffer: bool = False):
     """run.py:176-350 with use_viewdir=False.  Returns (rgb [b,H,W,3], depth [b,H,W],
     mask [b,H,W]) (+ intermediates dict); with any compute_* flag (run.py:227-257, 293-335)
     (rgb, depth, mask, normal_map [b,H,W,3] | None, semantic_map [b,H,W,10 | 3] | None) — the
@@ -383,6 +383,8 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
         return (*outs, inter) if return_intermediates else outs
     rgb_map, depth_map, mask = render_volume_density(sigma.squeeze(-1), rgb, ray_origins, ray_directions,
                                                      depth_values, white_background=white_background)
+    if zbuffer:
+        depth_map = zbuffer_depth(depth_map, ray_directions, tform_cam2world)
     if return_intermediates:
         return rgb_map, depth_map, mask, inter
     return rgb_map, depth_map, mask
@@ -391,6 +393,24 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
 # --------------------------------------------------------------------------------------
 # lib/pose_utils.py:48-75 — caller-side camera construction (used to build test cameras)
 # --------------------------------------------------------------------------------------
+
+def invert_space(mat):
+    """pose_utils.py:20-27."""
+    out_mat = torch.zeros_like(mat)
+    out_mat[:, :3, :3] = mat[:, :3, :3].transpose(-2, -1) / mat[:, 3:4, 3:4]
+    out_mat[:, 3, 3] = 1
+    out_mat[:, :3, 3] = -torch.sum(mat[:, :3, :3] / mat[:, 3:4, 3:4] * mat[:, :3, None, 3], dim=-2)
+    return out_mat
+
+
+def zbuffer_depth(depth_predicted, ray_directions, tform_cam2world):
+    """eval_nusc_persp.py:221-228 (the perspective eval scripts' render copy): ray distance ->
+    camera-space z of the flipped camera."""
+    tform_world2cam = invert_space(tform_cam2world)
+    view_directions = torch.sum(ray_directions[..., None, :] * tform_world2cam[:, None, None, :3, :3], dim=-1)
+    view_points3D = view_directions * depth_predicted.unsqueeze(-1)
+    return view_points3D[..., -1] * (-1)
+
 
 def quaternion_to_matrix(q):
     """pose_utils.py:30-45."""

@@ -44,14 +44,16 @@ sys.path.insert(0, os.path.dirname(OUT))
 from golden_io import load_seeded  # noqa: E402  (the seeded-weights recipe the tests share)
 
 
-def extract_render(args_ns, dataset_config):
-    src = open(os.path.join(REF, 'run.py')).read()
+def extract_render(args_ns, dataset_config, path='run.py'):
+    """`render` AST-extracted from run.py (or a script with its own copy, e.g. the perspective
+    eval scripts' z-buffer variant eval_nusc_persp.py:43-231) and exec'd with its globals."""
+    src = open(os.path.join(REF, path)).read()
     tree = ast.parse(src)
     fn = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == 'render'][0]
     mod = ast.Module(body=[fn], type_ignores=[])
-    ns = {'torch': torch, 'F': F, 'nerf_utils': nerf_utils, 'args': args_ns,
+    ns = {'torch': torch, 'F': F, 'nerf_utils': nerf_utils, 'pose_utils': pose_utils, 'args': args_ns,
           'dataset_config': dataset_config}
-    exec(compile(mod, os.path.join(REF, 'run.py'), 'exec'), ns)
+    exec(compile(mod, os.path.join(REF, path), 'exec'), ns)
     return ns['render']
 
 
@@ -85,7 +87,7 @@ def make_cameras(b, scene_range, flipped, seed, ortho=False):
 
 def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, randomize,
                 force_no_cam_grad=False, ortho=False, with_bbox=False, with_center=False,
-                attention_values=10, use_sdf=True):
+                attention_values=10, use_sdf=True, render_file='run.py'):
     torch.manual_seed(1000 + seed)
     gen = generator.Generator(512, scene_range, attention_values=attention_values, use_sdf=use_sdf,
                               disable_stylegan_noise=True)
@@ -113,7 +115,7 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     args_ns = types.SimpleNamespace(use_viewdir=False, fine_sampling=True, use_sdf=use_sdf,
                                     attention_values=attention_values)
     dataset_config = {'scene_range': scene_range, 'white_background': white_bg}
-    render = extract_render(args_ns, dataset_config)
+    render = extract_render(args_ns, dataset_config, render_file)
 
     rseed = 77 + seed
     torch.manual_seed(rseed)
@@ -159,7 +161,8 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
             out['d_focal'] = focal.grad
     meta = dict(H=H, W=W, S=S, R=R, scene_range=scene_range, white_bg=int(white_bg),
                 randomize=int(randomize), force_no_cam_grad=int(force_no_cam_grad),
-                ortho=int(ortho), attention_values=attention_values, use_sdf=int(use_sdf))
+                ortho=int(ortho), attention_values=attention_values, use_sdf=int(use_sdf),
+                zbuffer=int(render_file != 'run.py'))
     np.savez_compressed(os.path.join(OUT, f'render_{name}.npz'),
                         **{k: v.numpy() for k, v in out.items()},
                         **{f'meta_{k}': np.array(v) for k, v in meta.items()})
@@ -415,6 +418,12 @@ def inversion_case(seed=41, b=2, H=16, S=8, steps=3, scene_range=1.4, flipped=Tr
     print('inversion losses', losses, 'mask', masks)
 
 
+def zbuffer_cases():
+    """The perspective eval scripts' render copy (eval_nusc_persp.py:43-231): z-buffer depth."""
+    render_case('zbuffer', 10, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=False,
+                flipped=True, randomize=True, render_file='eval_nusc_persp.py')
+
+
 def field_variant_cases():
     """The reference's other field heads (generator.py:637-641, 665-666): colour by
     wide_sigmoid_rescaled of 3 decoder features (--attention_values 0), standard NeRF density
@@ -455,6 +464,7 @@ if __name__ == '__main__':
     render_case('persp_center_bbox', 3, b=2, H=8, W=12, S=8, R=8, scene_range=1.4,
                 white_bg=False, flipped=True, randomize=True, with_bbox=True, with_center=True)
     field_variant_cases()
+    zbuffer_cases()
     # eval outputs: normals + semantics; white background; coords
     extras_case('extras_ns', 4, b=2, H=8, W=8, S=16, R=16, scene_range=1.4, white_bg=False,
                 flipped=True, compute_normals=True, compute_semantics=True, compute_coords=False)

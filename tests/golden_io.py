@@ -8,6 +8,7 @@ import torch
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox']
 VARIANT_CASES = ['rgbhead', 'nerfdensity', 'nerf_rgbhead']   # attention_values 0 / use_sdf False
+ZBUFFER_CASES = ['zbuffer']        # eval_nusc_persp.py's render copy (z-buffer depth)
 EXTRAS_CASES = ['extras_ns', 'extras_nw', 'extras_coords']   # eval outputs, no gradients
 
 

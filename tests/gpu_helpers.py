@@ -41,7 +41,8 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
     rgb, depth, mask, _, _, _ = nfi.render(
         f, int(meta['H']), int(meta['W']), cam, focal, None if center is None else center.to(dev),
         None if bbox is None else bbox.to(dev), None, int(meta['S']), randomize=rnd,
-        force_no_cam_grad=ncg, u_coarse=uc, u_fine=uf, debug=debug)
+        force_no_cam_grad=ncg, u_coarse=uc, u_fine=uf, debug=debug,
+        depth_mode='zbuffer' if meta.get('zbuffer') else 'ray')
     out = {'rgb': rgb.detach().cpu(), 'depth': depth.detach().cpu(), 'mask': mask.detach().cpu()}
     if with_grad:
         loss = (rgb * inp['g_rgb'].to(dev)).sum() + (mask * inp['g_mask'].to(dev)).sum()
@@ -85,7 +86,8 @@ def run_oracle(inp, meta, with_grad=True, return_intermediates=False, z_fine=Non
                      int(meta['S']), randomize=rnd, white_background=bool(meta['white_bg']),
                      fine_sampling=bool(meta.get('fine', 1)), force_no_cam_grad=ncg,
                      u_coarse=inp['u_coarse'] if rnd else None, u_fine=inp['u_fine'] if rnd else None,
-                     return_intermediates=return_intermediates, z_fine=z_fine)
+                     return_intermediates=return_intermediates, z_fine=z_fine,
+                     zbuffer=bool(meta.get('zbuffer', 0)))
     rgb, depth, mask = res[:3]
     out = {'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach()}
     if return_intermediates:

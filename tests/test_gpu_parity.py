@@ -15,7 +15,7 @@ rel-L2 1e-4, d planes rel-L2 1e-3.
 import pytest
 import torch
 
-from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, load
+from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, ZBUFFER_CASES, load
 from gpu_helpers import (rel_l2, run_hip, run_hip_extras, run_oracle, run_oracle64, run_oracle_extras,
                          synthetic_inputs)
 
@@ -46,7 +46,7 @@ def check(hip, ref32, ref64):
     return report
 
 
-@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES)
+@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES + ZBUFFER_CASES)
 def test_golden_render(case):
     """HIP path vs the reference's own fp32 outputs/gradients (tests/golden) and fp64 truth."""
     d, meta = load(f'render_{case}')

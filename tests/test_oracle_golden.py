@@ -8,7 +8,7 @@ rounding of identical op graphs (in practice bit-exact).
 import pytest
 import torch
 
-from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, field_from, load
+from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, ZBUFFER_CASES, field_from, load
 from oracle import render_oracle as orc
 
 
@@ -26,13 +26,13 @@ def _run_oracle(d, meta):
                                   d.get('bbox'), meta['S'], randomize=bool(meta['randomize']),
                                   white_background=bool(meta['white_bg']),
                                   force_no_cam_grad=ncg, u_coarse=d['u_coarse'],
-                                  u_fine=d['u_fine'])
+                                  u_fine=d['u_fine'], zbuffer=bool(meta.get('zbuffer', 0)))
     loss = (rgb * d['g_rgb']).sum() + (mask * d['g_mask']).sum()
     loss.backward()
     return rgb, depth, mask, field, cam, focal
 
 
-@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES)
+@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES + ZBUFFER_CASES)
 def test_oracle_render_matches_reference(case):
     d, meta = load(f'render_{case}')
     rgb, depth, mask, field, cam, focal = _run_oracle(d, meta)
