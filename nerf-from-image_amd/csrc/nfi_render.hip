@@ -1456,6 +1456,9 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 // per-lane b128 row stores / reads and the per-entry row reads conflict-free, with
 // immediate-offset addressing).  60 rows, not 64, so that the stages, the tile texels and 4
 // workgroups fit one CU's LDS; the stage (2,160 floats) still holds a wave's 2,048-float image.
+#ifndef NFI_TILE_DBUF
+#define NFI_TILE_DBUF 0   // 1: two batches of rows in registers at occupancy 3 (measured 2.64 vs 2.28 ms)
+#endif
 constexpr int BATCH = 56;
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
@@ -1574,64 +1577,21 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       // indexed update (cur starts at slot 0 with nothing pending)
       int cur = 0;
       float a0 = 0.f, a1 = 0.f;
-      int4 vrec = A.list[min(b0 + l, b1 - 1)];
-#ifndef NFI_TILE_REC2
-#define NFI_TILE_REC2 0
-#endif
-#if NFI_TILE_REC2
-      // records two batches ahead: a batch's row loads then depend on a record that arrived a
-      // batch ago (one HBM round trip on the critical path instead of record + row).  Measured
-      // no faster (2.28-2.36 vs 2.21-2.25 ms: the extra registers spill at occupancy 4), kept off.
-      int4 vnext = A.list[min(b0 + BATCH + l, b1 - 1)];
-#endif
+      const cint4_p L = (cint4_p)A.list;
       float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
-#define NFI_LOAD_ROW(REC)                                                                       \
+#define NFI_LOAD_ROW(P, REC)                                                                     \
   {                                                                                              \
     const float4* src_ = reinterpret_cast<const float4*>(A.gfeat + (long long)(REC).x * NC);     \
-    r0 = src_[0]; r1 = src_[1]; r2 = src_[2]; r3 = src_[3];                                      \
-    r4 = src_[4]; r5 = src_[5]; r6 = src_[6]; r7 = src_[7];                                      \
+    P##0 = src_[0]; P##1 = src_[1]; P##2 = src_[2]; P##3 = src_[3];                              \
+    P##4 = src_[4]; P##5 = src_[5]; P##6 = src_[6]; P##7 = src_[7];                              \
   }
-      NFI_LOAD_ROW(vrec)
-      for (int base = b0; base < b1; base += BATCH) {
-        const int n = min(BATCH, b1 - base);
-        // rows past the chunk end are zeroed: the last step's surplus entries then add 0 (their
-        // records, from the next tile or the list padding, only move the run cursor)
-        if (l >= n) r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (l < BATCH) {
-          float4* dst = reinterpret_cast<float4*>(G + l * XS);
-          dst[0] = r0; dst[1] = r1; dst[2] = r2; dst[3] = r3;
-          dst[4] = r4; dst[5] = r5; dst[6] = r6; dst[7] = r7;
-        }
-        wave_lds_sync();
-        // pose: each lane's own entry against the staged texels (one lane per entry; before the
-        // next rows are in flight, which keeps the register count at occupancy 4)
-        if (A.dpc && l < n) entry_grid_grad(G, Tex, l, vrec, q, half, A.dpc);
-        // the next batch of rows loads while this one is summed
-#if NFI_TILE_REC2
-        vrec = vnext;
-        NFI_LOAD_ROW(vrec)
-        vnext = A.list[min(base + 2 * BATCH + l, b1 - 1)];
-#else
-        vrec = A.list[min(base + BATCH + l, b1 - 1)];
-        NFI_LOAD_ROW(vrec)
-#endif
-        NFI_STAMP(24)
-        // 8 entries per step, records (SGPRs) of the next step loaded while this one is summed.
-        // The surplus entries of the last step read the next tile's records or the zeroed list
-        // padding (chunk_map_kernel): valid cells, and their zeroed rows add 0.
-        const cint4_p L = (cint4_p)A.list;
-#ifndef NFI_TILE_PINGPONG
-#define NFI_TILE_PINGPONG 1
-#endif
-#if NFI_TILE_PINGPONG
-        // Scalar (record) and LDS (row) loads share lgkmcnt and scalar loads return out of order,
-        // so a step that waits for its LDS rows also waits for every scalar load in flight.  The
-        // next step's records are therefore issued only after this step's rows have been waited
-        // for (nfi_lgkm_consume + a compiler barrier), into the other half of a ping-pong pair: the
-        // one wait per step then covers a scalar load that had a whole step to arrive.
-        iv4 ra[8], rb[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) ra[k] = L[base + k];
+      // 8 entries per step.  Scalar (record) and LDS (row) loads share lgkmcnt and scalar loads
+      // return out of order, so a step that waits for its LDS rows also waits for every scalar load
+      // in flight: the next step's records are issued only after this step's rows have been
+      // waited for (a consume + compiler barrier), into the other half of a ping-pong pair — the
+      // one wait per step then covers a scalar load that had a whole step to arrive.  The surplus
+      // entries of the last step read the next tile's records or the zeroed list padding
+      // (chunk_map_kernel): valid cells, and their zeroed rows add 0.
 #define NFI_ENTRY(R, K)                                                                              \
   tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(R[K].y) & 31, __int_as_float(R[K].z), \
              __int_as_float(R[K].w), gv[K], wsgn, woff)
@@ -1641,43 +1601,58 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     _Pragma("unroll") for (int k = 0; k < 8; ++k) gv[k] = G[stage_at((U) + k, cl)];                 \
     asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
                  "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base + (U) + 8 + k];                 \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];                \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
   }
-        for (int u = 0; u < n; u += 16) {
-          NFI_STEP(u, ra, rb)
-          if (u + 8 >= n) break;
-          NFI_STEP(u + 8, rb, ra)
-        }
+      // One batch of <= BATCH entries: rows P (zeroed past the chunk end: the last step's surplus
+      // entries then add 0) -> the wave's LDS stage; the pose gradient of each lane's own entry
+      // against the staged texels; the rows of batch BASE + AHEAD issued into P (they load while
+      // this batch is summed); then the entry loop.
+#define NFI_BATCH(BASE, P, VREC, AHEAD)                                                              \
+  {                                                                                                  \
+    const int base_ = (BASE);                                                                        \
+    const int n = min(BATCH, b1 - base_);                                                            \
+    if (l >= n) P##0 = P##1 = P##2 = P##3 = P##4 = P##5 = P##6 = P##7 = make_float4(0.f, 0.f, 0.f, 0.f); \
+    if (l < BATCH) {                                                                                 \
+      float4* dst = reinterpret_cast<float4*>(G + l * XS);                                           \
+      dst[0] = P##0; dst[1] = P##1; dst[2] = P##2; dst[3] = P##3;                                    \
+      dst[4] = P##4; dst[5] = P##5; dst[6] = P##6; dst[7] = P##7;                                    \
+    }                                                                                                \
+    wave_lds_sync();                                                                                 \
+    if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
+    VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];                                                 \
+    NFI_LOAD_ROW(P, VREC)                                                                            \
+    NFI_STAMP(24)                                                                                    \
+    iv4 ra[8], rb[8];                                                                                \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];                             \
+    for (int u = 0; u < n; u += 16) {                                                                \
+      NFI_STEP(u, ra, rb)                                                                            \
+      if (u + 8 >= n) break;                                                                         \
+      NFI_STEP(u + 8, rb, ra)                                                                        \
+    }                                                                                                \
+    wave_lds_sync();                                                                                 \
+    NFI_STAMP(25)                                                                                    \
+  }
+#if NFI_TILE_DBUF
+      // two batches of rows in registers (occupancy 3): a batch's rows were issued two batches
+      // before they are staged
+      float4 s0, s1, s2, s3, s4, s5, s6, s7;
+      int4 vrec = A.list[min(b0 + l, b1 - 1)], vrecb = A.list[min(b0 + BATCH + l, b1 - 1)];
+      NFI_LOAD_ROW(r, vrec)
+      NFI_LOAD_ROW(s, vrecb)
+      for (int bb = b0; bb < b1; bb += 2 * BATCH) {
+        NFI_BATCH(bb, r, vrec, 2 * BATCH)
+        if (bb + BATCH >= b1) break;
+        NFI_BATCH(bb + BATCH, s, vrecb, 2 * BATCH)
+      }
+#else
+      int4 vrec = A.list[min(b0 + l, b1 - 1)];
+      NFI_LOAD_ROW(r, vrec)
+      for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCH(bb, r, vrec, BATCH)
+#endif
+#undef NFI_BATCH
 #undef NFI_STEP
 #undef NFI_ENTRY
-#else
-        iv4 rc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) rc[k] = L[base + k];
-        for (int u = 0; u < n; u += 8) {
-          float gv[8];
-          iv4 rn[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            gv[k] = G[stage_at(u + k, cl)];
-            rn[k] = L[base + u + 8 + k];
-          }
-#define NFI_ENTRY(K)                                                                                 \
-  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(rc[K].y) & 31, __int_as_float(rc[K].z), \
-             __int_as_float(rc[K].w), gv[K], wsgn, woff)
-          // one body for full and partial steps (a second copy of the body made the register
-          // allocator move the whole image at every step)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) NFI_ENTRY(k);
-#undef NFI_ENTRY
-#pragma unroll
-          for (int k = 0; k < 8; ++k) rc[k] = rn[k];
-        }
-#endif
-        wave_lds_sync();
-        NFI_STAMP(25)
-      }
 #undef NFI_LOAD_ROW
       img_add(img, cur, a0, a1);
     }
@@ -1907,7 +1882,7 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
 
 // d planes and the per-(sample, plane) grid gradients of the pose path, one workgroup per tile
 // chunk (the grid is sized for a bound on the chunk count; blocks past meta[0] exit at once).
-__global__ void __launch_bounds__(256, 4) tile_kernel(TileArgs A) {
+__global__ void __launch_bounds__(256, NFI_TILE_DBUF ? 3 : 4) tile_kernel(TileArgs A) {
   __shared__ __attribute__((aligned(16))) float lds[TILE_LDS];
   if ((long long)blockIdx.x >= A.meta[0]) return;
   tile_chunk(A, lds, (int)blockIdx.x);
