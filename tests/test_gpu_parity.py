@@ -172,3 +172,32 @@ def test_eval_outputs_full_size():
         e_ref = float((ref32[key].double() - ref64[key]).abs().max())
         print(f'  {key:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
         assert e_hip <= max(floor, K * e_ref), key
+
+
+def test_rays_missing_the_box():
+    """Part of the image misses the scene box: the reference gives the missed rays the min near /
+    max far of the hits (nerf_utils.py:260-261) and their samples zero weight; nfi matches the
+    fp64 oracle on every output and gradient."""
+    inp, meta = synthetic_inputs(B=2, H=16, W=16, S=32, R=32, scene_range=1.4, seed=13)
+    cam = inp['cam'].clone()
+    cam[:, :3, 3] += 1.6 * cam[:, :3, 0]          # slide the camera sideways along its x axis
+    inp['cam'] = cam
+    ref64 = run_oracle64(inp, meta)
+    assert int((ref64['mask'] == 0).sum()) > 16, 'the test view must leave rays outside the box'
+    assert float(ref64['mask'].max()) > 0.1, 'and keep some inside it'
+    check(run_hip(inp, meta, DEV), run_oracle(inp, meta), ref64)
+
+
+def test_all_rays_missing_the_box():
+    """No ray hits the box: the reference raises (min() of an empty tensor, nerf_utils.py:260);
+    nfi renders the background (divergence (i)) and returns zero gradients."""
+    inp, meta = synthetic_inputs(B=1, H=8, W=8, S=16, R=16, scene_range=1.4, seed=14)
+    cam = inp['cam'].clone()
+    cam[:, :3, 3] += 20.0 * cam[:, :3, 0]
+    inp['cam'] = cam
+    for white in (0, 1):
+        meta['white_bg'] = white
+        hip = run_hip(inp, meta, DEV)
+        assert float(hip['mask'].abs().max()) == 0.0
+        assert torch.all(hip['rgb'] == float(white))
+        assert float(hip['d_planes'].abs().max()) == 0.0 and float(hip['d_palette'].abs().max()) == 0.0
