@@ -168,16 +168,18 @@ int32_t nfi_segment_sum(const float* in, int32_t B, int32_t M, int32_t K, float*
  * sampling (N = 2S merged samples), 1..256 without. */
 int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
 
-/* Backward of nfi_render_forward from its saved state: per-ray compositing + field backward
- * (recomputes taps and decoder) writes per-sample feature gradients; d planes is then summed
- * per 16x16-cell plane tile in LDS (samples binned by tile) and flushed once per tile. */
+/* Backward of nfi_render_forward from its saved state: per-ray compositing backward, then the
+ * field backward (decoder input-gradient on the saved decoder inputs) writes per-sample feature
+ * gradients and appends each (sample, plane) entry to its 7x4-cell plane tile's bin; d planes is
+ * summed per tile chunk in registers and flushed once per chunk, each entry's grid gradient
+ * computed there against the tile's texels; d ray origins / directions are reduced per ray. */
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
 int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * 3 * ((R-2)/7+1) * ((R-2)/4+1) */
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 /* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
  * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,
- * 1 = compositing + field backward (d palette, d rays, per-sample feature gradients),
- * 2 = per-tile d planes accumulation. */
+ * 1 = compositing + field backward (d palette, per-sample feature gradients, tile entries),
+ * 2 = per-tile d planes accumulation + grid gradients, then d rays. */
 int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_grad_args* g, int32_t stage,
                                   void* stream);
 
