@@ -99,9 +99,22 @@ def planes_texel_major(planes: torch.Tensor) -> torch.Tensor:
     if planes.dim() != 5 or planes.shape[1] != 3 or planes.shape[2] != 32 or planes.shape[3] != planes.shape[4]:
         raise ValueError(f'planes must be [B,3,32,R,R], got {tuple(planes.shape)}')
     tm = planes.permute(0, 1, 3, 4, 2)
-    if tm.stride(-1) == 1 and tm.stride(2) == tm.shape[3] * tm.stride(3):
+    # the view is used only when it is also dense (non-overlapping, no gaps): the backward writes
+    # d planes with the view's strides into torch.zeros_like(view), which keeps the strides only
+    # for dense tensors (a batch-sliced or channel-sliced channels_last buffer is copied instead)
+    if tm.stride(-1) == 1 and tm.stride(2) == tm.shape[3] * tm.stride(3) and _dense(tm):
         return tm
     return _PlanesTexelMajor.apply(planes)
+
+
+def _dense(t: torch.Tensor) -> bool:
+    """True when t's elements tile its storage span exactly (torch's non-overlapping-and-dense)."""
+    expected = 1
+    for size, stride in sorted(((s, st) for s, st in zip(t.shape, t.stride()) if s != 1), key=lambda p: p[1]):
+        if stride != expected:
+            return False
+        expected *= size
+    return True
 
 
 # ----------------------------------------------------------------------------------------
@@ -309,7 +322,10 @@ class _VolumeRender(torch.autograd.Function):
         n = B * H * W
         g_rgb = torch.zeros((n, 3), device=dev) if g_rgb is None else g_rgb.contiguous()
         g_mask = torch.zeros((n,), device=dev) if g_mask is None else g_mask.contiguous()
-        d_planes = torch.zeros_like(planes_tm)   # preserves (texel-major) strides
+        d_planes = torch.zeros_like(planes_tm)   # preserves (texel-major) strides: planes_tm is dense
+        if d_planes.stride() != planes_tm.stride():
+            raise RuntimeError(f'nfi: d planes strides {d_planes.stride()} differ from the planes view '
+                               f'{planes_tm.stride()} (non-dense planes view)')
         npl = ((2 * opts.samples if opts.fine else opts.samples) + 63) // 64
         d_pal_ray = torch.empty((n * npl, 30), device=dev) if pal is not None else None
         need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]

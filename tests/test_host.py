@@ -75,3 +75,15 @@ def test_frozen_decoder_required():
 def test_planes_shape_checked():
     with pytest.raises(RuntimeError):
         ops.planes_texel_major(torch.zeros(1, 3, 32, 8, 8))
+
+
+def test_dense_view_check():
+    # planes_texel_major keeps a channels_last view only when it is dense (d planes are written
+    # with the view's strides into zeros_like(view)); sliced buffers must take the copy path
+    cl = torch.zeros(4, 96, 8, 8).to(memory_format=torch.channels_last)
+    tm = cl.view(4, 3, 32, 8, 8).permute(0, 1, 3, 4, 2)
+    assert ops._dense(tm)
+    assert torch.zeros_like(tm).stride() == tm.stride()
+    assert not ops._dense(cl[::2].view(2, 3, 32, 8, 8).permute(0, 1, 3, 4, 2))
+    cl128 = torch.zeros(2, 128, 8, 8).to(memory_format=torch.channels_last)
+    assert not ops._dense(cl128[:, :96].view(2, 3, 32, 8, 8).permute(0, 1, 3, 4, 2))
