@@ -271,7 +271,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
-    kern = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) for k, v in timers.items()}  # ms/launch
+    # ms per step of each stage: the sum of its launches (the backward runs each stage once per
+    # image half, ops.BACKWARD_PIPELINE; the halves' tile passes overlap the field backward)
+    kern = {k: sum(a.elapsed_time(b) for a, b in v) / args.steps for k, v in timers.items()}
+    launches = {k: len(v) / args.steps for k, v in timers.items()}
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
 
@@ -309,7 +312,7 @@ def main():
             traffic = round(ctr['hbm_bytes_corrected'] / 1e9, 3)
     except (OSError, ValueError, KeyError):
         pass
-    stages = {k: {'ms': round(v, 4),
+    stages = {k: {'ms': round(v, 4), 'launches_per_step': launches[k],
                   'tap_GBps': round(samples_per_step * model[k][0] / (v * 1e-3) / 1e9, 1),
                   'fp32_TFLOPs': round(samples_per_step * model[k][1] / (v * 1e-3) / 1e12, 2)}
               for k, v in kern.items() if k in model}

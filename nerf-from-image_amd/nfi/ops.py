@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -40,21 +41,40 @@ KERNEL_TIMERS: Optional[dict] = None
 
 
 class _timed:
-    def __init__(self, name, dev):
-        self.name, self.dev = name, dev
+    """HIP events around one C-ABI call, recorded on the stream it launches on."""
+
+    def __init__(self, name, dev, stream=None):
+        self.name, self.dev, self.stream = name, dev, stream
 
     def __enter__(self):
         if KERNEL_TIMERS is not None:
+            self.s = self.stream if self.stream is not None else torch.cuda.current_stream(self.dev)
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
-            self.e0.record(torch.cuda.current_stream(self.dev))
+            self.e0.record(self.s)
         return self
 
     def __exit__(self, *exc):
         if KERNEL_TIMERS is not None:
-            self.e1.record(torch.cuda.current_stream(self.dev))
+            self.e1.record(self.s)
             KERNEL_TIMERS.setdefault(self.name, []).append((self.e0, self.e1))
         return False
+
+
+# Optional: the backward of a batch of >= 2 images in two image halves, the tile pass of the first
+# half on a side stream beside the field backward of the second.  Measured slower on MI355X (p3d
+# B=8: 7.49 vs 7.39 ms per step; the overlapped launches stretch to 2.61 / 3.39 ms from 2.27 /
+# 2.25: the two compete for the memory pipeline, not for different units), so off by default.
+BACKWARD_PIPELINE = os.environ.get('NFI_BACKWARD_PIPELINE', '0') == '1'
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(key)
+    if s is None:
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _require_device(*ts):
@@ -320,8 +340,8 @@ class _VolumeRender(torch.autograd.Function):
         B, H, W = ctx.shape
         dev = ro.device
         n = B * H * W
-        g_rgb = torch.zeros((n, 3), device=dev) if g_rgb is None else g_rgb.contiguous()
-        g_mask = torch.zeros((n,), device=dev) if g_mask is None else g_mask.contiguous()
+        g_rgb = torch.zeros((n, 3), device=dev) if g_rgb is None else g_rgb.contiguous().view(n, 3)
+        g_mask = torch.zeros((n,), device=dev) if g_mask is None else g_mask.contiguous().view(n)
         d_planes = torch.zeros_like(planes_tm)   # preserves (texel-major) strides: planes_tm is dense
         if d_planes.stride() != planes_tm.stride():
             raise RuntimeError(f'nfi: d planes strides {d_planes.stride()} differ from the planes view '
@@ -331,23 +351,68 @@ class _VolumeRender(torch.autograd.Function):
         need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
         g_ro = torch.empty((n, 3), device=dev) if need_coords else None
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
-        args = _VolumeRender._args(planes_tm, dec, pal, ro, rd, near, far, opts, B, H * W, None, None, 0,
-                                   None, None, None, t_saved, s_saved, c_saved, y_saved, perm, None, None)
-        args.x_saved = _ptr(x_saved)
-        nbytes = lib.nfi_render_backward_workspace_bytes(ctypes.byref(args))
-        if nbytes < 0:
-            _lib.check(-1, 'nfi_render_backward_workspace_bytes')
-        ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
-        if DEBUG_BACKWARD is not None:          # diagnostics: the backward workspace (per-sample state)
-            DEBUG_BACKWARD['workspace'] = ws
-        gargs = _lib.NfiRenderGradArgs(g_rgb=_ptr(g_rgb), g_mask=_ptr(g_mask), d_planes=_ptr(d_planes),
-                                       d_palette_ray=_ptr(d_pal_ray), g_ro=_ptr(g_ro), g_rd=_ptr(g_rd),
-                                       tile_counts=_ptr(tile_counts), workspace=_ptr(ws), workspace_bytes=nbytes)
-        st = _stream(dev)
-        for stage, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
-            with _timed(name, dev):
-                _lib.check(lib.nfi_render_backward_stage(ctypes.byref(args), ctypes.byref(gargs), stage, st),
+        HW = H * W
+        N = 2 * opts.samples if opts.fine else opts.samples
+        per_img = None
+        if tile_counts is not None:
+            per_img = tile_counts.numel() // B
+
+        def part(b0, nb):
+            """C-ABI arguments of the backward of images b0 .. b0+nb-1 (every per-image / per-ray
+            buffer offset to the part; the d planes tile bins are keyed per image)."""
+            r0, r1 = b0 * HW, (b0 + nb) * HW
+            a = _VolumeRender._args(planes_tm[b0:b0 + nb], dec, None if pal is None else pal[b0:b0 + nb],
+                                    ro[b0:b0 + nb], rd[b0:b0 + nb], near[b0:b0 + nb], far[b0:b0 + nb], opts, nb,
+                                    HW, None, None, 0, None, None, None, t_saved[r0:r1], s_saved[r0:r1],
+                                    c_saved[r0:r1], y_saved[r0:r1], perm[r0:r1], None, None)
+            a.x_saved = _ptr(x_saved[r0 * N:r1 * N])
+            nbytes = lib.nfi_render_backward_workspace_bytes(ctypes.byref(a))
+            if nbytes < 0:
+                _lib.check(-1, 'nfi_render_backward_workspace_bytes')
+            ws = torch.empty((nbytes,), device=dev, dtype=torch.uint8)
+            if DEBUG_BACKWARD is not None:      # diagnostics: the backward workspace (per-sample state)
+                DEBUG_BACKWARD['workspace'] = ws
+            tc = None if tile_counts is None else tile_counts[b0 * per_img:(b0 + nb) * per_img]
+            g = _lib.NfiRenderGradArgs(
+                g_rgb=_ptr(g_rgb[r0:r1]), g_mask=_ptr(g_mask[r0:r1]), d_planes=_ptr(d_planes[b0:b0 + nb]),
+                d_palette_ray=_ptr(None if d_pal_ray is None else d_pal_ray[r0 * npl:r1 * npl]),
+                g_ro=_ptr(None if g_ro is None else g_ro[r0:r1]), g_rd=_ptr(None if g_rd is None else g_rd[r0:r1]),
+                tile_counts=_ptr(tc), workspace=_ptr(ws), workspace_bytes=nbytes)
+            return a, g, ws
+
+        def stage(p, k, name, strm):
+            a, g, _ = p
+            with _timed(name, dev, strm):
+                _lib.check(lib.nfi_render_backward_stage(ctypes.byref(a), ctypes.byref(g), k,
+                                                         ctypes.c_void_p(strm.cuda_stream)),
                            'nfi_render_backward_stage')
+
+        main = torch.cuda.current_stream(dev)
+        if BACKWARD_PIPELINE and B >= 2 and DEBUG_BACKWARD is None:
+            # two image halves: the tile pass of half 0 (VALU / LDS / gather bound) runs on a side
+            # stream beside the field backward of half 1 (matrix-core bound)
+            parts = [part(0, B // 2), part(B // 2, B - B // 2)]
+            side = _side_stream(dev)
+            events = []
+            for p in parts:
+                stage(p, 0, 'bwd_bins', main)
+                stage(p, 1, 'bwd_field', main)
+                ev = torch.cuda.Event()
+                ev.record(main)
+                events.append(ev)
+            for p, ev in zip(parts, events):
+                side.wait_event(ev)
+                stage(p, 2, 'bwd_tiles', side)
+                p[2].record_stream(side)
+            for t in (d_planes, g_ro, g_rd, t_saved, tile_counts, planes_tm, ro, rd, near, far):
+                if t is not None:
+                    t.record_stream(side)
+            main.wait_stream(side)
+        else:
+            p = part(0, B)
+            for k, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
+                stage(p, k, name, main)
+        st = _stream(dev)
         d_pal = None
         if pal is not None:
             d_pal = torch.empty((B, 30), device=dev)

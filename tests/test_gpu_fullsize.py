@@ -74,3 +74,20 @@ def test_loss_linear_in_palette(full):
     lhs = float(moved['loss'] - base['loss'])
     rhs = eps * float((base['d_palette'].cpu() * delta).sum())
     assert abs(lhs - rhs) <= 1e-3 * abs(rhs) + 1e-2, (lhs, rhs)
+
+
+def test_backward_image_halves_match(full):
+    """ops.BACKWARD_PIPELINE (off by default): the backward in two image halves on two streams
+    gives the single-launch gradients (d planes up to float-atomic order)."""
+    from nfi import ops
+    inp, meta = full
+    a = _render(inp, meta, seed=3)
+    old = ops.BACKWARD_PIPELINE
+    ops.BACKWARD_PIPELINE = True
+    try:
+        b = _render(inp, meta, seed=3)
+    finally:
+        ops.BACKWARD_PIPELINE = old
+    assert torch.equal(a['d_palette'], b['d_palette'])
+    for k in ('d_planes', 'd_cam', 'd_focal'):
+        assert rel_l2(b[k], a[k]) < 1e-5, k
