@@ -15,6 +15,19 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-mun
          '-Wall', '-Wno-unused-result']
 
 
+def source_digest() -> str:
+    """sha256 (16 hex) of the HIP sources and headers the library is built from: stamps profiler
+    counter files (profiles/latest_counters.json) so bench.py can tell whether they describe the
+    kernels it runs."""
+    import hashlib
+    h = hashlib.sha256()
+    inc = os.path.join(os.path.dirname(os.path.dirname(HERE)), 'include')
+    for path in [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(inc, x) for x in ('nfi.h', 'nfi_producer.h')]:
+        with open(path, 'rb') as fh:
+            h.update(os.path.basename(path).encode() + b'\0' + fh.read())
+    return h.hexdigest()[:16]
+
+
 def _stale() -> bool:
     if not os.path.exists(OUT):
         return True

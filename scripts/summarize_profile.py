@@ -47,7 +47,9 @@ for r in stats:
         continue
     kern[short] = {'avg_us': float(r['AverageNs']) / 1e3, 'fetch_kib': f, 'write_kib': w,
                    'hbm_bytes_corrected': 2 * f * 1024 + w * 1024}
-json.dump({'tag': tag, 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), '
+sys.path.insert(0, os.path.join(root, 'nerf-from-image_amd'))
+from nfi.build import source_digest  # noqa: E402
+json.dump({'tag': tag, 'source_digest': source_digest(), 'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), '
            'FETCH_SIZE x2 per MI355X_MICROARCH.md HBM section', 'kernels': kern},
           open(os.path.join(root, 'profiles', 'latest_counters.json'), 'w'), indent=1)
 print(out)
