@@ -33,8 +33,9 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 10
-#define NFI_DEC_SIZE 7184 /* floats in the packed decoder buffer */
+#define NFI_ABI_VERSION 11
+#define NFI_DEC_SIZE 7184   /* floats in the packed decoder buffer (11 outputs) */
+#define NFI_DEC_SIZE_VIEWDIR 11312 /* ... with the view-direction mapper (33 outputs) */
 
 enum {
   NFI_OK = 0,
@@ -65,9 +66,17 @@ typedef struct nfi_camera {
  *                          (:665-666, :36-39); decoder [4,64] zero-padded to [11,64]; palette
  *                          unused (may be NULL); no semantics
  *   NFI_HEAD_NERF_DENSITY  use_sdf False: sigma = softplus(d - 1) * (1 - mask) (:637-641);
- *                          inv_alpha / beta unused; no normals */
+ *                          inv_alpha / beta unused; no normals
+ *   NFI_HEAD_VIEWDIR       --use_viewdir (generator.py:189-252, 376-377, 661-663): the decoder has
+ *                          33 outputs (distance + 32 features; dec packed with nout 33) and the
+ *                          colour logits are output(leaky_relu(xray + features, 0.2)) with
+ *                          xray [B*HW,32] the per-ray mapper trunk of the ray direction
+ *                          (ViewDirectionMapper.forward :223-238, computed by the caller) and
+ *                          vhead the gain-scaled output layer: [vhead_out,32] weights then
+ *                          [vhead_out] bias, vhead_out = 10 (attention) or 3 (RGB_SIGMOID) */
 #define NFI_HEAD_RGB_SIGMOID 1
 #define NFI_HEAD_NERF_DENSITY 2
+#define NFI_HEAD_VIEWDIR 4
 typedef struct nfi_field {
   const float* planes;
   int64_t sb, sq, st;
@@ -77,6 +86,10 @@ typedef struct nfi_field {
   const float* palette;
   float inv_alpha, beta, scene_range;
   int32_t heads;
+  const float* xray;   /* NFI_HEAD_VIEWDIR only (else NULL) */
+  const float* vhead;
+  int32_t vhead_out;
+  int32_t _pad2;
 } nfi_field;
 
 /* One render call: rays of B images × HW pixels, S coarse samples (+ S fine if fine). */
@@ -105,7 +118,8 @@ typedef struct nfi_render_args {
   float* t_saved;      /* [B*HW,N]   */
   float* sigma_saved;  /* [B*HW,N]   */
   float* rgb_saved;    /* [B*HW,3,N] */
-  float* y_saved;      /* [B*HW,11,N] decoder outputs (distance, 10 logits) in evaluation order:
+  float* y_saved;      /* [B*HW,NOUT,N] decoder outputs (distance, 10 logits; NOUT = 33 with
+                          NFI_HEAD_VIEWDIR: distance, 32 features) in evaluation order:
                           coarse 0..S-1 then fine S..2S-1 (lets the backward skip the forward MLP) */
   int16_t* perm;       /* [B*HW,N] merged sample k -> evaluation index */
   float* x_saved;      /* [B*HW*N,32] decoder inputs (mean tap features) in evaluation order; optional
@@ -134,6 +148,7 @@ typedef struct nfi_render_grad_args {
   const int32_t* tile_counts; /* the forward's tile_counts, or NULL (the backward counts itself) */
   void* workspace;      /* device scratch of nfi_render_backward_workspace_bytes() bytes */
   int64_t workspace_bytes;
+  float* d_xray;        /* NFI_HEAD_VIEWDIR: [B*HW,32] dL/d xray, ACCUMULATED into (zero it); else NULL */
 } nfi_render_grad_args;
 
 int32_t nfi_abi_version(void);
@@ -144,6 +159,12 @@ const char* nfi_last_error(void);
  * NFI_HEAD_RGB_SIGMOID is passed zero-padded to 11 rows). */
 int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, const float* b2,
                          float g1, float g2, float gb, float* dec, void* stream);
+/* The same for a decoder of nout outputs: 11 (= nfi_decoder_pack) or 33 (NFI_HEAD_VIEWDIR:
+ * TriplanarDecoder(32, 32), generator.py:376-377); w2 [nout,64], b2 [nout]; dec holds
+ * nfi_decoder_size(nout) floats. */
+int64_t nfi_decoder_size(int32_t nout);
+int32_t nfi_decoder_pack_n(const float* w1, const float* b1, const float* w2, const float* b2, int32_t nout,
+                           float g1, float g2, float gb, float* dec, void* stream);
 
 /* [B,3,32,R,R] channel-major planes (generator.py:476-477) <-> texel-major [B,3,R,R,32]. */
 int32_t nfi_planes_to_texel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream);

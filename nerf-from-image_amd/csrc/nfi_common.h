@@ -23,13 +23,37 @@ constexpr int NA = 10;     // attention values (palette rows)
 //   DT3 [hb][l][t]     W2s[4t + (l>>4)][16hb + (l&15)]          d hidden = W2s^T gy, A (t = 0..2)
 //   DT4 [cb][hb][l][r] W1s[16hb + 4(l>>4) + r][16cb + (l&15)]   d x = W1s^T d z, A
 //   DB2 [16]           b2s (zero padded)
-constexpr int DT1 = 0;
-constexpr int DB1 = DT1 + 4 * 64 * 8;
-constexpr int DT2 = DB1 + 4 * 64 * 4;
-constexpr int DT3 = DT2 + 4 * 64 * 4;
-constexpr int DT4 = DT3 + 4 * 64 * 4;
-constexpr int DB2 = DT4 + 2 * 4 * 64 * 4;
-constexpr int DEC_SIZE = DB2 + 16;             // 7184 floats
+// The same layout for a decoder of NOUT outputs (NOB row blocks of 16; the d hidden product
+// W2s^T dY^T runs over KT k-steps of 4 output rows, stored padded to KTP):
+//   DT2 [ob][hb][l][r] W2s[16ob + (l&15)][16hb + 4(l>>4) + r]
+//   DT3 [hb][l][t]     W2s[4t + (l>>4)][16hb + (l&15)]          (t < KTP; rows >= NOUT zero)
+//   DB2 [16 NOB]       b2s
+// NOUT = 11: 1 distance + 10 attention logits (or 3 colour features, zero padded) — the
+// inversion field; NOUT = 33: 1 distance + 32 features for the view-direction mapper
+// (--use_viewdir, generator.py:376-377).
+template <int NOUT>
+struct DecL {
+  static constexpr int NOB = (NOUT + 15) / 16;
+  static constexpr int KT = (NOUT + 3) / 4;
+  static constexpr int KTP = (KT + 3) / 4 * 4;
+  static constexpr int DT1 = 0;
+  static constexpr int DB1 = DT1 + 4 * 64 * 8;
+  static constexpr int DT2 = DB1 + 4 * 64 * 4;
+  static constexpr int DT3 = DT2 + NOB * 4 * 64 * 4;
+  static constexpr int DT4 = DT3 + 4 * 64 * KTP;
+  static constexpr int DB2 = DT4 + 2 * 4 * 64 * 4;
+  static constexpr int SIZE = DB2 + 16 * NOB;
+};
+constexpr int NOV = 33;    // decoder outputs with the view-direction mapper
+constexpr int NVF = 32;    // view-direction mapper features (generator.py:376-377, 398-399)
+constexpr int DT1 = DecL<NO>::DT1;
+constexpr int DB1 = DecL<NO>::DB1;
+constexpr int DT2 = DecL<NO>::DT2;
+constexpr int DT3 = DecL<NO>::DT3;
+constexpr int DT4 = DecL<NO>::DT4;
+constexpr int DB2 = DecL<NO>::DB2;
+constexpr int DEC_SIZE = DecL<NO>::SIZE;       // 7184 floats
+static_assert(DEC_SIZE == 7184 && DT4 == 5120, "inversion decoder layout");
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

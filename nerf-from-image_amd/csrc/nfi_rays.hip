@@ -281,33 +281,35 @@ __global__ void __launch_bounds__(64) segsum_pass2(const float* __restrict__ par
 // ---------------------------------------------------------------------------------------
 // Decoder packing (EqualizedLinear gains, stylegan.py:173-176)
 // ---------------------------------------------------------------------------------------
+template <int NOUT>
 __global__ void decoder_pack_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
                                     const float* __restrict__ w2, const float* __restrict__ b2, float g1,
                                     float g2, float gb, float* __restrict__ dec) {
+  using L = DecL<NOUT>;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= DEC_SIZE) return;
-  // (w1 [64,32], w2 [11,64] row-major; scaled as EqualizedLinear does, stylegan.py:173-176)
+  if (t >= L::SIZE) return;
+  // (w1 [64,32], w2 [NOUT,64] row-major; scaled as EqualizedLinear does, stylegan.py:173-176)
   auto W1 = [&](int h, int c) { return w1[h * NC + c] * g1; };
-  auto W2 = [&](int o, int h) { return (o < NO) ? w2[o * NH + h] * g2 : 0.f; };
+  auto W2 = [&](int o, int h) { return (o < NOUT) ? w2[o * NH + h] * g2 : 0.f; };
   float v = 0.f;
-  if (t < DB1) {
+  if (t < L::DB1) {
     const int hb = t / 512, l = (t / 8) % 64, k = t % 8;
     v = W1(16 * hb + (l & 15), 8 * (l >> 4) + k);
-  } else if (t < DT2) {
-    const int u = t - DB1, hb = u / 256, l = (u / 4) % 64, r = u % 4;
+  } else if (t < L::DT2) {
+    const int u = t - L::DB1, hb = u / 256, l = (u / 4) % 64, r = u % 4;
     v = b1[16 * hb + 4 * (l >> 4) + r] * gb;
-  } else if (t < DT3) {
-    const int u = t - DT2, hb = u / 256, l = (u / 4) % 64, r = u % 4;
-    v = W2(l & 15, 16 * hb + 4 * (l >> 4) + r);
-  } else if (t < DT4) {
-    const int u = t - DT3, hb = u / 256, l = (u / 4) % 64, k = u % 4;
-    v = (k < 3) ? W2(4 * k + (l >> 4), 16 * hb + (l & 15)) : 0.f;
-  } else if (t < DB2) {
-    const int u = t - DT4, cb = u / 1024, hb = (u / 256) % 4, l = (u / 4) % 64, r = u % 4;
+  } else if (t < L::DT3) {
+    const int u = t - L::DT2, ob = u / 1024, hb = (u / 256) % 4, l = (u / 4) % 64, r = u % 4;
+    v = W2(16 * ob + (l & 15), 16 * hb + 4 * (l >> 4) + r);
+  } else if (t < L::DT4) {
+    const int u = t - L::DT3, hb = u / (64 * L::KTP), l = (u / L::KTP) % 64, k = u % L::KTP;
+    v = (k < L::KT) ? W2(4 * k + (l >> 4), 16 * hb + (l & 15)) : 0.f;
+  } else if (t < L::DB2) {
+    const int u = t - L::DT4, cb = u / 1024, hb = (u / 256) % 4, l = (u / 4) % 64, r = u % 4;
     v = W1(16 * hb + 4 * (l >> 4) + r, 16 * cb + (l & 15));
   } else {
-    const int k = t - DB2;
-    v = (k < NO) ? b2[k] * gb : 0.f;
+    const int k = t - L::DB2;
+    v = (k < NOUT) ? b2[k] * gb : 0.f;
   }
   dec[t] = v;
 }
@@ -357,6 +359,7 @@ using namespace nfi;
 
 extern "C" {
 
+static_assert(DecL<NO>::SIZE == NFI_DEC_SIZE && DecL<NOV>::SIZE == NFI_DEC_SIZE_VIEWDIR, "nfi.h decoder sizes");
 int32_t nfi_abi_version(void) { return NFI_ABI_VERSION; }
 const char* nfi_last_error(void) { return nfi::g_err.c_str(); }
 
@@ -411,9 +414,25 @@ int32_t nfi_segment_sum(const float* in, int32_t B, int32_t M, int32_t K, float*
 
 int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, const float* b2, float g1,
                          float g2, float gb, float* dec, void* stream) {
+  return nfi_decoder_pack_n(w1, b1, w2, b2, NO, g1, g2, gb, dec, stream);
+}
+
+int64_t nfi_decoder_size(int32_t nout) {
+  if (nout == NO) return DecL<NO>::SIZE;
+  if (nout == NOV) return DecL<NOV>::SIZE;
+  return -1;
+}
+
+int32_t nfi_decoder_pack_n(const float* w1, const float* b1, const float* w2, const float* b2, int32_t nout,
+                           float g1, float g2, float gb, float* dec, void* stream) {
   NFI_REQUIRE(w1 && b1 && w2 && b2 && dec, "decoder_pack: null pointer");
-  decoder_pack_kernel<<<(DEC_SIZE + 255) / 256, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1, g2, gb,
-                                                                                dec);
+  NFI_REQUIRE(nout == NO || nout == NOV, "decoder_pack: nout must be %d or %d (got %d)", NO, NOV, nout);
+  if (nout == NO)
+    decoder_pack_kernel<NO><<<(DecL<NO>::SIZE + 255) / 256, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1,
+                                                                                            g2, gb, dec);
+  else
+    decoder_pack_kernel<NOV><<<(DecL<NOV>::SIZE + 255) / 256, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1,
+                                                                                              g2, gb, dec);
   NFI_CHECK_LAUNCH("decoder_pack_kernel");
   return NFI_OK;
 }

@@ -371,9 +371,12 @@ __device__ __forceinline__ f4v layer1(f4v ta, f4v tb, f4v b, f4v xa, f4v xb) {
 }
 
 // Decoder forward for the points of the wave's X tile (LDS, rows of XS floats); returns point
-// l's 11 outputs.  The tile is reused as scratch (callers re-sync before writing it).
+// l's NOUT outputs.  The tile is reused as scratch (callers re-sync before writing it).
+template <int NOUT>
 __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, float* __restrict__ X,
-                                                 float y[NO]) {
+                                                 float y[NOUT]) {
+  using L = DecL<NOUT>;
+  constexpr int NOB = L::NOB;
   const int l = lane_id(), j = l & 15, q = l >> 4;
   f4v xa[4], xb[4];
 #pragma unroll
@@ -381,67 +384,92 @@ __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, 
     xa[sb] = ld4(X + (16 * sb + j) * XS + 8 * q);
     xb[sb] = ld4(X + (16 * sb + j) * XS + 8 * q + 4);
   }
-  f4v Y[4];
+  f4v Y[NOB][4];
 #pragma unroll
-  for (int sb = 0; sb < 4; ++sb) Y[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) Y[ob][sb] = f4v{0.f, 0.f, 0.f, 0.f};
 #ifndef NFI_MLP_PREFETCH
 #define NFI_MLP_PREFETCH 1
 #endif
 #if NFI_MLP_PREFETCH
   // operand tables of hidden block hb + 1 are loaded while block hb runs (L1/L2 round trips
   // otherwise serialise with the MFMA chains: 16 more VGPRs, within occupancy 3)
-  f4v ta = ld4(dec + DT1 + l * 8), tb = ld4(dec + DT1 + l * 8 + 4);
-  f4v b = ld4(dec + DB1 + l * 4), t2 = ld4(dec + DT2 + l * 4);
+  f4v ta = ld4(dec + L::DT1 + l * 8), tb = ld4(dec + L::DT1 + l * 8 + 4);
+  f4v b = ld4(dec + L::DB1 + l * 4);
+  f4v t2[NOB];
+#pragma unroll
+  for (int ob = 0; ob < NOB; ++ob) t2[ob] = ld4(dec + L::DT2 + (ob * 256 + l) * 4);
 #pragma unroll
   for (int hb = 0; hb < 4; ++hb) {
-    f4v nta = ta, ntb = tb, nb = b, nt2 = t2;
+    f4v nta = ta, ntb = tb, nb = b, nt2[NOB];
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob) nt2[ob] = t2[ob];
     if (hb < 3) {
       const int hn = hb + 1;
-      nta = ld4(dec + DT1 + (hn * 64 + l) * 8);
-      ntb = ld4(dec + DT1 + (hn * 64 + l) * 8 + 4);
-      nb = ld4(dec + DB1 + (hn * 64 + l) * 4);
-      nt2 = ld4(dec + DT2 + (hn * 64 + l) * 4);
+      nta = ld4(dec + L::DT1 + (hn * 64 + l) * 8);
+      ntb = ld4(dec + L::DT1 + (hn * 64 + l) * 8 + 4);
+      nb = ld4(dec + L::DB1 + (hn * 64 + l) * 4);
+#pragma unroll
+      for (int ob = 0; ob < NOB; ++ob) nt2[ob] = ld4(dec + L::DT2 + ((ob * 4 + hn) * 64 + l) * 4);
     }
     __builtin_amdgcn_sched_barrier(0);   // (keeps the scheduler from sinking the loads to their use)
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
       const f4v z = layer1(ta, tb, b, xa[sb], xb[sb]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Y[sb] = mfma4(t2[r], softplus(z[r]), Y[sb]);
+      for (int r = 0; r < 4; ++r) {
+        const float sp = softplus(z[r]);
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) Y[ob][sb] = mfma4(t2[ob][r], sp, Y[ob][sb]);
+      }
     }
     ta = nta;
     tb = ntb;
     b = nb;
-    t2 = nt2;
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob) t2[ob] = nt2[ob];
   }
 #else
 #pragma unroll
   for (int hb = 0; hb < 4; ++hb) {
-    const f4v ta = ld4(dec + DT1 + (hb * 64 + l) * 8), tb = ld4(dec + DT1 + (hb * 64 + l) * 8 + 4);
-    const f4v b = ld4(dec + DB1 + (hb * 64 + l) * 4);
-    const f4v t2 = ld4(dec + DT2 + (hb * 64 + l) * 4);
+    const f4v ta = ld4(dec + L::DT1 + (hb * 64 + l) * 8), tb = ld4(dec + L::DT1 + (hb * 64 + l) * 8 + 4);
+    const f4v b = ld4(dec + L::DB1 + (hb * 64 + l) * 4);
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
       const f4v z = layer1(ta, tb, b, xa[sb], xb[sb]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Y[sb] = mfma4(t2[r], softplus(z[r]), Y[sb]);
+      for (int r = 0; r < 4; ++r) {
+        const float sp = softplus(z[r]);
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob)
+          Y[ob][sb] = mfma4(ld4(dec + L::DT2 + ((ob * 4 + hb) * 64 + l) * 4)[r], sp, Y[ob][sb]);
+      }
     }
   }
 #endif
-  // lane (j, q) holds outputs 4q..4q+3 of point 16sb + j: transpose through the tile
+  // lane (j, q) holds outputs 16ob + 4q..4q+3 of point 16sb + j: transpose through the tile
+  // (outputs past NOUT's last quad are not stored: 33 outputs use columns 0..35 of the XS = 36 row)
   wave_lds_sync();
 #pragma unroll
-  for (int sb = 0; sb < 4; ++sb) *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 4 * q) = Y[sb];
+  for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+      if (16 * NOB <= XS || ob + 1 < NOB || 16 * ob + 4 * q < NOUT)
+        *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 16 * ob + 4 * q) = Y[ob][sb];
   wave_lds_sync();
 #pragma unroll
-  for (int o = 0; o < NO; ++o) y[o] = X[l * XS + o] + dec[DB2 + o];
+  for (int o = 0; o < NOUT; ++o) y[o] = X[l * XS + o] + dec[L::DB2 + o];
 }
+static_assert(4 * DecL<NOV>::KT <= XS, "33 decoder outputs fit an X tile row");
 
 // Decoder input-gradient (weights frozen during inversion, run.py:630-632) for 64 points:
 // xa/xb as layer1's operands for blocks sb; dY^T operands gyb[sb][t] = dY[16sb + j][4t + q];
 // returns dX^T accumulators gxo[cb][sb] (lane: channels 16cb + 4q + reg of point 16sb + j).
+template <int NOUT>
 __device__ __forceinline__ void mlp_backward_mfma(const float* __restrict__ dec, const f4v xa[4], const f4v xb[4],
-                                                  const float gyb[4][3], f4v gxo[2][4]) {
+                                                  const float gyb[4][DecL<NOUT>::KT], f4v gxo[2][4]) {
+  using L = DecL<NOUT>;
   const int l = lane_id();
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb)
@@ -449,18 +477,19 @@ __device__ __forceinline__ void mlp_backward_mfma(const float* __restrict__ dec,
     for (int sb = 0; sb < 4; ++sb) gxo[cb][sb] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int hb = 0; hb < 4; ++hb) {
-    const f4v ta = ld4(dec + DT1 + (hb * 64 + l) * 8), tb = ld4(dec + DT1 + (hb * 64 + l) * 8 + 4);
-    const f4v b = ld4(dec + DB1 + (hb * 64 + l) * 4);
-    const f4v t3 = ld4(dec + DT3 + (hb * 64 + l) * 4);
-    const f4v t40 = ld4(dec + DT4 + ((0 * 4 + hb) * 64 + l) * 4);
-    const f4v t41 = ld4(dec + DT4 + ((1 * 4 + hb) * 64 + l) * 4);
+    const f4v ta = ld4(dec + L::DT1 + (hb * 64 + l) * 8), tb = ld4(dec + L::DT1 + (hb * 64 + l) * 8 + 4);
+    const f4v b = ld4(dec + L::DB1 + (hb * 64 + l) * 4);
+    f4v t3[L::KTP / 4];
+#pragma unroll
+    for (int u = 0; u < L::KTP / 4; ++u) t3[u] = ld4(dec + L::DT3 + (hb * 64 + l) * L::KTP + 4 * u);
+    const f4v t40 = ld4(dec + L::DT4 + ((0 * 4 + hb) * 64 + l) * 4);
+    const f4v t41 = ld4(dec + L::DT4 + ((1 * 4 + hb) * 64 + l) * 4);
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
       const f4v z = layer1(ta, tb, b, xa[sb], xb[sb]);
       f4v gh = f4v{0.f, 0.f, 0.f, 0.f};
-      gh = mfma4(t3[0], gyb[sb][0], gh);
-      gh = mfma4(t3[1], gyb[sb][1], gh);
-      gh = mfma4(t3[2], gyb[sb][2], gh);
+#pragma unroll
+      for (int t = 0; t < L::KT; ++t) gh = mfma4(t3[t >> 2][t & 3], gyb[sb][t], gh);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float gz = gh[r] * softplus_grad(z[r]);
@@ -525,6 +554,49 @@ __device__ __forceinline__ void head_forward(const float y[NO], float mask, floa
 #pragma unroll
     for (int k = 0; k < NA; ++k) a = fmaf(h.p[k], pal[k * 3 + c], a);
     h.rgb[c] = a;
+  }
+}
+
+// View-direction mapper closure (generator.py:242-250, applied at :661-663) on one point: the
+// colour logits are output(leaky_relu(xray + features, 0.2)) with xr the ray's mapper trunk
+// output (generator.py:223-238, run.py:216-219) and vh the gain-scaled output layer ([O][32]
+// weights, then [O] bias; O = 10 attention logits or 3 colour features).  y11 = {distance,
+// logits zero-padded to 10} is what head_forward reads for the other fields.
+__device__ __forceinline__ void viewdir_head_in(const float y[NOV], const float* __restrict__ xr,
+                                                const float* __restrict__ vh, int O, float y11[NO]) {
+  float hv[NVF];
+#pragma unroll
+  for (int k = 0; k < NVF; ++k) {
+    const float pre = fadd(xr[k], y[1 + k]);
+    hv[k] = pre > 0.f ? pre : fmul(pre, 0.2f);     // LeakyReLU(0.2) (ATen: x > 0 ? x : x * slope)
+  }
+  y11[0] = y[0];
+#pragma unroll
+  for (int o = 0; o < NA; ++o) {
+    float acc = 0.f;
+    if (o < O) {
+#pragma unroll
+      for (int k = 0; k < NVF; ++k) acc = fmaf(hv[k], vh[o * NVF + k], acc);
+      acc = fadd(acc, vh[O * NVF + o]);
+    }
+    y11[1 + o] = acc;
+  }
+}
+
+// Backward of viewdir_head_in: g11 = dL/d y11 -> dL/d y (33); dL/d xray = dL/d features (the sum
+// xray + features passes the gradient to both).
+__device__ __forceinline__ void viewdir_head_bwd(const float y[NOV], const float* __restrict__ xr,
+                                                 const float* __restrict__ vh, int O, const float g11[NO],
+                                                 float gy[NOV]) {
+  gy[0] = g11[0];
+#pragma unroll
+  for (int k = 0; k < NVF; ++k) {
+    float g = 0.f;
+#pragma unroll
+    for (int o = 0; o < NA; ++o)
+      if (o < O) g = fmaf(vh[o * NVF + k], g11[1 + o], g);
+    const float pre = fadd(xr[k], y[1 + k]);
+    gy[1 + k] = pre > 0.f ? g : fmul(g, 0.2f);
   }
 }
 
@@ -625,6 +697,7 @@ __device__ __forceinline__ void load_ray(const nfi_render_args& a, long long r, 
 }
 
 // Evaluate the field at the (up to 64) points t (one per lane; lanes >= npts ignored).
+template <int NOUT>
 __device__ __forceinline__ void field_eval(const nfi_render_args& a, const PlaneView& pv, const RayCtx& R,
                                            float t, int npts, float* __restrict__ X, float& sigma,
                                            float rgb[3], int eval_base NFI_STAMP_PARAM) {
@@ -643,17 +716,24 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
     }
   }
   NFI_STAMP(1)
-  float y[NO];
-  mlp_forward_tile(a.field.dec, X, y);
+  float y[NOUT];
+  mlp_forward_tile<NOUT>(a.field.dec, X, y);
   NFI_STAMP(2)
   if (a.y_saved && lane_id() < npts) {     // (no saved state in forward-only calls)
     const int N = a.fine ? 2 * a.S : a.S;
-    float* ys = a.y_saved + R.r * NO * N + eval_base + lane_id();
+    float* ys = a.y_saved + R.r * NOUT * N + eval_base + lane_id();
 #pragma unroll
-    for (int k = 0; k < NO; ++k) ys[k * N] = y[k];
+    for (int k = 0; k < NOUT; ++k) ys[k * N] = y[k];
   }
   Head h;
-  head_forward(y, P.mask, a.field.inv_alpha, a.field.beta, a.field.palette + R.b * (NA * 3), a.field.heads, h);
+  if constexpr (NOUT == NOV) {
+    float y11[NO];
+    viewdir_head_in(y, a.field.xray + R.r * NVF, a.field.vhead, a.field.vhead_out, y11);
+    head_forward(y11, P.mask, a.field.inv_alpha, a.field.beta, a.field.palette + R.b * (NA * 3), a.field.heads,
+                 h);
+  } else {
+    head_forward(y, P.mask, a.field.inv_alpha, a.field.beta, a.field.palette + R.b * (NA * 3), a.field.heads, h);
+  }
   sigma = h.sigma;
   rgb[0] = h.rgb[0];
   rgb[1] = h.rgb[1];
@@ -693,11 +773,12 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 // ---------------------------------------------------------------------------------------
 // Forward kernel.  SPL = coarse samples per lane (S <= 64*SPL), NPL = merged per lane.
 // ---------------------------------------------------------------------------------------
-template <int SPL, int NPL, bool FINE>
 #ifndef NFI_FWD_OCC
 #define NFI_FWD_OCC 3
 #endif
-__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? NFI_FWD_OCC : 2) render_fwd_kernel(nfi_render_args a) {
+template <int SPL, int NPL, bool FINE, int NOUT>
+__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NFI_FWD_OCC : 2)
+    render_fwd_kernel(nfi_render_args a) {
   constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
   // per-wave LDS: the X tile; the merge / sample_pdf arrays alias it (they are live only
   // outside field_eval), which keeps a workgroup at 36 KiB
@@ -742,7 +823,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? NFI_FWD_OCC : 2)
     tc[e] = t;
     sc[e] = 0.f;
     cc[e][0] = cc[e][1] = cc[e][2] = 0.f;
-    if (e * 64 < S) field_eval(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64 NFI_STAMP_ARG);
+    if (e * 64 < S) field_eval<NOUT>(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64 NFI_STAMP_ARG);
   }
 
   if constexpr (FINE) {
@@ -848,7 +929,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2) ? NFI_FWD_OCC : 2)
     for (int e = 0; e < SPL; ++e) {
       sf[e] = 0.f;
       cf[e][0] = cf[e][1] = cf[e][2] = 0.f;
-      if (e * 64 < S) field_eval(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64 NFI_STAMP_ARG);
+      if (e * 64 < S) field_eval<NOUT>(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64 NFI_STAMP_ARG);
     }
     // ---- merge: stable sort of cat(z_coarse, z_fine) (run.py:283-288, 312-319) ----
 #pragma unroll
@@ -1017,6 +1098,7 @@ struct BwdArgs {
   int* cursor;            // [K] tile fill cursors (NULL: bins filled by bin_fill_kernel)
   int4* list;             // [3*rays*N] tile entries
   TileGrid tg;            // tile grid of a plane
+  float* d_xray;          // [rays][32] dL/d view-direction mapper output (NFI_HEAD_VIEWDIR), accumulated
 };
 
 // Compositing backward (nerf_utils.py:125-163 under autograd), one wave per ray:
@@ -1106,8 +1188,10 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 #endif
 // VARIANT = false: the inversion field (heads == 0 at compile time, the register budget of the
 // hot path is not shared with the other heads); true: nfi_field.heads read at run time.
-template <bool VARIANT>
-__global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
+// NOUT = 33: the view-direction mapper field (NFI_HEAD_VIEWDIR, always with VARIANT).
+template <bool VARIANT, int NOUT>
+__global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
+  using L = DecL<NOUT>;
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -1165,27 +1249,34 @@ __global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_rende
   }
   NFI_STAMP(17)
   // decoder outputs saved by the forward (no forward MLP here)
-  float y[NO];
+  float y[NOUT];
   {
-    const float* ys = a.y_saved + r * NO * N + ei;
+    const float* ys = a.y_saved + r * NOUT * N + ei;
 #pragma unroll
-    for (int k = 0; k < NO; ++k) y[k] = v ? ys[k * N] : 0.f;
+    for (int k = 0; k < NOUT; ++k) y[k] = v ? ys[k * N] : 0.f;
   }
   float gy[NO];
+  float y11[NO];
+  if constexpr (NOUT == NOV) {
+    viewdir_head_in(y, a.field.xray + r * NVF, a.field.vhead, a.field.vhead_out, y11);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NO; ++k) y11[k] = y[k];
+  }
   {
     Head h;
     const int heads = VARIANT ? a.field.heads : 0;
-    head_forward(y, pmask, a.field.inv_alpha, a.field.beta, pal, heads, h);
+    head_forward(y11, pmask, a.field.inv_alpha, a.field.beta, pal, heads, h);
     const float gs = v ? g.gsig[r * N + i] : 0.f;
     if (heads & NFI_HEAD_NERF_DENSITY) {
       // sigma -> d: softplus_backward of d - 1 (ATen: z > 20 ? g : g * e^z / (e^z + 1)), :637-641
-      const float z = fsub(y[0], 1.f);
+      const float z = fsub(y11[0], 1.f);
       const float gm = fmul(gs, fsub(1.f, pmask));
       const float ez = expf(z);
       gy[0] = z > 20.f ? gm : gm * (ez / (ez + 1.f));
     } else {
       // sigma -> distance  (generator.py:629-636, laplace_cdf generator.py:30-33)
-      const float xn = -y[0];
+      const float xn = -y11[0];
       const float sgn = tsign(xn);
       const float ex2 = expf(-fabsf(xn) / a.field.beta);
       const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
@@ -1234,23 +1325,40 @@ __global__ void __launch_bounds__(256, NFI_FIELD_OCC) field_bwd_kernel(nfi_rende
     const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
     if (l < NA * 3) g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = sh;
   }
-  // dY^T operands through the tile: row = point, 12 columns (11 outputs + zero)
+  // dY^T operands through the tile: row = point, 4 KT columns (NOUT outputs + zeros)
+  float gyo[NOUT];
+  if constexpr (NOUT == NOV) {
+    viewdir_head_bwd(y, a.field.xray + r * NVF, a.field.vhead, a.field.vhead_out, gy, gyo);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NO; ++k) gyo[k] = gy[k];
+  }
   wave_lds_sync();
 #pragma unroll
-  for (int o = 0; o < NO; ++o) X[l * XS + o] = gy[o];
-  X[l * XS + NO] = 0.f;
+  for (int o = 0; o < NOUT; ++o) X[l * XS + o] = gyo[o];
+#pragma unroll
+  for (int o = NOUT; o < 4 * L::KT; ++o) X[l * XS + o] = 0.f;
   wave_lds_sync();
-  float gyb[4][3];
+  float gyb[4][L::KT];
   {
     const int j = l & 15, q = l >> 4;
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
-      for (int t = 0; t < 3; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+      for (int t = 0; t < L::KT; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+  }
+  if constexpr (NOUT == NOV) {
+    // dL/d xray of this ray chunk: column sums of the feature gradients (tile columns 1..32)
+    const int col = l & 31, r0 = (l >> 5) * 32;
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jj = 0; jj < 32; ++jj) s4[jj & 3] += X[(r0 + jj) * XS + 1 + col];
+    const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
+    if (l < NVF) unsafeAtomicAdd(g.d_xray + r * NVF + l, sh);
   }
   NFI_STAMP(18)
   f4v gxo[2][4];
-  mlp_backward_mfma(a.field.dec, xa, xb, gyb, gxo);
+  mlp_backward_mfma<NOUT>(a.field.dec, xa, xb, gyb, gxo);
   NFI_STAMP(19)
   // x = (e1+e2+e3)/3: each plane's tap feature gradient is dX/3.  Lane (j, q) holds channels
   // 16cb + 4q.. of point 16sb + j
@@ -1694,8 +1802,9 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 //              dY = e_0, then the tap derivative by a re-gather with a per-point reduction.
 // Forward-only (the reference's callers of these outputs render without gradients).
 // ---------------------------------------------------------------------------------------
-template <int NPL>
+template <int NPL, int NOUT>
 __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
+  using L = DecL<NOUT>;
   __shared__ __attribute__((aligned(16))) float lds[4 * (XTILE + 256)];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -1763,8 +1872,18 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
       if (i < N) {
         const int ei = a.perm[r * N + i];
         float y[NA];
+        if constexpr (NOUT == NOV) {
+          // logits of the view-direction mapper closure (generator.py:661-663, 672-674)
+          float yv[NOV], y11[NO];
 #pragma unroll
-        for (int k = 0; k < NA; ++k) y[k] = a.y_saved[r * NO * N + (1 + k) * N + ei];
+          for (int k = 0; k < NOV; ++k) yv[k] = a.y_saved[r * NOV * N + k * N + ei];
+          viewdir_head_in(yv, a.field.xray + r * NVF, a.field.vhead, a.field.vhead_out, y11);
+#pragma unroll
+          for (int k = 0; k < NA; ++k) y[k] = y11[1 + k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < NA; ++k) y[k] = a.y_saved[r * NO * N + (1 + k) * N + ei];
+        }
         // softmax as head_forward forms it
         float m = y[0];
 #pragma unroll
@@ -1796,7 +1915,7 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
       const int npts = min(64, N - e * 64);
       // d sdf / d x for the chunk's points: decoder backward with dY = e_0 on the matrix cores
       f4v xa[4], xb[4];
-      float gyb[4][3];
+      float gyb[4][L::KT];
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb) {
         const int ip = e * 64 + 16 * sb + j16;
@@ -1808,10 +1927,10 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
           xb[sb] = ld4(xr + 4);
         }
 #pragma unroll
-        for (int tt = 0; tt < 3; ++tt) gyb[sb][tt] = (tt == 0 && q == 0) ? 1.f : 0.f;
+        for (int tt = 0; tt < L::KT; ++tt) gyb[sb][tt] = (tt == 0 && q == 0) ? 1.f : 0.f;
       }
       f4v gxo[2][4];
-      mlp_backward_mfma(a.field.dec, xa, xb, gyb, gxo);
+      mlp_backward_mfma<NOUT>(a.field.dec, xa, xb, gyb, gxo);
       wave_lds_sync();
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb)
@@ -1982,7 +2101,7 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   return w;
 }
 
-template <int SPL, int NPL, bool FINE>
+template <int SPL, int NPL, bool FINE, int NOUT>
 static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
   const long long nrays = (long long)a->B * a->HW;
   if (a->tile_counts) {
@@ -1990,14 +2109,15 @@ static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
     NFI_REQUIRE(hipMemsetAsync(a->tile_counts, 0, (size_t)a->B * 3 * tg.nx * tg.ny * 4, s) == hipSuccess,
                 "render_forward: memset failed");
   }
-  render_fwd_kernel<SPL, NPL, FINE><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
+  render_fwd_kernel<SPL, NPL, FINE, NOUT><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
   NFI_CHECK_LAUNCH("render_fwd_kernel");
   if (a->extras) {
     const int N = FINE ? 2 * a->S : a->S;
     const unsigned grid = (unsigned)((nrays + 3) / 4);
-    if (N <= 64) extras_kernel<1><<<grid, 256, 0, s>>>(*a);
-    else if (N <= 128) extras_kernel<2><<<grid, 256, 0, s>>>(*a);
-    else extras_kernel<4><<<grid, 256, 0, s>>>(*a);
+    constexpr int EN = NOUT;
+    if (N <= 64) extras_kernel<1, EN><<<grid, 256, 0, s>>>(*a);
+    else if (N <= 128) extras_kernel<2, EN><<<grid, 256, 0, s>>>(*a);
+    else extras_kernel<4, EN><<<grid, 256, 0, s>>>(*a);
     NFI_CHECK_LAUNCH("extras_kernel");
   }
   return NFI_OK;
@@ -2044,17 +2164,19 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   // 2) per-ray compositing backward, then per-(ray, 64-sample chunk) field backward
   const int NPL = (N + 63) / 64;
   BwdArgs bg{g->g_rgb, g->g_mask, g->d_palette_ray, g->g_ro, g->g_rd, w.gfeat, w.gsig, w.wts, NPL,
-             fwd_counts ? w.cursor : nullptr, w.list, tg};
+             fwd_counts ? w.cursor : nullptr, w.list, tg, g->d_xray};
   const unsigned rb = (unsigned)((nrays + 3) / 4);
   if (do_field) {
     if (NPL <= 1) composite_bwd_kernel<1><<<rb, 256, 0, s>>>(*a, bg);
     else if (NPL <= 2) composite_bwd_kernel<2><<<rb, 256, 0, s>>>(*a, bg);
     else composite_bwd_kernel<4><<<rb, 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("composite_bwd_kernel");
-    if (a->field.heads)
-      field_bwd_kernel<true><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+    if (a->field.heads & NFI_HEAD_VIEWDIR)
+      field_bwd_kernel<true, NOV><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+    else if (a->field.heads)
+      field_bwd_kernel<true, NO><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
     else
-      field_bwd_kernel<false><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
+      field_bwd_kernel<false, NO><<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg);
     NFI_CHECK_LAUNCH("field_bwd_kernel");
   }
 #if defined(NFI_ABLATE) && NFI_ABLATE == 5
@@ -2084,17 +2206,25 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   return NFI_OK;
 }
 
-static int dispatch_fwd(const nfi_render_args* a, hipStream_t s) {
+template <int NOUT>
+static int dispatch_fwd_n(const nfi_render_args* a, hipStream_t s) {
   const int S = a->S;
   if (a->fine) {
-    if (S >= 3 && S <= 32) return launch_fwd<1, 1, true>(a, s);
-    if (S >= 3 && S <= 64) return launch_fwd<1, 2, true>(a, s);
-    if (S >= 3 && S <= 128) return launch_fwd<2, 4, true>(a, s);
+    if (S >= 3 && S <= 32) return launch_fwd<1, 1, true, NOUT>(a, s);
+    if (S >= 3 && S <= 64) return launch_fwd<1, 2, true, NOUT>(a, s);
+    if (S >= 3 && S <= 128) return launch_fwd<2, 4, true, NOUT>(a, s);
   } else {
-    if (S >= 1 && S <= 64) return launch_fwd<1, 1, false>(a, s);
-    if (S >= 1 && S <= 128) return launch_fwd<2, 2, false>(a, s);
-    if (S >= 1 && S <= 256) return launch_fwd<4, 4, false>(a, s);
+    if (S >= 1 && S <= 64) return launch_fwd<1, 1, false, NOUT>(a, s);
+    if (S >= 1 && S <= 128) return launch_fwd<2, 2, false, NOUT>(a, s);
+    if (S >= 1 && S <= 256) return launch_fwd<4, 4, false, NOUT>(a, s);
   }
+  return NFI_EINVAL;
+}
+
+static int dispatch_fwd(const nfi_render_args* a, hipStream_t s) {
+  const int S = a->S;
+  const int e = (a->field.heads & NFI_HEAD_VIEWDIR) ? dispatch_fwd_n<NOV>(a, s) : dispatch_fwd_n<NO>(a, s);
+  if (e != NFI_EINVAL) return e;
   set_error("render: unsupported samples per ray S=%d (fine=%d): need 3..128 with fine sampling, "
             "1..256 without", S, (int)a->fine);
   return NFI_EINVAL;
@@ -2107,8 +2237,12 @@ static bool supported_S(const nfi_render_args* a) {
 static int validate(const nfi_render_args* a) {
   NFI_REQUIRE(a != nullptr, "render: null args");
   const nfi_field& f = a->field;
-  NFI_REQUIRE((f.heads & ~(NFI_HEAD_RGB_SIGMOID | NFI_HEAD_NERF_DENSITY)) == 0, "render: unknown heads bits 0x%x",
-              f.heads);
+  NFI_REQUIRE((f.heads & ~(NFI_HEAD_RGB_SIGMOID | NFI_HEAD_NERF_DENSITY | NFI_HEAD_VIEWDIR)) == 0,
+              "render: unknown heads bits 0x%x", f.heads);
+  NFI_REQUIRE(!(f.heads & NFI_HEAD_VIEWDIR) ||
+                  (f.xray && f.vhead && f.vhead_out == ((f.heads & NFI_HEAD_RGB_SIGMOID) ? 3 : NA)),
+              "render: NFI_HEAD_VIEWDIR needs xray, vhead and vhead_out = %d (got %d)",
+              (f.heads & NFI_HEAD_RGB_SIGMOID) ? 3 : NA, f.vhead_out);
   NFI_REQUIRE(f.planes && f.dec && (f.palette || (f.heads & NFI_HEAD_RGB_SIGMOID)), "render: null field pointer");
   NFI_REQUIRE(f.R >= 2 && f.R <= 1024, "render: plane resolution R=%d out of range [2,1024]", f.R);
   NFI_REQUIRE(f.st >= NC && 3LL * f.sq < (1LL << 31) && (long long)f.R * f.R * f.st < (1LL << 31),
@@ -2168,6 +2302,7 @@ int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args
   NFI_REQUIRE(a->x_saved && a->t_saved,
               "render_backward: the forward's saved state (x_saved, t/sigma/rgb/y/perm) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
+  NFI_REQUIRE(!(a->field.heads & NFI_HEAD_VIEWDIR) || g->d_xray, "render_backward: NFI_HEAD_VIEWDIR needs d_xray");
   return nfi::launch_bwd(a, g, (hipStream_t)stream, -1);
 }
 
@@ -2182,6 +2317,7 @@ int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_gra
               "render_backward: the forward's saved state (x_saved, t/sigma/rgb/y/perm) is required");
   NFI_REQUIRE((g->g_ro == nullptr) == (g->g_rd == nullptr), "render_backward: g_ro/g_rd must both be set or null");
   NFI_REQUIRE(stage >= 0 && stage <= 2, "render_backward_stage: stage %d not in 0..2", stage);
+  NFI_REQUIRE(!(a->field.heads & NFI_HEAD_VIEWDIR) || g->d_xray, "render_backward: NFI_HEAD_VIEWDIR needs d_xray");
   return nfi::launch_bwd(a, g, (hipStream_t)stream, stage);
 }
 

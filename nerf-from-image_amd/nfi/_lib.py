@@ -12,8 +12,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 10
+ABI_VERSION = 11
 DEC_SIZE = 7184
+DEC_SIZE_VIEWDIR = 11312
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
@@ -30,7 +31,8 @@ class NfiField(ctypes.Structure):
                 ('st', ctypes.c_int64), ('R', ctypes.c_int32), ('_pad', ctypes.c_int32),
                 ('dec', c_void_p), ('palette', c_void_p), ('inv_alpha', ctypes.c_float),
                 ('beta', ctypes.c_float), ('scene_range', ctypes.c_float),
-                ('heads', ctypes.c_int32)]
+                ('heads', ctypes.c_int32), ('xray', c_void_p), ('vhead', c_void_p),
+                ('vhead_out', ctypes.c_int32), ('_pad2', ctypes.c_int32)]
 
 
 class NfiRenderArgs(ctypes.Structure):
@@ -51,7 +53,8 @@ class NfiRenderArgs(ctypes.Structure):
 class NfiRenderGradArgs(ctypes.Structure):
     _fields_ = [('g_rgb', c_void_p), ('g_mask', c_void_p), ('d_planes', c_void_p),
                 ('d_palette_ray', c_void_p), ('g_ro', c_void_p), ('g_rd', c_void_p),
-                ('tile_counts', c_void_p), ('workspace', c_void_p), ('workspace_bytes', ctypes.c_int64)]
+                ('tile_counts', c_void_p), ('workspace', c_void_p), ('workspace_bytes', ctypes.c_int64),
+                ('d_xray', c_void_p)]
 
 
 # symbol -> (restype, argtypes); every entry point of include/nfi.h
@@ -60,6 +63,9 @@ SIGNATURES = {
     'nfi_last_error': (ctypes.c_char_p, []),
     'nfi_decoder_pack': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float,
                                           ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
+    'nfi_decoder_size': (ctypes.c_int64, [ctypes.c_int32]),
+    'nfi_decoder_pack_n': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
+                                            ctypes.c_float, ctypes.c_float, ctypes.c_float, c_void_p, c_void_p]),
     'nfi_planes_to_texel_major': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                    c_void_p, c_void_p]),
     'nfi_planes_to_channel_major': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32,

@@ -218,36 +218,50 @@ class RenderOptions:
     beta: float = 0.1            # Generator.beta
     extras: int = 0              # eval outputs: 1 normals, 2 semantics, 4 coords (nfi_render_args.extras)
     heads: int = 0               # nfi_field.heads: HEAD_RGB_SIGMOID (attention_values 0) | HEAD_NERF_DENSITY (no SDF)
+                                 # | HEAD_VIEWDIR (view-direction mapper)
 
 
 HEAD_RGB_SIGMOID = 1             # include/nfi.h NFI_HEAD_RGB_SIGMOID
 DEBUG_BACKWARD = None            # a dict: the next backward stores its workspace there (diagnostics)
 HEAD_NERF_DENSITY = 2            # include/nfi.h NFI_HEAD_NERF_DENSITY
+HEAD_VIEWDIR = 4                 # include/nfi.h NFI_HEAD_VIEWDIR
 
 
 def pack_decoder(w1, b1, w2, b2, lr_multiplier: float = 1.0) -> torch.Tensor:
     """EqualizedLinear gains (stylegan.py:173-176) folded into the packed decoder buffer.  A
     [4, 64] output layer (attention_values 0: distance + 3 colour features) is zero-padded to the
-    kernels' 11 rows."""
+    kernels' 11 rows; a [33, 64] layer (the view-direction mapper's decoder, generator.py:376-377)
+    is packed in its own layout (nfi_decoder_pack_n, nout 33)."""
     _require_device(w1, b1, w2, b2)
+    nout = 33 if w2.shape[0] == 33 else 11
     if w2.shape[0] < 11:
         w2 = torch.cat([w2.detach(), w2.new_zeros(11 - w2.shape[0], w2.shape[1])])
         b2 = torch.cat([b2.detach(), b2.new_zeros(11 - b2.shape[0])])
+    if w2.shape[0] != nout:
+        raise ValueError(f'decoder output layer must have <= 11 or 33 rows, got {w2.shape[0]}')
     lib = _lib.load()
-    dec = torch.empty((_lib.DEC_SIZE,), device=w1.device)
+    dec = torch.empty((int(lib.nfi_decoder_size(nout)),), device=w1.device)
     g1 = float(torch.tensor(lr_multiplier / math.sqrt(w1.shape[1]), dtype=torch.float32))
     g2 = float(torch.tensor(lr_multiplier / math.sqrt(w2.shape[1]), dtype=torch.float32))
     gb = float(torch.tensor(lr_multiplier, dtype=torch.float32))
-    _lib.check(lib.nfi_decoder_pack(_ptr(w1.detach().contiguous()), _ptr(b1.detach().contiguous()),
-                                    _ptr(w2.detach().contiguous()), _ptr(b2.detach().contiguous()),
-                                    g1, g2, gb, _ptr(dec), _stream(w1.device)), 'nfi_decoder_pack')
+    _lib.check(lib.nfi_decoder_pack_n(_ptr(w1.detach().contiguous()), _ptr(b1.detach().contiguous()),
+                                      _ptr(w2.detach().contiguous()), _ptr(b2.detach().contiguous()), nout,
+                                      g1, g2, gb, _ptr(dec), _stream(w1.device)), 'nfi_decoder_pack_n')
     return dec
+
+
+def pack_viewdir_head(weight, bias, lr_multiplier: float = 1.0) -> torch.Tensor:
+    """ViewDirectionMapper.output (EqualizedLinear(32, O), generator.py:216-218) -> the kernels'
+    vhead buffer: [O,32] gain-scaled weights then [O] scaled bias (nfi_field.vhead)."""
+    _require_device(weight, bias)
+    gain = float(torch.tensor(lr_multiplier / math.sqrt(weight.shape[1]), dtype=torch.float32))
+    return torch.cat([(weight.detach() * gain).reshape(-1), (bias.detach() * lr_multiplier).reshape(-1)]).contiguous()
 
 
 class _VolumeRender(torch.autograd.Function):
     @staticmethod
     def forward(ctx, planes_tm, palette, ro, rd, near, far, dec, opts: RenderOptions,
-                u_coarse, u_fine, seed: int, debug: Optional[dict]):
+                u_coarse, u_fine, seed: int, debug: Optional[dict], xray=None, vhead=None):
         lib = _lib.load()
         B, _, R, R2, C = planes_tm.shape
         H, W = ro.shape[1], ro.shape[2]
@@ -266,7 +280,9 @@ class _VolumeRender(torch.autograd.Function):
         t_saved = torch.empty((n, N), device=dev) if keep else None
         s_saved = torch.empty((n, N), device=dev) if keep else None
         c_saved = torch.empty((n, 3, N), device=dev) if keep else None
-        y_saved = torch.empty((n, 11, N), device=dev) if keep else None
+        nout = 33 if opts.heads & HEAD_VIEWDIR else 11
+        y_saved = torch.empty((n, nout, N), device=dev) if keep else None
+        xray_c = None if xray is None else xray.contiguous()
         perm = torch.empty((n, N), device=dev, dtype=torch.int16) if keep else None
         # decoder inputs for the backward (saves it the re-gather) and for the normals pass
         need_x = any(ctx.needs_input_grad) or bool(opts.extras & 1)
@@ -284,6 +300,7 @@ class _VolumeRender(torch.autograd.Function):
                                    uc, uf, seed, rgb, depth, mask, t_saved, s_saved, c_saved, y_saved, perm,
                                    zc, zf)
         args.x_saved = _ptr(x_saved)
+        _VolumeRender._set_viewdir(args, opts, xray_c, vhead)
         args.extras = int(opts.extras)
         args.normal_map = _ptr(nmap) if nmap.numel() else None
         args.semantic_map = _ptr(smap) if smap.numel() else None
@@ -302,7 +319,7 @@ class _VolumeRender(torch.autograd.Function):
             debug['sigma_sorted'] = s_saved
             debug['rgb_sorted'] = c_saved
         ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved,
-                              y_saved, perm, x_saved, tile_counts)
+                              y_saved, perm, x_saved, tile_counts, xray_c, vhead)
         ctx.opts = opts
         ctx.shape = (B, H, W)
         ctx.mark_non_differentiable(depth, nmap, smap)
@@ -311,6 +328,15 @@ class _VolumeRender(torch.autograd.Function):
         if smap.numel():
             smap = smap.view(B, H, W, -1)
         return rgb.view(B, H, W, 3), depth.view(B, H, W), mask.view(B, H, W), nmap, smap
+
+    @staticmethod
+    def _set_viewdir(args, opts, xray, vhead):
+        if opts.heads & HEAD_VIEWDIR:
+            if xray is None or vhead is None:
+                raise ValueError('HEAD_VIEWDIR needs xray and vhead')
+            args.field.xray = _ptr(xray)
+            args.field.vhead = _ptr(vhead)
+            args.field.vhead_out = 3 if opts.heads & HEAD_RGB_SIGMOID else 10
 
     @staticmethod
     def _args(planes_tm, dec, pal, ro, rd, near, far, opts, B, HW, uc, uf, seed, rgb, depth, mask,
@@ -335,7 +361,7 @@ class _VolumeRender(torch.autograd.Function):
     def backward(ctx, g_rgb, g_depth, g_mask, g_nmap=None, g_smap=None):
         lib = _lib.load()
         planes_tm, pal, ro, rd, near, far, dec, t_saved, s_saved, c_saved, y_saved, perm, x_saved, \
-            tile_counts = ctx.saved_tensors
+            tile_counts, xray, vhead = ctx.saved_tensors
         opts = ctx.opts
         B, H, W = ctx.shape
         dev = ro.device
@@ -349,6 +375,7 @@ class _VolumeRender(torch.autograd.Function):
         npl = ((2 * opts.samples if opts.fine else opts.samples) + 63) // 64
         d_pal_ray = torch.empty((n * npl, 30), device=dev) if pal is not None else None
         need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        d_xray = torch.zeros((n, 32), device=dev) if xray is not None else None
         g_ro = torch.empty((n, 3), device=dev) if need_coords else None
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
         HW = H * W
@@ -366,6 +393,7 @@ class _VolumeRender(torch.autograd.Function):
                                     HW, None, None, 0, None, None, None, t_saved[r0:r1], s_saved[r0:r1],
                                     c_saved[r0:r1], y_saved[r0:r1], perm[r0:r1], None, None)
             a.x_saved = _ptr(x_saved[r0 * N:r1 * N])
+            _VolumeRender._set_viewdir(a, opts, None if xray is None else xray.view(n, -1)[r0:r1], vhead)
             nbytes = lib.nfi_render_backward_workspace_bytes(ctypes.byref(a))
             if nbytes < 0:
                 _lib.check(-1, 'nfi_render_backward_workspace_bytes')
@@ -377,7 +405,8 @@ class _VolumeRender(torch.autograd.Function):
                 g_rgb=_ptr(g_rgb[r0:r1]), g_mask=_ptr(g_mask[r0:r1]), d_planes=_ptr(d_planes[b0:b0 + nb]),
                 d_palette_ray=_ptr(None if d_pal_ray is None else d_pal_ray[r0 * npl:r1 * npl]),
                 g_ro=_ptr(None if g_ro is None else g_ro[r0:r1]), g_rd=_ptr(None if g_rd is None else g_rd[r0:r1]),
-                tile_counts=_ptr(tc), workspace=_ptr(ws), workspace_bytes=nbytes)
+                tile_counts=_ptr(tc), workspace=_ptr(ws), workspace_bytes=nbytes,
+                d_xray=_ptr(None if d_xray is None else d_xray[r0:r1]))
             return a, g, ws
 
         def stage(p, k, name, strm):
@@ -422,18 +451,34 @@ class _VolumeRender(torch.autograd.Function):
             d_pal = d_pal.view(B, 10, 3)
         d_ro = g_ro.view(B, H, W, 3) if need_coords else None
         d_rd = g_rd.view(B, H, W, 3) if need_coords else None
-        return (d_planes, d_pal, d_ro, d_rd, None, None, None, None, None, None, None, None)
+        d_xr = None
+        if xray is not None and ctx.needs_input_grad[12]:
+            d_xr = d_xray.view(xray.shape)
+        return (d_planes, d_pal, d_ro, d_rd, None, None, None, None, None, None, None, None, d_xr, None)
 
 
 def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOptions,
-                  u_coarse=None, u_fine=None, seed: Optional[int] = None, debug: Optional[dict] = None):
+                  u_coarse=None, u_fine=None, seed: Optional[int] = None, debug: Optional[dict] = None,
+                  xray=None, vhead=None):
     """Fused coarse+fine render of rays (run.py:202-348).  planes_tm: texel-major
     [B,3,R,R,32] (see planes_texel_major); palette [B,10,3] (None with opts.heads &
     HEAD_RGB_SIGMOID); ro, rd [B,H,W,3]; near, far
     [B,H,W].  Returns rgb [B,H,W,3], depth [B,H,W] (no grad), mask [B,H,W]; with opts.extras
     also the normal map [B,H,W,3] and the semantic [B,H,W,10] / coords [B,H,W,3] map (no grad;
-    None when not requested)."""
-    _require_device(planes_tm, palette, ro, rd, near, far, dec, u_coarse, u_fine)
+    None when not requested).  opts.heads & HEAD_VIEWDIR: xray [B,H,W,32] is the per-ray
+    view-direction mapper trunk output (differentiable) and vhead its packed output layer
+    (pack_viewdir_head); dec is then a 33-output decoder."""
+    _require_device(planes_tm, palette, ro, rd, near, far, dec, u_coarse, u_fine, xray, vhead)
+    if bool(opts.heads & HEAD_VIEWDIR) != (xray is not None and vhead is not None):
+        raise ValueError('xray and vhead are required exactly with HEAD_VIEWDIR')
+    nout = 33 if opts.heads & HEAD_VIEWDIR else 11
+    if dec.numel() != int(_lib.load().nfi_decoder_size(nout)):
+        raise ValueError(f'packed decoder has {dec.numel()} floats; the field needs a {nout}-output decoder')
+    if xray is not None:
+        if xray.shape != (*ro.shape[:3], 32):
+            raise ValueError(f'xray must be [B,H,W,32], got {tuple(xray.shape)}')
+        if vhead.numel() != (3 if opts.heads & HEAD_RGB_SIGMOID else 10) * 33:
+            raise ValueError('vhead must hold the [O,32] weights and [O] bias of the mapper output layer')
     if planes_tm.dim() != 5 or planes_tm.shape[-1] != 32 or planes_tm.stride(-1) != 1:
         raise ValueError('planes_tm must be texel-major [B,3,R,R,32] with unit channel stride')
     if planes_tm.stride(2) != planes_tm.shape[3] * planes_tm.stride(3):
@@ -453,7 +498,7 @@ def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOption
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if opts.randomize else 0
     rgb, depth, mask, nmap, smap = _VolumeRender.apply(planes_tm, palette, ro, rd, near, far, dec, opts,
-                                                       u_coarse, u_fine, seed, debug)
+                                                       u_coarse, u_fine, seed, debug, xray, vhead)
     if opts.extras:
         return rgb, depth, mask, (nmap if nmap.numel() else None), (smap if smap.numel() else None)
     return rgb, depth, mask

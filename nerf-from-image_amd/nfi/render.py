@@ -22,6 +22,7 @@ from typing import Any, Optional, Sequence
 import torch
 
 from . import ops
+from .viewdir import viewdir_trunk
 
 
 @dataclass
@@ -72,6 +73,7 @@ class TriplaneField:
     model_outputs: dict = dc_field(default_factory=dict)
     attention_values: int = 10           # Generator.attention_values (0: wide-sigmoid colour head)
     use_sdf: bool = True                 # Generator.use_sdf (False: softplus(d - 1) density)
+    viewdir_mapper: Any = None           # Generator.viewdir_mapper (--use_viewdir; w2 is then [33,64])
 
 
 def _as_float(x) -> float:
@@ -101,7 +103,8 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
     """Runs the parts of Generator.forward (generator.py:423-503) that produce the path's
     inputs — ws, AttentionMapper palette, synthesis tri-planes — on the reference's own
     modules: unconditional, no encoder, no viewdir; attention_values 10 (the inversion
-    configuration) or 0, use_sdf or not."""
+    configuration) or 0, use_sdf or not, with or without the view-direction mapper (whose
+    per-ray trunk render() runs on the rays, run.py:216-219)."""
     extra_model_inputs = extra_model_inputs or {}
     for k in extra_model_inputs:
         if k not in ('freeze_noise', 'attention_values', 'attention_values_bias'):
@@ -110,8 +113,8 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
         raise NotImplementedError('encoder-/class-conditioned generators are outside the inversion path')
     nattn = int(getattr(gen, 'attention_values', 0))
     use_sdf = bool(getattr(gen, 'use_sdf', False))
-    if nattn not in (0, 10) or getattr(gen, 'use_viewdir', False):
-        raise NotImplementedError('nfi renders fields with 10 or 0 attention values and no viewdir mapper')
+    if nattn not in (0, 10):
+        raise NotImplementedError('nfi renders fields with 10 or 0 attention values')
     if c.dim() == 3:
         ws = c.expand(-1, gen.mapping_network.backbone.num_ws, -1).contiguous() if c.shape[1] == 1 else c
     else:
@@ -140,7 +143,8 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
     alpha, beta = _sdf_params(gen) if use_sdf else (1.0, 0.1)
     return TriplaneField(planes=planes, palette=palette, w1=dec[0].weight, b1=dec[0].bias,
                          w2=dec[2].weight, b2=dec[2].bias, alpha=alpha, beta=beta,
-                         model_outputs=outs, attention_values=nattn, use_sdf=use_sdf)
+                         model_outputs=outs, attention_values=nattn, use_sdf=use_sdf,
+                         viewdir_mapper=gen.viewdir_mapper if getattr(gen, 'use_viewdir', False) else None)
 
 
 def _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs) -> TriplaneField:
@@ -182,16 +186,18 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
         raise ValueError('compute_semantics needs attention values (run.py:232)')
     # run.py:334-335: the coords map takes the semantic map's place
     extras = (1 if compute_normals else 0) | (4 if compute_coords else (2 if compute_semantics else 0))
-    if cfg.use_viewdir:
-        raise NotImplementedError('the view-direction mapper (--use_viewdir) is not built')
     f = _resolve_field(target_model, model_input, extra_model_outputs, extra_model_inputs)
     _check_frozen(f)
+    if bool(cfg.use_viewdir) != (f.viewdir_mapper is not None):
+        raise ValueError('args.use_viewdir and the generator\'s view-direction mapper disagree '
+                         '(the reference requires both or neither, generator.py:464-465, 661-663)')
     if compute_normals and not f.use_sdf:
         raise ValueError('compute_normals needs an SDF field (generator.py:600-601)')
     if compute_semantics and not f.attention_values:
         raise ValueError('compute_semantics needs attention values (generator.py:670-671)')
     heads = ((ops.HEAD_RGB_SIGMOID if f.attention_values == 0 else 0)
-             | (0 if f.use_sdf else ops.HEAD_NERF_DENSITY))
+             | (0 if f.use_sdf else ops.HEAD_NERF_DENSITY)
+             | (ops.HEAD_VIEWDIR if f.viewdir_mapper is not None else 0))
     ro, rd, near, far = ops.rays(tform_cam2world, focal_length, center, bbox, height, width,
                                  cfg.scene_range)
     if debug is not None:
@@ -200,6 +206,12 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
         # run.py:211-214 detaches query points and directions (the reference's fine points keep a
         # gradient path to ray origins; its callers of this mode run under no_grad)
         ro, rd = ro.detach(), rd.detach()
+    xray = vhead = None
+    if f.viewdir_mapper is not None:
+        # run.py:216-219: viewdirs = the (unit, possibly detached) ray directions; the mapper's
+        # per-ray trunk (generator.py:223-238) here, its per-sample closure in the kernels
+        xray = viewdir_trunk(f.viewdir_mapper, rd.unsqueeze(-2)).squeeze(-2)
+        vhead = ops.pack_viewdir_head(f.viewdir_mapper.output.weight, f.viewdir_mapper.output.bias)
     planes_tm = ops.planes_texel_major(f.planes)
     dec = ops.pack_decoder(f.w1, f.b1, f.w2, f.b2)
     opts = ops.RenderOptions(samples=int(depth_samples_per_ray), fine=bool(cfg.fine_sampling),
@@ -207,7 +219,7 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
                              scene_range=float(cfg.scene_range), inv_alpha=1.0 / float(f.alpha),
                              beta=float(f.beta), extras=extras, heads=heads)
     out = ops.volume_render(planes_tm, f.palette, ro, rd, near, far, dec, opts,
-                            u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug)
+                            u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug, xray=xray, vhead=vhead)
     if extras:
         rgb, depth, mask, normals, semantics = out
     else:

@@ -234,6 +234,42 @@ class Field:
     scene_range: float
     attention_values: int = 10
     use_sdf: bool = True
+    viewdir: Optional[dict] = None   # --use_viewdir: ViewDirectionMapper parameters (state_dict keys)
+
+
+def viewdir_trunk(params: dict, viewdir):
+    """ViewDirectionMapper.forward generator.py:223-238 (the per-ray trunk): viewdir [..., 1, 3]
+    -> x [..., 1, 32].  fc1..fc4 have no bias; LayerNorm eps 1e-5 with affine parameters."""
+    def lin(x, name):
+        return equalized_linear(x, params[f'{name}.weight'], params.get(f'{name}.bias',
+                                                                         torch.zeros(params[f'{name}.weight'].shape[0],
+                                                                                     dtype=x.dtype)))
+
+    def norm(x, name):
+        return F.layer_norm(x, (x.shape[-1],), params[f'{name}.weight'], params[f'{name}.bias'], 1e-5)
+
+    scale = math.sqrt(2) / 2
+    relu = lambda t: F.leaky_relu(t, 0.2)  # noqa: E731
+    x = relu(lin(viewdir, 'fc0'))
+    shortcut = x
+    x = relu(norm(lin(x, 'fc1'), 'norm1'))
+    x = relu(norm(lin(x, 'fc2'), 'norm2'))
+    x = (x + shortcut) * scale
+    shortcut = x
+    x = relu(norm(lin(x, 'fc3'), 'norm3'))
+    x = relu(norm(lin(x, 'fc4'), 'norm4'))
+    x = (x + shortcut) * scale
+    x = relu(lin(x, 'fc5'))
+    return lin(x, 'fc6')
+
+
+def viewdir_closure(params: dict, x, features):
+    """mapper_closure generator.py:242-250: output(leaky_relu(x + features)) with x [b,H,W,1,32]
+    broadcast over each ray's samples."""
+    shape = features.shape
+    f = features.view(*x.shape[:-2], -1, x.shape[-1])
+    y = F.leaky_relu(x + f, 0.2).view(shape)
+    return equalized_linear(y, params['output.weight'], params['output.bias'])
 
 
 def triplanar_decoder(planes, coords, w1, b1, w2, b2):
@@ -250,8 +286,9 @@ def triplanar_decoder(planes, coords, w1, b1, w2, b2):
     return x[..., 1:], x[..., :1]                          # features, density_or_distance
 
 
-def sampler(field: Field, x_in, extras=()):
-    """The `sampler` closure generator.py:587-681 with use_viewdir=False; use_sdf=True,
+def sampler(field: Field, x_in, extras=(), xray=None):
+    """The `sampler` closure generator.py:587-681 (with field.viewdir: the view-direction mapper
+    closure on the features, :661-663, xray = its per-ray trunk output); use_sdf=True,
     attention_values=10 is the inversion configuration (the other density / colour heads follow
     field.use_sdf / field.attention_values).  Returns (sigma, rgb), or with `extras` ⊂
     {'normals','semantics','coords'} (sigma, rgb, dict): normals = normalize(d distance / d x_in)
@@ -285,6 +322,8 @@ def sampler(field: Field, x_in, extras=()):
     else:                                                    # standard NeRF density, :637-641
         density_pre = density_or_distance[..., -1] - 1
         sigma = F.softplus(density_pre) * (1 - mask)
+    if field.viewdir is not None:                            # :661-663
+        features = viewdir_closure(field.viewdir, xray, features)
     if field.attention_values == 0:                          # :665-666
         rgb = wide_sigmoid_rescaled(features)
     else:
@@ -308,7 +347,7 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
            return_intermediates: bool = False, compute_normals: bool = False,
            compute_semantics: bool = False, compute_coords: bool = False,
            z_fine: Optional[torch.Tensor] = None, zbuffer: bool = False):
-    """run.py:176-350 with use_viewdir=False.  Returns (rgb [b,H,W,3], depth [b,H,W],
+    """run.py:176-350 (args.use_viewdir = field.viewdir is not None).  Returns (rgb [b,H,W,3], depth [b,H,W],
     mask [b,H,W]) (+ intermediates dict); with any compute_* flag (run.py:227-257, 293-335)
     (rgb, depth, mask, normal_map [b,H,W,3] | None, semantic_map [b,H,W,10 | 3] | None) — the
     coords map replaces the semantic map when compute_coords (run.py:334-335)."""
@@ -326,11 +365,14 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
         query_points = query_points.detach()
         depth_values = depth_values.detach()
         ray_directions = ray_directions.detach()
+    xray = None
+    if field.viewdir is not None:                            # run.py:216-219, generator.py:464-465
+        xray = viewdir_trunk(field.viewdir, ray_directions.unsqueeze(-2))
     ex = {}
     if extras:
-        sigma, rgb, ex = sampler(field, query_points, extras)
+        sigma, rgb, ex = sampler(field, query_points, extras, xray=xray)
     else:
-        sigma, rgb = sampler(field, query_points)
+        sigma, rgb = sampler(field, query_points, xray=xray)
     sigma = sigma.view(*query_points.shape[:-1], -1)
     rgb = rgb.view(*query_points.shape[:-1], -1)
     ex = {k: v.view(*query_points.shape[:-1], -1) for k, v in ex.items()}
@@ -354,9 +396,9 @@ def render(field: Field, height: int, width: int, tform_cam2world, focal_length,
         query_points_fine = ray_origins[..., None, :] + ray_directions[..., None, :] * z_samples[..., :, None]
         ex_fine = {}
         if extras:
-            sigma_fine, rgb_fine, ex_fine = sampler(field, query_points_fine, extras)
+            sigma_fine, rgb_fine, ex_fine = sampler(field, query_points_fine, extras, xray=xray)
         else:
-            sigma_fine, rgb_fine = sampler(field, query_points_fine)
+            sigma_fine, rgb_fine = sampler(field, query_points_fine, xray=xray)
         sigma_fine = sigma_fine.view(*query_points_fine.shape[:-1], -1)
         rgb_fine = rgb_fine.view(*query_points_fine.shape[:-1], -1)
 

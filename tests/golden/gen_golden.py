@@ -87,16 +87,24 @@ def make_cameras(b, scene_range, flipped, seed, ortho=False):
 
 def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, randomize,
                 force_no_cam_grad=False, ortho=False, with_bbox=False, with_center=False,
-                attention_values=10, use_sdf=True, render_file='run.py'):
+                attention_values=10, use_sdf=True, render_file='run.py', use_viewdir=False):
     torch.manual_seed(1000 + seed)
     gen = generator.Generator(512, scene_range, attention_values=attention_values, use_sdf=use_sdf,
-                              disable_stylegan_noise=True)
+                              use_viewdir=use_viewdir, disable_stylegan_noise=True)
     gen.eval()
     with torch.no_grad():
         if use_sdf:
             gen.decoder.net[2].bias[0] -= 0.97     # mask mean ~0.6 instead of ~5e-4
             gen.beta.fill_(0.1)
             gen.alpha.fill_(1.0)
+        if use_viewdir:
+            # the mapper's output layer is zero-initialised (generator.py:219-220) and its
+            # LayerNorms are identity at init: seeded values so every term is exercised
+            gv = torch.Generator().manual_seed(3000 + seed)
+            for k, p in gen.viewdir_mapper.named_parameters():
+                r = torch.randn(p.shape, generator=gv)
+                p.copy_(1 + 0.2 * r if k.startswith('norm') and k.endswith('weight')
+                        else 0.2 * r if k.endswith('bias') else r)
     planes = (1.87 * torch.randn(b, 3, 32, R, R)).requires_grad_()
     gen.synthesis_network = PlanesLeaf(planes)
     palette = generator.wide_sigmoid_rescaled(torch.randn(b, 10, 3)).detach().requires_grad_()
@@ -112,7 +120,7 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     if with_center:
         center = 0.5 + 0.05 * torch.randn(b, 2)
     ws = torch.zeros(b, 15, 512)
-    args_ns = types.SimpleNamespace(use_viewdir=False, fine_sampling=True, use_sdf=use_sdf,
+    args_ns = types.SimpleNamespace(use_viewdir=use_viewdir, fine_sampling=True, use_sdf=use_sdf,
                                     attention_values=attention_values)
     dataset_config = {'scene_range': scene_range, 'white_background': white_bg}
     render = extract_render(args_ns, dataset_config, render_file)
@@ -147,6 +155,8 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     }
     if attention_values:
         out['palette'], out['d_palette'] = palette.detach(), palette.grad
+    if use_viewdir:
+        out.update({f'vd_{k}': v.detach() for k, v in gen.viewdir_mapper.state_dict().items()})
     if use_sdf:
         out['alpha'], out['beta'] = gen.alpha.detach(), gen.beta.detach()
     if focal is not None:
@@ -162,7 +172,7 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     meta = dict(H=H, W=W, S=S, R=R, scene_range=scene_range, white_bg=int(white_bg),
                 randomize=int(randomize), force_no_cam_grad=int(force_no_cam_grad),
                 ortho=int(ortho), attention_values=attention_values, use_sdf=int(use_sdf),
-                zbuffer=int(render_file != 'run.py'))
+                zbuffer=int(render_file != 'run.py'), use_viewdir=int(use_viewdir))
     np.savez_compressed(os.path.join(OUT, f'render_{name}.npz'),
                         **{k: v.numpy() for k, v in out.items()},
                         **{f'meta_{k}': np.array(v) for k, v in meta.items()})
@@ -436,6 +446,16 @@ def field_variant_cases():
                 flipped=False, randomize=False, attention_values=0, use_sdf=False)
 
 
+def viewdir_cases():
+    """--use_viewdir (generator.py:189-252, 376-377, 464-465, 661-663; run.py:216-219): the
+    decoder's 32 features pass through the view-direction mapper closure; attention colour head
+    (pose gradients flow through the mapper) and the wide-sigmoid head with a white background."""
+    render_case('viewdir', 11, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=False,
+                flipped=True, randomize=True, use_viewdir=True)
+    render_case('viewdir_rgbhead', 12, b=1, H=8, W=8, S=8, R=12, scene_range=0.55, white_bg=True,
+                flipped=False, randomize=False, attention_values=0, use_viewdir=True)
+
+
 SDF_SHIFT = 0.0
 
 
@@ -464,6 +484,7 @@ if __name__ == '__main__':
     render_case('persp_center_bbox', 3, b=2, H=8, W=12, S=8, R=8, scene_range=1.4,
                 white_bg=False, flipped=True, randomize=True, with_bbox=True, with_center=True)
     field_variant_cases()
+    viewdir_cases()
     zbuffer_cases()
     # eval outputs: normals + semantics; white background; coords
     extras_case('extras_ns', 4, b=2, H=8, W=8, S=16, R=16, scene_range=1.4, white_bg=False,

@@ -8,6 +8,7 @@ import torch
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox']
 VARIANT_CASES = ['rgbhead', 'nerfdensity', 'nerf_rgbhead']   # attention_values 0 / use_sdf False
+VIEWDIR_CASES = ['viewdir', 'viewdir_rgbhead']               # --use_viewdir
 ZBUFFER_CASES = ['zbuffer']        # eval_nusc_persp.py's render copy (z-buffer depth)
 EXTRAS_CASES = ['extras_ns', 'extras_nw', 'extras_coords']   # eval outputs, no gradients
 
@@ -26,13 +27,19 @@ def load(name):
     return d, meta
 
 
+def viewdir_params(d):
+    """The fixture's ViewDirectionMapper state_dict (keys 'vd_<name>'), or None."""
+    p = {k[3:]: v for k, v in d.items() if k.startswith('vd_')}
+    return p or None
+
+
 def field_from(d, meta):
     from oracle.render_oracle import Field
     return Field(planes=d['planes'], w1=d['w1'], b1=d['b1'], w2=d['w2'], b2=d['b2'],
                  palette=d.get('palette'), alpha=d.get('alpha'), beta=d.get('beta'),
                  scene_range=float(meta['scene_range']),
                  attention_values=int(meta.get('attention_values', 10)),
-                 use_sdf=bool(meta.get('use_sdf', 1)))
+                 use_sdf=bool(meta.get('use_sdf', 1)), viewdir=viewdir_params(d))
 
 
 PRODUCER_SKIP = ('resample_filter', 'noise_const')

@@ -30,11 +30,18 @@ def run_hip(inp, meta, dev, debug=None, with_grad=True):
         focal = focal.to(dev).requires_grad_(with_grad and not ncg)
     center = inp.get('center')
     bbox = inp.get('bbox')
+    mapper = None
+    if meta.get('use_viewdir', 0):
+        from nfi.viewdir import ViewDirectionMapper
+        mapper = ViewDirectionMapper(nattn if nattn else 3)
+        mapper.load_state_dict({k[3:]: v for k, v in inp.items() if k.startswith('vd_')})
+        mapper = mapper.to(dev).requires_grad_(False)
+    nfi.configure(use_viewdir=mapper is not None)
     f = nfi.TriplaneField(planes=planes, palette=palette, w1=inp['w1'].to(dev), b1=inp['b1'].to(dev),
                           w2=inp['w2'].to(dev), b2=inp['b2'].to(dev),
                           alpha=float(inp['alpha']) if use_sdf else 1.0,
                           beta=float(inp['beta']) if use_sdf else 0.1,
-                          attention_values=nattn, use_sdf=use_sdf)
+                          attention_values=nattn, use_sdf=use_sdf, viewdir_mapper=mapper)
     rnd = bool(meta['randomize'])
     uc = inp['u_coarse'].to(dev) if rnd else None
     uf = inp['u_fine'].to(dev) if rnd else None
@@ -72,11 +79,12 @@ def run_oracle64(inp, meta, with_grad=True, return_intermediates=False, z_fine=N
 def run_oracle(inp, meta, with_grad=True, return_intermediates=False, z_fine=None):
     ncg = bool(meta.get('force_no_cam_grad', 0))
     nattn = int(meta.get('attention_values', 10))
+    vd = {k[3:]: v for k, v in inp.items() if k.startswith('vd_')} or None
     field = orc.Field(planes=inp['planes'].clone().requires_grad_(with_grad),
                       w1=inp['w1'], b1=inp['b1'], w2=inp['w2'], b2=inp['b2'],
                       palette=inp['palette'].clone().requires_grad_(with_grad) if nattn else None,
                       alpha=inp.get('alpha'), beta=inp.get('beta'), scene_range=float(meta['scene_range']),
-                      attention_values=nattn, use_sdf=bool(meta.get('use_sdf', 1)))
+                      attention_values=nattn, use_sdf=bool(meta.get('use_sdf', 1)), viewdir=vd)
     cam = inp['cam'].clone().requires_grad_(with_grad and not ncg)
     focal = inp.get('focal')
     if focal is not None:
@@ -144,9 +152,17 @@ def run_hip_extras(inp, meta, dev):
     """nfi.render with compute_normals / compute_semantics / compute_coords (eval outputs)."""
     nfi.configure(scene_range=float(meta['scene_range']), white_background=bool(meta['white_bg']),
                   fine_sampling=True)
+    mapper = None
+    if any(k.startswith('vd_') for k in inp):
+        from nfi.viewdir import ViewDirectionMapper
+        mapper = ViewDirectionMapper(10)
+        mapper.load_state_dict({k[3:]: v for k, v in inp.items() if k.startswith('vd_')})
+        mapper = mapper.to(dev).requires_grad_(False)
+    nfi.configure(use_viewdir=mapper is not None)
     f = nfi.TriplaneField(planes=inp['planes'].to(dev), palette=inp['palette'].to(dev),
                           w1=inp['w1'].to(dev), b1=inp['b1'].to(dev), w2=inp['w2'].to(dev),
-                          b2=inp['b2'].to(dev), alpha=float(inp['alpha']), beta=float(inp['beta']))
+                          b2=inp['b2'].to(dev), alpha=float(inp['alpha']), beta=float(inp['beta']),
+                          viewdir_mapper=mapper)
     with torch.no_grad():
         rgb, depth, mask, nmap, smap, _ = nfi.render(
             f, int(meta['H']), int(meta['W']), inp['cam'].to(dev), inp['focal'].to(dev), None, None, None,
@@ -168,7 +184,8 @@ def run_oracle_extras(inp, meta, dtype=torch.float32):
         cast = {k: (v.to(dtype) if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in inp.items()}
         field = orc.Field(planes=cast['planes'], w1=cast['w1'], b1=cast['b1'], w2=cast['w2'], b2=cast['b2'],
                           palette=cast['palette'], alpha=cast['alpha'], beta=cast['beta'],
-                          scene_range=float(meta['scene_range']))
+                          scene_range=float(meta['scene_range']),
+                          viewdir={k[3:]: v for k, v in cast.items() if k.startswith('vd_')} or None)
         rgb, depth, mask, nmap, smap = orc.render(
             field, int(meta['H']), int(meta['W']), cast['cam'], cast['focal'], None, None, int(meta['S']),
             randomize=True, white_background=bool(meta['white_bg']), force_no_cam_grad=True,

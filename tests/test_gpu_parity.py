@@ -15,7 +15,7 @@ rel-L2 1e-4, d planes rel-L2 1e-3.
 import pytest
 import torch
 
-from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, ZBUFFER_CASES, load
+from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, VIEWDIR_CASES, ZBUFFER_CASES, load
 from gpu_helpers import (rel_l2, run_hip, run_hip_extras, run_oracle, run_oracle64, run_oracle_extras,
                          synthetic_inputs)
 
@@ -46,7 +46,7 @@ def check(hip, ref32, ref64):
     return report
 
 
-@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES + ZBUFFER_CASES)
+@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES + VIEWDIR_CASES + ZBUFFER_CASES)
 def test_golden_render(case):
     """HIP path vs the reference's own fp32 outputs/gradients (tests/golden) and fp64 truth."""
     d, meta = load(f'render_{case}')
@@ -158,6 +158,22 @@ def test_eval_outputs(case):
         e_ref = float((d[key].double() - ref64[key]).abs().max())
         print(f'  {key:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
         assert e_hip <= max(floor, K * e_ref), f'{key}: hip err {e_hip:.3g} vs ref fp32 err {e_ref:.3g}'
+
+
+def test_viewdir_eval_outputs():
+    """Normals and semantics of a --use_viewdir field (semantics = softmax of the mapper's logits,
+    generator.py:661-674; normals from the 33-output decoder's distance) vs the fp64 oracle, on the
+    inputs of the reference's viewdir fixture."""
+    d, meta = load('render_viewdir')
+    meta = dict(meta, compute_normals=1, compute_semantics=1, compute_coords=0)
+    hip = run_hip_extras(d, meta, DEV)
+    ref32 = run_oracle_extras(d, meta, torch.float32)
+    ref64 = run_oracle_extras(d, meta, torch.float64)
+    for key, floor in (('rgb', 2e-5), ('normals', 1e-4), ('semantics', 2e-5)):
+        e_hip = float((hip[key].double() - ref64[key]).abs().max())
+        e_ref = float((ref32[key].double() - ref64[key]).abs().max())
+        print(f'  {key:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
+        assert e_hip <= max(floor, K * e_ref), key
 
 
 def test_eval_outputs_full_size():

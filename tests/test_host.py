@@ -56,13 +56,19 @@ def test_field_heads_follow_the_field():
         nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
 
 
-def test_viewdir_variant_raises():
+def test_viewdir_config_must_match_the_field():
+    """--use_viewdir without a mapper in the generator (or the reverse) is rejected up front (the
+    reference would fail inside the sampler, generator.py:464-465, 661-663)."""
     nfi.configure(use_viewdir=True)
     try:
-        with pytest.raises(NotImplementedError):
+        with pytest.raises(ValueError, match='use_viewdir'):
             nfi.render(_field(), 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
     finally:
         nfi.configure(use_viewdir=False)
+    f = _field()
+    f.viewdir_mapper = torch.nn.Identity()
+    with pytest.raises(ValueError, match='use_viewdir'):
+        nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
 
 
 def test_frozen_decoder_required():

@@ -8,7 +8,7 @@ rounding of identical op graphs (in practice bit-exact).
 import pytest
 import torch
 
-from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, ZBUFFER_CASES, field_from, load
+from golden_io import EXTRAS_CASES, RENDER_CASES, VARIANT_CASES, VIEWDIR_CASES, ZBUFFER_CASES, field_from, load
 from oracle import render_oracle as orc
 
 
@@ -32,7 +32,7 @@ def _run_oracle(d, meta):
     return rgb, depth, mask, field, cam, focal
 
 
-@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES + ZBUFFER_CASES)
+@pytest.mark.parametrize('case', RENDER_CASES + VARIANT_CASES + VIEWDIR_CASES + ZBUFFER_CASES)
 def test_oracle_render_matches_reference(case):
     d, meta = load(f'render_{case}')
     rgb, depth, mask, field, cam, focal = _run_oracle(d, meta)
