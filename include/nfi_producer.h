@@ -89,6 +89,27 @@ int32_t nfi_vgg_bias_relu_forward(const float* x, const float* bias, float* y, f
 int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float* y, float* gx,
                               int32_t P, int32_t H, int32_t W, void* stream);
 
+/* Winograd F(4x4, 3x3) convolution (stride 1, padding 1), the 3x3 convolutions of the LPIPS VGG16
+ * trunk (lpips 0.1 via metrics.py:107) and of the synthesis layers (stylegan.py:130-145), i.e.
+ * F.conv2d(x, w, padding=1) in fp32.  The layer is three transforms here around 36 independent
+ * [Co x Ci] x [Ci x P] fp32 matrix products that the caller runs as one batched GEMM
+ * (P = N * H/4 * W/4 tiles; M[k] = U[k] V[k], k = 0..35).  csrc/nfi_conv.hip.
+ *
+ * w [Co,Ci,3,3] -> U [36,Co,Ci]; flip != 0: the data-gradient weights U [36,Ci,Co] of rot180(w)
+ * (conv_transpose2d(g, w, padding=1) == conv2d(g, rot180(w) with channels swapped, padding=1)). */
+int32_t nfi_wino_weight_transform(const float* w, float* U, int32_t Co, int32_t Ci, int32_t flip,
+                                  void* stream);
+
+/* x [N,C,H,W] (16-byte aligned, H and W multiples of 4) -> V [36,C,P]. */
+int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C, int32_t H, int32_t W,
+                                 void* stream);
+
+/* M [36,Co,P] -> y [N,Co,H,W].  bias == NULL: y = the convolution.  bias != NULL: y =
+ * relu(conv + bias[co]) (the LPIPS VGG16 block epilogue, as nfi_vgg_bias_relu_forward) and, when
+ * pooled != NULL, pooled [N,Co,H/2,W/2] = MaxPool2d(2, 2)(y). */
+int32_t nfi_wino_output_transform(const float* M, const float* bias, float* y, float* pooled, int32_t N,
+                                  int32_t Co, int32_t H, int32_t W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,6 +112,12 @@ SIGNATURES = {
                                                    ctypes.c_int32, c_void_p]),
     'nfi_vgg_relu_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, c_void_p]),
+    'nfi_wino_weight_transform': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                   ctypes.c_int32, c_void_p]),
+    'nfi_wino_input_transform': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                  ctypes.c_int32, ctypes.c_int32, c_void_p]),
+    'nfi_wino_output_transform': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
+                                                   ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p]),
 }
 
 _lib = None

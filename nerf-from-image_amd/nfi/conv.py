@@ -1,0 +1,155 @@
+"""3x3 convolutions of the inversion step's caller side as Winograd F(4x4, 3x3) on MI355X: the
+LPIPS VGG16 trunk (lpips 0.1 via lib/metrics.py:107) and the synthesis layers
+(models/stylegan.py:130-145, §8(f) #1) call F.conv2d(x, w, padding=1) with frozen weights
+(run.py:630-632; LPIPS is never trained), in fp32 (TF32 off, run.py:59-60).
+
+Per layer: input transform (HIP) -> 36 batched [Co x Ci] x [Ci x P] fp32 GEMMs on the matrix cores
+(torch.bmm -> hipBLASLt, a plain library GEMM) -> output transform (HIP, with the VGG block's
+bias + ReLU + 2x2 max pool fused).  Weight transforms are computed once per frozen weight.  The
+data gradient is the same pipeline with the rot180 / channel-swapped weights (the weights
+receive no gradient: asking for one raises).  csrc/nfi_conv.hip, include/nfi_producer.h.
+
+F(4,3) multiplies 4x fewer products than the direct convolution (MIOpen's fp32 Winograd is
+F(2,3), 2.25x, on the vector ALUs).  Its transforms cost fp32 rounding: a few 1e-6 of the
+largest output (tests/test_gpu_conv.py bounds it by 2e-5 against an fp64 convolution, next to
+MIOpen's own error), the order of cuDNN's fp32 Winograd algorithms the reference may run.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .ops import _require_device, _stream
+
+# layers with fewer input channels than this stay on MIOpen (the VGG trunk's 3-channel first
+# layer: K = 3 is no GEMM)
+MIN_CHANNELS = 16
+ENABLED = True
+DGRAD = True          # data gradient as Winograd too (False: MIOpen's conv2d_input; diagnostics)
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _call(name, *args):
+    lib = _lib.load()
+    _lib.check(getattr(lib, name)(*args), name)
+
+
+def applicable(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """True when conv2d(x, weight, padding=1) runs as Winograd here: a device tensor, 3x3 kernel,
+    H and W multiples of 4, enough input channels for a GEMM."""
+    return (ENABLED and x.is_cuda and x.dim() == 4 and weight.shape[2:] == (3, 3)
+            and x.shape[1] >= MIN_CHANNELS and x.shape[2] % 4 == 0 and x.shape[3] % 4 == 0
+            and x.dtype == torch.float32)
+
+
+def weights(weight: torch.Tensor):
+    """(U [36,Co,Ci], Ut [36,Ci,Co]) of a frozen [Co,Ci,3,3] weight, cached until the weight is
+    modified in place or replaced."""
+    tag = (weight.data_ptr(), weight._version, weight.device)
+    hit = getattr(weight, '_nfi_winograd', None)
+    if hit is not None and hit[0] == tag:
+        return hit[1]
+    _require_device(weight)
+    w = weight.detach().contiguous()
+    Co, Ci = w.shape[:2]
+    U = torch.empty((36, Co, Ci), device=w.device)
+    Ut = torch.empty((36, Ci, Co), device=w.device)
+    st = _stream(w.device)
+    _call('nfi_wino_weight_transform', _p(w), _p(U), Co, Ci, 0, st)
+    _call('nfi_wino_weight_transform', _p(w), _p(Ut), Co, Ci, 1, st)
+    weight._nfi_winograd = (tag, (U, Ut))      # cached on the (frozen) parameter itself
+    return U, Ut
+
+
+def _winograd(x, U, bias=None, pool=False):
+    """x [N,Ci,H,W] (contiguous) with transformed weights U [36,Co,Ci] -> y [N,Co,H,W]
+    (and the pooled map when pool)."""
+    N, Ci, H, W = x.shape
+    Co = U.shape[1]
+    P = N * (H // 4) * (W // 4)
+    st = _stream(x.device)
+    V = torch.empty((36, Ci, P), device=x.device)
+    _call('nfi_wino_input_transform', _p(x), _p(V), N, Ci, H, W, st)
+    M = torch.bmm(U, V)
+    del V
+    y = torch.empty((N, Co, H, W), device=x.device)
+    m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
+    _call('nfi_wino_output_transform', _p(M), _p(bias), _p(y), _p(m), N, Co, H, W, st)
+    return (y, m) if pool else y
+
+
+def _dgrad(g, ctx):
+    if DGRAD:
+        return _winograd(g, ctx.Ut)
+    return torch.nn.grad.conv2d_input(ctx.xshape, ctx.weight, g, 1, 1)
+
+
+def _frozen_weight(*ts):
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts):
+        raise NotImplementedError('nfi.conv: convolution weights are frozen in the inversion path '
+                                  '(no weight gradient); call requires_grad_(False) on the module')
+
+
+class _Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        _require_device(x, weight)
+        x = x.contiguous()
+        U, Ut = weights(weight)
+        ctx.Ut, ctx.xshape, ctx.weight = Ut, x.shape, weight.detach()
+        return _winograd(x, U)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _dgrad(g.contiguous(), ctx), None
+
+
+class _VggBlock(torch.autograd.Function):
+    """relu(conv2d(x, w, padding=1) + b) (+ MaxPool2d(2, 2)) with the epilogue in the output
+    transform; backward: nfi_vgg_relu_backward, then the data-gradient Winograd."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, pool: bool):
+        _require_device(x, weight, bias)
+        x = x.contiguous()
+        U, Ut = weights(weight)
+        r = _winograd(x, U, bias.detach().contiguous(), pool)
+        y = r[0] if pool else r
+        ctx.save_for_backward(y)
+        ctx.Ut, ctx.xshape, ctx.weight = Ut, x.shape, weight.detach()
+        ctx.set_materialize_grads(False)
+        return r
+
+    @staticmethod
+    def backward(ctx, gy, gm=None):
+        y, = ctx.saved_tensors
+        if gy is None and gm is None:
+            return None, None, None, None
+        N, C, H, W = y.shape
+        gz = torch.empty_like(y)
+        gy = None if gy is None else gy.contiguous()
+        gm = None if gm is None else gm.contiguous()
+        _call('nfi_vgg_relu_backward', _p(gy), _p(gm), _p(y), _p(gz), N * C, H, W, _stream(y.device))
+        return _dgrad(gz, ctx), None, None, None
+
+
+def conv3x3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """F.conv2d(x, weight, padding=1) (no bias): Winograd when applicable and the weight is
+    frozen; MIOpen otherwise (other shapes, or a weight that is being trained)."""
+    if not applicable(x, weight) or weight.requires_grad:
+        return F.conv2d(x, weight, None, 1, 1)
+    return _Conv.apply(x, weight)
+
+
+def vgg_block(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pool: bool):
+    """relu(conv2d(x, weight, bias, padding=1)) and, when pool, also MaxPool2d(2, 2) of it:
+    (y, pooled).  Requires applicable(x, weight)."""
+    _frozen_weight(weight, bias)
+    return _VggBlock.apply(x, weight, bias, pool)

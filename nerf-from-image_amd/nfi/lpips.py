@@ -36,6 +36,8 @@ class VGG16Features(nn.Module):
     """torchvision.models.vgg16().features[:30] with the same module indices (state_dict keys
     'features.<i>.weight'/'bias' load directly)."""
 
+    winograd = True    # fused path: 3x3 layers as Winograd F(4,3) (nfi.conv) where applicable
+
     def __init__(self):
         super().__init__()
         layers, c = [], 3
@@ -57,11 +59,19 @@ class VGG16Features(nn.Module):
             return out
         # each conv block as MIOpen's bias-free convolution + one HIP epilogue pass (bias, ReLU and
         # the following MaxPool2d when there is one; producer_ops.vgg_epilogue)
-        from . import producer_ops
+        from . import conv as wconv, producer_ops
         f, i = self.features, 0
         while i < len(f):
             conv = f[i]
             pool = i + 2 < len(f) and isinstance(f[i + 2], nn.MaxPool2d)
+            if self.winograd and wconv.applicable(x, conv.weight):
+                # Winograd F(4,3): the epilogue (bias, ReLU, pool) runs in the output transform
+                r = wconv.vgg_block(x, conv.weight, conv.bias, pool)
+                y, x = r if pool else (r, r)
+                if i + 1 in TAPS:
+                    out.append(y)
+                i += 3 if pool else 2
+                continue
             z = F.conv2d(x, conv.weight, None, 1, 1)
             if z.shape[-1] % 4 == 0 and not (pool and z.shape[-2] % 2):
                 r = producer_ops.vgg_epilogue(z, conv.bias, pool)

@@ -37,6 +37,11 @@ def _hip():
     return producer_ops
 
 
+def _conv():
+    from . import conv
+    return conv
+
+
 def blur_kernel() -> torch.Tensor:
     """[1,3,3,1] x [1,3,3,1] / 64 (stylegan.py `bilinear_filter`)."""
     k = torch.tensor([1.0, 3.0, 3.0, 1.0])
@@ -144,7 +149,7 @@ class ModulatedConv(nn.Module):
         if self.up:
             t = F.conv_transpose2d(xs, self.weight.transpose(0, 1), stride=2)
             return ops.fir_up_act(t, dcoefs, self.bias, SQRT2)
-        return ops.act(F.conv2d(xs, self.weight, padding=1), dcoefs, self.bias, SQRT2)
+        return ops.act(_conv().conv3x3(xs, self.weight), dcoefs, self.bias, SQRT2)
 
 
 class ToPlanes(nn.Module):

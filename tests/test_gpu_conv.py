@@ -1,0 +1,95 @@
+"""Winograd F(4x4, 3x3) convolutions (nfi.conv, csrc/nfi_conv.hip) against an fp64 convolution:
+forward, the data gradient, and the fused VGG16 block epilogue.  Bar: the largest error relative
+to the largest output is <= 2e-5 (F(4,3)'s fp32 transform rounding is a few 1e-6; MIOpen's error
+on the same case is computed beside it for the record; TF32 is off in both, run.py:59-60)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from nfi import conv
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+SHAPES = [(2, 16, 24, 8, 8), (3, 64, 64, 16, 12), (2, 128, 96, 32, 32), (1, 512, 512, 8, 8),
+          (2, 64, 64, 128, 128), (1, 32, 3, 4, 4)]
+
+
+def _err(a, ref):
+    return float((a.detach().double().cpu() - ref).abs().max() / ref.abs().max())
+
+
+@pytest.mark.parametrize('N,Ci,Co,H,W', SHAPES)
+def test_winograd_conv_forward_and_data_gradient(N, Ci, Co, H, W):
+    g = torch.Generator(device=DEV).manual_seed(Ci * Co + H)
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=g)
+    xa = x.clone().requires_grad_()
+    y = conv.conv3x3(xa, w)
+    y.backward(gy)
+    xd = x.double().cpu().requires_grad_()
+    yd = F.conv2d(xd, w.double().cpu(), padding=1)
+    yd.backward(gy.double().cpu())
+    xm = x.clone().requires_grad_()
+    ym = F.conv2d(xm, w, padding=1)
+    ym.backward(gy)
+    e_w, e_m = _err(y, yd), _err(ym, yd)
+    ge_w, ge_m = _err(xa.grad, xd.grad), _err(xm.grad, xd.grad)
+    print(f'winograd {e_w:.2e} / {ge_w:.2e}, miopen {e_m:.2e} / {ge_m:.2e} (forward / data gradient)')
+    assert e_w <= max(8 * e_m, 2e-5), (e_w, e_m)
+    assert ge_w <= max(8 * ge_m, 2e-5), (ge_w, ge_m)
+
+
+@pytest.mark.parametrize('pool', [False, True])
+@pytest.mark.parametrize('N,Ci,Co,H', [(2, 64, 64, 16), (3, 128, 256, 8), (1, 16, 32, 4)])
+def test_winograd_vgg_block(N, Ci, Co, H, pool):
+    """relu(conv + b) (+ MaxPool2d(2, 2)) from the output transform; backward through the ReLU /
+    pool routing and the data-gradient Winograd."""
+    g = torch.Generator(device=DEV).manual_seed(N + Ci + H)
+    x = torch.randn((N, Ci, H, H), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    xa = x.clone().requires_grad_()
+    out = conv.vgg_block(xa, w, b, pool)
+    xd = x.double().cpu().requires_grad_()
+    yd = torch.relu(F.conv2d(xd, w.double().cpu(), b.double().cpu(), padding=1))
+    gy = torch.randn((N, Co, H, H), device=DEV, generator=g)
+    if pool:
+        y, m = out
+        md = F.max_pool2d(yd, 2, 2)
+        gm = torch.randn(m.shape, device=DEV, generator=g)
+        torch.autograd.backward([y, m], [gy, gm])
+        torch.autograd.backward([yd, md], [gy.double().cpu(), gm.double().cpu()])
+        assert _err(m, md) < 2e-5
+    else:
+        y = out
+        y.backward(gy)
+        yd.backward(gy.double().cpu())
+    assert _err(y, yd) < 2e-5
+    # the ReLU mask / pool argmax can flip on values within rounding of 0 / of a tie
+    rel = float((xa.grad.double().cpu() - xd.grad).norm() / xd.grad.norm())
+    assert rel < 1e-4, rel
+
+
+def test_weight_cache_follows_in_place_updates():
+    w = torch.randn((16, 16, 3, 3), device=DEV)
+    U1, _ = conv.weights(w)
+    U1c = U1.clone()
+    assert conv.weights(w)[0] is U1
+    with torch.no_grad():
+        w.mul_(2)
+    U2, _ = conv.weights(w)
+    torch.testing.assert_close(U2, 2 * U1c)
+
+
+def test_trainable_weight_takes_the_library_path():
+    """A weight that requires grad (training, not the inversion) gets its gradient from MIOpen;
+    the fused VGG block refuses it."""
+    x = torch.randn((1, 16, 8, 8), device=DEV)
+    w = torch.randn((16, 16, 3, 3), device=DEV, requires_grad=True)
+    conv.conv3x3(x, w).sum().backward()
+    assert w.grad is not None
+    with pytest.raises(NotImplementedError):
+        conv.vgg_block(x, w, torch.zeros(16, device=DEV), False)

@@ -61,20 +61,50 @@ def test_vgg_epilogue_matches_torch(N, C, H, W, pool):
     assert torch.equal(xa.grad, xr.grad)
 
 
-def test_lpips_backends_agree():
-    torch.manual_seed(0)
-    net = lpips.LPIPS(backend='torch').to(DEV)
-    a = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV)).requires_grad_()
-    b = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV))
-    ref = net(a, b)
-    ref.sum().backward()
-    ga = a.grad.clone()
-    a.grad = None
-    net.backend = 'hip'
+def _lpips_eval(net, a, b):
+    a = a.detach().clone().requires_grad_()
     out = net(a, b)
     out.sum().backward()
-    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-6)
-    assert float((a.grad - ga).norm() / ga.norm()) < 1e-4
+    return out.detach().double().cpu(), a.grad.double().cpu()
+
+
+def test_lpips_backends_agree():
+    """hip backend (Winograd F(4,3) trunk, fused epilogues and distance head) and hip with the
+    MIOpen trunk against an fp64 evaluation of the torch formulation; the torch backend in fp32
+    (MIOpen) is measured beside them.  The Winograd trunk's fp32 transform rounding (a few 1e-6
+    per layer, tests/test_gpu_conv.py) compounds over 13 layers and the ReLU masks to ~2e-4 in
+    the image gradient: about 10x the MIOpen path's, still fp32-grade."""
+    import copy
+    torch.manual_seed(0)
+    net = lpips.LPIPS(backend='torch').to(DEV)
+    a = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV))
+    b = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV))
+    net64 = copy.deepcopy(net).double().cpu()
+    ref, gref = _lpips_eval(net64, a.double().cpu(), b.double().cpu())
+
+    def errs(r):
+        return float((r[0] - ref).abs().max() / ref.abs().max()), float((r[1] - gref).norm() / gref.norm())
+
+    e_torch = errs(_lpips_eval(net, a, b))
+    net.backend = 'hip'
+    e_wino = errs(_lpips_eval(net, a, b))
+    try:
+        lpips.VGG16Features.winograd = False
+        e_miopen = errs(_lpips_eval(net, a, b))
+    finally:
+        lpips.VGG16Features.winograd = True
+    print(f'vs fp64 (loss, image gradient): torch fp32 {e_torch}, hip+miopen {e_miopen}, hip+winograd {e_wino}')
+    assert e_miopen[0] < 1e-5 and e_miopen[1] < max(4 * e_torch[1], 1e-5)
+    assert e_wino[0] < 1e-5 and e_wino[1] < 1e-3
+    # where the Winograd gradient error sits: a forward near-tie (a 2x2 max-pool window or a ReLU
+    # input within rounding of 0) decided the other way reroutes one feature gradient, a local
+    # jump; elsewhere the gradient is as accurate as the forward
+    g = _lpips_eval(net, a, b)[1]
+    rel = ((g - gref).abs() / gref.abs().max()).flatten()
+    q = torch.quantile(rel[torch.randperm(rel.numel())[:100000]], torch.tensor([0.5, 0.99, 0.999], dtype=rel.dtype))
+    print('winograd |d image| error / max, quantiles 50/99/99.9 %:', q.tolist(),
+          'share > 1e-4:', float((rel > 1e-4).double().mean()))
+    assert float(q[1]) < 1e-5
 
 
 def test_vgg_inversion_loss_runs():

@@ -101,19 +101,29 @@ def test_up_add(B, C, n, with_img):
 
 
 def test_backends_agree_on_gpu():
-    """Full producer: 'hip' against 'torch' (the reference's op sequence) on the same device."""
+    """Full producer: 'hip' (Winograd F(4,3) 3x3 convolutions, fused epilogues) and 'torch' (the
+    reference's op sequence, fp32) against the same op sequence in float64 on the device.  d ws
+    is ill-conditioned (sums over 2 x 96 x 256^2 plane gradients with cancellation): the torch
+    fp32 path itself is off by ~5e-4; 'hip' must stay within 4x of that (the GPU parity
+    convention of tests/test_gpu_parity.py)."""
+    import copy
     torch.manual_seed(3)
     gen = producer.InversionGenerator(1.4).to(DEV).requires_grad_(False)
-    ws = (0.6 * _rand(2, 15, 512, seed=16)).requires_grad_()
+    ws = (0.6 * _rand(2, 15, 512, seed=16))
     g = _rand(2, 3, 32, 256, 256, seed=17)
-    out = {}
-    for be in ('hip', 'torch'):
-        gen.set_backend(be)
-        w = ws.detach().clone().requires_grad_()
-        planes, pal = gen.planes_and_palette(w)
-        ((planes * g).sum() + pal.sum()).backward()
-        out[be] = (planes.detach(), w.grad)
-    scale = float(out['torch'][0].abs().max())
-    assert float((out['hip'][0] - out['torch'][0]).abs().max()) < 1e-4 * scale
-    gerr = float((out['hip'][1] - out['torch'][1]).norm() / out['torch'][1].norm())
-    assert gerr < 1e-3, gerr
+
+    def ev(gn, dtype, be):
+        gn.set_backend(be)
+        w = ws.to(dtype).detach().clone().requires_grad_()
+        planes, pal = gn.planes_and_palette(w)
+        ((planes * g.to(dtype)).sum() + pal.sum()).backward()
+        return planes.detach().double(), w.grad.double()
+
+    ref = ev(copy.deepcopy(gen).double(), torch.float64, 'torch')
+    err = {}
+    for be in ('torch', 'hip'):
+        p, d = ev(gen, torch.float32, be)
+        err[be] = (float((p - ref[0]).abs().max() / ref[0].abs().max()), float((d - ref[1]).norm() / ref[1].norm()))
+    print('vs fp64 (planes max/max, d ws rel L2):', err)
+    assert err['hip'][0] < max(4 * err['torch'][0], 1e-5)
+    assert err['hip'][1] < max(4 * err['torch'][1], 1e-4)
