@@ -15,14 +15,18 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-mun
          '-Wall', '-Wno-unused-result']
 
 
+RENDER_SOURCES = ['nfi_rays.hip', 'nfi_render.hip', 'nfi_common.h', 'nfi_host.h']
+
+
 def source_digest() -> str:
-    """sha256 (16 hex) of the HIP sources and headers the library is built from: stamps profiler
-    counter files (profiles/latest_counters.json) so bench.py can tell whether they describe the
-    kernels it runs."""
+    """sha256 (16 hex) of the sources the renderer's kernels are built from (csrc/nfi_rays.hip,
+    nfi_render.hip, their headers and include/nfi.h): stamps profiler counter files
+    (profiles/latest_counters.json, renderer kernels) so bench.py can tell whether they describe
+    the kernels it runs.  The caller-side operators (producer, Winograd) are not part of it."""
     import hashlib
     h = hashlib.sha256()
     inc = os.path.join(os.path.dirname(os.path.dirname(HERE)), 'include')
-    for path in [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [os.path.join(inc, x) for x in ('nfi.h', 'nfi_producer.h')]:
+    for path in [os.path.join(CSRC, s) for s in RENDER_SOURCES] + [os.path.join(inc, 'nfi.h')]:
         with open(path, 'rb') as fh:
             h.update(os.path.basename(path).encode() + b'\0' + fh.read())
     return h.hexdigest()[:16]

@@ -25,6 +25,8 @@ def dur(x):
 def group(name):
     if 'nfi::syn::lpips' in name:
         return 'LPIPS distance head (nfi HIP)'
+    if 'nfi::wino::' in name:
+        return 'Winograd transforms (nfi HIP)'
     if 'nfi::syn::' in name:
         return 'producer epilogues (nfi HIP)'
     if 'nfi::' in name:
