@@ -39,7 +39,9 @@ def quaternion_to_matrix(q: torch.Tensor) -> torch.Tensor:
 def _flip(mat: torch.Tensor, camera_flipped: bool) -> torch.Tensor:
     if not camera_flipped:
         return mat
-    sign = mat.new_tensor([1.0, -1.0, -1.0, -1.0])     # pose_utils.py:61: columns 1..3
+    # pose_utils.py:61: columns 1..3 (built on the device: no host copy inside a captured step)
+    sign = torch.full((4,), -1.0, dtype=mat.dtype, device=mat.device)
+    sign[:1].fill_(1.0)
     return torch.cat([mat[:, :3] * sign, mat[:, 3:]], dim=1)
 
 
@@ -56,7 +58,7 @@ def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
         focal = None
     top = torch.cat([rot, (rot * t3[:, None, :]).sum(-1, keepdim=True)], dim=-1)
     bottom = torch.zeros(b, 1, 4, dtype=top.dtype, device=top.device)
-    bottom[:, 0, 3] = 1
+    bottom[:, 0, 3].fill_(1.0)
     return _flip(torch.cat([top, bottom], dim=1), camera_flipped), focal
 
 
@@ -67,7 +69,7 @@ def invert_space(mat: torch.Tensor) -> torch.Tensor:
     out = torch.zeros_like(mat)
     out[:, :3, :3] = rot.transpose(-2, -1)
     out[:, :3, 3] = -(rot * mat[:, :3, None, 3]).sum(-2)
-    out[:, 3, 3] = 1
+    out[:, 3, 3].fill_(1.0)
     return out
 
 
@@ -136,6 +138,8 @@ class InversionConfig:
     no_split: bool = False               # --inv_no_split: one w shared by the 15 slots
     camera_flipped: bool = True          # dataset_config['camera_flipped']
     overlap_target: bool = True          # 'vgg' losses: target features on a side stream (GPU)
+    graph: bool = False                  # GPU: replay the step as a captured HIP graph (see invert;
+                                         # measured slower than eager launches on ROCm 7.2)
 
 
 @dataclass
@@ -262,71 +266,223 @@ def invert(generator, target_img: torch.Tensor, cam2world: torch.Tensor, focal: 
     renderer's random draws per iteration (parity tests); `render_fn` replaces nfi.render with
     a callable of the same signature (tests only).  `on_checkpoint(it, (z_, z0_, t2_, s_, q_))`
     runs before the first step if 0 is in `checkpoints` and after step it if it is
-    (evaluate_inversion, run.py:2020-2110 and 2302-2305; see nfi.report.evaluate)."""
+    (evaluate_inversion, run.py:2020-2110 and 2302-2305; see nfi.report.evaluate).
+
+    On a HIP device with cfg.graph (and no injected draws / render_fn), the whole step — producer,
+    render, loss, backward, Adam, the post-step projections — is captured once as a HIP graph
+    (torch.cuda.CUDAGraph over the ROCm runtime) after two eager steps, and replayed: ~900
+    kernel launches per step become one graph launch.  Measured on MI355X (B=4, 30 steps): L1
+    step 13.2 ms eager vs 14.1 ms replayed, vgg 24.6 vs 25.6 ms — the replay of ~900 nodes costs
+    more GPU time than it saves host time (the eager loop keeps the queue full), and the vgg
+    loss's side stream no longer overlaps — so it is off by default.  The graph and its static tensors (latent,
+    pose, Adam moments, target) are kept per (generator, loss network, shapes, config) and reused
+    by later batches of the same shape, as the reference's loop over dataset batches
+    (run.py:1874) would; each batch copies its inputs into them and resets Adam.  The renderer's
+    stratified / inverse-CDF draws then come from torch's device generator (graph-safe) instead
+    of the kernels' host-seeded Philox stream: same distribution, another stream."""
+    use_graph = (cfg.graph and target_img.is_cuda and uniforms is None and render_fn is None)
+    if use_graph:
+        return _invert_graphed(generator, target_img, cam2world, focal, w_init, cfg, center, bbox,
+                               on_step, lpips_net, checkpoints, on_checkpoint)
     b = target_img.shape[0]
-    res = cfg.resolution
     rfn = render_fn or _nfi_render
-    z_ = w_init.detach().clone().expand(b, -1, -1).contiguous()
-    if cfg.no_split:
-        z_ = z_.mean(dim=1, keepdim=True)
-    z_ = (z_ / cfg.gain_z).requires_grad_()
-    z0_, t2_, s_, q_ = matrix_to_pose(cam2world, focal, cfg.camera_flipped)
-    params = [z_]
-    if cfg.optimize_pose:
-        pose = [p for p in (z0_, q_, s_, t2_) if p is not None]
-        for p in pose:
-            p.requires_grad_()
-        params += pose
-    opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas)
-    target = target_img[..., :3]
+    st = _State(generator, target_img, cam2world, focal, w_init, cfg, center, bbox, lpips_net,
+                capturable=False)
     losses = []
     if on_checkpoint is not None and 0 in checkpoints:
-        on_checkpoint(0, (z_, z0_, t2_, s_, q_))
-    # the prediction-independent half of the 'vgg' losses (augmentation grid, LPIPS features of the
-    # target and its copies) runs on a side stream, concurrently with the producer and the render
-    side = None
-    if cfg.loss in VGG_LOSSES and target.is_cuda and cfg.overlap_target:
-        side = torch.cuda.Stream(device=target.device)
+        on_checkpoint(0, st.views())
     t0 = time.perf_counter()
     for it in range(cfg.steps):
-        prepared = None
-        if side is not None:
-            main = torch.cuda.current_stream(target.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                prepared = vgg_target(cfg.loss, target, lpips_net, cfg.white_background)
-        cam, foc = pose_to_matrix(z0_, t2_, s_, F.normalize(q_, dim=-1), cfg.camera_flipped)
         kw = {}
         if uniforms is not None:
             kw['u_coarse'], kw['u_fine'] = uniforms(it)
-        ws = z_ * cfg.gain_z
+        loss = st.step(rfn, kw)
+        losses.append(loss.detach())
+        if on_step is not None:
+            on_step(it, loss)
+        if on_checkpoint is not None and it + 1 in checkpoints:
+            on_checkpoint(it + 1, st.views())
+    if torch.cuda.is_available() and target_img.is_cuda:
+        torch.cuda.synchronize(target_img.device)
+    secs = time.perf_counter() - t0
+    assert b == st.b
+    return st.result(losses, secs)
+
+
+class _State:
+    """The optimised tensors of one inversion batch (run.py:1984-2007) and one step of the loop
+    (run.py:2256-2310) over them."""
+
+    def __init__(self, generator, target_img, cam2world, focal, w_init, cfg, center, bbox, lpips_net,
+                 capturable: bool):
+        self.gen, self.cfg, self.lpips_net = generator, cfg, lpips_net
+        self.b = target_img.shape[0]
+        z_ = w_init.detach().clone().expand(self.b, -1, -1).contiguous()
+        if cfg.no_split:
+            z_ = z_.mean(dim=1, keepdim=True)
+        self.z_ = (z_ / cfg.gain_z).requires_grad_()
+        self.z0_, self.t2_, self.s_, self.q_ = matrix_to_pose(cam2world, focal, cfg.camera_flipped)
+        params = [self.z_]
+        if cfg.optimize_pose:
+            pose = [p for p in (self.z0_, self.q_, self.s_, self.t2_) if p is not None]
+            for p in pose:
+                p.requires_grad_()
+            params += pose
+        self.params = params
+        self.opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas, capturable=capturable)
+        self.target = target_img[..., :3]
+        if capturable:
+            self.target = self.target.contiguous()
+        self.center, self.bbox = center, bbox
+        # the prediction-independent half of the 'vgg' losses (augmentation grid, LPIPS features
+        # of the target and its copies) runs on a side stream, concurrently with the producer and
+        # the render
+        self.side = None
+        if cfg.loss in VGG_LOSSES and self.target.is_cuda and cfg.overlap_target:
+            self.side = torch.cuda.Stream(device=self.target.device)
+
+    def views(self):
+        return self.z_, self.z0_, self.t2_, self.s_, self.q_
+
+    def load(self, target_img, cam2world, focal, w_init, center, bbox):
+        """A new batch into the same (static) tensors; Adam restarts (run.py:2007 builds a new
+        optimiser per batch)."""
+        cfg = self.cfg
+        with torch.no_grad():
+            z_ = w_init.detach().expand(self.b, -1, -1)
+            if cfg.no_split:
+                z_ = z_.mean(dim=1, keepdim=True)
+            self.z_.copy_(z_ / cfg.gain_z)
+            z0, t2, s, q = matrix_to_pose(cam2world, focal, cfg.camera_flipped)
+            for dst, src in ((self.z0_, z0), (self.t2_, t2), (self.s_, s), (self.q_, q)):
+                if dst is not None:
+                    dst.copy_(src)
+            self.target.copy_(target_img[..., :3])
+            for dst, src in ((self.center, center), (self.bbox, bbox)):
+                if dst is not None:
+                    dst.copy_(src)
+            for p in self.params:
+                state = self.opt.state.get(p)
+                if state:
+                    state['step'].zero_()
+                    state['exp_avg'].zero_()
+                    state['exp_avg_sq'].zero_()
+
+    def step(self, rfn, kw):
+        """One step (run.py:2256-2310): producer + render, loss, backward, Adam, projections.
+        Returns the loss (the per-batch sum, as the reference's `loss.sum()`)."""
+        cfg = self.cfg
+        prepared = None
+        side = self.side
+        if side is not None:
+            main = torch.cuda.current_stream(self.target.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                prepared = vgg_target(cfg.loss, self.target, self.lpips_net, cfg.white_background)
+        cam, foc = pose_to_matrix(self.z0_, self.t2_, self.s_, F.normalize(self.q_, dim=-1), cfg.camera_flipped)
+        ws = self.z_ * cfg.gain_z
         if cfg.no_split:
             ws = ws.expand(-1, 15, -1)
-        rgb = rfn(generator, res, res, cam, foc, center, bbox, ws, cfg.samples,
+        rgb = rfn(self.gen, cfg.resolution, cfg.resolution, cam, foc, self.center, self.bbox, ws, cfg.samples,
                   force_no_cam_grad=not cfg.optimize_pose, **kw)[0]
         if side is not None:
             main.wait_stream(side)
             for t in ([prepared[0]] if prepared[0] is not None else []) + list(prepared[1]):
                 t.record_stream(main)
-        loss = image_loss(cfg.loss, rgb, target, lpips_net, cfg.white_background, prepared=prepared)
+        loss = image_loss(cfg.loss, rgb, self.target, self.lpips_net, cfg.white_background, prepared=prepared)
         loss.backward()
-        opt.step()
-        opt.zero_grad()
+        self.opt.step()
+        self.opt.zero_grad()
         with torch.no_grad():
-            q_.copy_(F.normalize(q_, dim=-1))
-            if z0_ is not None:
-                z0_.clamp_(-4, 4)
-            s_.abs_()
-        losses.append(loss.detach())
+            self.q_.copy_(F.normalize(self.q_, dim=-1))
+            if self.z0_ is not None:
+                self.z0_.clamp_(-4, 4)
+            self.s_.abs_()
+        return loss
+
+    def result(self, losses, secs):
+        cfg = self.cfg
+        ws = (self.z_.detach() * cfg.gain_z)
+        if cfg.no_split:
+            ws = ws.expand(-1, 15, -1)
+        z0 = self.z0_
+        return InversionResult(ws=ws.clone(), z0=None if z0 is None else z0.detach().clone(),
+                               t2=self.t2_.detach().clone(), s=self.s_.detach().clone(),
+                               q=self.q_.detach().clone(), losses=[float(x) for x in losses], seconds=secs)
+
+
+_GRAPHS: dict = {}
+EAGER_STEPS = 2           # eager steps before the capture (Adam state, frozen caches, library plans)
+
+
+def _graph_key(generator, target_img, cam2world, focal, w_init, cfg, center, bbox, lpips_net):
+    import dataclasses
+
+    def shape(t):
+        return None if t is None else (tuple(t.shape), t.dtype, t.device)
+    return (id(generator), id(lpips_net), shape(target_img), shape(cam2world), shape(focal), shape(w_init),
+            shape(center), shape(bbox), dataclasses.astuple(cfg))
+
+
+def _invert_graphed(generator, target_img, cam2world, focal, w_init, cfg, center, bbox, on_step, lpips_net,
+                    checkpoints, on_checkpoint):
+    key = _graph_key(generator, target_img, cam2world, focal, w_init, cfg, center, bbox, lpips_net)
+    entry = _GRAPHS.get(key)
+    fresh = entry is None or entry['gen'] is not generator or entry['net'] is not lpips_net
+    if fresh:
+        cen = None if center is None else center.detach().clone()
+        bb = None if bbox is None else bbox.detach().clone()
+        st = _State(generator, target_img, cam2world, focal, w_init, cfg, cen, bb, lpips_net, capturable=True)
+        entry = {'gen': generator, 'net': lpips_net, 'state': st, 'graph': None, 'loss': None}
+        _GRAPHS.clear()              # one live graph (its memory pool) at a time
+        _GRAPHS[key] = entry
+    else:
+        st = entry['state']
+        st.load(target_img, cam2world, focal, w_init, center, bbox)
+    dev = target_img.device
+    losses = []
+    if on_checkpoint is not None and 0 in checkpoints:
+        on_checkpoint(0, st.views())
+    t0 = time.perf_counter()
+    loss = None
+    for it in range(cfg.steps):
+        if entry['graph'] is None and it == EAGER_STEPS and cfg.steps > EAGER_STEPS:
+            # the capture records one step without running it; replays run it.  The eager steps'
+            # autograd graphs must be gone first: a live one keeps the leaves' AccumulateGrad nodes
+            # bound to the eager stream, and the capture would then wait on that stream
+            loss = None
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                entry['loss'] = st.step(_nfi_render, {})
+            entry['graph'] = g
+        if entry['graph'] is not None:
+            entry['graph'].replay()
+            loss = entry['loss']
+        else:
+            # eager steps take the same device draws the graph does
+            with _capturing_draws():
+                loss = st.step(_nfi_render, {})
+        losses.append(loss.detach().clone())
         if on_step is not None:
             on_step(it, loss)
         if on_checkpoint is not None and it + 1 in checkpoints:
-            on_checkpoint(it + 1, (z_, z0_, t2_, s_, q_))
-    if torch.cuda.is_available() and target_img.is_cuda:
-        torch.cuda.synchronize(target_img.device)
+            on_checkpoint(it + 1, st.views())
+    torch.cuda.synchronize(dev)
     secs = time.perf_counter() - t0
-    ws = (z_.detach() * cfg.gain_z)
-    if cfg.no_split:
-        ws = ws.expand(-1, 15, -1)
-    return InversionResult(ws=ws, z0=None if z0_ is None else z0_.detach(), t2=t2_.detach(),
-                           s=s_.detach(), q=q_.detach(), losses=[float(x) for x in losses], seconds=secs)
+    return st.result(losses, secs)
+
+
+class _capturing_draws:
+    """Eager steps of a graphed inversion draw the renderer's uniforms from torch's device
+    generator too (ops.volume_render does so while a capture is running)."""
+
+    def __enter__(self):
+        from . import ops
+        self.prev, ops.DEVICE_DRAWS = ops.DEVICE_DRAWS, True
+        return self
+
+    def __exit__(self, *exc):
+        from . import ops
+        ops.DEVICE_DRAWS = self.prev
+        return False

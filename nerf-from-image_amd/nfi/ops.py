@@ -39,6 +39,11 @@ FORWARD_TILE_COUNTS = True
 
 KERNEL_TIMERS: Optional[dict] = None
 
+# randomized renders draw their uniforms with torch.rand on the device (graph-safe) instead of the
+# kernels' host-seeded Philox stream: always while a HIP graph is being captured, and when set
+# (the eager steps of a graphed inversion, nfi.inversion)
+DEVICE_DRAWS = False
+
 
 class _timed:
     """HIP events around one C-ABI call, recorded on the stream it launches on."""
@@ -47,7 +52,8 @@ class _timed:
         self.name, self.dev, self.stream = name, dev, stream
 
     def __enter__(self):
-        if KERNEL_TIMERS is not None:
+        self.on = KERNEL_TIMERS is not None and not torch.cuda.is_current_stream_capturing()
+        if self.on:
             self.s = self.stream if self.stream is not None else torch.cuda.current_stream(self.dev)
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e1 = torch.cuda.Event(enable_timing=True)
@@ -55,7 +61,7 @@ class _timed:
         return self
 
     def __exit__(self, *exc):
-        if KERNEL_TIMERS is not None:
+        if self.on:
             self.e1.record(self.s)
             KERNEL_TIMERS.setdefault(self.name, []).append((self.e0, self.e1))
         return False
@@ -492,6 +498,14 @@ def volume_render(planes_tm, palette, ro, rd, near, far, dec, opts: RenderOption
     if ro.shape[0] != B or (palette is not None and palette.shape != (B, 10, 3)):
         raise ValueError('batch mismatch between planes, palette and rays')
     n = ro.shape[0] * ro.shape[1] * ro.shape[2]
+    if opts.randomize and (DEVICE_DRAWS or torch.cuda.is_current_stream_capturing()):
+        # a captured HIP graph replays its launch arguments: a host-drawn Philox seed would repeat
+        # on every replay, so the draws come from torch's graph-safe device generator instead
+        # (fresh on each replay; the same U[0,1) the kernels' own Philox stream provides)
+        if u_coarse is None:
+            u_coarse = torch.rand(n * opts.samples, device=ro.device)
+        if u_fine is None and opts.fine:
+            u_fine = torch.rand(n * opts.samples, device=ro.device)
     for name, u in (('u_coarse', u_coarse), ('u_fine', u_fine)):
         if u is not None and u.numel() != n * opts.samples:
             raise ValueError(f'{name} must have B*H*W*S = {n * opts.samples} elements')

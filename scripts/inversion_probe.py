@@ -14,7 +14,7 @@ import nfi  # noqa: E402
 from nfi import inversion, lpips, producer  # noqa: E402
 
 
-def run(B, loss, steps=10, cl=False):
+def run(B, loss, steps=10, cl=False, graph=True, overlap=True):
     dev = torch.device('cuda:0')
     cfg = bench.CONFIGS['p3d_fwdbwd']
     cfg = cfg[:3] + (B,) + cfg[4:]
@@ -27,7 +27,8 @@ def run(B, loss, steps=10, cl=False):
     net = lpips.LPIPS().to(dev) if loss == 'vgg' else None
     if net is not None and cl:
         net = net.to(memory_format=torch.channels_last)
-    icfg = inversion.InversionConfig(steps=2, resolution=128, samples=64, loss=loss)
+    icfg = inversion.InversionConfig(steps=inversion.EAGER_STEPS + 1, resolution=128, samples=64, loss=loss,
+                                     graph=graph, overlap_target=overlap)
     inversion.invert(gen, target, batch['cam'], batch['focal'], w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     icfg.steps = steps
@@ -38,7 +39,7 @@ def run(B, loss, steps=10, cl=False):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps
     cpu = (enq[-1] - enq[0]) / (steps - 1)
-    print(f'B={B:3d} loss={loss:4s} cl={cl}: {wall * 1e3:7.2f} ms/step  {wall * 30 / B:.4f} s/img  '
+    print(f'B={B:3d} loss={loss:4s} cl={cl} graph={graph} overlap={overlap}: {wall * 1e3:7.2f} ms/step  {wall * 30 / B:.4f} s/img  '
           f'(enqueue {cpu * 1e3:.2f} ms/step between on_step calls)', flush=True)
 
 
@@ -46,8 +47,7 @@ if __name__ == '__main__':
     if len(sys.argv) > 1:          # python scripts/inversion_probe.py B loss steps
         run(int(sys.argv[1]), sys.argv[2], steps=int(sys.argv[3]))
         sys.exit(0)
-    for B in (4, 8, 16):
-        run(B, 'l1')
-    for B in (4, 8):
-        run(B, 'vgg')
-    run(8, 'vgg', cl=True)
+    for loss in ('l1', 'vgg'):
+        for graph in (False, True):
+            for overlap in ((True, False) if loss == 'vgg' else (True,)):
+                run(4, loss, steps=30, graph=graph, overlap=overlap)
