@@ -124,9 +124,9 @@ class ModulatedConv(nn.Module):
 
     backend = 'hip'
 
-    def forward(self, x, w):
+    def forward(self, x, w, pre=None):
         if self.backend == 'hip':
-            return self._forward_hip(x, w)
+            return self._forward_hip(x, w, pre)
         styles = self.affine(w)                                           # [b, in]
         wmod = self.weight[None] * styles[:, None, :, None, None]         # [b, out, in, 3, 3]
         dcoefs = (wmod.square().sum(dim=(2, 3, 4)) + 1e-8).rsqrt()        # [b, out]
@@ -140,11 +140,14 @@ class ModulatedConv(nn.Module):
         x = (x + self.bias[None, :, None, None]) * SQRT2
         return F.leaky_relu(x, 0.2)
 
-    def _forward_hip(self, x, w):
+    def _forward_hip(self, x, w, pre=None):
         ops = _hip()
-        styles = self.affine(w)
-        w2 = frozen_value(self, 'w2', lambda: self.weight.square().sum(dim=(2, 3)), self.weight)  # [out, in]
-        dcoefs = (styles.square() @ w2.t() + 1e-8).rsqrt()                # [b, out]
+        if pre is None:
+            styles = self.affine(w)
+            w2 = frozen_value(self, 'w2', lambda: self.weight.square().sum(dim=(2, 3)), self.weight)  # [out, in]
+            dcoefs = (styles.square() @ w2.t() + 1e-8).rsqrt()                # [b, out]
+        else:                                  # from SynthesisNetwork's style bank
+            styles, dcoefs = pre
         xs = ops.scale(x, styles)
         if self.up:
             t = F.conv_transpose2d(xs, self.weight.transpose(0, 1), stride=2)
@@ -164,8 +167,8 @@ class ToPlanes(nn.Module):
 
     backend = 'hip'
 
-    def forward(self, x, w):
-        styles = self.affine(w) * self.weight_gain
+    def forward(self, x, w, pre=None):
+        styles = self.affine(w) * self.weight_gain if pre is None else pre
         if self.backend == 'hip':
             return F.conv2d(_hip().scale(x, styles), self.weight)          # bias added in up_add
         x = F.conv2d(x * styles[:, :, None, None], self.weight)
@@ -189,15 +192,18 @@ class SynthesisBlock(nn.Module):
 
     backend = 'hip'
 
-    def forward(self, x, img, ws):
+    def forward(self, x, img, ws, bank=None):
+        """ws: this block's rows of the latent; bank: their precomputed (styles, dcoefs) per layer
+        in the order conv0, conv1, torgb (SynthesisNetwork.style_bank), or None."""
         k = 0
+        pre = bank or (None, None, None)
         if self.in_ch == 0:
-            x = self.const[None].expand(ws.shape[0], -1, -1, -1)
+            x = self.const[None].expand(ws[0].shape[0], -1, -1, -1)
         else:
-            x = self.conv0(x, ws[:, k])
+            x = self.conv0(x, ws[k], pre[0])
             k += 1
-        x = self.conv1(x, ws[:, k])
-        y = self.torgb(x, ws[:, k + 1])
+        x = self.conv1(x, ws[k], pre[k])
+        y = self.torgb(x, ws[k + 1], pre[k + 1])
         if self.backend == 'hip':
             return x, _hip().up_add(img, y, self.torgb.bias)
         img = y if img is None else upsample2x(img, self.resample_filter) + y
@@ -221,13 +227,86 @@ class SynthesisNetwork(nn.Module):
         self.num_ws += 1   # the last block's toRGB
 
     def forward(self, ws, noise_mode: str = 'const'):
+        # ws [b, num_ws, w_dim] or its rows (a sequence of [b, w_dim]); the rows are split once
+        # (one unbind: its backward is one stack, not a zero-filled [b, num_ws, w_dim] gradient and
+        # an accumulation per slice)
+        bank = None
+        if torch.is_tensor(ws) and ws.is_cuda and self.b4.backend == 'hip':
+            bank = iter(self.style_bank(ws))
+        rows = ws.unbind(1) if torch.is_tensor(ws) else ws
         x = img = None
         k = 0
         for r in self.resolutions:
             blk = getattr(self, f'b{r}')
-            x, img = blk(x, img, ws[:, k:k + blk.num_conv + 1])
+            pre = None if bank is None else [next(bank) for _ in range(blk.num_conv + 1)]
+            x, img = blk(x, img, rows[k:k + blk.num_conv + 1], pre)
             k += blk.num_conv
         return img
+
+    def _bank_layers(self):
+        """(module, latent row, is_conv) of every modulated layer in execution order."""
+        out, base = [], 0
+        for r in self.resolutions:
+            blk = getattr(self, f'b{r}')
+            k = base                      # SynthesisNetwork.forward hands block r rows[base:]
+            if blk.in_ch:
+                out.append((blk.conv0, k, True))
+                k += 1
+            out.append((blk.conv1, k, True))
+            out.append((blk.torgb, k + 1, False))
+            base += blk.num_conv
+        return out
+
+    def style_bank(self, ws):
+        """The styles (affine of the layer's latent row, stylegan.py:337 / :375-377) and the
+        demodulation coefficients (:140-142) of all 21 modulated layers as two batched products
+        instead of ~35 small GEMMs and their elementwise tails: S = X W^T + b over the stacked
+        gain-folded affine weights ([21, 512, 512], zero-padded rows), D = rsqrt(S^2 W2^T + 1e-8)
+        over the stacked sums of squared conv weights ([14, 512, 512]).  Frozen parameters only
+        (the stacks are built once per parameter version, frozen_value).  Returns, per layer in
+        execution order, (styles [b, in], dcoefs [b, out]) for convolutions and styles for toRGB
+        (its 1/sqrt(in) weight gain folded in)."""
+        layers = self._bank_layers()
+        params = []
+        for m, _, conv in layers:
+            params += [m.affine.weight, m.affine.bias] + ([m.weight] if conv else [])
+
+        def build():
+            dev = ws.device
+            L = len(layers)
+            wdim = layers[0][0].affine.weight.shape[1]
+            cmax = max(m.affine.weight.shape[0] for m, _, _ in layers)
+            conv_ids = [i for i, (_, _, c) in enumerate(layers) if c]
+            omax = max(layers[i][0].weight.shape[0] for i in conv_ids)
+            A = torch.zeros((L, cmax, wdim), device=dev)
+            bias = torch.zeros((L, 1, cmax), device=dev)
+            W2 = torch.zeros((len(conv_ids), omax, cmax), device=dev)
+            for i, (m, _, conv) in enumerate(layers):
+                g = 1.0 if conv else m.weight_gain
+                n = m.affine.weight.shape[0]
+                A[i, :n] = m.affine.weight * (m.affine.weight_gain * g)
+                bias[i, 0, :n] = m.affine.bias * (m.affine.bias_gain * g)
+            for j, i in enumerate(conv_ids):
+                w = layers[i][0].weight
+                W2[j, :w.shape[0], :w.shape[1]] = w.square().sum(dim=(2, 3))
+            rows = torch.tensor([k for _, k, _ in layers], device=dev)
+            return A.transpose(1, 2), bias, W2.transpose(1, 2), rows, torch.tensor(conv_ids, device=dev)
+
+        At, bias, W2t, rows, conv_ids = frozen_value(self, 'style_bank', build, *params)
+        S = torch.baddbmm(bias, ws.index_select(1, rows).transpose(0, 1), At)        # [L, b, cmax]
+        D = (torch.bmm(S.index_select(0, conv_ids).square(), W2t) + 1e-8).rsqrt()   # [Lc, b, omax]
+        styles, dcoefs = S.unbind(0), iter(D.unbind(0))
+        out = []
+        for (m, _, conv), s in zip(layers, styles):
+            n = m.affine.weight.shape[0]
+            s = s if n == s.shape[1] else s[:, :n]
+            if conv:
+                d = next(dcoefs)
+                o = m.weight.shape[0]
+                out.append((s, d if o == d.shape[1] else d[:, :o]))
+            else:
+                out.append(s)
+        return out
 
 
 class MappingNetwork(nn.Module):

@@ -179,3 +179,13 @@ def test_hip_backend_refuses_cpu_tensors():
         gen.planes_and_palette(torch.zeros(1, 15, 512))
     with pytest.raises(ValueError):
         gen.set_backend('cpu')
+
+
+def test_style_bank_layer_rows():
+    """The style bank feeds every modulated layer the latent row SynthesisNetwork.forward gives it
+    (block r gets rows[base : base + num_conv + 1]; conv0, conv1, toRGB in order)."""
+    net = producer.SynthesisNetwork(512, 32, 96)
+    rows = [k for _, k, _ in net._bank_layers()]
+    # 4: conv1 0, rgb 1 | 8: conv0 1, conv1 2, rgb 3 | 16: 3, 4, 5 | 32: 5, 6, 7
+    assert rows == [0, 1, 1, 2, 3, 3, 4, 5, 5, 6, 7]
+    assert max(rows) + 1 == net.num_ws
