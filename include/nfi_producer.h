@@ -110,6 +110,16 @@ int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C,
 int32_t nfi_wino_output_transform(const float* M, const float* bias, float* y, float* pooled, int32_t N,
                                   int32_t Co, int32_t H, int32_t W, void* stream);
 
+/* The fused layer: input transform, the 36 products on the matrix cores (v_mfma_f32_16x16x4_f32,
+ * accumulators resident for a 32-tile x 32-channel block) and the output transform in one kernel,
+ * same epilogue contract as nfi_wino_output_transform.  Ua = nfi_wino_pack_weights(U) (the
+ * per-lane MFMA operand layout [36][CoP/16][Ci/4][64], CoP = Co rounded up to 32, zero rows;
+ * nfi_wino_packed_size floats).  Ci % 8 == 0, H and W multiples of 4, x and y 16-byte aligned. */
+int64_t nfi_wino_packed_size(int32_t Co, int32_t Ci);
+int32_t nfi_wino_pack_weights(const float* U, float* Ua, int32_t Co, int32_t Ci, void* stream);
+int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, float* y, float* pooled,
+                            int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

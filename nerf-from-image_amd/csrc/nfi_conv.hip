@@ -26,6 +26,25 @@
 namespace nfi {
 namespace wino {
 
+// V and M stream through HBM once each; NFI_WINO_NT 1 marks those accesses nontemporal
+#ifndef NFI_WINO_NT
+#define NFI_WINO_NT 1
+#endif
+__device__ __forceinline__ void st_stream(float v, float* p) {
+#if NFI_WINO_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ float ld_stream(const float* p) {
+#if NFI_WINO_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 // Interpolation points 0, 1, -1, 2, -1/2 and infinity: in fp32 this point set has about half
 // the transform rounding error of the usual 0, +-1, +-2 (measured by emulation: 2.4e-6 vs 4.3e-6
 // mean, 8e-6 vs 2.8e-5 max of a 256-channel tile relative to its largest output); the input
@@ -131,7 +150,7 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
     float o[6];
     bt_col(s[r], o);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) __builtin_nontemporal_store(o[j], out + (r * 6 + j) * plane);
+    for (int j = 0; j < 6; ++j) st_stream(o[j], out + (r * 6 + j) * plane);
   }
 }
 
@@ -153,7 +172,7 @@ __global__ void __launch_bounds__(256) output_kernel(const float* __restrict__ M
 #pragma unroll
   for (int r = 0; r < 6; ++r)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) m[r][j] = __builtin_nontemporal_load(src + (r * 6 + j) * plane);
+    for (int j = 0; j < 6; ++j) m[r][j] = ld_stream(src + (r * 6 + j) * plane);
   // columns: s = A^T m (4x6), then rows: o = s A (4x4)
   float s[4][6];
 #pragma unroll
@@ -187,6 +206,257 @@ __global__ void __launch_bounds__(256) output_kernel(const float* __restrict__ M
       *reinterpret_cast<float2*>(pd + (int64_t)r * W2) =
           make_float2(fmaxf(fmaxf(o[2 * r][0], o[2 * r][1]), fmaxf(o[2 * r + 1][0], o[2 * r + 1][1])),
                       fmaxf(fmaxf(o[2 * r][2], o[2 * r][3]), fmaxf(o[2 * r + 1][2], o[2 * r + 1][3])));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused layer: input transform, the 36 products and the output transform in one kernel, so V
+// and M never leave the chip (the unfused path writes and re-reads 2.25x the input and the
+// output through HBM).  Output-stationary: a workgroup owns FP = 32 tiles x FC = 32 output
+// channels for all 36 products; wave w accumulates products 9w .. 9w+8 (9 x 2 x 2
+// v_mfma_f32_16x16x4_f32 tiles = 144 accumulator registers).  K loop over the input channels
+// in chunks of FK = 8: every thread loads one (channel, tile) 6x6 patch, transforms it and
+// writes its 36 values to an LDS V image (double buffered, the next chunk's patch is loaded
+// during the current chunk's MFMAs); the A operands (U) are pre-packed per lane
+// (nfi_wino_pack_weights: one coalesced 256-B load per MFMA operand).  Epilogue: the
+// accumulators go through LDS one 16-channel half at a time (36 x 16 x 32 floats, the V
+// buffers' space) and each thread transforms two (channel, tile) outputs with the same bias /
+// ReLU / max-pool epilogue as output_kernel.
+// ---------------------------------------------------------------------------------------
+constexpr int FP = 32, FC = 64, FK = 8;
+constexpr int HB = FC / 16;                   // 16-channel MFMA row blocks per workgroup
+constexpr int VIMG = 36 * FK * FP;            // floats per V image
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// U [36][Co][Ci] -> Ua [36][CoP/16][Ci/4][64] (lane l: row l & 15, k l >> 4 of a 16x4 A operand;
+// rows past Co are zero)
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ U, float* __restrict__ Ua,
+                                                   int Co, int Ci, int CB, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int l = (int)(i & 63);
+  const int64_t q = i >> 6;
+  const int KC4 = Ci >> 2;
+  const int kc = (int)(q % KC4);
+  const int64_t q2 = q / KC4;
+  const int cb = (int)(q2 % CB);
+  const int xi = (int)(q2 / CB);
+  const int co = 16 * cb + (l & 15), ci = 4 * kc + (l >> 4);
+  Ua[i] = co < Co ? U[((int64_t)xi * Co + co) * Ci + ci] : 0.f;
+}
+
+__device__ __forceinline__ void load_patch(const float* __restrict__ xp, int H, int W, int ty, int tx,
+                                           bool valid, float (&d)[6][6]) {
+  const int x0 = 4 * tx;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int yy = 4 * ty - 1 + r;
+    if (!valid || yy < 0 || yy >= H) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) d[r][j] = 0.f;
+      continue;
+    }
+    const float* row = xp + (int64_t)yy * W;
+    const float4 m = *reinterpret_cast<const float4*>(row + x0);
+    d[r][0] = x0 > 0 ? row[x0 - 1] : 0.f;
+    d[r][1] = m.x;
+    d[r][2] = m.y;
+    d[r][3] = m.z;
+    d[r][4] = m.w;
+    d[r][5] = x0 + 4 < W ? row[x0 + 4] : 0.f;
+  }
+}
+
+// B^T d B of a patch, written to V image slot (xi, row, col): dst[xi * FK * FP]
+__device__ __forceinline__ void stage_patch(float (&d)[6][6], float* __restrict__ dst) {
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float col[6], o[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) col[r] = d[r][j];
+    bt_col(col, o);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) d[r][j] = o[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    float o[6];
+    bt_col(d[r], o);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) dst[(r * 6 + j) * (FK * FP)] = o[j];
+  }
+}
+
+// A^T m A of one tile plus the epilogue, stored to y (and pooled)
+__device__ __forceinline__ void emit_tile(float (&m)[6][6], float b, int mode, float* __restrict__ dst, int W,
+                                          float* __restrict__ pd, int W2) {
+  float s[4][6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float col[6], o[4];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) col[r] = m[r][j];
+    at_col(col, o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[r][j] = o[r];
+  }
+  float o[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) at_col(s[r], o[r]);
+  if (mode == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[r][j] = fmaxf(o[r][j] + b, 0.f);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    *reinterpret_cast<float4*>(dst + (int64_t)r * W) = make_float4(o[r][0], o[r][1], o[r][2], o[r][3]);
+  if (pd != nullptr) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      *reinterpret_cast<float2*>(pd + (int64_t)r * W2) =
+          make_float2(fmaxf(fmaxf(o[2 * r][0], o[2 * r][1]), fmaxf(o[2 * r + 1][0], o[2 * r + 1][1])),
+                      fmaxf(fmaxf(o[2 * r][2], o[2 * r][3]), fmaxf(o[2 * r + 1][2], o[2 * r + 1][3])));
+  }
+}
+
+// grid (ceil(P / FP), CoP / FC), 256 threads, one workgroup per CU (occupancy 1: 288
+// accumulator registers per lane, the next chunk's A operands and patch prefetched a whole
+// chunk ahead).  Ci % FK == 0.
+__global__ void __launch_bounds__(256, 1) fused_kernel(const float* __restrict__ x, const float* __restrict__ Ua,
+                                                       const float* __restrict__ bias, float* __restrict__ y,
+                                                       float* __restrict__ pooled, int Ci, int Co, int H, int W,
+                                                       int TW, int T, int64_t P, int CB, int mode, int nPB,
+                                                       int nCB) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * VIMG];
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  // XCD-aware block order: workgroup b runs on XCD b % 8; XCD x takes the contiguous range
+  // [x * G / 8, (x + 1) * G / 8) of the (channel block, tile block) grid in channel-block-major
+  // order, so the A operands of a channel block (36 x 64 x Ci floats) stay in that XCD's L2
+  const int G = gridDim.x;                         // nPB * nCB rounded up to a multiple of 8
+  const int logical = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int cbk = logical / nPB;
+  if (cbk >= nCB) return;                          // padding workgroups
+  const int64_t p0 = (int64_t)(logical - cbk * nPB) * FP;
+  const int cb0 = cbk * HB;
+  const int KC4 = Ci >> 2, nk = Ci / FK;
+  // staging role: channel cl of the chunk, tile pl of the block
+  const int pl = t & 31, cl = t >> 5;
+  const int64_t ps = p0 + pl;
+  const bool pvalid = ps < P;
+  int sn = 0, sty = 0, stx = 0;
+  if (pvalid) {
+    sn = (int)(ps / T);
+    const int tt = (int)(ps - (int64_t)sn * T);
+    sty = tt / TW;
+    stx = tt - sty * TW;
+  }
+  const int64_t HW = (int64_t)H * W;
+  const float* xs = x + ((int64_t)sn * Ci + cl) * HW;
+  // V image [36][FK][FP]; odd channel rows rotated by 16 columns so that the two k rows a
+  // half-wave reads (ds_read_b32 lane groups of 32) fall in different banks
+  float* vdst = lds + cl * FP + ((pl + 16 * (cl & 1)) & 31);
+  const int kk = l >> 4, cc = l & 15;
+
+  f4v acc[9][HB][2];
+#pragma unroll
+  for (int a = 0; a < 9; ++a)
+#pragma unroll
+    for (int h = 0; h < HB; ++h)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) acc[a][h][g] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // A operands, one product ahead: [h][s], one float per lane each
+  const float* ua = Ua + (((int64_t)(9 * w) * CB + cb0) * KC4) * 64 + l;
+  auto load_a = [&](int xl, int c, float (&A)[HB][2]) {
+#pragma unroll
+    for (int h = 0; h < HB; ++h)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) A[h][s2] = ua[(((int64_t)xl * CB + h) * KC4 + 2 * c + s2) * 64];
+  };
+
+  float d[6][6];
+  float an[HB][2];
+  load_patch(xs, H, W, sty, stx, pvalid, d);
+  load_a(0, 0, an);
+  stage_patch(d, vdst);
+  __syncthreads();
+  for (int c = 0; c < nk; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nk) load_patch(xs + (int64_t)(c + 1) * FK * HW, H, W, sty, stx, pvalid, d);
+    const float* V = lds + cur * VIMG;
+    float bn[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+        bn[s2][g] = V[((9 * w) * FK + 4 * s2 + kk) * FP + ((16 * g + cc + 16 * (kk & 1)) & 31)];
+#pragma unroll
+    for (int xl = 0; xl < 9; ++xl) {
+      const int xi = 9 * w + xl;
+      float a[HB][2], b[2][2];
+#pragma unroll
+      for (int h = 0; h < HB; ++h)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) a[h][s2] = an[h][s2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int g = 0; g < 2; ++g) b[s2][g] = bn[s2][g];
+      if (xl + 1 < 9) {
+        load_a(xl + 1, c, an);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+            bn[s2][g] = V[((xi + 1) * FK + 4 * s2 + kk) * FP + ((16 * g + cc + 16 * (kk & 1)) & 31)];
+      } else if (c + 1 < nk) {
+        load_a(0, c + 1, an);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int h = 0; h < HB; ++h)
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+            acc[xl][h][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h][s2], b[s2][g], acc[xl][h][g], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c + 1 < nk) stage_patch(d, vdst + (cur ^ 1) * VIMG);
+    __syncthreads();
+  }
+
+  // epilogue, one 16-channel block at a time: M image [36][16][FP]
+  const int W2 = W >> 1, H2 = H >> 1;
+#pragma unroll
+  for (int h = 0; h < HB; ++h) {
+#pragma unroll
+    for (int xl = 0; xl < 9; ++xl)
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          lds[((9 * w + xl) * 16 + 4 * kk + i) * FP + 16 * g + cc] = acc[xl][h][g][i];
+    __syncthreads();
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      const int col = (t >> 5) + 8 * rep;
+      const int co = cbk * FC + 16 * h + col;
+      const int64_t p = p0 + (t & 31);
+      if (co < Co && p < P) {
+        float m[6][6];
+#pragma unroll
+        for (int xi = 0; xi < 36; ++xi) m[xi / 6][xi % 6] = lds[(xi * 16 + col) * FP + (t & 31)];
+        const int n = (int)(p / T);
+        const int tt = (int)(p - (int64_t)n * T);
+        const int ty = tt / TW, tx = tt - ty * TW;
+        float* dst = y + (((int64_t)n * Co + co) * H + 4 * ty) * W + 4 * tx;
+        float* pd = pooled ? pooled + (((int64_t)n * Co + co) * H2 + 2 * ty) * W2 + 2 * tx : nullptr;
+        emit_tile(m, mode == 1 ? bias[co] : 0.f, mode, dst, W, pd, W2);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -235,6 +505,44 @@ int32_t nfi_wino_output_transform(const float* M, const float* bias, float* y, f
   hipLaunchKernelGGL(output_kernel, dim3((unsigned)((P + 255) / 256), Co), dim3(256), 0,
                      (hipStream_t)stream, M, bias, y, pooled, Co, H, W, TW, T, P, bias ? 1 : 0);
   NFI_CHECK_LAUNCH("wino output_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_wino_pack_weights(const float* U, float* Ua, int32_t Co, int32_t Ci, void* stream) {
+  NFI_REQUIRE(U && Ua, "wino_pack_weights: null pointer");
+  NFI_REQUIRE(Co > 0 && Ci > 0 && Ci % 4 == 0, "wino_pack_weights: bad shape (Ci % 4 == 0)");
+  const int CB = (Co + FC - 1) / FC * HB;
+  const int64_t n = (int64_t)36 * CB * (Ci / 4) * 64;
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, U, Ua,
+                     Co, Ci, CB, n);
+  NFI_CHECK_LAUNCH("wino pack_kernel");
+  return NFI_OK;
+}
+
+int64_t nfi_wino_packed_size(int32_t Co, int32_t Ci) {
+  if (Co <= 0 || Ci <= 0 || Ci % 4) return -1;
+  return (int64_t)36 * ((Co + FC - 1) / FC * FC) * Ci;
+}
+
+int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, float* y, float* pooled,
+                            int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(x && Ua && y, "wino_conv_fused: null pointer");
+  NFI_REQUIRE(N > 0 && Ci > 0 && Ci % FK == 0 && Co > 0 && H >= 4 && W >= 4 && H % 4 == 0 && W % 4 == 0,
+              "wino_conv_fused: bad shape (Ci % 8, H % 4, W % 4 must be 0)");
+  NFI_REQUIRE(pooled == nullptr || bias != nullptr, "wino_conv_fused: pooling needs the bias/ReLU epilogue");
+  NFI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && (pooled == nullptr || ((uintptr_t)pooled & 7) == 0),
+              "wino_conv_fused: misaligned tensors");
+  const int TW = W / 4, T = (H / 4) * TW;
+  const int64_t P = (int64_t)N * T;
+  const int CoP = (Co + FC - 1) / FC * FC;
+  NFI_REQUIRE((P + FP - 1) / FP < (1ll << 31) && CoP / FC <= 65535, "wino_conv_fused: too large");
+  // 1-D grid of nPB * nCB workgroups rounded up to a multiple of 8 (fused_kernel maps them to XCDs)
+  const int64_t nPB = (P + FP - 1) / FP, nCB = CoP / FC;
+  const int64_t G = (nPB * nCB + 7) / 8 * 8;
+  NFI_REQUIRE(G < (1ll << 31), "wino_conv_fused: too large");
+  hipLaunchKernelGGL(fused_kernel, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x, Ua, bias, y, pooled,
+                     Ci, Co, H, W, TW, T, P, CoP / 16, bias ? 1 : 0, (int)nPB, (int)nCB);
+  NFI_CHECK_LAUNCH("wino fused_kernel");
   return NFI_OK;
 }
 

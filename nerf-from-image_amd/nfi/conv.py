@@ -30,6 +30,14 @@ from .ops import _require_device, _stream
 MIN_CHANNELS = 16
 ENABLED = True
 DGRAD = True          # data gradient as Winograd too (False: MIOpen's conv2d_input; diagnostics)
+FUSED = True          # one fused kernel per layer (nfi_wino_conv_fused) for layers with Ci % 8 == 0
+                      # and Ci <= FUSED_MAX_CI; else the three-pass form (transforms + hipBLASLt GEMM)
+# The fused kernel keeps V and M on chip but its 36-way split accumulators leave small per-product
+# tiles: 39-53 TFLOP/s of Winograd products on MI355X vs 100-137 for hipBLASLt's batched GEMM.  It
+# wins where the three-pass form's HBM round trips dominate — the 64-channel, large-map layers
+# (LPIPS 64->64 @128^2: 0.50 vs 0.68 ms) — and loses on the deeper ones (512->512 @16^2: 0.37 vs
+# 0.21 ms); scripts/wino_layers.py.
+FUSED_MAX_CI = 64
 
 
 def _p(t):
@@ -50,8 +58,10 @@ def applicable(x: torch.Tensor, weight: torch.Tensor) -> bool:
 
 
 def weights(weight: torch.Tensor):
-    """(U [36,Co,Ci], Ut [36,Ci,Co]) of a frozen [Co,Ci,3,3] weight, cached until the weight is
-    modified in place or replaced."""
+    """(U, Ut) of a frozen [Co,Ci,3,3] weight, cached until the weight is modified in place or
+    replaced: each a (transformed [36,Co,Ci] or [36,Ci,Co], MFMA-packed or None) pair — the
+    packed form (nfi_wino_pack_weights) feeds the fused kernel when its input-channel count is a
+    multiple of 8."""
     tag = (weight.data_ptr(), weight._version, weight.device)
     hit = getattr(weight, '_nfi_winograd', None)
     if hit is not None and hit[0] == tag:
@@ -64,23 +74,37 @@ def weights(weight: torch.Tensor):
     st = _stream(w.device)
     _call('nfi_wino_weight_transform', _p(w), _p(U), Co, Ci, 0, st)
     _call('nfi_wino_weight_transform', _p(w), _p(Ut), Co, Ci, 1, st)
-    weight._nfi_winograd = (tag, (U, Ut))      # cached on the (frozen) parameter itself
-    return U, Ut
+    out = ((U, _pack(U, Co, Ci, st)), (Ut, _pack(Ut, Ci, Co, st)))
+    weight._nfi_winograd = (tag, out)          # cached on the (frozen) parameter itself
+    return out
 
 
-def _winograd(x, U, bias=None, pool=False):
-    """x [N,Ci,H,W] (contiguous) with transformed weights U [36,Co,Ci] -> y [N,Co,H,W]
-    (and the pooled map when pool)."""
+def _pack(U, Co, Ci, st):
+    if Ci % 8:
+        return None
+    lib = _lib.load()
+    Ua = torch.empty((int(lib.nfi_wino_packed_size(Co, Ci)),), device=U.device)
+    _call('nfi_wino_pack_weights', _p(U), _p(Ua), Co, Ci, st)
+    return Ua
+
+
+def _winograd(x, Uw, bias=None, pool=False):
+    """x [N,Ci,H,W] (contiguous) with transformed weights Uw = (U [36,Co,Ci], packed or None) ->
+    y [N,Co,H,W] (and the pooled map when pool)."""
+    U, Ua = Uw
     N, Ci, H, W = x.shape
     Co = U.shape[1]
-    P = N * (H // 4) * (W // 4)
     st = _stream(x.device)
+    y = torch.empty((N, Co, H, W), device=x.device)
+    m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
+    if FUSED and Ua is not None and Ci <= FUSED_MAX_CI:
+        _call('nfi_wino_conv_fused', _p(x), _p(Ua), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
+        return (y, m) if pool else y
+    P = N * (H // 4) * (W // 4)
     V = torch.empty((36, Ci, P), device=x.device)
     _call('nfi_wino_input_transform', _p(x), _p(V), N, Ci, H, W, st)
     M = torch.bmm(U, V)
     del V
-    y = torch.empty((N, Co, H, W), device=x.device)
-    m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
     _call('nfi_wino_output_transform', _p(M), _p(bias), _p(y), _p(m), N, Co, H, W, st)
     return (y, m) if pool else y
 

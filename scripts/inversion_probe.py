@@ -14,7 +14,7 @@ import nfi  # noqa: E402
 from nfi import inversion, lpips, producer  # noqa: E402
 
 
-def run(B, loss, steps=10, cl=False, graph=True, overlap=True):
+def run(B, loss, steps=10, cl=False, graph=False, overlap=True):
     dev = torch.device('cuda:0')
     cfg = bench.CONFIGS['p3d_fwdbwd']
     cfg = cfg[:3] + (B,) + cfg[4:]

@@ -73,15 +73,42 @@ def test_winograd_vgg_block(N, Ci, Co, H, pool):
     assert rel < 1e-4, rel
 
 
+@pytest.mark.parametrize('pool', [False, True])
+@pytest.mark.parametrize('N,Ci,Co,H,W', [(3, 64, 64, 16, 12), (2, 8, 40, 8, 20), (1, 256, 96, 4, 4),
+                                         (5, 128, 128, 32, 32)])
+def test_fused_kernel_matches_three_pass(N, Ci, Co, H, W, pool):
+    """The fused Winograd kernel (transforms + MFMA products in one pass) against the three-pass
+    form (HIP transforms around hipBLASLt's batched GEMM): same transforms, different summation
+    order of the products only.  Partial tile blocks (P % 32 != 0), Co not a multiple of 32."""
+    g = torch.Generator(device=DEV).manual_seed(N * Ci + Co)
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    Uw, _ = conv.weights(w)
+    assert Uw[1] is not None
+    outs = []
+    for fused in (True, False):
+        conv.FUSED, conv.FUSED_MAX_CI = fused, 1 << 20
+        try:
+            r = conv._winograd(x, Uw, b if pool else None, pool)
+        finally:
+            conv.FUSED, conv.FUSED_MAX_CI = True, 64
+        outs.append(r if pool else (r,))
+    for a, ref in zip(*outs):
+        scale = float(ref.abs().max())
+        assert float((a - ref).abs().max()) <= 1e-5 * scale, float((a - ref).abs().max()) / scale
+
+
 def test_weight_cache_follows_in_place_updates():
     w = torch.randn((16, 16, 3, 3), device=DEV)
-    U1, _ = conv.weights(w)
-    U1c = U1.clone()
-    assert conv.weights(w)[0] is U1
+    (U1, A1), _ = conv.weights(w)
+    U1c, A1c = U1.clone(), A1.clone()
+    assert conv.weights(w)[0][0] is U1
     with torch.no_grad():
         w.mul_(2)
-    U2, _ = conv.weights(w)
+    (U2, A2), _ = conv.weights(w)
     torch.testing.assert_close(U2, 2 * U1c)
+    torch.testing.assert_close(A2, 2 * A1c)
 
 
 def test_trainable_weight_takes_the_library_path():
