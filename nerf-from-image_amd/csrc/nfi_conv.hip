@@ -79,6 +79,38 @@ __device__ __forceinline__ void at_col(const float* m, float* o) {
   o[3] = (b + m[5]) + 8.f * m[3] - 0.125f * m[4];
 }
 
+// The 6x6 input patch of tile (ty, tx), zero outside the map (padding 1) or when !valid.
+// Branch-free: every load is issued at a clamped, valid address and the padding is applied by
+// selects afterwards, so the 18 loads stay in flight together (a per-row load-or-zero branch
+// makes the compiler wait vmcnt(0) at each branch and serialises them).
+__device__ __forceinline__ void load_patch(const float* __restrict__ xp, int H, int W, int ty, int tx,
+                                           bool valid, float (&d)[6][6]) {
+  const int x0 = 4 * tx;
+  const int xl = max(x0 - 1, 0), xr = min(x0 + 4, W - 1);
+  float4 m4[6];
+  float lv[6], rv[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int yy = min(max(4 * ty - 1 + r, 0), H - 1);
+    const float* row = xp + (int64_t)yy * W;
+    m4[r] = *reinterpret_cast<const float4*>(row + x0);
+    lv[r] = row[xl];
+    rv[r] = row[xr];
+  }
+  const bool okl = valid && x0 > 0, okr = valid && x0 + 4 < W;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int yy = 4 * ty - 1 + r;
+    const bool ok = valid && yy >= 0 && yy < H;
+    d[r][0] = (ok && okl) ? lv[r] : 0.f;
+    d[r][1] = ok ? m4[r].x : 0.f;
+    d[r][2] = ok ? m4[r].y : 0.f;
+    d[r][3] = ok ? m4[r].z : 0.f;
+    d[r][4] = ok ? m4[r].w : 0.f;
+    d[r][5] = (ok && okr) ? rv[r] : 0.f;
+  }
+}
+
 __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ w, float* __restrict__ U,
                                                      int Co, int Ci, int flip) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -113,25 +145,8 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
   const int t = (int)(p - (int64_t)n * T);
   const int ty = t / TW, tx = t - ty * TW;
   const float* xp = x + ((int64_t)n * C + c) * H * W;
-  const int x0 = 4 * tx;
   float d[6][6];
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    const int y = 4 * ty - 1 + r;
-    if (y < 0 || y >= H) {
-#pragma unroll
-      for (int j = 0; j < 6; ++j) d[r][j] = 0.f;
-      continue;
-    }
-    const float* row = xp + (int64_t)y * W;
-    const float4 m = *reinterpret_cast<const float4*>(row + x0);
-    d[r][0] = x0 > 0 ? row[x0 - 1] : 0.f;
-    d[r][1] = m.x;
-    d[r][2] = m.y;
-    d[r][3] = m.z;
-    d[r][4] = m.w;
-    d[r][5] = x0 + 4 < W ? row[x0 + 4] : 0.f;
-  }
+  load_patch(xp, H, W, ty, tx, true, d);
   // columns: s = B^T d (per column), then rows: v = s B
   float s[6][6];
 #pragma unroll
@@ -243,28 +258,6 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ U, 
   const int xi = (int)(q2 / CB);
   const int co = 16 * cb + (l & 15), ci = 4 * kc + (l >> 4);
   Ua[i] = co < Co ? U[((int64_t)xi * Co + co) * Ci + ci] : 0.f;
-}
-
-__device__ __forceinline__ void load_patch(const float* __restrict__ xp, int H, int W, int ty, int tx,
-                                           bool valid, float (&d)[6][6]) {
-  const int x0 = 4 * tx;
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    const int yy = 4 * ty - 1 + r;
-    if (!valid || yy < 0 || yy >= H) {
-#pragma unroll
-      for (int j = 0; j < 6; ++j) d[r][j] = 0.f;
-      continue;
-    }
-    const float* row = xp + (int64_t)yy * W;
-    const float4 m = *reinterpret_cast<const float4*>(row + x0);
-    d[r][0] = x0 > 0 ? row[x0 - 1] : 0.f;
-    d[r][1] = m.x;
-    d[r][2] = m.y;
-    d[r][3] = m.z;
-    d[r][4] = m.w;
-    d[r][5] = x0 + 4 < W ? row[x0 + 4] : 0.f;
-  }
 }
 
 // B^T d B of a patch, written to V image slot (xi, row, col): dst[xi * FK * FP]
