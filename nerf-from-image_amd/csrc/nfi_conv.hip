@@ -135,9 +135,12 @@ __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ w
   }
 }
 
-// grid (ceil(P / 256), C)
-__global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x, float* __restrict__ V,
-                                                    int C, int H, int W, int TW, int T, int64_t P) {
+// grid (ceil(P / 256), C).  scale (optional, [N][C]): the transform of x * scale[n][c] (the
+// modulation of the synthesis layers, stylegan.py:130, applied to the input of the convolution;
+// the transform is linear, so the per-(image, channel) factor multiplies the 36 outputs)
+__global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                                    float* __restrict__ V, int C, int H, int W, int TW, int T,
+                                                    int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c = blockIdx.y;
   if (p >= P) return;
@@ -147,6 +150,13 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
   const float* xp = x + ((int64_t)n * C + c) * H * W;
   float d[6][6];
   load_patch(xp, H, W, ty, tx, true, d);
+  if (scale != nullptr) {
+    const float sc = scale[(int64_t)n * C + c];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) d[r][j] *= sc;
+  }
   // columns: s = B^T d (per column), then rows: v = s B
   float s[6][6];
 #pragma unroll
@@ -471,8 +481,8 @@ int32_t nfi_wino_weight_transform(const float* w, float* U, int32_t Co, int32_t 
   return NFI_OK;
 }
 
-int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C, int32_t H, int32_t W,
-                                 void* stream) {
+int32_t nfi_wino_input_transform_scaled(const float* x, const float* scale, float* V, int32_t N, int32_t C,
+                                        int32_t H, int32_t W, void* stream) {
   NFI_REQUIRE(x && V, "wino_input_transform: null pointer");
   NFI_REQUIRE(N > 0 && C > 0 && C <= 65535 && H >= 4 && W >= 4 && H % 4 == 0 && W % 4 == 0,
               "wino_input_transform: bad shape (H, W multiples of 4)");
@@ -480,9 +490,14 @@ int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C,
   const int TW = W / 4, T = (H / 4) * TW;
   const int64_t P = (int64_t)N * T;
   hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
-                     (hipStream_t)stream, x, V, C, H, W, TW, T, P);
+                     (hipStream_t)stream, x, scale, V, C, H, W, TW, T, P);
   NFI_CHECK_LAUNCH("wino input_kernel");
   return NFI_OK;
+}
+
+int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C, int32_t H, int32_t W,
+                                 void* stream) {
+  return nfi_wino_input_transform_scaled(x, nullptr, V, N, C, H, W, stream);
 }
 
 int32_t nfi_wino_output_transform(const float* M, const float* bias, float* y, float* pooled, int32_t N,

@@ -116,6 +116,8 @@ SIGNATURES = {
                                                    ctypes.c_int32, c_void_p]),
     'nfi_wino_input_transform': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                   ctypes.c_int32, ctypes.c_int32, c_void_p]),
+    'nfi_wino_input_transform_scaled': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, ctypes.c_int32,
+                                                         ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_wino_output_transform': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_wino_packed_size': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),

@@ -18,6 +18,7 @@ MIOpen's own error), the order of cuDNN's fp32 Winograd algorithms the reference
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -30,6 +31,7 @@ from .ops import _require_device, _stream
 MIN_CHANNELS = 16
 ENABLED = True
 DGRAD = True          # data gradient as Winograd too (False: MIOpen's conv2d_input; diagnostics)
+FOLD_SCALE = os.environ.get('NFI_FOLD_SCALE', '1') == '1'   # modulation folded into the input transform
 FUSED = True          # one fused kernel per layer (nfi_wino_conv_fused) for layers with Ci % 8 == 0
                       # and Ci <= FUSED_MAX_CI; else the three-pass form (transforms + hipBLASLt GEMM)
 # The fused kernel keeps V and M on chip but its 36-way split accumulators leave small per-product
@@ -88,21 +90,25 @@ def _pack(U, Co, Ci, st):
     return Ua
 
 
-def _winograd(x, Uw, bias=None, pool=False):
+def _winograd(x, Uw, bias=None, pool=False, scale=None):
     """x [N,Ci,H,W] (contiguous) with transformed weights Uw = (U [36,Co,Ci], packed or None) ->
-    y [N,Co,H,W] (and the pooled map when pool)."""
+    y [N,Co,H,W] (and the pooled map when pool).  scale [N,Ci]: convolve x * scale[n, c]
+    (three-pass form: folded into the input transform)."""
     U, Ua = Uw
     N, Ci, H, W = x.shape
     Co = U.shape[1]
     st = _stream(x.device)
     y = torch.empty((N, Co, H, W), device=x.device)
     m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
+    if scale is not None and FUSED and Ua is not None and Ci <= FUSED_MAX_CI:
+        x = x * scale[:, :, None, None]          # (the fused kernel takes no scale)
+        scale = None
     if FUSED and Ua is not None and Ci <= FUSED_MAX_CI:
         _call('nfi_wino_conv_fused', _p(x), _p(Ua), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
         return (y, m) if pool else y
     P = N * (H // 4) * (W // 4)
     V = torch.empty((36, Ci, P), device=x.device)
-    _call('nfi_wino_input_transform', _p(x), _p(V), N, Ci, H, W, st)
+    _call('nfi_wino_input_transform_scaled', _p(x), _p(scale), _p(V), N, Ci, H, W, st)
     M = torch.bmm(U, V)
     del V
     _call('nfi_wino_output_transform', _p(M), _p(bias), _p(y), _p(m), N, Co, H, W, st)
@@ -133,6 +139,33 @@ class _Conv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return _dgrad(g.contiguous(), ctx), None
+
+
+class _ModConv(torch.autograd.Function):
+    """conv2d(x * s[:, :, None, None], w, padding=1): the modulated convolution of a synthesis
+    layer (stylegan.py:130-133 with the weight shared over the batch), the modulation folded into
+    the Winograd input transform.  Backward: the data-gradient Winograd, then d x = g' s and
+    d s = sum_hw g' x in one pass (nfi_syn_scale_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, s, weight):
+        _require_device(x, s, weight)
+        x = x.contiguous()
+        s = s.contiguous()
+        U, Ut = weights(weight)
+        ctx.save_for_backward(x, s)
+        ctx.Ut, ctx.xshape, ctx.weight = Ut, x.shape, weight.detach()
+        return _winograd(x, U, scale=s)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, s = ctx.saved_tensors
+        gxs = _dgrad(g.contiguous(), ctx)
+        B, C, H, W = x.shape
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
+        _call('nfi_syn_scale_backward', _p(gxs), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W, _stream(x.device))
+        return gx, ds, None
 
 
 class _VggBlock(torch.autograd.Function):
@@ -170,6 +203,15 @@ def conv3x3(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     if not applicable(x, weight) or weight.requires_grad:
         return F.conv2d(x, weight, None, 1, 1)
     return _Conv.apply(x, weight)
+
+
+def modulated_conv3x3(x: torch.Tensor, s: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """F.conv2d(x * s[:, :, None, None], weight, padding=1) for a frozen weight (the synthesis
+    layers' modulation, stylegan.py:130); Winograd with the scale folded in when applicable."""
+    if not FOLD_SCALE or not applicable(x, weight) or weight.requires_grad:
+        from .producer_ops import scale as _scale
+        return conv3x3(_scale(x, s), weight)
+    return _ModConv.apply(x, s, weight)
 
 
 def vgg_block(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, pool: bool):

@@ -25,24 +25,53 @@ from .render import render as _nfi_render
 # ---------------------------------------------------------------------------------------------
 # pose parameterisation (lib/pose_utils.py)
 
+_CONST: dict = {}
+
+
+def _const(name: str, dev, dtype, build):
+    """Small constant tensors of the pose math, built once per (device, dtype): no host copy
+    inside a step (a captured graph forbids one, and a pageable copy drains the launch queue)."""
+    key = (name, dev, dtype)
+    t = _CONST.get(key)
+    if t is None:
+        t = _CONST[key] = build().to(device=dev, dtype=dtype)
+    return t
+
+
+def _quat_table():
+    """[16, 9]: the reference's rotation entries (pose_utils.py:41-45, row-major, before the
+    transpose) as combinations of the products q_i q_j, (w, x, y, z) = 0..3; entry k =
+    [1, 0, 0, 0, 1, 0, 0, 0, 1][k] + sum_ij q_i q_j T[4i + j, k]."""
+    W, X, Y, Z = range(4)
+    terms = [[(-2, Y, Y), (-2, Z, Z)], [(2, X, Y), (-2, W, Z)], [(2, X, Z), (2, W, Y)],
+             [(2, X, Y), (2, W, Z)], [(-2, X, X), (-2, Z, Z)], [(2, Y, Z), (-2, W, X)],
+             [(2, X, Z), (-2, W, Y)], [(2, Y, Z), (2, W, X)], [(-2, X, X), (-2, Y, Y)]]
+    T = torch.zeros(16, 9, dtype=torch.float64)
+    for k, ts in enumerate(terms):
+        for c, i, j in ts:
+            T[4 * i + j, k] += c
+    return T
+
+
 def quaternion_to_matrix(q: torch.Tensor) -> torch.Tensor:
     """pose_utils.py:41-45: the matrix whose rows are the unit vectors rotated by q, i.e. the
-    transpose of the rotation matrix of q = (w, x, y, z)."""
-    w, x, y, z = q.unbind(-1)
-    r = torch.stack([
-        1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
-        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
-        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=-1)
+    transpose of the rotation matrix of q = (w, x, y, z).  Its entries are 1 or 0 plus quadratic
+    forms in q: one outer product and one contraction with a constant table (4 kernels forward and
+    backward instead of ~40 scalar-sized ones)."""
+    T = _const('quat', q.device, q.dtype, _quat_table)
+    eye = _const('eye9', q.device, q.dtype, lambda: torch.eye(3, dtype=torch.float64).reshape(9))
+    qq = (q.unsqueeze(-1) * q.unsqueeze(-2)).reshape(q.shape[:-1] + (16, 1))
+    r = (qq * T).sum(-2) + eye
     return r.view(q.shape[:-1] + (3, 3)).transpose(-2, -1)
 
 
 def _flip(mat: torch.Tensor, camera_flipped: bool) -> torch.Tensor:
+    """pose_utils.py:61: columns 1..3 of rows 0..2 negated."""
     if not camera_flipped:
         return mat
-    # pose_utils.py:61: columns 1..3 (built on the device: no host copy inside a captured step)
-    sign = torch.full((4,), -1.0, dtype=mat.dtype, device=mat.device)
-    sign[:1].fill_(1.0)
-    return torch.cat([mat[:, :3] * sign, mat[:, 3:]], dim=1)
+    sign = _const('flip', mat.device, mat.dtype,
+                  lambda: torch.tensor([[1.0, -1.0, -1.0, -1.0]] * 3 + [[1.0, 1.0, 1.0, 1.0]]))
+    return mat * sign
 
 
 def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
@@ -51,15 +80,14 @@ def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
     b = q.shape[0]
     if z0 is not None:
         f = 1 + z0.exp()
-        t3 = torch.cat([t2 / s[:, None], (f / s)[:, None]], dim=-1)
+        t3 = torch.cat([t2, f[:, None]], dim=-1) / s[:, None]    # (t2 / s, f / s): same divisions
         focal = f / 2
     else:
         t3 = torch.cat([t2, torch.ones_like(t2[:, :1])], dim=-1) / s[:, None]
         focal = None
     top = torch.cat([rot, (rot * t3[:, None, :]).sum(-1, keepdim=True)], dim=-1)
-    bottom = torch.zeros(b, 1, 4, dtype=top.dtype, device=top.device)
-    bottom[:, 0, 3].fill_(1.0)
-    return _flip(torch.cat([top, bottom], dim=1), camera_flipped), focal
+    bottom = _const('bottom', top.device, top.dtype, lambda: torch.tensor([[[0.0, 0.0, 0.0, 1.0]]]))
+    return _flip(torch.cat([top, bottom.expand(b, 1, 4)], dim=1), camera_flipped), focal
 
 
 def invert_space(mat: torch.Tensor) -> torch.Tensor:

@@ -148,11 +148,10 @@ class ModulatedConv(nn.Module):
             dcoefs = (styles.square() @ w2.t() + 1e-8).rsqrt()                # [b, out]
         else:                                  # from SynthesisNetwork's style bank
             styles, dcoefs = pre
-        xs = ops.scale(x, styles)
         if self.up:
-            t = F.conv_transpose2d(xs, self.weight.transpose(0, 1), stride=2)
+            t = F.conv_transpose2d(ops.scale(x, styles), self.weight.transpose(0, 1), stride=2)
             return ops.fir_up_act(t, dcoefs, self.bias, SQRT2)
-        return ops.act(_conv().conv3x3(xs, self.weight), dcoefs, self.bias, SQRT2)
+        return ops.act(_conv().modulated_conv3x3(x, styles, self.weight), dcoefs, self.bias, SQRT2)
 
 
 class ToPlanes(nn.Module):

@@ -32,9 +32,17 @@ def main():
     inversion.invert(gen, target, batch['cam'], batch['focal'], w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     icfg.steps = 4
-    with profile(activities=[ProfilerActivity.CPU]) as prof:
+    with profile(activities=[ProfilerActivity.CPU], with_stack=len(sys.argv) > 3) as prof:
         inversion.invert(gen, target, batch['cam'], batch['focal'], w_avg, icfg, lpips_net=net)
         torch.cuda.synchronize()
+    if len(sys.argv) > 3:            # python scripts/step_profile.py l1 4 stacks: callers of the busiest ops
+        ev = prof.key_averages(group_by_stack_n=6)
+        rows = sorted((e for e in ev if e.key in ('aten::mul', 'aten::copy_', 'aten::add_', 'aten::fill_', 'aten::add')),
+                      key=lambda e: -e.count)[:25]
+        for e in rows:
+            stack = [f for f in e.stack if 'nfi' in f or 'inversion' in f or 'producer' in f][:4]
+            print(f'{e.key:14s} n={e.count:4d} self={e.self_cpu_time_total:8.0f}us  ' + ' <- '.join(stack))
+        return
     ev = prof.key_averages()
     print(ev.table(sort_by='self_cpu_time_total', row_limit=45))
     print(ev.table(sort_by='count', row_limit=30))

@@ -120,3 +120,23 @@ def test_trainable_weight_takes_the_library_path():
     assert w.grad is not None
     with pytest.raises(NotImplementedError):
         conv.vgg_block(x, w, torch.zeros(16, device=DEV), False)
+
+
+@pytest.mark.parametrize('N,C,Co,H', [(2, 128, 96, 16), (4, 512, 512, 4), (3, 16, 32, 8)])
+def test_modulated_conv(N, C, Co, H):
+    """conv2d(x * s, w) with the modulation folded into the input transform, against the fp64
+    formulation: output, d x and d s (the synthesis layers' style gradient)."""
+    g = torch.Generator(device=DEV).manual_seed(N + C + H)
+    x = torch.randn((N, C, H, H), device=DEV, generator=g)
+    s = torch.rand((N, C), device=DEV, generator=g) + 0.5
+    w = torch.randn((Co, C, 3, 3), device=DEV, generator=g) / (3 * C ** 0.5)
+    gy = torch.randn((N, Co, H, H), device=DEV, generator=g)
+    xa, sa = x.clone().requires_grad_(), s.clone().requires_grad_()
+    y = conv.modulated_conv3x3(xa, sa, w)
+    y.backward(gy)
+    xd, sd = x.double().cpu().requires_grad_(), s.double().cpu().requires_grad_()
+    yd = F.conv2d(xd * sd[:, :, None, None], w.double().cpu(), padding=1)
+    yd.backward(gy.double().cpu())
+    assert _err(y, yd) < 2e-5
+    assert _err(xa.grad, xd.grad) < 2e-5
+    assert float((sa.grad.double().cpu() - sd.grad).norm() / sd.grad.norm()) < 1e-4
