@@ -120,21 +120,29 @@ __global__ void __launch_bounds__(256) fir_up_act_kernel(const float* __restrict
   const int rem = (int)(i - (int64_t)p * per);
   const int yy = rem / q4, x0 = (rem - yy * q4) * 4;
   const float* tp = t + (int64_t)p * T * T;
+  // branch-free: all 28 loads at clamped addresses, out-of-range taps zeroed by selects (a
+  // load-or-zero branch per tap makes the compiler wait for each load before the next)
+  float v[4][7];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = min(max(yy - 1 + r, 0), T - 1);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) v[r][j] = tp[row * T + min(max(x0 - 1 + j, 0), T - 1)];
+  }
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = yy - 1 + r;
-    if (row < 0 || row >= T) continue;
-    float v[7];
+    const bool rok = row >= 0 && row < T;
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
       const int col = x0 - 1 + j;
-      v[j] = (col >= 0 && col < T) ? tp[row * T + col] : 0.f;
+      v[r][j] = (rok && col >= 0 && col < T) ? v[r][j] : 0.f;
     }
     const float kr = k4(r);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      acc[k] += kr * ((v[k] + v[k + 3]) + 3.f * (v[k + 1] + v[k + 2]));
+      acc[k] += kr * ((v[r][k] + v[r][k + 3]) + 3.f * (v[r][k + 1] + v[r][k + 2]));
   }
   const float dp = d[p], b = bias[p % C];
   const float inv = 1.f / 16.f;
@@ -155,18 +163,25 @@ __global__ void __launch_bounds__(256) fir_up_bwd_kernel(const float* __restrict
   const int rem = (int)(i - (int64_t)p * T * T);
   const int r = rem / T, c = rem - r * T;
   const float* gp = go + (int64_t)p * W2 * W2;
+  // branch-free (clamped loads, masked): see fir_up_act_kernel
+  float g[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = min(max(r + 1 - a, 0), W2 - 1);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) g[a][bb] = gp[row * W2 + min(max(c + 1 - bb, 0), W2 - 1)];
+  }
   float acc = 0.f;
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int row = r + 1 - a;
-    if (row < 0 || row >= W2) continue;
     float h = 0.f;
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int col = c + 1 - bb;
-      if (col >= 0 && col < W2) h += k4(bb) * gp[row * W2 + col];
+      h += k4(bb) * ((col >= 0 && col < W2) ? g[a][bb] : 0.f);
     }
-    acc += k4(a) * h;
+    acc += (row >= 0 && row < W2) ? k4(a) * h : 0.f;
   }
   gt[i] = acc * (1.f / 16.f);
 }
