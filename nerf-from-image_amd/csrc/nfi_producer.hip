@@ -209,21 +209,28 @@ __global__ void __launch_bounds__(256) up_add_kernel(const float* __restrict__ i
     const int r0 = (yy & 1) ? q : q - 1;
     const float w0 = (yy & 1) ? 3.f : 1.f, w1 = (yy & 1) ? 1.f : 3.f;
     const int m = x0 >> 1;
+    // branch-free: clamped loads, out-of-range taps zeroed by selects (see fir_up_act_kernel)
+    float v[2][4];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int row = min(max(r0 + rr, 0), n - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[rr][j] = ip[row * n + min(max(m - 1 + j, 0), n - 1)];
+    }
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
       const int row = r0 + rr;
-      if (row < 0 || row >= n) continue;
-      float v[4];
+      const bool rok = row >= 0 && row < n;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = m - 1 + j;
-        v[j] = (col >= 0 && col < n) ? ip[row * n + col] : 0.f;
+        v[rr][j] = (rok && col >= 0 && col < n) ? v[rr][j] : 0.f;
       }
       const float wr = rr == 0 ? w0 : w1;
-      acc[0] += wr * (v[0] + 3.f * v[1]);
-      acc[1] += wr * (3.f * v[1] + v[2]);
-      acc[2] += wr * (v[1] + 3.f * v[2]);
-      acc[3] += wr * (3.f * v[2] + v[3]);
+      acc[0] += wr * (v[rr][0] + 3.f * v[rr][1]);
+      acc[1] += wr * (3.f * v[rr][1] + v[rr][2]);
+      acc[2] += wr * (v[rr][1] + 3.f * v[rr][2]);
+      acc[3] += wr * (3.f * v[rr][2] + v[rr][3]);
     }
   }
   const float inv = 1.f / 16.f;
@@ -242,18 +249,25 @@ __global__ void __launch_bounds__(256) up_bwd_kernel(const float* __restrict__ g
   const int rem = (int)(i - (int64_t)p * n * n);
   const int q = rem / n, m = rem - q * n;
   const float* gp = g + (int64_t)p * W2 * W2;
+  // branch-free (clamped loads, masked): see fir_up_act_kernel
+  float gv[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = min(max(2 * q - 1 + a, 0), W2 - 1);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) gv[a][bb] = gp[row * W2 + min(max(2 * m - 1 + bb, 0), W2 - 1)];
+  }
   float acc = 0.f;
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int row = 2 * q - 1 + a;
-    if (row < 0 || row >= W2) continue;
     float h = 0.f;
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int col = 2 * m - 1 + bb;
-      if (col >= 0 && col < W2) h += k4(bb) * gp[row * W2 + col];
+      h += k4(bb) * ((col >= 0 && col < W2) ? gv[a][bb] : 0.f);
     }
-    acc += k4(a) * h;
+    acc += (row >= 0 && row < W2) ? k4(a) * h : 0.f;
   }
   gimg[i] = acc * (1.f / 16.f);
 }
