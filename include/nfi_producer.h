@@ -104,6 +104,11 @@ int32_t nfi_wino_weight_transform(const float* w, float* U, int32_t Co, int32_t 
 int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C, int32_t H, int32_t W,
                                  void* stream);
 
+/* The same for x * scale[n][c] (scale [N,C]; NULL: 1): the style modulation of the synthesis
+ * layers (stylegan.py:130) folded into the transform. */
+int32_t nfi_wino_input_transform_scaled(const float* x, const float* scale, float* V, int32_t N, int32_t C,
+                                        int32_t H, int32_t W, void* stream);
+
 /* M [36,Co,P] -> y [N,Co,H,W].  bias == NULL: y = the convolution.  bias != NULL: y =
  * relu(conv + bias[co]) (the LPIPS VGG16 block epilogue, as nfi_vgg_bias_relu_forward) and, when
  * pooled != NULL, pooled [N,Co,H/2,W/2] = MaxPool2d(2, 2)(y). */

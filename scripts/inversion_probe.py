@@ -43,6 +43,9 @@ def run(B, loss, steps=10, cl=False, graph=False, overlap=True):
           f'(enqueue {cpu * 1e3:.2f} ms/step between on_step calls)', flush=True)
 
 
+if os.environ.get('NFI_BLAS'):         # A/B of the BLAS backend behind torch.bmm / mm ('cublas' = rocBLAS)
+    torch.backends.cuda.preferred_blas_library(os.environ['NFI_BLAS'])
+
 if __name__ == '__main__':
     if len(sys.argv) > 1:          # python scripts/inversion_probe.py B loss steps
         run(int(sys.argv[1]), sys.argv[2], steps=int(sys.argv[3]))
