@@ -1119,10 +1119,21 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
   const float gr0 = g.g_rgb[r * 3 + 0], gr1 = g.g_rgb[r * 3 + 1], gr2 = g.g_rgb[r * 3 + 2];
   const float gm = g.g_mask[r] - (a.white_bg ? (gr0 + gr1 + gr2) : 0.f);
   float t[NPL], sg[NPL], al[NPL], aa[NPL], ex[NPL], dist[NPL], raw[NPL], T[NPL], ee[NPL];
+  float c0[NPL], c1[NPL], c2[NPL];
+  // every load issues up front at a clamped index (a branch around a load makes the compiler
+  // wait for it before the next one); the lanes past N take their zeros by selects below
 #pragma unroll
   for (int e = 0; e < NPL; ++e) {
-    const int i = e * 64 + l;
-    t[e] = (i < N) ? a.t_saved[r * N + i] : 0.f;
+    const int ic = min(e * 64 + l, N - 1);
+    t[e] = a.t_saved[r * N + ic];
+    sg[e] = a.sigma_saved[r * N + ic];
+    c0[e] = a.rgb_saved[(r * 3 + 0) * N + ic];
+    c1[e] = a.rgb_saved[(r * 3 + 1) * N + ic];
+    c2[e] = a.rgb_saved[(r * 3 + 2) * N + ic];
+  }
+#pragma unroll
+  for (int e = 0; e < NPL; ++e) {
+    t[e] = (e * 64 + l < N) ? t[e] : 0.f;
     Lt[e * 64 + l] = t[e];
   }
   wave_lds_sync();
@@ -1130,20 +1141,13 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
   for (int e = 0; e < NPL; ++e) {
     const int i = e * 64 + l;
     const bool v = i < N;
-    sg[e] = v ? a.sigma_saved[r * N + i] : 0.f;
-    raw[e] = (i < N - 1) ? fsub(Lt[i + 1], t[e]) : 0.f;
+    sg[e] = v ? sg[e] : 0.f;
+    raw[e] = (i < N - 1) ? fsub(Lt[min(i + 1, NMAX - 1)], t[e]) : 0.f;
     dist[e] = fmul(raw[e], R.rdn);
     alpha_of(sg[e], dist[e], al[e], aa[e], ex[e]);
-    float c0 = 0.f, c1 = 0.f, c2 = 0.f;
-    if (v) {
-      c0 = a.rgb_saved[(r * 3 + 0) * N + i];
-      c1 = a.rgb_saved[(r * 3 + 1) * N + i];
-      c2 = a.rgb_saved[(r * 3 + 2) * N + i];
-    } else {
-      al[e] = 0.f;
-      aa[e] = 1.f;
-    }
-    ee[e] = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm : 0.f;
+    al[e] = v ? al[e] : 0.f;
+    aa[e] = v ? aa[e] : 1.f;
+    ee[e] = v ? (gr0 * c0[e] + gr1 * c1[e] + gr2 * c2[e]) + gm : 0.f;
   }
   excl_prod<NPL>(aa, T);
   float grdn = 0.f;
@@ -2015,43 +2019,58 @@ __global__ void __launch_bounds__(256, NFI_TILE_DBUF ? 3 : 4) tile_kernel(TileAr
 // coordinates (x, y), (x, z), (y, z); generator.py:312-326, 604), dL/d ro = sum_j dL/dp_j and
 // dL/d rd = sum_j t_j dL/dp_j (p = ro + rd t, run.py:283-288).  Samples outside the box have no
 // entries (their sigma and weight are 0, so their feature gradient is exactly zero).
+// One wave per ray over its NPL chunks of 64 (no atomics: composite_bwd_kernel wrote g_ro / g_rd
+// earlier on the stream, this wave owns the ray's six sums and adds them in place).
+template <int NPL>
 __global__ void __launch_bounds__(256) dcoord_reduce_kernel(nfi_render_args a, BwdArgs g, const float* __restrict__ dpc) {
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
-  const long long job = (long long)blockIdx.x * 4 + wv;
-  const long long r = job / g.npl;
-  const int e = (int)(job % g.npl);
+  const long long r = ray_of_block(blockIdx.x, 4, a) + wv;
   if (r >= nrays) return;
   const int N = a.fine ? 2 * a.S : a.S;
-  if (e * 64 >= N) return;
   const float sr = a.field.scene_range;
   RayCtx R;
   load_ray(a, r, R);
-  const int i = e * 64 + l;
-  const bool v = i < N;
-  const float te = v ? a.t_saved[r * N + i] : R.near_;
-  // the in-box test of point_params (the tile entries were made with the same arithmetic)
-  float cx[3];
+  // every load at a clamped index, issued together (the grid-gradient row of a dead sample is
+  // never written: whatever it holds is dropped by the select)
+  float ts[NPL];
+  float2 xy[NPL], xz[NPL], yz[NPL];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(R.o[k], fmul(R.d[k], te)), sr);
-  const bool live = v && !(fabsf(cx[0]) > 1.f || fabsf(cx[1]) > 1.f || fabsf(cx[2]) > 1.f);
-  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-  if (live) {
-    const float2* p = reinterpret_cast<const float2*>(dpc + (r * N + i) * 6);
-    const float2 xy = p[0], xz = p[1], yz = p[2];
-    d0 = xy.x + xz.x;
-    d1 = xy.y + yz.x;
-    d2 = xz.y + yz.y;
+  for (int e = 0; e < NPL; ++e) {
+    const int ic = min(e * 64 + l, N - 1);
+    ts[e] = a.t_saved[r * N + ic];
+    const float2* p = reinterpret_cast<const float2*>(dpc + (r * N + ic) * 6);
+    xy[e] = p[0];
+    xz[e] = p[1];
+    yz[e] = p[2];
   }
-  const float gro0 = wave_sum(d0) / sr, gro1 = wave_sum(d1) / sr, gro2 = wave_sum(d2) / sr;
-  const float grd0 = wave_sum(d0 * te) / sr, grd1 = wave_sum(d1 * te) / sr, grd2 = wave_sum(d2 * te) / sr;
-  if (l == 0) {
-    unsafeAtomicAdd(g.g_ro + r * 3 + 0, gro0);
-    unsafeAtomicAdd(g.g_ro + r * 3 + 1, gro1);
-    unsafeAtomicAdd(g.g_ro + r * 3 + 2, gro2);
-    unsafeAtomicAdd(g.g_rd + r * 3 + 0, grd0);
-    unsafeAtomicAdd(g.g_rd + r * 3 + 1, grd1);
-    unsafeAtomicAdd(g.g_rd + r * 3 + 2, grd2);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < NPL; ++e) {
+    const bool v = e * 64 + l < N;
+    const float te = v ? ts[e] : R.near_;
+    // the in-box test of point_params (the tile entries were made with the same arithmetic)
+    float cx[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cx[k] = fdiv(fadd(R.o[k], fmul(R.d[k], te)), sr);
+    const bool live = v && !(fabsf(cx[0]) > 1.f || fabsf(cx[1]) > 1.f || fabsf(cx[2]) > 1.f);
+    const float d0 = live ? xy[e].x + xz[e].x : 0.f;
+    const float d1 = live ? xy[e].y + yz[e].x : 0.f;
+    const float d2 = live ? xz[e].y + yz[e].y : 0.f;
+    s0 += d0;
+    s1 += d1;
+    s2 += d2;
+    u0 = fmaf(d0, te, u0);
+    u1 = fmaf(d1, te, u1);
+    u2 = fmaf(d2, te, u2);
+  }
+  const float gro0 = wave_sum(s0) / sr, gro1 = wave_sum(s1) / sr, gro2 = wave_sum(s2) / sr;
+  const float grd0 = wave_sum(u0) / sr, grd1 = wave_sum(u1) / sr, grd2 = wave_sum(u2) / sr;
+  if (l < 3) {
+    const float ro = l == 0 ? gro0 : (l == 1 ? gro1 : gro2);
+    const float rd = l == 0 ? grd0 : (l == 1 ? grd1 : grd2);
+    g.g_ro[r * 3 + l] += ro;
+    g.g_rd[r * 3 + l] += rd;
   }
 }
 
@@ -2199,7 +2218,9 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
 #else
     if (g->g_ro) {
 #endif
-      dcoord_reduce_kernel<<<(unsigned)((nrays * NPL + 3) / 4), 256, 0, s>>>(*a, bg, w.dpc);
+      if (NPL <= 1) dcoord_reduce_kernel<1><<<rb, 256, 0, s>>>(*a, bg, w.dpc);
+      else if (NPL <= 2) dcoord_reduce_kernel<2><<<rb, 256, 0, s>>>(*a, bg, w.dpc);
+      else dcoord_reduce_kernel<4><<<rb, 256, 0, s>>>(*a, bg, w.dpc);
       NFI_CHECK_LAUNCH("dcoord_reduce_kernel");
     }
   }
