@@ -62,6 +62,31 @@ __device__ __forceinline__ float dpp_mov(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+// DPP lane move whose lanes without a source (past the row / wave edge, or in a row outside
+// ROWS) keep `fill` — the identity of the scan it feeds, so no lane test follows the move.
+// Controls: row_shr:d 0x110+d, row_shl:d 0x100+d, wave_shr:1 0x138, wave_shl:1 0x130,
+// row_bcast:15 0x142, row_bcast:31 0x143.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ float dpp_fill(float v, float fill) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(fill), __float_as_int(v), CTRL, ROWS, 0xF, false));
+}
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ double dpp_fill(double v, double fill) {
+  const unsigned long long vi = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long fi = (unsigned long long)__double_as_longlong(fill);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)fi, (int)(unsigned)vi, CTRL, ROWS, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(fi >> 32), (int)(unsigned)(vi >> 32), CTRL, ROWS,
+                                                            0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double readlane(double v, int l) {
+  const unsigned long long vi = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)vi, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(vi >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // Sum over the 64 lanes; result in every lane.  DPP inside rows of 16, then cross-row swaps.
 __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]  (xor 1)

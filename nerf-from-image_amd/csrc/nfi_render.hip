@@ -605,22 +605,24 @@ __device__ __forceinline__ void viewdir_head_bwd(const float y[NOV], const float
 // Products and sums of the per-ray recurrences are accumulated in fp64 (ATen's CPU cumprod /
 // cumsum accumulate float inputs in double).
 // ---------------------------------------------------------------------------------------
+// Inclusive scans on DPP (no LDS round trip): Hillis-Steele inside rows of 16 (row_shr 1, 2, 4,
+// 8), then row 15's total into rows 1 and 3 and lane 31's into rows 2 and 3 (row_bcast 15 / 31).
 __device__ __forceinline__ double wave_incl_prod_d(double v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const double t = __shfl_up(v, d);
-    if (l >= d) v *= t;
-  }
+  v *= dpp_fill<0x111>(v, 1.0);
+  v *= dpp_fill<0x112>(v, 1.0);
+  v *= dpp_fill<0x114>(v, 1.0);
+  v *= dpp_fill<0x118>(v, 1.0);
+  v *= dpp_fill<0x142, 0xA>(v, 1.0);
+  v *= dpp_fill<0x143, 0xC>(v, 1.0);
   return v;
 }
 __device__ __forceinline__ double wave_incl_sum_d(double v) {
-  const int l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const double t = __shfl_up(v, d);
-    if (l >= d) v += t;
-  }
+  v += dpp_fill<0x111>(v, 0.0);
+  v += dpp_fill<0x112>(v, 0.0);
+  v += dpp_fill<0x114>(v, 0.0);
+  v += dpp_fill<0x118>(v, 0.0);
+  v += dpp_fill<0x142, 0xA>(v, 0.0);
+  v += dpp_fill<0x143, 0xC>(v, 0.0);
   return v;
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -636,10 +638,9 @@ __device__ __forceinline__ void excl_prod(const float (&a)[E], float (&T)[E]) {
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const double inc = wave_incl_prod_d((double)a[e]);
-    double ex = __shfl_up(inc, 1);
-    if (lane_id() == 0) ex = 1.0;
+    const double ex = dpp_fill<0x138>(inc, 1.0);   // wave_shr:1, lane 0 takes 1
     T[e] = (float)(carry * ex);
-    carry = carry * __shfl(inc, 63);
+    carry = carry * readlane(inc, 63);
   }
 }
 
@@ -886,7 +887,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NF
       const double inc = wave_incl_sum_d((double)pdf) + carry;
       if (i < S - 2) cdf[i + 1] = (float)inc;
       if (i < S - 1) bins[i] = mid[e];
-      carry = __shfl(inc, 63);
+      carry = readlane(inc, 63);
     }
     if (l == 0) cdf[0] = 0.f;
     wave_lds_sync();
@@ -1155,17 +1156,33 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 #pragma unroll
   for (int e = NPL - 1; e >= 0; --e) {
     const int i = e * 64 + l;
+    // suffix composition of the maps x -> A x + B on DPP: inside rows of 16 (row_shl 1, 2, 4, 8;
+    // the identity (1, 0) past the row's end), then each row's result composed with the totals of
+    // the rows above it (read from lanes 16, 32, 48 once, composed on uniform values)
     float A = aa[e], B = ee[e] * al[e];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const float A2 = __shfl_down(A, d), B2 = __shfl_down(B, d);
-      if (l + d < 64) {
-        B = fmaf(A, B2, B);
-        A = A * A2;
-      }
+    {
+      float A2 = dpp_fill<0x101>(A, 1.f), B2 = dpp_fill<0x101>(B, 0.f);
+      B = fmaf(A, B2, B), A = A * A2;
+      A2 = dpp_fill<0x102>(A, 1.f), B2 = dpp_fill<0x102>(B, 0.f);
+      B = fmaf(A, B2, B), A = A * A2;
+      A2 = dpp_fill<0x104>(A, 1.f), B2 = dpp_fill<0x104>(B, 0.f);
+      B = fmaf(A, B2, B), A = A * A2;
+      A2 = dpp_fill<0x108>(A, 1.f), B2 = dpp_fill<0x108>(B, 0.f);
+      B = fmaf(A, B2, B), A = A * A2;
     }
-    const float An = __shfl_down(A, 1), Bn = __shfl_down(B, 1);
-    const float Sk = (l < 63) ? fmaf(An, cB, Bn) : cB;
+    {
+      const float a1 = readlane(A, 16), b1 = readlane(B, 16), a2 = readlane(A, 32), b2 = readlane(B, 32);
+      const float a3 = readlane(A, 48), b3 = readlane(B, 48);
+      const float c1a = a2 * a3, c1b = fmaf(a2, b3, b2);            // rows 2, 3
+      const float c0a = a1 * c1a, c0b = fmaf(a1, c1b, b1);          // rows 1, 2, 3
+      const int row = l >> 4;
+      const float ca = row == 0 ? c0a : (row == 1 ? c1a : (row == 2 ? a3 : 1.f));
+      const float cb = row == 0 ? c0b : (row == 1 ? c1b : (row == 2 ? b3 : 0.f));
+      B = fmaf(A, cb, B);
+      A = A * ca;
+    }
+    const float An = dpp_fill<0x130>(A, 1.f), Bn = dpp_fill<0x130>(B, 0.f);   // wave_shl:1
+    const float Sk = fmaf(An, cB, Bn);                       // lane 63: the identity -> cB
     cB = fmaf(readlane(A, 0), cB, readlane(B, 0));
     const float dal = T[e] * (ee[e] - Sk);                   // dL/d alpha_k
     grdn += dal * sg[e] * ex[e] * raw[e];                    // dists = raw * ||rd||
