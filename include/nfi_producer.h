@@ -49,6 +49,12 @@ int32_t nfi_syn_fir_up_act_forward(const float* t, const float* d, const float* 
  * gt [P,2n+1,2n+1]. */
 int32_t nfi_syn_fir_up_backward(const float* go, float* gt, int32_t P, int32_t n, void* stream);
 
+/* The stride-2 3x3 transposed convolution of the up-sampling layers (stylegan.py:99-101,
+ * conv_transpose2d(x, w^T, stride=2)) as one GEMM over all 9 taps plus this scatter: the caller
+ * computes P [B][9][C][n][n] = W9 x (W9 [9*C, Ci] = w permuted to [ky][kx][co][ci]); this sums the
+ * taps into t [B][C][2n+1][2n+1], t[Y][X] = sum of P[3ky+kx][.][iy][ix] over Y = 2iy+ky, X = 2ix+kx. */
+int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, int32_t n, void* stream);
+
 /* Skip path (stylegan.py:428-433 + 380-381): out [P,2n,2n] = upsample2d(img [P,n,n]) + c +
  * bias[c]; img may be NULL (first block: out = c + bias). */
 int32_t nfi_syn_up_add_forward(const float* img, const float* c, const float* bias, float* out,

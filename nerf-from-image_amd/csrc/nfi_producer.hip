@@ -152,6 +152,34 @@ __global__ void __launch_bounds__(256) fir_up_act_kernel(const float* __restrict
                      act(ov.w, dp, b, gain));
 }
 
+// Stride-2 3x3 transposed convolution from its per-tap products: P [B][9][C][n][n] (tap k =
+// 3 ky + kx of W9 x, one GEMM for all taps) -> t [B][C][2n+1][2n+1], t[Y][X] = sum over the taps
+// with Y = 2 iy + ky, X = 2 ix + kx.  Row Y takes ky = Y&1 at iy = Y>>1 and, when Y is even, also
+// ky = 2 at iy = Y/2 - 1 (the same for columns): at most 4 products per output, loaded at clamped
+// addresses and masked (branch-free).
+__global__ void __launch_bounds__(256) tap_scatter_kernel(const float* __restrict__ P,
+                                                          float* __restrict__ t, int64_t total,
+                                                          int C, int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int T = 2 * n + 1;
+  const int64_t plane = i / (T * T);
+  const int rem = (int)(i - plane * T * T);
+  const int Y = rem / T, X = rem - Y * T;
+  const int b = (int)(plane / C), c = (int)(plane - (int64_t)b * C);
+  const int64_t nn = (int64_t)n * n, tap = (int64_t)C * nn;
+  const float* Pc = P + ((int64_t)b * 9 * C + c) * nn;
+  const int kya = Y & 1, iya = Y >> 1, kxa = X & 1, ixa = X >> 1;
+  const bool ya = iya < n, yb = !(Y & 1) && iya >= 1, xa = ixa < n, xb = !(X & 1) && ixa >= 1;
+  const int ra = min(iya, n - 1), rb = max(iya - 1, 0), ca = min(ixa, n - 1), cb = max(ixa - 1, 0);
+  const float paa = Pc[(kya * 3 + kxa) * tap + ra * n + ca];
+  const float pab = Pc[(kya * 3 + 2) * tap + ra * n + cb];
+  const float pba = Pc[(6 + kxa) * tap + rb * n + ca];
+  const float pbb = Pc[8 * tap + rb * n + cb];
+  const float s = ((ya && xa ? paa : 0.f) + (ya && xb ? pab : 0.f)) + ((yb && xa ? pba : 0.f) + (yb && xb ? pbb : 0.f));
+  t[i] = s;
+}
+
 // adjoint FIR: gt[r][c] = sum_ij k_i k_j / 16 * go[r+1-i][c+1-j]
 __global__ void __launch_bounds__(256) fir_up_bwd_kernel(const float* __restrict__ go,
                                                          float* __restrict__ gt, int64_t total,
@@ -503,6 +531,15 @@ int32_t nfi_syn_fir_up_act_forward(const float* t, const float* d, const float* 
   fir_up_act_kernel<<<blocks(n4), 256, 0, (hipStream_t)stream>>>(t, d, bias, (float4*)o, (float4*)y,
                                                                   n4, C, n, gain);
   NFI_CHECK_LAUNCH("fir_up_act_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, int32_t n, void* stream) {
+  NFI_REQUIRE(P && t, "syn_up_conv_scatter: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && n >= 1, "syn_up_conv_scatter: bad shape");
+  const int64_t total = (int64_t)B * C * (2 * n + 1) * (2 * n + 1);
+  tap_scatter_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(P, t, total, C, n);
+  NFI_CHECK_LAUNCH("tap_scatter_kernel");
   return NFI_OK;
 }
 

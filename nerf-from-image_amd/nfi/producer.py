@@ -149,7 +149,7 @@ class ModulatedConv(nn.Module):
         else:                                  # from SynthesisNetwork's style bank
             styles, dcoefs = pre
         if self.up:
-            t = F.conv_transpose2d(ops.scale(x, styles), self.weight.transpose(0, 1), stride=2)
+            t = ops.up_conv(ops.scale(x, styles), self.weight)
             return ops.fir_up_act(t, dcoefs, self.bias, SQRT2)
         return ops.act(_conv().modulated_conv3x3(x, styles, self.weight), dcoefs, self.bias, SQRT2)
 

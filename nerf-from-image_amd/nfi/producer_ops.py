@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 
 import torch
+import torch.nn.functional as F
 
 from . import _lib
 from .ops import _require_device, _stream
@@ -114,6 +115,51 @@ class _FirUpAct(torch.autograd.Function):
         gt = torch.empty((B, C, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
         _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * C, n, dev)
         return gt, dd, None, None
+
+
+def _up_weights(w):
+    """(W9 [9*Co, Ci] = w[co, ci, ky, kx] at row (3ky+kx)*Co + co, the conv-transpose weight
+    w^T [Ci, Co, 3, 3] contiguous) of a frozen w, cached on the tensor per storage version."""
+    key = (w.data_ptr(), w._version, w.device)
+    hit = getattr(w, '_nfi_upconv', None)
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            co, ci = w.shape[:2]
+            hit = (key, (w.detach().permute(2, 3, 0, 1).reshape(9 * co, ci).contiguous(),
+                         w.detach().transpose(0, 1).contiguous()))
+        w._nfi_upconv = hit
+    return hit[1]
+
+
+class _UpConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W9, wt):
+        x = x.contiguous()
+        B, Ci, n, _ = x.shape
+        Co = W9.shape[0] // 9
+        P = torch.matmul(W9, x.view(B, Ci, n * n))                          # [B, 9*Co, n*n]
+        t = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=x.device, dtype=x.dtype)
+        _call('nfi_syn_up_conv_scatter', _p(P), _p(t), B, Co, n, _stream(x.device))
+        ctx.save_for_backward(wt)
+        return t
+
+    @staticmethod
+    def backward(ctx, gt):
+        wt, = ctx.saved_tensors
+        return F.conv2d(gt, wt, stride=2), None, None                      # conv_transpose2d's adjoint
+
+
+def up_conv(x, w):
+    """F.conv_transpose2d(x, w.transpose(0, 1), stride=2) for w [Co, Ci, 3, 3] (stylegan.py:99-101,
+    the synthesis up-sampling layers): the 9 taps as one GEMM (hipBLASLt, 125-137 TFLOP/s on the
+    256^2 generator's layers where MIOpen's transposed kernels reach 50-70) and the tap scatter
+    nfi_syn_up_conv_scatter; the data gradient is the stride-2 convolution (MIOpen).  A weight
+    that takes gradients goes to MIOpen's conv_transpose2d."""
+    _require_device(x, w)
+    if torch.is_grad_enabled() and w.requires_grad:
+        return F.conv_transpose2d(x, w.transpose(0, 1), stride=2)
+    W9, wt = _up_weights(w)
+    return _UpConv.apply(x, W9, wt)
 
 
 class _UpAdd(torch.autograd.Function):

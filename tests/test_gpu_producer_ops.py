@@ -79,6 +79,33 @@ def test_fir_up_act(B, C, n):
     _close(d.grad, drf.grad, rel=1e-5)
 
 
+@pytest.mark.parametrize('B,Ci,Co,n', [(1, 8, 4, 1), (2, 16, 8, 2), (3, 32, 24, 5), (2, 64, 32, 16),
+                                        (1, 512, 256, 8)])
+def test_up_conv(B, Ci, Co, n):
+    """GEMM over the 9 taps + scatter == conv_transpose2d(x, w^T, stride=2) (fp64 reference:
+    err <= 4x MIOpen's fp32 error, floor 1e-6 of the max), and its data gradient."""
+    x = _rand(B, Ci, n, n, seed=16).requires_grad_()
+    w = _rand(Co, Ci, 3, 3, seed=17) / (3 * Ci ** 0.5)
+    g = _rand(B, Co, 2 * n + 1, 2 * n + 1, seed=18)
+    t = producer_ops.up_conv(x, w)
+    t.backward(g)
+    x64 = x.detach().double().requires_grad_()
+    r64 = F.conv_transpose2d(x64, w.double().transpose(0, 1), stride=2)
+    r64.backward(g.double())
+    r32 = F.conv_transpose2d(x.detach(), w.transpose(0, 1), stride=2)
+    assert t.shape == r64.shape
+    r64 = r64.detach()
+    s = float(r64.abs().max())
+    err, err32 = float((t.detach().double() - r64).abs().max()), float((r32.double() - r64).abs().max())
+    assert err <= max(1e-6 * s, 4 * err32), (err, err32, s)
+    gs = float(x64.grad.abs().max())
+    assert float((x.grad.double() - x64.grad).abs().max()) <= 2e-6 * gs
+    # a weight that takes gradients goes to MIOpen's transposed convolution (same values)
+    wg = w.clone().requires_grad_()
+    tg = producer_ops.up_conv(x.detach(), wg).detach()
+    assert float((tg.double() - r64).abs().max()) <= max(1e-6 * s, 4 * err32)
+
+
 @pytest.mark.parametrize('B,C,n', [(2, 3, 2), (2, 5, 4), (1, 96, 16), (2, 96, 128)])
 @pytest.mark.parametrize('with_img', [True, False])
 def test_up_add(B, C, n, with_img):
