@@ -55,6 +55,10 @@ int32_t nfi_syn_fir_up_backward(const float* go, float* gt, int32_t P, int32_t n
  * taps into t [B][C][2n+1][2n+1], t[Y][X] = sum of P[3ky+kx][.][iy][ix] over Y = 2iy+ky, X = 2ix+kx. */
 int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, int32_t n, void* stream);
 
+/* Its adjoint: gt [B][C][2n+1][2n+1] -> dP [B][9][C][n][n], dP[3ky+kx][c][iy][ix] =
+ * gt[c][2iy+ky][2ix+kx]; the data gradient of the transposed convolution is then W9^T dP. */
+int32_t nfi_syn_up_conv_gather(const float* gt, float* dP, int32_t B, int32_t C, int32_t n, void* stream);
+
 /* Skip path (stylegan.py:428-433 + 380-381): out [P,2n,2n] = upsample2d(img [P,n,n]) + c +
  * bias[c]; img may be NULL (first block: out = c + bias). */
 int32_t nfi_syn_up_add_forward(const float* img, const float* c, const float* bias, float* out,

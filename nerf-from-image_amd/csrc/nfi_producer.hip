@@ -180,6 +180,31 @@ __global__ void __launch_bounds__(256) tap_scatter_kernel(const float* __restric
   t[i] = s;
 }
 
+// Its adjoint's operand (the data gradient of the transposed convolution is W9^T dP): gt
+// [B][C][2n+1][2n+1] -> dP [B][9][C][n][n], dP[3ky+kx][c][iy][ix] = gt[c][2iy+ky][2ix+kx] (always
+// inside gt).  One thread per (b, c, iy, ix): its 3x3 window, 9 coalesced row stores.
+__global__ void __launch_bounds__(256) tap_gather_kernel(const float* __restrict__ gt,
+                                                         float* __restrict__ dP, int64_t total,
+                                                         int C, int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t nn = (int64_t)n * n;
+  const int64_t plane = i / nn;                  // b * C + c
+  const int pix = (int)(i - plane * nn);
+  const int iy = pix / n, ix = pix - iy * n;
+  const int b = (int)(plane / C), c = (int)(plane - (int64_t)b * C);
+  const int T = 2 * n + 1;
+  const float* g = gt + plane * T * T + (2 * iy) * T + 2 * ix;
+  float v[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) v[ky * 3 + kx] = g[ky * T + kx];
+  float* d = dP + ((int64_t)b * 9 * C + c) * nn + pix;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) d[k * C * nn] = v[k];
+}
+
 // adjoint FIR: gt[r][c] = sum_ij k_i k_j / 16 * go[r+1-i][c+1-j]
 __global__ void __launch_bounds__(256) fir_up_bwd_kernel(const float* __restrict__ go,
                                                          float* __restrict__ gt, int64_t total,
@@ -540,6 +565,15 @@ int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, 
   const int64_t total = (int64_t)B * C * (2 * n + 1) * (2 * n + 1);
   tap_scatter_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(P, t, total, C, n);
   NFI_CHECK_LAUNCH("tap_scatter_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_conv_gather(const float* gt, float* dP, int32_t B, int32_t C, int32_t n, void* stream) {
+  NFI_REQUIRE(gt && dP, "syn_up_conv_gather: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && n >= 1, "syn_up_conv_gather: bad shape");
+  const int64_t total = (int64_t)B * C * n * n;
+  tap_gather_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(gt, dP, total, C, n);
+  NFI_CHECK_LAUNCH("tap_gather_kernel");
   return NFI_OK;
 }
 

@@ -97,6 +97,8 @@ SIGNATURES = {
                                                  c_void_p]),
     'nfi_syn_up_conv_scatter': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_int32, c_void_p]),
+    'nfi_syn_up_conv_gather': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                ctypes.c_int32, c_void_p]),
     'nfi_syn_up_add_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_syn_up_backward': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,

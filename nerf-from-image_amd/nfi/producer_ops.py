@@ -118,48 +118,53 @@ class _FirUpAct(torch.autograd.Function):
 
 
 def _up_weights(w):
-    """(W9 [9*Co, Ci] = w[co, ci, ky, kx] at row (3ky+kx)*Co + co, the conv-transpose weight
-    w^T [Ci, Co, 3, 3] contiguous) of a frozen w, cached on the tensor per storage version."""
+    """(W9 [9*Co, Ci] = w[co, ci, ky, kx] at row (3ky+kx)*Co + co, and W9^T contiguous) of a
+    frozen w, cached on the tensor per storage version."""
     key = (w.data_ptr(), w._version, w.device)
     hit = getattr(w, '_nfi_upconv', None)
     if hit is None or hit[0] != key:
         with torch.no_grad():
             co, ci = w.shape[:2]
-            hit = (key, (w.detach().permute(2, 3, 0, 1).reshape(9 * co, ci).contiguous(),
-                         w.detach().transpose(0, 1).contiguous()))
+            W9 = w.detach().permute(2, 3, 0, 1).reshape(9 * co, ci).contiguous()
+            hit = (key, (W9, W9.t().contiguous()))
         w._nfi_upconv = hit
     return hit[1]
 
 
 class _UpConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W9, wt):
+    def forward(ctx, x, W9, W9t):
         x = x.contiguous()
         B, Ci, n, _ = x.shape
         Co = W9.shape[0] // 9
         P = torch.matmul(W9, x.view(B, Ci, n * n))                          # [B, 9*Co, n*n]
         t = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=x.device, dtype=x.dtype)
         _call('nfi_syn_up_conv_scatter', _p(P), _p(t), B, Co, n, _stream(x.device))
-        ctx.save_for_backward(wt)
+        ctx.save_for_backward(W9t)
+        ctx.shape = (B, Ci, Co, n)
         return t
 
     @staticmethod
     def backward(ctx, gt):
-        wt, = ctx.saved_tensors
-        return F.conv2d(gt, wt, stride=2), None, None                      # conv_transpose2d's adjoint
+        W9t, = ctx.saved_tensors
+        B, Ci, Co, n = ctx.shape
+        gt = gt.contiguous()
+        dP = torch.empty((B, 9 * Co, n * n), device=gt.device, dtype=gt.dtype)
+        _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, _stream(gt.device))
+        return torch.matmul(W9t, dP).view(B, Ci, n, n), None, None         # conv_transpose2d's adjoint
 
 
 def up_conv(x, w):
     """F.conv_transpose2d(x, w.transpose(0, 1), stride=2) for w [Co, Ci, 3, 3] (stylegan.py:99-101,
-    the synthesis up-sampling layers): the 9 taps as one GEMM (hipBLASLt, 125-137 TFLOP/s on the
-    256^2 generator's layers where MIOpen's transposed kernels reach 50-70) and the tap scatter
-    nfi_syn_up_conv_scatter; the data gradient is the stride-2 convolution (MIOpen).  A weight
-    that takes gradients goes to MIOpen's conv_transpose2d."""
+    the synthesis up-sampling layers) as GEMMs over the 9 taps: forward P = W9 x (hipBLASLt,
+    125-137 TFLOP/s on the 256^2 generator's layers where MIOpen's transposed kernels reach 50-70)
+    and the tap scatter nfi_syn_up_conv_scatter; data gradient W9^T dP after the tap gather
+    nfi_syn_up_conv_gather.  A weight that takes gradients goes to MIOpen's conv_transpose2d."""
     _require_device(x, w)
     if torch.is_grad_enabled() and w.requires_grad:
         return F.conv_transpose2d(x, w.transpose(0, 1), stride=2)
-    W9, wt = _up_weights(w)
-    return _UpConv.apply(x, W9, wt)
+    W9, W9t = _up_weights(w)
+    return _UpConv.apply(x, W9, W9t)
 
 
 class _UpAdd(torch.autograd.Function):

@@ -33,7 +33,7 @@ def scatter(P, n):
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     dev = torch.device('cuda:0')
-    tot = [0.0, 0.0]
+    tot = [0.0, 0.0, 0.0, 0.0]
     for ci, co, n in LAYERS:
         x = torch.randn(B, ci, n, n, device=dev)
         w = torch.randn(co, ci, 3, 3, device=dev) / (3 * ci ** .5)
@@ -51,7 +51,21 @@ def main():
               f'({gf / t_g:.0f} TF)  err miopen {e_m:.1e} gemm9 {e_g:.1e}', flush=True)
         tot[0] += t_m
         tot[1] += t_g
-    print(f'total: miopen {tot[0]:.3f} ms  gemm9 (no scatter) {tot[1]:.3f} ms')
+        # the data gradient: stride-2 convolution (MIOpen) vs im2col (F.unfold) + one GEMM
+        gt = torch.randn(B, co, 2 * n + 1, 2 * n + 1, device=dev)
+        wr = wt.reshape(ci, co * 9)
+        ref_b = F.conv2d(gt.double(), wt.double(), stride=2)
+        got_b = torch.matmul(wr, F.unfold(gt, 3, stride=2)).view(B, ci, n, n)
+        e_b = float((got_b - ref_b).abs().max()) / float(ref_b.abs().max())
+        tb_m = timeit(lambda: F.conv2d(gt, wt, stride=2))
+        tb_u = timeit(lambda: F.unfold(gt, 3, stride=2))
+        tb_g = timeit(lambda: torch.matmul(wr, F.unfold(gt, 3, stride=2)))
+        print(f'   bwd: miopen {tb_m:.3f} ms ({gf / tb_m:.0f} TF)  unfold {tb_u:.3f} + gemm = {tb_g:.3f} ms  '
+              f'err {e_b:.1e}', flush=True)
+        tot[2] += tb_m
+        tot[3] += tb_g
+    print(f'total: miopen {tot[0]:.3f} ms  gemm9 (no scatter) {tot[1]:.3f} ms; bwd miopen {tot[2]:.3f} '
+          f'unfold+gemm {tot[3]:.3f} ms')
 
 
 if __name__ == '__main__':
