@@ -28,14 +28,19 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// block (256) sum -> one atomic per block into *dst
+// block (256) sum -> *dst: stored when the plane is one block (gridDim.x == 1: no zero-fill
+// launch before), else one atomic per block into the zero-filled *dst
 __device__ __forceinline__ void block_sum_atomic(float v, float* dst) {
   __shared__ float part[4];
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) part[w] = v;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(dst, (part[0] + part[1]) + (part[2] + part[3]));
+  if (threadIdx.x == 0) {
+    const float s = (part[0] + part[1]) + (part[2] + part[3]);
+    if (gridDim.x == 1) *dst = s;
+    else atomicAdd(dst, s);
+  }
 }
 
 __global__ void __launch_bounds__(256) act_fwd_kernel(const float4* __restrict__ o,
@@ -63,19 +68,25 @@ __global__ void __launch_bounds__(256) act_bwd_kernel(const float4* __restrict__
   const float dp = d[p], b = bias[p % C];
   const int64_t base = (int64_t)p * HW4;
   float acc = 0.f;
+  // branch-free loads (clamped index; a lane past the plane adds 0 and stores nothing)
+  float4 gv[4], ov[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = min(blockIdx.x * RED_CHUNK4 + k * 256 + (int)threadIdx.x, HW4 - 1);
+    gv[k] = g[base + j];
+    ov[k] = o[base + j];
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int j = blockIdx.x * RED_CHUNK4 + k * 256 + threadIdx.x;
-    if (j < HW4) {
-      const float4 gv = g[base + j], ov = o[base + j];
-      float4 gz;
-      gz.x = gv.x * gain * act_slope(ov.x, dp, b);
-      gz.y = gv.y * gain * act_slope(ov.y, dp, b);
-      gz.z = gv.z * gain * act_slope(ov.z, dp, b);
-      gz.w = gv.w * gain * act_slope(ov.w, dp, b);
-      acc += (gz.x * ov.x + gz.y * ov.y) + (gz.z * ov.z + gz.w * ov.w);
-      go[base + j] = make_float4(gz.x * dp, gz.y * dp, gz.z * dp, gz.w * dp);
-    }
+    float4 gz;
+    gz.x = gv[k].x * gain * act_slope(ov[k].x, dp, b);
+    gz.y = gv[k].y * gain * act_slope(ov[k].y, dp, b);
+    gz.z = gv[k].z * gain * act_slope(ov[k].z, dp, b);
+    gz.w = gv[k].w * gain * act_slope(ov[k].w, dp, b);
+    const float part = (gz.x * ov[k].x + gz.y * ov[k].y) + (gz.z * ov[k].z + gz.w * ov[k].w);
+    acc += j < HW4 ? part : 0.f;
+    if (j < HW4) go[base + j] = make_float4(gz.x * dp, gz.y * dp, gz.z * dp, gz.w * dp);
   }
   block_sum_atomic(acc, dd + p);
 }
@@ -90,14 +101,20 @@ __global__ void __launch_bounds__(256) scale_bwd_kernel(const float4* __restrict
   const float sp = s[p];
   const int64_t base = (int64_t)p * HW4;
   float acc = 0.f;
+  // branch-free loads (clamped index; a lane past the plane adds 0 and stores nothing)
+  float4 gv[4], xv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = min(blockIdx.x * RED_CHUNK4 + k * 256 + (int)threadIdx.x, HW4 - 1);
+    gv[k] = g[base + j];
+    xv[k] = x[base + j];
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int j = blockIdx.x * RED_CHUNK4 + k * 256 + threadIdx.x;
-    if (j < HW4) {
-      const float4 gv = g[base + j], xv = x[base + j];
-      acc += (gv.x * xv.x + gv.y * xv.y) + (gv.z * xv.z + gv.w * xv.w);
-      if (gx) gx[base + j] = make_float4(gv.x * sp, gv.y * sp, gv.z * sp, gv.w * sp);
-    }
+    const float part = (gv[k].x * xv[k].x + gv[k].y * xv[k].y) + (gv[k].z * xv[k].z + gv[k].w * xv[k].w);
+    acc += j < HW4 ? part : 0.f;
+    if (gx && j < HW4) gx[base + j] = make_float4(gv[k].x * sp, gv[k].y * sp, gv[k].z * sp, gv[k].w * sp);
   }
   block_sum_atomic(acc, ds + p);
 }
@@ -536,11 +553,11 @@ int32_t nfi_syn_act_backward(const float* g, const float* o, const float* d, con
   NFI_REQUIRE(g && o && d && bias && go && dd, "syn_act_backward: null pointer");
   NFI_REQUIRE(P > 0 && C > 0 && P % C == 0 && HW > 0 && HW % 4 == 0, "syn_act_backward: bad shape");
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(dd, 0, sizeof(float) * P, s) != hipSuccess) {
+  const int HW4 = HW / 4;
+  if (HW4 > RED_CHUNK4 && hipMemsetAsync(dd, 0, sizeof(float) * P, s) != hipSuccess) {
     nfi::set_error("syn_act_backward: memset failed");
     return NFI_ELAUNCH;
   }
-  const int HW4 = HW / 4;
   act_bwd_kernel<<<dim3((HW4 + RED_CHUNK4 - 1) / RED_CHUNK4, P), 256, 0, s>>>(
       (const float4*)g, (const float4*)o, d, bias, (float4*)go, dd, C, HW4, gain);
   NFI_CHECK_LAUNCH("act_bwd_kernel");
@@ -609,11 +626,11 @@ int32_t nfi_syn_scale_backward(const float* g, const float* x, const float* s, f
   NFI_REQUIRE(g && x && s && ds, "syn_scale_backward: null pointer");
   NFI_REQUIRE(P > 0 && HW > 0 && HW % 4 == 0, "syn_scale_backward: bad shape");
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(ds, 0, sizeof(float) * P, st) != hipSuccess) {
+  const int HW4 = HW / 4;
+  if (HW4 > RED_CHUNK4 && hipMemsetAsync(ds, 0, sizeof(float) * P, st) != hipSuccess) {
     nfi::set_error("syn_scale_backward: memset failed");
     return NFI_ELAUNCH;
   }
-  const int HW4 = HW / 4;
   scale_bwd_kernel<<<dim3((HW4 + RED_CHUNK4 - 1) / RED_CHUNK4, P), 256, 0, st>>>(
       (const float4*)g, (const float4*)x, s, (float4*)gx, ds, HW4);
   NFI_CHECK_LAUNCH("scale_bwd_kernel");

@@ -169,7 +169,7 @@ class ToPlanes(nn.Module):
     def forward(self, x, w, pre=None):
         styles = self.affine(w) * self.weight_gain if pre is None else pre
         if self.backend == 'hip':
-            return F.conv2d(_hip().scale(x, styles), self.weight)          # bias added in up_add
+            return _hip().modulated_conv1x1(x, styles, self.weight)       # bias added in up_add
         x = F.conv2d(x * styles[:, :, None, None], self.weight)
         return x + self.bias[None, :, None, None]
 

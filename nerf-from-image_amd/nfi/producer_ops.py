@@ -167,6 +167,48 @@ def up_conv(x, w):
     return _UpConv.apply(x, W9, W9t)
 
 
+class _ModConv1x1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s, Wf, Wt):
+        x = x.contiguous()
+        s = s.contiguous()
+        B, C, H, W = x.shape
+        O = Wf.shape[0]
+        y = torch.bmm(Wf[None] * s[:, None, :], x.view(B, C, H * W)).view(B, O, H, W)
+        ctx.save_for_backward(x, s, Wt)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, s, Wt = ctx.saved_tensors
+        B, C, H, W = x.shape
+        gxs = torch.matmul(Wt, gy.reshape(B, -1, H * W))                  # d(x * s) [B, C, HW]
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
+        _call('nfi_syn_scale_backward', _p(gxs), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W,
+              _stream(x.device))
+        return gx, ds, None, None
+
+
+def modulated_conv1x1(x, s, weight):
+    """F.conv2d(x * s[:, :, None, None], weight) for a frozen 1x1 weight [O, C, 1, 1] (the toRGB /
+    to-planes layers, stylegan.py:363-384): the modulation goes into a per-image weight (W * s_b,
+    [B, O, C]: O = 96 rows, far smaller than x) and the layer is one batched GEMM; the backward is
+    W^T dy (one GEMM) and nfi_syn_scale_backward (d x = s * that, d s = sum x * that).  A weight that
+    takes gradients goes to MIOpen."""
+    _require_device(x, s, weight)
+    if torch.is_grad_enabled() and weight.requires_grad:
+        return F.conv2d(x * s[:, :, None, None], weight)
+    key = (weight.data_ptr(), weight._version, weight.device)
+    hit = getattr(weight, '_nfi_1x1', None)
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            Wf = weight.detach().reshape(weight.shape[0], -1).contiguous()
+            hit = (key, (Wf, Wf.t().contiguous()))
+        weight._nfi_1x1 = hit
+    return _ModConv1x1.apply(x, s, *hit[1])
+
+
 class _UpAdd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, img, c, bias):

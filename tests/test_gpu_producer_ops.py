@@ -106,6 +106,29 @@ def test_up_conv(B, Ci, Co, n):
     assert float((tg.double() - r64).abs().max()) <= max(1e-6 * s, 4 * err32)
 
 
+@pytest.mark.parametrize('B,C,O,H', [(1, 8, 3, 2), (2, 32, 96, 4), (3, 512, 96, 16), (2, 128, 96, 128)])
+def test_modulated_conv1x1(B, C, O, H):
+    """bmm(W * s_b, x) == conv2d(x * s, W) for the 1x1 to-planes layers; d x and d s (fp64
+    reference, 4x the fp32 torch formulation's error, floor 2e-6 of the max)."""
+    x = _rand(B, C, H, H, seed=19).requires_grad_()
+    s = _rand(B, C, seed=20).requires_grad_()
+    w = _rand(O, C, 1, 1, seed=21) / C ** 0.5
+    g = _rand(B, O, H, H, seed=22)
+    y = producer_ops.modulated_conv1x1(x, s, w)
+    y.backward(g)
+    x64, s64 = x.detach().double().requires_grad_(), s.detach().double().requires_grad_()
+    y64 = F.conv2d(x64 * s64[:, :, None, None], w.double())
+    y64.backward(g.double())
+    x32, s32 = x.detach().clone().requires_grad_(), s.detach().clone().requires_grad_()
+    y32 = F.conv2d(x32 * s32[:, :, None, None], w)
+    y32.backward(g)
+    for got, ref, r32 in ((y.detach(), y64.detach(), y32.detach()), (x.grad, x64.grad, x32.grad),
+                          (s.grad, s64.grad, s32.grad)):
+        m = float(ref.abs().max())
+        err, err32 = float((got.double() - ref).abs().max()), float((r32.double() - ref).abs().max())
+        assert err <= max(2e-6 * m, 4 * err32), (err, err32, m)
+
+
 @pytest.mark.parametrize('B,C,n', [(2, 3, 2), (2, 5, 4), (1, 96, 16), (2, 96, 128)])
 @pytest.mark.parametrize('with_img', [True, False])
 def test_up_add(B, C, n, with_img):
