@@ -426,6 +426,128 @@ __global__ void __launch_bounds__(256) lpips_bwd_kernel(const float* __restrict_
   }
 }
 
+// One-read forms for C = 16 * CPW channels: a workgroup of 16 waves takes 64 pixels, wave j
+// holds channels [j*CPW, (j+1)*CPW) of its lane's pixel in registers; the per-pixel channel sums
+// (||f0||^2, ||f1||^2, then the weighted squared difference / the backward's two dot products)
+// are wave partials combined through LDS in a fixed order.  f0 and f1 are read from HBM once
+// (the loops above read them twice, and the second pass misses the caches at these sizes).
+constexpr int LP_WAVES = 16;
+
+template <int CPW>
+__global__ void __launch_bounds__(1024) lpips_fwd_regs_kernel(const float* __restrict__ f0,
+                                                              const float* __restrict__ f1,
+                                                              const float* __restrict__ w,
+                                                              float* __restrict__ out,
+                                                              float* __restrict__ inv0,
+                                                              float* __restrict__ inv1, int N, int HW) {
+  constexpr int C = LP_WAVES * CPW;
+  __shared__ float red[3][LP_WAVES][64];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t total = (int64_t)N * HW;
+  const int64_t pix = (int64_t)blockIdx.x * 64 + l;
+  const bool live = pix < total;
+  const int64_t pc = live ? pix : total - 1;
+  const int n = (int)(pc / HW), hw = (int)(pc - (int64_t)n * HW);
+  const int64_t off = ((int64_t)n * C + wv * CPW) * HW + hw;
+  float xa[CPW], xb[CPW];
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    xa[k] = f0[off + (int64_t)k * HW];
+    xb[k] = f1[off + (int64_t)k * HW];
+  }
+  float ra = 0.f, rb = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    ra = fmaf(xa[k], xa[k], ra);
+    rb = fmaf(xb[k], xb[k], rb);
+  }
+  red[0][wv][l] = ra;
+  red[1][wv][l] = rb;
+  __syncthreads();
+  float RA = 0.f, RB = 0.f;
+#pragma unroll
+  for (int j = 0; j < LP_WAVES; ++j) {
+    RA += red[0][j][l];
+    RB += red[1][j][l];
+  }
+  const float ia = 1.f / (sqrtf(RA) + LP_EPS), ib = 1.f / (sqrtf(RB) + LP_EPS);
+  float d = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    const float t = xa[k] * ia - xb[k] * ib;
+    d += w[wv * CPW + k] * t * t;
+  }
+  red[2][wv][l] = d;
+  __syncthreads();
+  if (wv != 0) return;
+  float D = 0.f;
+#pragma unroll
+  for (int j = 0; j < LP_WAVES; ++j) D += red[2][j][l];
+  D *= 1.f / (float)HW;
+  if (live) {
+    inv0[pix] = ia;
+    inv1[pix] = ib;
+  }
+  if (HW % 64 == 0) {               // the whole wave is one image
+    D = wave_sum(D);
+    if (l == 0 && live) atomicAdd(out + n, D);
+  } else if (live) {
+    atomicAdd(out + n, D);
+  }
+}
+
+template <int CPW>
+__global__ void __launch_bounds__(1024) lpips_bwd_regs_kernel(const float* __restrict__ g,
+                                                              const float* __restrict__ f0,
+                                                              const float* __restrict__ f1,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ inv0,
+                                                              const float* __restrict__ inv1,
+                                                              float* __restrict__ gf0, int N, int HW) {
+  constexpr int C = LP_WAVES * CPW;
+  __shared__ float red[2][LP_WAVES][64];
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t total = (int64_t)N * HW;
+  const int64_t pix = (int64_t)blockIdx.x * 64 + l;
+  const bool live = pix < total;
+  const int64_t pc = live ? pix : total - 1;
+  const int n = (int)(pc / HW), hw = (int)(pc - (int64_t)n * HW);
+  const int64_t off = ((int64_t)n * C + wv * CPW) * HW + hw;
+  float xa[CPW], xb[CPW];
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    xa[k] = f0[off + (int64_t)k * HW];
+    xb[k] = f1[off + (int64_t)k * HW];
+  }
+  const float ia = inv0[pc], ib = inv1[pc];
+  const float s = 2.f * g[n] / (float)HW;
+  // u_c = s w_c (a_c ia - b_c ib); grad_k = ia u_k - ia^2 (a_k / r) sum_c u_c a_c, r = ||a||
+  float ua = 0.f, r2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) {
+    xb[k] = s * w[wv * CPW + k] * (xa[k] * ia - xb[k] * ib);   // u_k (b is not needed again)
+    ua += xb[k] * xa[k];
+    r2 += xa[k] * xa[k];
+  }
+  red[0][wv][l] = ua;
+  red[1][wv][l] = r2;
+  __syncthreads();
+  float UA = 0.f, R2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < LP_WAVES; ++j) {
+    UA += red[0][j][l];
+    R2 += red[1][j][l];
+  }
+  if (!live) return;
+  const float r = sqrtf(R2);
+  // all-zero feature vector: torch's sqrt backward gives 0*inf = NaN here; we give 0
+  const float k2 = r == 0.f ? 0.f : ia * ia * UA / r;
+  const float sa = r == 0.f ? 0.f : ia;
+  float* o = gf0 + off;
+#pragma unroll
+  for (int k = 0; k < CPW; ++k) o[(int64_t)k * HW] = sa * xb[k] - k2 * xa[k];
+}
+
 // ---------------------------------------------------------------------------------------
 // VGG16 block epilogue of the LPIPS trunk (torchvision vgg16.features as lpips 0.1 runs it):
 // conv output x (MIOpen, no bias) -> y = ReLU(x + bias[c]) and, before a MaxPool2d(2, 2), the
@@ -647,7 +769,14 @@ int32_t nfi_lpips_head_forward(const float* f0, const float* f1, const float* w,
     nfi::set_error("lpips_head_forward: memset failed");
     return NFI_ELAUNCH;
   }
-  lpips_fwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(f0, f1, w, out, inv0, inv1, N, C, HW);
+  const unsigned pb = (unsigned)(((int64_t)N * HW + 63) / 64);
+  switch (C) {
+    case 64: lpips_fwd_regs_kernel<4><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 128: lpips_fwd_regs_kernel<8><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 256: lpips_fwd_regs_kernel<16><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 512: lpips_fwd_regs_kernel<32><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    default: lpips_fwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(f0, f1, w, out, inv0, inv1, N, C, HW);
+  }
   NFI_CHECK_LAUNCH("lpips_fwd_kernel");
   return NFI_OK;
 }
@@ -657,8 +786,15 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
                                 int32_t C, int32_t HW, void* stream) {
   NFI_REQUIRE(g && f0 && f1 && w && inv0 && inv1 && gf0, "lpips_head_backward: null pointer");
   NFI_REQUIRE(N > 0 && C > 0 && HW > 0, "lpips_head_backward: bad shape");
-  lpips_bwd_kernel<<<blocks((int64_t)N * HW), 256, 0, (hipStream_t)stream>>>(g, f0, f1, w, inv0,
-                                                                              inv1, gf0, N, C, HW);
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned pb = (unsigned)(((int64_t)N * HW + 63) / 64);
+  switch (C) {
+    case 64: lpips_bwd_regs_kernel<4><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 128: lpips_bwd_regs_kernel<8><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 256: lpips_bwd_regs_kernel<16><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 512: lpips_bwd_regs_kernel<32><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    default: lpips_bwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, C, HW);
+  }
   NFI_CHECK_LAUNCH("lpips_bwd_kernel");
   return NFI_OK;
 }

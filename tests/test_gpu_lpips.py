@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device('cuda:0')
 
 
-@pytest.mark.parametrize('N,C,H', [(3, 64, 32), (2, 512, 8), (5, 7, 3)])
+@pytest.mark.parametrize('N,C,H', [(3, 64, 32), (2, 512, 8), (5, 7, 3), (2, 128, 5), (4, 256, 16), (64, 64, 128)])
 def test_lpips_head_matches_torch(N, C, H):
     g = torch.Generator(device=DEV).manual_seed(C)
     f0 = torch.randn((N, C, H, H), device=DEV, generator=g).relu().requires_grad_()
