@@ -1,8 +1,10 @@
 /*
  * nfi producer C-ABI: the memory-bound operators of the tri-plane producer (the StyleGAN2
  * synthesis network of yuliangguo/nerf-from-image, models/stylegan.py:293-490) around its
- * convolutions, fused for MI355X (gfx950).  The convolutions themselves stay library calls
- * (MIOpen through PyTorch-ROCm); everything between them is here:
+ * convolutions, fused for MI355X (gfx950), and the convolutions' own memory-bound halves: the
+ * matrix products run as hipBLASLt GEMMs through PyTorch-ROCm (3x3: Winograd F(4,3), below;
+ * up-sampling: one GEMM over the 9 taps + the tap scatter / gather here; 1x1: one batched GEMM
+ * with the modulation folded into a per-image weight).  Everything between them is here:
  *
  *   modulated-conv epilogue  stylegan.py:140-145, 345-356   x*dcoefs + bias, *sqrt(2), leaky ReLU
  *   up-sampling FIR epilogue stylegan.py:99-103 (filter2d gain 4, pad 1) + the epilogue above
@@ -10,6 +12,7 @@
  *   channel-scale backward   stylegan.py:130                d(x*styles): g*styles and sum(g*x)
  *   LPIPS distance head      metrics.py:130-146 (lpips 0.1) normalise, difference, lin, mean
  *   LPIPS VGG16 epilogue     bias + ReLU (+ 2x2 max pool) after each trunk convolution
+ *   LPIPS augmented copies   run.py:720-767 (grid_sample of 15 affine copies, gathered adjoint)
  *
  * Tensors are NCHW float32, contiguous; "planes" P = B*C images of one channel; per-plane
  * scales `d` have P entries ([B,C] row-major), per-channel biases C entries.  `stream` is a
@@ -54,6 +57,12 @@ int32_t nfi_syn_fir_up_backward(const float* go, float* gt, int32_t P, int32_t n
  * computes P [B][9][C][n][n] = W9 x (W9 [9*C, Ci] = w permuted to [ky][kx][co][ci]); this sums the
  * taps into t [B][C][2n+1][2n+1], t[Y][X] = sum of P[3ky+kx][.][iy][ix] over Y = 2iy+ky, X = 2ix+kx. */
 int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, int32_t n, void* stream);
+
+/* The scatter fused with nfi_syn_fir_up_act_forward's FIR + epilogue (t stays on chip): P as
+ * above -> o [B][C][2n][2n] (FIR output, for the backward) and y = lrelu(gain (o d[p] + bias[c])),
+ * the operations of scatter then fir_up_act.  2n % 64 == 0. */
+int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const float* bias, float* o, float* y,
+                                        int32_t B, int32_t C, int32_t n, float gain, void* stream);
 
 /* Its adjoint: gt [B][C][2n+1][2n+1] -> dP [B][9][C][n][n], dP[3ky+kx][c][iy][ix] =
  * gt[c][2iy+ky][2ix+kx]; the data gradient of the transposed convolution is then W9^T dP. */
@@ -134,6 +143,20 @@ int64_t nfi_wino_packed_size(int32_t Co, int32_t Ci);
 int32_t nfi_wino_pack_weights(const float* U, float* Ua, int32_t Co, int32_t Ci, void* stream);
 int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, float* y, float* pooled,
                             int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W, void* stream);
+
+/* The 'vgg' inversion loss's augmented copies (run.py:720-767 augment_impl as optimize_iter calls
+ * it, run.py:2211-2235): img [B][H][W][3] (the rendered / target image, channels last), grid
+ * [B*K][Ho][Wo][2] (affine_grid of each copy's rotation / scale / translation, copy j = b*K + k)
+ * -> out [B*K][3][Ho][Wo] = grid_sample(img[b] - shift, grid[j], bilinear, zeros,
+ * align_corners=False) + shift (shift 1 for white-background datasets, else 0).  Replaces the
+ * expand-to-K-copies + F.grid_sample of the reference. */
+int32_t nfi_aug_sample_forward(const float* img, const float* grid, float* out, int32_t B, int32_t K, int32_t H,
+                               int32_t W, int32_t Ho, int32_t Wo, float shift, void* stream);
+
+/* Its adjoint summed over the K copies: gout [B*K][3][Ho][Wo] -> gimg [B][H][W][3] (overwritten),
+ * gathered per input pixel (no atomics; grid_sampler_2d_backward's weights). */
+int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gimg, int32_t B, int32_t K, int32_t H,
+                                int32_t W, int32_t Ho, int32_t Wo, void* stream);
 
 #ifdef __cplusplus
 }

@@ -197,6 +197,70 @@ __global__ void __launch_bounds__(256) tap_scatter_kernel(const float* __restric
   t[i] = s;
 }
 
+// The same scatter fused with the FIR + epilogue (fir_up_act_kernel), for 2n >= 64: one workgroup
+// per 16 x 64 output tile of one plane; the tile's products P (9 taps x 11 x 36) are staged in
+// LDS with coalesced loads, the (16+3) x (64+3) transposed-conv values t are formed in LDS with
+// tap_scatter_kernel's arithmetic and each thread filters 4 outputs with fir_up_act_kernel's (the
+// two-kernel path's operations, up to FMA contraction), without t's round trip through HBM.
+constexpr int UF_TY = 16, UF_TX = 64;
+constexpr int UF_PY = UF_TY / 2 + 3, UF_PX = UF_TX / 2 + 4;   // 11 x 36 products per tap
+constexpr int UF_RY = UF_TY + 3, UF_RX = UF_TX + 3;           // 19 x 67 t values
+__global__ void __launch_bounds__(256) up_fir_act_kernel(const float* __restrict__ P, const float* __restrict__ d,
+                                                         const float* __restrict__ bias, float4* __restrict__ o,
+                                                         float4* __restrict__ y, int C, int n, float gain) {
+  __shared__ float Ps[9][UF_PY][UF_PX];
+  __shared__ float Ts[UF_RY][UF_RX + 1];
+  const int W2 = 2 * n, T = 2 * n + 1;
+  const int tiles_x = W2 / UF_TX;
+  const int tile = blockIdx.x, p = blockIdx.y;              // p = b * C + c
+  const int Y0 = (tile / tiles_x) * UF_TY, X0 = (tile % tiles_x) * UF_TX;
+  const int b = p / C, c = p - b * C;
+  const int64_t nn = (int64_t)n * n, tap = (int64_t)C * nn;
+  const float* Pc = P + ((int64_t)b * 9 * C + c) * nn;
+  const int iy0 = Y0 / 2 - 2, ix0 = X0 / 2 - 2;
+  for (int k = threadIdx.x; k < 9 * UF_PY * UF_PX; k += 256) {
+    const int tp = k / (UF_PY * UF_PX), r = (k / UF_PX) % UF_PY, q = k % UF_PX;
+    const int iy = iy0 + r, ix = ix0 + q;
+    const bool in = iy >= 0 && iy < n && ix >= 0 && ix < n;
+    const float v = Pc[tp * tap + (int64_t)min(max(iy, 0), n - 1) * n + min(max(ix, 0), n - 1)];
+    Ps[tp][r][q] = in ? v : 0.f;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < UF_RY * UF_RX; k += 256) {
+    const int r = k / UF_RX, q = k - r * UF_RX;
+    const int Yt = Y0 - 1 + r, Xt = X0 - 1 + q;             // t coordinates (may be outside [0, 2n])
+    float s = 0.f;
+    if (Yt >= 0 && Yt < T && Xt >= 0 && Xt < T) {
+      const int kya = Yt & 1, iya = Yt >> 1, kxa = Xt & 1, ixa = Xt >> 1;
+      const bool ya = iya < n, yb = !(Yt & 1) && iya >= 1, xa = ixa < n, xb = !(Xt & 1) && ixa >= 1;
+      const int ra = iya - iy0, rb = iya - 1 - iy0, ca = ixa - ix0, cb = ixa - 1 - ix0;
+      const float paa = Ps[kya * 3 + kxa][ra][ca], pab = Ps[kya * 3 + 2][ra][cb];
+      const float pba = Ps[6 + kxa][rb][ca], pbb = Ps[8][rb][cb];
+      s = ((ya && xa ? paa : 0.f) + (ya && xb ? pab : 0.f)) + ((yb && xa ? pba : 0.f) + (yb && xb ? pbb : 0.f));
+    }
+    Ts[r][q] = s;
+  }
+  __syncthreads();
+  const int r0 = threadIdx.x / (UF_TX / 4), x4 = (threadIdx.x % (UF_TX / 4)) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) v[j] = Ts[r0 + r][x4 + j];
+    const float kr = k4(r);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] += kr * ((v[k] + v[k + 3]) + 3.f * (v[k + 1] + v[k + 2]));
+  }
+  const float dp = d[p], bb = bias[c];
+  const float inv = 1.f / 16.f;
+  const float4 ov = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+  const int64_t i = ((int64_t)p * W2 * W2 + (int64_t)(Y0 + r0) * W2 + X0 + x4) / 4;
+  o[i] = ov;
+  y[i] = make_float4(act(ov.x, dp, bb, gain), act(ov.y, dp, bb, gain), act(ov.z, dp, bb, gain),
+                     act(ov.w, dp, bb, gain));
+}
+
 // Its adjoint's operand (the data gradient of the transposed convolution is W9^T dP): gt
 // [B][C][2n+1][2n+1] -> dP [B][9][C][n][n], dP[3ky+kx][c][iy][ix] = gt[c][2iy+ky][2ix+kx] (always
 // inside gt).  One thread per (b, c, iy, ix): its 3x3 window, 9 coalesced row stores.
@@ -649,6 +713,114 @@ __global__ void __launch_bounds__(256) vgg_relu_pool_bwd_kernel(const float* __r
                                                         yv.z > 0.f ? gv.z : 0.f, yv.w > 0.f ? gv.w : 0.f);
 }
 
+// ---------------------------------------------------------------------------------------
+// The 'vgg' loss's augmented copies (run.py:720-767 augment_impl, as optimize_iter calls it at
+// run.py:2211-2235): K copies of each image [B][H][W][3] resampled through their own affine grid
+// [B*K][Ho][Wo][2] by grid_sample(bilinear, zeros, align_corners=False) after the white-background
+// shift (img - shift, + shift after).  The arithmetic restates ATen's grid_sampler_2d (source index
+// ((g + 1) * size - 1) / 2, floor corners, weights nw = (ix_se - ix)(iy_se - iy), ..., corners
+// accumulated nw, ne, sw, se).  The image is read in place (no expanded contiguous copies).
+// ---------------------------------------------------------------------------------------
+struct Samp {
+  float ix, iy;
+  int x0, y0;
+};
+__device__ __forceinline__ Samp samp_at(const float* __restrict__ g, int W, int H) {
+  Samp s;
+  s.ix = ((g[0] + 1.f) * (float)W - 1.f) / 2.f;
+  s.iy = ((g[1] + 1.f) * (float)H - 1.f) / 2.f;
+  s.x0 = (int)floorf(s.ix);
+  s.y0 = (int)floorf(s.iy);
+  return s;
+}
+
+// one thread per output pixel of one copy, its 3 channels
+__global__ void __launch_bounds__(256) aug_fwd_kernel(const float* __restrict__ img, const float* __restrict__ grid,
+                                                      float* __restrict__ out, int64_t total, int K, int H, int W,
+                                                      int Ho, int Wo, float shift) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t HWo = (int64_t)Ho * Wo;
+  const int64_t j = i / HWo;                     // copy b*K + k
+  const int pix = (int)(i - j * HWo);
+  const int b = (int)(j / K);
+  const Samp s = samp_at(grid + i * 2, W, H);
+  const float fx = (float)s.x0, fy = (float)s.y0;
+  const float nw = (fx + 1.f - s.ix) * (fy + 1.f - s.iy), ne = (s.ix - fx) * (fy + 1.f - s.iy);
+  const float sw = (fx + 1.f - s.ix) * (s.iy - fy), se = (s.ix - fx) * (s.iy - fy);
+  const float* im = img + (int64_t)b * H * W * 3;
+  float acc[3] = {0.f, 0.f, 0.f};
+  const int cx[4] = {s.x0, s.x0 + 1, s.x0, s.x0 + 1}, cy[4] = {s.y0, s.y0, s.y0 + 1, s.y0 + 1};
+  const float wt[4] = {nw, ne, sw, se};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bool in = cx[q] >= 0 && cx[q] < W && cy[q] >= 0 && cy[q] < H;
+    const int64_t o = ((int64_t)min(max(cy[q], 0), H - 1) * W + min(max(cx[q], 0), W - 1)) * 3;
+    const float v0 = im[o] - shift, v1 = im[o + 1] - shift, v2 = im[o + 2] - shift;
+    acc[0] = in ? acc[0] + v0 * wt[q] : acc[0];
+    acc[1] = in ? acc[1] + v1 * wt[q] : acc[1];
+    acc[2] = in ? acc[2] + v2 * wt[q] : acc[2];
+  }
+  float* op = out + j * 3 * HWo + pix;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) op[c * HWo] = acc[c] + shift;
+}
+
+// Adjoint, gathered (no atomics): one thread per input pixel (b, Y, X); for each copy the output
+// pixels whose sample has (Y, X) as a corner lie in the preimage of the 2x2 box around (Y, X)
+// under the copy's affine map (read off the grid itself: its value at (0,0), (0,1), (1,0)),
+// enumerated over that preimage's bounding box + 1 and tested with the forward's exact arithmetic.
+__global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ grid,
+                                                      float* __restrict__ gimg, int64_t total, int K, int H, int W,
+                                                      int Ho, int Wo) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t HW = (int64_t)H * W, HWo = (int64_t)Ho * Wo;
+  const int b = (int)(i / HW);
+  const int pix = (int)(i - (int64_t)b * HW);
+  const int Y = pix / W, X = pix - Y * W;
+  float acc[3] = {0.f, 0.f, 0.f};
+  for (int k = 0; k < K; ++k) {
+    const int64_t j = (int64_t)b * K + k;
+    const float* gj = grid + j * HWo * 2;
+    // source position as an affine function of the output pixel: s(x, y) = s00 + x dx + y dy
+    const Samp s00 = samp_at(gj, W, H), s01 = samp_at(gj + 2 * min(1, Wo - 1), W, H),
+               s10 = samp_at(gj + 2 * (int64_t)min(1, Ho - 1) * Wo, W, H);
+    const float ax = Wo > 1 ? s01.ix - s00.ix : 1.f, bx = Ho > 1 ? s10.ix - s00.ix : 0.f;
+    const float ay = Wo > 1 ? s01.iy - s00.iy : 0.f, by = Ho > 1 ? s10.iy - s00.iy : 1.f;
+    const float det = ax * by - bx * ay;
+    if (!(fabsf(det) > 1e-12f)) continue;        // degenerate map (never drawn: scale > 0)
+    const float i00 = by / det, i01 = -bx / det, i10 = -ay / det, i11 = ax / det;
+    // the samples with corner (X, Y) have ix in [X-1, X+1), iy in [Y-1, Y+1): the preimage of
+    // that box is centred on the preimage of (X, Y), half extent |inverse| (1, 1) (+1 margin)
+    const float px = (float)X - s00.ix, py = (float)Y - s00.iy;
+    const float cx = i00 * px + i01 * py, cy = i10 * px + i11 * py;
+    const float ex = fabsf(i00) + fabsf(i01) + 1.f, ey = fabsf(i10) + fabsf(i11) + 1.f;
+    const int xlo = max((int)floorf(cx - ex), 0), xhi = min((int)ceilf(cx + ex), Wo - 1);
+    const int ylo = max((int)floorf(cy - ey), 0), yhi = min((int)ceilf(cy + ey), Ho - 1);
+    const float* go = gout + j * 3 * HWo;
+    for (int y = ylo; y <= yhi; ++y) {
+      for (int x = xlo; x <= xhi; ++x) {
+        const int64_t o = (int64_t)y * Wo + x;
+        const Samp s = samp_at(gj + o * 2, W, H);
+        const int dxc = X - s.x0, dyc = Y - s.y0;
+        if (dxc < 0 || dxc > 1 || dyc < 0 || dyc > 1) continue;
+        const float fx = (float)s.x0, fy = (float)s.y0;
+        const float wxv = dxc ? (s.ix - fx) : (fx + 1.f - s.ix);
+        const float wyv = dyc ? (s.iy - fy) : (fy + 1.f - s.iy);
+        const float w = wxv * wyv;
+        acc[0] += w * go[o];
+        acc[1] += w * go[HWo + o];
+        acc[2] += w * go[2 * HWo + o];
+      }
+    }
+  }
+  float* gp = gimg + i * 3;
+  gp[0] = acc[0];
+  gp[1] = acc[1];
+  gp[2] = acc[2];
+}
+
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace syn
@@ -704,6 +876,17 @@ int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, 
   const int64_t total = (int64_t)B * C * (2 * n + 1) * (2 * n + 1);
   tap_scatter_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(P, t, total, C, n);
   NFI_CHECK_LAUNCH("tap_scatter_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const float* bias, float* o, float* y,
+                                        int32_t B, int32_t C, int32_t n, float gain, void* stream) {
+  NFI_REQUIRE(P && d && bias && o && y, "syn_up_conv_fir_act_forward: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && n > 0 && (2 * n) % UF_TX == 0, "syn_up_conv_fir_act_forward: bad shape");
+  const int W2 = 2 * n;
+  up_fir_act_kernel<<<dim3((unsigned)((W2 / UF_TY) * (W2 / UF_TX)), (unsigned)(B * C)), 256, 0,
+                      (hipStream_t)stream>>>(P, d, bias, (float4*)o, (float4*)y, C, n, gain);
+  NFI_CHECK_LAUNCH("up_fir_act_kernel");
   return NFI_OK;
 }
 
@@ -833,6 +1016,26 @@ int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float
     vgg_relu_bwd_kernel<<<blocks(n4), 256, 0, st>>>((const float4*)gy, (const float4*)y, (float4*)gx, n4);
     NFI_CHECK_LAUNCH("vgg_relu_bwd_kernel");
   }
+  return NFI_OK;
+}
+
+int32_t nfi_aug_sample_forward(const float* img, const float* grid, float* out, int32_t B, int32_t K, int32_t H,
+                               int32_t W, int32_t Ho, int32_t Wo, float shift, void* stream) {
+  NFI_REQUIRE(img && grid && out, "aug_sample_forward: null pointer");
+  NFI_REQUIRE(B > 0 && K > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, "aug_sample_forward: bad shape");
+  const int64_t total = (int64_t)B * K * Ho * Wo;
+  aug_fwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(img, grid, out, total, K, H, W, Ho, Wo, shift);
+  NFI_CHECK_LAUNCH("aug_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gimg, int32_t B, int32_t K, int32_t H,
+                                int32_t W, int32_t Ho, int32_t Wo, void* stream) {
+  NFI_REQUIRE(gout && grid && gimg, "aug_sample_backward: null pointer");
+  NFI_REQUIRE(B > 0 && K > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, "aug_sample_backward: bad shape");
+  const int64_t total = (int64_t)B * H * W;
+  aug_bwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(gout, grid, gimg, total, K, H, W, Ho, Wo);
+  NFI_CHECK_LAUNCH("aug_bwd_kernel");
   return NFI_OK;
 }
 

@@ -19,6 +19,7 @@ from typing import Callable, Optional
 import torch
 import torch.nn.functional as F
 
+from . import producer_ops
 from .render import render as _nfi_render
 
 
@@ -243,7 +244,10 @@ def vgg_target(kind: str, target: torch.Tensor, lpips_net, white_background: boo
     b = tgt.shape[0]
     grid = augment_grid((15 * b, 6) + tuple(tgt.shape[2:]), 1.0, tgt.device, generator=augment_generator)
     with torch.no_grad():
-        aug_tgt = apply_grid(_copies(tgt), grid, white_background)
+        if target.is_cuda:
+            aug_tgt = producer_ops.aug_sample(target[..., :3], grid, 15, white_background)
+        else:
+            aug_tgt = apply_grid(_copies(tgt), grid, white_background)
     return grid, lpips_net.target_features(torch.cat((tgt, aug_tgt), dim=0))
 
 
@@ -272,7 +276,9 @@ def image_loss(kind: str, rgb: torch.Tensor, target: torch.Tensor, lpips_net=Non
                                                                      white_background, augment_generator)
         pred = rgb.permute(0, 3, 1, 2)
         if kind != 'vgg_nocrop':
-            pred = torch.cat((pred, apply_grid(_copies(pred), grid, white_background)), dim=0)
+            aug = (producer_ops.aug_sample(rgb, grid, 15, white_background) if rgb.is_cuda
+                   else apply_grid(_copies(pred), grid, white_background))
+            pred = torch.cat((pred, aug), dim=0)
         loss = loss + lpips_net(pred, f1=f1).mean() * b
     if kind in ('l1', 'mixed'):
         loss = loss + F.l1_loss(rgb, target) * b

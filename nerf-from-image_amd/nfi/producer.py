@@ -6,12 +6,13 @@ generator.py:475-477), AttentionMapper -> palette [b,10,3] (generator.py:132-186
 generator.py:263-282) and the frozen SDF decoder weights.
 
 Two backends, chosen explicitly (never a silent fallback):
-  'hip'   (default) the convolutions are library calls (MIOpen via PyTorch-ROCm) and everything
-          between them runs in the fused HIP kernels of csrc/nfi_producer.hip (producer_ops.py):
-          modulation backward, demodulation + bias + gain + leaky-ReLU epilogue, the up-sampling
-          FIR fused with that epilogue, the skip-image upsample + add; the demodulation
-          coefficients as one [b,in]x[in,out] product (sum_k W^2 precomputed per forward);
-          device tensors only;
+  'hip'   (default) the convolutions' products are hipBLASLt GEMMs (3x3: Winograd F(4,3),
+          nfi/conv.py; stride-2 up-sampling: one GEMM over the 9 taps + HIP tap scatter fused with
+          the FIR and epilogue; 1x1 to-planes: one batched GEMM with the modulation folded into a
+          per-image weight) and everything between them runs in the fused HIP kernels of
+          csrc/nfi_producer.hip (producer_ops.py): modulation backward, demodulation + bias + gain
+          + leaky-ReLU epilogue, the skip-image upsample + add; the styles and demodulation
+          coefficients of all layers as two batched products (style_bank); device tensors only;
   'torch' the reference's op sequence restated in plain PyTorch (any device) — the CPU-pinned
           restatement the tests check against the reference's fixtures.
 Parameter and buffer names equal the reference Generator's state_dict keys, so a G_ema
@@ -149,8 +150,7 @@ class ModulatedConv(nn.Module):
         else:                                  # from SynthesisNetwork's style bank
             styles, dcoefs = pre
         if self.up:
-            t = ops.up_conv(ops.scale(x, styles), self.weight)
-            return ops.fir_up_act(t, dcoefs, self.bias, SQRT2)
+            return ops.up_conv_act(ops.scale(x, styles), self.weight, dcoefs, self.bias, SQRT2)
         return ops.act(_conv().modulated_conv3x3(x, styles, self.weight), dcoefs, self.bias, SQRT2)
 
 

@@ -167,6 +167,55 @@ def up_conv(x, w):
     return _UpConv.apply(x, W9, W9t)
 
 
+class _UpConvAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W9, W9t, d, bias, gain: float):
+        _frozen(bias)
+        x = x.contiguous()
+        d = d.contiguous()
+        B, Ci, n, _ = x.shape
+        Co = W9.shape[0] // 9
+        P = torch.matmul(W9, x.view(B, Ci, n * n))                          # [B, 9*Co, n*n]
+        o = torch.empty((B, Co, 2 * n, 2 * n), device=x.device, dtype=x.dtype)
+        y = torch.empty_like(o)
+        _call('nfi_syn_up_conv_fir_act_forward', _p(P), _p(d), _p(bias), _p(o), _p(y), B, Co, n,
+              ctypes.c_float(gain), _stream(x.device))
+        ctx.save_for_backward(o, d, bias, W9t)
+        ctx.gain = gain
+        ctx.shape = (B, Ci, Co, n)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        o, d, bias, W9t = ctx.saved_tensors
+        B, Ci, Co, n = ctx.shape
+        g = g.contiguous()
+        dev = _stream(o.device)
+        go = torch.empty_like(o)
+        dd = torch.empty_like(d)
+        _call('nfi_syn_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(go), _p(dd), B * Co, Co,
+              4 * n * n, ctypes.c_float(ctx.gain), dev)
+        gt = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
+        _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * Co, n, dev)
+        dP = torch.empty((B, 9 * Co, n * n), device=o.device, dtype=o.dtype)
+        _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, dev)
+        gx = torch.matmul(W9t, dP).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
+        return gx, None, None, dd, None, None
+
+
+def up_conv_act(x, w, d, bias, gain: float):
+    """The up-sampling layer after the modulation: fir_up_act(up_conv(x, w), d, bias, gain)
+    (stylegan.py:99-103 + the demodulation epilogue :145, :348-356).  For 2n >= 64 the tap scatter,
+    FIR and epilogue are one kernel (nfi_syn_up_conv_fir_act_forward: the (2n+1)^2 transposed-conv
+    output never reaches HBM); smaller layers run the separate kernels."""
+    _require_device(x, w, d, bias)
+    n = x.shape[-1]
+    if (2 * n) % 64 or (torch.is_grad_enabled() and w.requires_grad):
+        return fir_up_act(up_conv(x, w), d, bias, gain)
+    W9, W9t = _up_weights(w)
+    return _UpConvAct.apply(x, W9, W9t, d, bias, gain)
+
+
 class _ModConv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, s, Wf, Wt):
@@ -207,6 +256,42 @@ def modulated_conv1x1(x, s, weight):
             hit = (key, (Wf, Wf.t().contiguous()))
         weight._nfi_1x1 = hit
     return _ModConv1x1.apply(x, s, *hit[1])
+
+
+class _AugSample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, grid, copies: int, shift: float):
+        img = img.contiguous()
+        grid = grid.contiguous()
+        B, H, W, _ = img.shape
+        Ho, Wo = grid.shape[1:3]
+        out = torch.empty((B * copies, 3, Ho, Wo), device=img.device, dtype=img.dtype)
+        _call('nfi_aug_sample_forward', _p(img), _p(grid), _p(out), B, copies, H, W, Ho, Wo,
+              ctypes.c_float(shift), _stream(img.device))
+        ctx.save_for_backward(grid)
+        ctx.shape = (B, copies, H, W, Ho, Wo)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        grid, = ctx.saved_tensors
+        B, K, H, W, Ho, Wo = ctx.shape
+        gout = gout.contiguous()
+        gimg = torch.empty((B, H, W, 3), device=gout.device, dtype=gout.dtype)
+        _call('nfi_aug_sample_backward', _p(gout), _p(grid), _p(gimg), B, K, H, W, Ho, Wo, _stream(gout.device))
+        return gimg, None, None, None
+
+
+def aug_sample(img, grid, copies: int, white_background: bool = False):
+    """The 'vgg' loss's augmented copies (run.py:720-767, 2211-2235): img [B, H, W, 3] (channels
+    last, as rendered) -> [B*copies, 3, Ho, Wo] = grid_sample(img[b] (- 1), grid[b*copies + k],
+    bilinear, zeros, align_corners=False) (+ 1 on white backgrounds), without materializing the
+    expanded copies; the backward gathers each input pixel's share from all copies (no atomics,
+    nfi_aug_sample_backward) into d img [B, H, W, 3]."""
+    _require_device(img, grid)
+    if img.shape[-1] != 3 or grid.shape[0] != img.shape[0] * copies or grid.shape[-1] != 2:
+        raise ValueError(f'aug_sample: img {tuple(img.shape)} / grid {tuple(grid.shape)} / copies {copies}')
+    return _AugSample.apply(img, grid.detach(), copies, 1.0 if white_background else 0.0)
 
 
 class _UpAdd(torch.autograd.Function):

@@ -117,6 +117,39 @@ def test_vgg_inversion_loss_runs():
     assert torch.isfinite(res.ws).all()
 
 
+@pytest.mark.parametrize('B,H,W,white,scale', [(2, 64, 64, False, None), (1, 32, 48, True, None),
+                                                (4, 128, 128, False, None), (2, 40, 40, False, 0.3),
+                                                (2, 40, 40, True, 3.0)])
+def test_aug_sample_matches_grid_sample(B, H, W, white, scale):
+    """The augmented copies (nfi_aug_sample_forward / _backward) against the reference's
+    expand-to-15-copies + grid_sample(bilinear, zeros, align_corners=False) in fp64: values and
+    the gradient summed over the copies (gathered, no atomics).  `scale` forces every copy's zoom
+    (0.3: each output pixel's corners spread over ~3 input pixels; 3.0: many samples per pixel)."""
+    g = torch.Generator(device=DEV).manual_seed(H + B)
+    img = torch.tanh(torch.randn((B, H, W, 3), device=DEV, generator=g)).requires_grad_()
+    grid = inversion.augment_grid((15 * B, 6, H, W), 1.0, DEV, generator=g)
+    if scale is not None:       # rescale the affine maps about the centre
+        grid = grid / scale
+    gout = torch.randn((15 * B, 3, H, W), device=DEV, generator=g)
+    out = producer_ops.aug_sample(img, grid, 15, white)
+    out.backward(gout)
+    i64 = img.detach().double().requires_grad_()
+    ref = inversion.apply_grid(inversion._copies(i64.permute(0, 3, 1, 2)), grid.double(), white)
+    ref.backward(gout.double())
+    i32 = img.detach().clone().requires_grad_()
+    r32 = inversion.apply_grid(inversion._copies(i32.permute(0, 3, 1, 2)), grid, white)
+    r32.backward(gout)
+    assert out.shape == ref.shape
+    ref = ref.detach()
+    # the fp32 source coordinates ((g + 1) W - 1) / 2 carry ~ulp(W) error: 4x torch fp32's own
+    # error against fp64 (the GPU parity convention), floor 1e-6
+    err, err32 = float((out.detach().double() - ref).abs().max()), float((r32.detach().double() - ref).abs().max())
+    assert err <= max(1e-6, 4 * err32), (err, err32)
+    gr = i64.grad
+    gerr, gerr32 = float((img.grad.double() - gr).abs().max()), float((i32.grad.double() - gr).abs().max())
+    assert gerr <= max(1e-6 * float(gr.abs().max()), 4 * gerr32), (gerr, gerr32)
+
+
 def test_vgg_target_on_side_stream_matches_inline():
     """The target half of the 'vgg' loss (grid + target features) computed on a side stream gives
     the inline loss and gradient (same device draws, same kernels); the inversion

@@ -106,6 +106,26 @@ def test_up_conv(B, Ci, Co, n):
     assert float((tg.double() - r64).abs().max()) <= max(1e-6 * s, 4 * err32)
 
 
+@pytest.mark.parametrize('B,Ci,Co,n', [(2, 16, 8, 32), (1, 32, 16, 64), (2, 24, 8, 4)])
+def test_up_conv_act_fused_matches_two_kernel_path(B, Ci, Co, n):
+    """The fused scatter + FIR + epilogue kernel (2n % 64 == 0) matches up_conv then fir_up_act
+    (the same operations; the compiler's FMA contraction may differ by an ulp), and so do the
+    gradients (same backward kernels); n = 4 takes the unfused path."""
+    x = _rand(B, Ci, n, n, seed=23).requires_grad_()
+    w = _rand(Co, Ci, 3, 3, seed=24) / (3 * Ci ** 0.5)
+    d = (_rand(B, Co, seed=25).abs() + 0.1).requires_grad_()
+    bias = 0.3 * _rand(Co, seed=26)
+    g = _rand(B, Co, 2 * n, 2 * n, seed=27)
+    y = producer_ops.up_conv_act(x, w, d, bias, GAIN)
+    y.backward(g)
+    x2, d2 = x.detach().clone().requires_grad_(), d.detach().clone().requires_grad_()
+    y2 = producer_ops.fir_up_act(producer_ops.up_conv(x2, w), d2, bias, GAIN)
+    y2.backward(g)
+    _close(y.detach(), y2.detach(), rel=1e-7)
+    _close(x.grad, x2.grad, rel=1e-7)
+    _close(d.grad, d2.grad, rel=1e-7)
+
+
 @pytest.mark.parametrize('B,C,O,H', [(1, 8, 3, 2), (2, 32, 96, 4), (3, 512, 96, 16), (2, 128, 96, 128)])
 def test_modulated_conv1x1(B, C, O, H):
     """bmm(W * s_b, x) == conv2d(x * s, W) for the 1x1 to-planes layers; d x and d s (fp64
