@@ -490,15 +490,13 @@ __global__ void __launch_bounds__(256) lpips_bwd_kernel(const float* __restrict_
   }
 }
 
-// One-read forms for C = 16 * CPW channels: a workgroup of 16 waves takes 64 pixels, wave j
+// One-read forms for C = WAVES * CPW channels: a workgroup of WAVES waves takes 64 pixels, wave j
 // holds channels [j*CPW, (j+1)*CPW) of its lane's pixel in registers; the per-pixel channel sums
 // (||f0||^2, ||f1||^2, then the weighted squared difference / the backward's two dot products)
 // are wave partials combined through LDS in a fixed order.  f0 and f1 are read from HBM once
 // (the loops above read them twice, and the second pass misses the caches at these sizes).
-constexpr int LP_WAVES = 16;
-
-template <int CPW>
-__global__ void __launch_bounds__(1024) lpips_fwd_regs_kernel(const float* __restrict__ f0,
+template <int LP_WAVES, int CPW>
+__global__ void __launch_bounds__(64 * LP_WAVES) lpips_fwd_regs_kernel(const float* __restrict__ f0,
                                                               const float* __restrict__ f1,
                                                               const float* __restrict__ w,
                                                               float* __restrict__ out,
@@ -560,8 +558,8 @@ __global__ void __launch_bounds__(1024) lpips_fwd_regs_kernel(const float* __res
   }
 }
 
-template <int CPW>
-__global__ void __launch_bounds__(1024) lpips_bwd_regs_kernel(const float* __restrict__ g,
+template <int LP_WAVES, int CPW>
+__global__ void __launch_bounds__(64 * LP_WAVES) lpips_bwd_regs_kernel(const float* __restrict__ g,
                                                               const float* __restrict__ f0,
                                                               const float* __restrict__ f1,
                                                               const float* __restrict__ w,
@@ -727,8 +725,9 @@ struct Samp {
 };
 __device__ __forceinline__ Samp samp_at(const float* __restrict__ g, int W, int H) {
   Samp s;
-  s.ix = ((g[0] + 1.f) * (float)W - 1.f) / 2.f;
-  s.iy = ((g[1] + 1.f) * (float)H - 1.f) / 2.f;
+  const float2 gv = *reinterpret_cast<const float2*>(g);
+  s.ix = ((gv.x + 1.f) * (float)W - 1.f) / 2.f;
+  s.iy = ((gv.y + 1.f) * (float)H - 1.f) / 2.f;
   s.x0 = (int)floorf(s.ix);
   s.y0 = (int)floorf(s.iy);
   return s;
@@ -766,36 +765,43 @@ __global__ void __launch_bounds__(256) aug_fwd_kernel(const float* __restrict__ 
   for (int c = 0; c < 3; ++c) op[c * HWo] = acc[c] + shift;
 }
 
-// Adjoint, gathered (no atomics): one thread per input pixel (b, Y, X); for each copy the output
-// pixels whose sample has (Y, X) as a corner lie in the preimage of the 2x2 box around (Y, X)
-// under the copy's affine map (read off the grid itself: its value at (0,0), (0,1), (1,0)),
-// enumerated over that preimage's bounding box + 1 and tested with the forward's exact arithmetic.
+// Adjoint, gathered (no atomics): 16 lanes per input pixel (b, Y, X), lane k taking copies k,
+// k + 16, ...; for each copy the output pixels whose sample has (Y, X) as a corner lie in the
+// preimage of the 2x2 box around (Y, X) under the copy's affine map (read off the grid itself:
+// its value at (0,0), (0,1), (1,0)), enumerated over that preimage's bounding box + 1 and tested
+// with the forward's exact arithmetic; the 16 lanes' sums are combined by shuffles.
 __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ grid,
                                                       float* __restrict__ gimg, int64_t total, int K, int H, int W,
                                                       int Ho, int Wo) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // input pixel
+  const int kl = threadIdx.x & 15;
+  const bool live = i < total;
+  const int64_t ic = live ? i : total - 1;
   const int64_t HW = (int64_t)H * W, HWo = (int64_t)Ho * Wo;
-  const int b = (int)(i / HW);
-  const int pix = (int)(i - (int64_t)b * HW);
+  const int b = (int)(ic / HW);
+  const int pix = (int)(ic - (int64_t)b * HW);
   const int Y = pix / W, X = pix - Y * W;
   float acc[3] = {0.f, 0.f, 0.f};
-  for (int k = 0; k < K; ++k) {
+  for (int k = kl; k < K; k += 16) {
     const int64_t j = (int64_t)b * K + k;
     const float* gj = grid + j * HWo * 2;
-    // source position as an affine function of the output pixel: s(x, y) = s00 + x dx + y dy
-    const Samp s00 = samp_at(gj, W, H), s01 = samp_at(gj + 2 * min(1, Wo - 1), W, H),
-               s10 = samp_at(gj + 2 * (int64_t)min(1, Ho - 1) * Wo, W, H);
-    const float ax = Wo > 1 ? s01.ix - s00.ix : 1.f, bx = Ho > 1 ? s10.ix - s00.ix : 0.f;
-    const float ay = Wo > 1 ? s01.iy - s00.iy : 0.f, by = Ho > 1 ? s10.iy - s00.iy : 1.f;
+    // source position as an affine function of the output pixel, s(x, y) = s00 + x dx + y dy,
+    // its slopes read across the whole grid (the grid's rounding ~1e-6 px then moves them by
+    // ~1e-8 per pixel)
+    const Samp s00 = samp_at(gj, W, H), s01 = samp_at(gj + 2 * (Wo - 1), W, H),
+               s10 = samp_at(gj + 2 * (int64_t)(Ho - 1) * Wo, W, H);
+    const float ax = Wo > 1 ? (s01.ix - s00.ix) / (float)(Wo - 1) : 1.f;
+    const float ay = Wo > 1 ? (s01.iy - s00.iy) / (float)(Wo - 1) : 0.f;
+    const float bx = Ho > 1 ? (s10.ix - s00.ix) / (float)(Ho - 1) : 0.f;
+    const float by = Ho > 1 ? (s10.iy - s00.iy) / (float)(Ho - 1) : 1.f;
     const float det = ax * by - bx * ay;
     if (!(fabsf(det) > 1e-12f)) continue;        // degenerate map (never drawn: scale > 0)
     const float i00 = by / det, i01 = -bx / det, i10 = -ay / det, i11 = ax / det;
     // the samples with corner (X, Y) have ix in [X-1, X+1), iy in [Y-1, Y+1): the preimage of
-    // that box is centred on the preimage of (X, Y), half extent |inverse| (1, 1) (+1 margin)
+    // that box is centred on the preimage of (X, Y), half extent |inverse| (1, 1) (+0.05 px)
     const float px = (float)X - s00.ix, py = (float)Y - s00.iy;
     const float cx = i00 * px + i01 * py, cy = i10 * px + i11 * py;
-    const float ex = fabsf(i00) + fabsf(i01) + 1.f, ey = fabsf(i10) + fabsf(i11) + 1.f;
+    const float ex = fabsf(i00) + fabsf(i01) + 0.05f, ey = fabsf(i10) + fabsf(i11) + 0.05f;
     const int xlo = max((int)floorf(cx - ex), 0), xhi = min((int)ceilf(cx + ex), Wo - 1);
     const int ylo = max((int)floorf(cy - ey), 0), yhi = min((int)ceilf(cy + ey), Ho - 1);
     const float* go = gout + j * 3 * HWo;
@@ -815,10 +821,13 @@ __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ 
       }
     }
   }
-  float* gp = gimg + i * 3;
-  gp[0] = acc[0];
-  gp[1] = acc[1];
-  gp[2] = acc[2];
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) {
+    acc[0] += __shfl_xor(acc[0], m, 64);
+    acc[1] += __shfl_xor(acc[1], m, 64);
+    acc[2] += __shfl_xor(acc[2], m, 64);
+  }
+  if (live && kl < 3) gimg[i * 3 + kl] = kl == 0 ? acc[0] : (kl == 1 ? acc[1] : acc[2]);
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -954,10 +963,10 @@ int32_t nfi_lpips_head_forward(const float* f0, const float* f1, const float* w,
   }
   const unsigned pb = (unsigned)(((int64_t)N * HW + 63) / 64);
   switch (C) {
-    case 64: lpips_fwd_regs_kernel<4><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
-    case 128: lpips_fwd_regs_kernel<8><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
-    case 256: lpips_fwd_regs_kernel<16><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
-    case 512: lpips_fwd_regs_kernel<32><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 64: lpips_fwd_regs_kernel<4, 16><<<pb, 256, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 128: lpips_fwd_regs_kernel<8, 16><<<pb, 512, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 256: lpips_fwd_regs_kernel<16, 16><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
+    case 512: lpips_fwd_regs_kernel<16, 32><<<pb, 1024, 0, st>>>(f0, f1, w, out, inv0, inv1, N, HW); break;
     default: lpips_fwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(f0, f1, w, out, inv0, inv1, N, C, HW);
   }
   NFI_CHECK_LAUNCH("lpips_fwd_kernel");
@@ -972,10 +981,10 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
   hipStream_t st = (hipStream_t)stream;
   const unsigned pb = (unsigned)(((int64_t)N * HW + 63) / 64);
   switch (C) {
-    case 64: lpips_bwd_regs_kernel<4><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
-    case 128: lpips_bwd_regs_kernel<8><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
-    case 256: lpips_bwd_regs_kernel<16><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
-    case 512: lpips_bwd_regs_kernel<32><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 64: lpips_bwd_regs_kernel<4, 16><<<pb, 256, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 128: lpips_bwd_regs_kernel<8, 16><<<pb, 512, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 256: lpips_bwd_regs_kernel<16, 16><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
+    case 512: lpips_bwd_regs_kernel<16, 32><<<pb, 1024, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, HW); break;
     default: lpips_bwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, C, HW);
   }
   NFI_CHECK_LAUNCH("lpips_bwd_kernel");
@@ -1034,7 +1043,7 @@ int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gim
   NFI_REQUIRE(gout && grid && gimg, "aug_sample_backward: null pointer");
   NFI_REQUIRE(B > 0 && K > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, "aug_sample_backward: bad shape");
   const int64_t total = (int64_t)B * H * W;
-  aug_bwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(gout, grid, gimg, total, K, H, W, Ho, Wo);
+  aug_bwd_kernel<<<blocks(total * 16), 256, 0, (hipStream_t)stream>>>(gout, grid, gimg, total, K, H, W, Ho, Wo);
   NFI_CHECK_LAUNCH("aug_bwd_kernel");
   return NFI_OK;
 }
