@@ -64,6 +64,13 @@ int32_t nfi_syn_up_conv_scatter(const float* P, float* t, int32_t B, int32_t C, 
 int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const float* bias, float* o, float* y,
                                         int32_t B, int32_t C, int32_t n, float gain, void* stream);
 
+/* The backward of nfi_syn_up_conv_fir_act_forward's FIR + epilogue and of the scatter in one pass
+ * (n % 32 == 0): g = d y [B][C][2n][2n], o (saved) -> dP [B][9][C][n][n] (the operand of the data
+ * gradient W9^T dP) and dd[p] = sum gz o (overwritten) — nfi_syn_act_backward, then
+ * nfi_syn_fir_up_backward, then nfi_syn_up_conv_gather, without go and gt in memory. */
+int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
+                                     float* dd, int32_t B, int32_t C, int32_t n, float gain, void* stream);
+
 /* Its adjoint: gt [B][C][2n+1][2n+1] -> dP [B][9][C][n][n], dP[3ky+kx][c][iy][ix] =
  * gt[c][2iy+ky][2ix+kx]; the data gradient of the transposed convolution is then W9^T dP. */
 int32_t nfi_syn_up_conv_gather(const float* gt, float* dP, int32_t B, int32_t C, int32_t n, void* stream);

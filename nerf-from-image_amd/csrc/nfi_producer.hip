@@ -218,12 +218,22 @@ __global__ void __launch_bounds__(256) up_fir_act_kernel(const float* __restrict
   const int64_t nn = (int64_t)n * n, tap = (int64_t)C * nn;
   const float* Pc = P + ((int64_t)b * 9 * C + c) * nn;
   const int iy0 = Y0 / 2 - 2, ix0 = X0 / 2 - 2;
-  for (int k = threadIdx.x; k < 9 * UF_PY * UF_PX; k += 256) {
+  // all 14 loads of a thread in flight together (clamped element index, masked stores)
+  constexpr int PN = 9 * UF_PY * UF_PX, PIT = (PN + 255) / 256;
+  float pv[PIT];
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int k = min(it * 256 + (int)threadIdx.x, PN - 1);
     const int tp = k / (UF_PY * UF_PX), r = (k / UF_PX) % UF_PY, q = k % UF_PX;
     const int iy = iy0 + r, ix = ix0 + q;
     const bool in = iy >= 0 && iy < n && ix >= 0 && ix < n;
     const float v = Pc[tp * tap + (int64_t)min(max(iy, 0), n - 1) * n + min(max(ix, 0), n - 1)];
-    Ps[tp][r][q] = in ? v : 0.f;
+    pv[it] = in ? v : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int k = it * 256 + threadIdx.x;
+    if (k < PN) (&Ps[0][0][0])[k] = pv[it];
   }
   __syncthreads();
   for (int k = threadIdx.x; k < UF_RY * UF_RX; k += 256) {
@@ -259,6 +269,82 @@ __global__ void __launch_bounds__(256) up_fir_act_kernel(const float* __restrict
   o[i] = ov;
   y[i] = make_float4(act(ov.x, dp, bb, gain), act(ov.y, dp, bb, gain), act(ov.z, dp, bb, gain),
                      act(ov.w, dp, bb, gain));
+}
+
+// The backward of the up-sampling layer tail in one pass, for n % 32 == 0: the epilogue's backward
+// (act_bwd_kernel: gz = g gain slope(o), go = gz d[p], dd[p] += sum gz o), the FIR adjoint
+// (fir_up_bwd_kernel) and the tap gather (tap_gather_kernel) — one workgroup per 8 x 32 block of
+// dP's (iy, ix) for all 9 taps of one plane: go (20 x 68, masked to 0 outside the plane) and gt
+// (17 x 65) are formed in LDS with those kernels' arithmetic; go and gt never reach HBM.  dd is
+// summed over each tile's own 16 x 64 block of the plane (one atomic per workgroup; zeroed by the
+// caller).
+constexpr int UB_TY = 8, UB_TX = 32;                                   // dP block (iy, ix)
+constexpr int UB_GY = 2 * UB_TY + 4, UB_GX = 2 * UB_TX + 4;            // 20 x 68 go values
+constexpr int UB_RY = 2 * UB_TY + 1, UB_RX = 2 * UB_TX + 1;            // 17 x 65 gt values
+__global__ void __launch_bounds__(256) up_bwd_fused_kernel(const float* __restrict__ g, const float* __restrict__ o,
+                                                           const float* __restrict__ d, const float* __restrict__ bias,
+                                                           float* __restrict__ dP, float* __restrict__ dd, int C,
+                                                           int n, float gain) {
+  __shared__ float Gs[UB_GY][UB_GX + 1];
+  __shared__ float Rs[UB_RY][UB_RX + 1];
+  __shared__ float part[4];
+  const int W2 = 2 * n;
+  const int tiles_x = n / UB_TX;
+  const int tile = blockIdx.x, p = blockIdx.y;
+  const int iy0 = (tile / tiles_x) * UB_TY, ix0 = (tile % tiles_x) * UB_TX;
+  const int b = p / C, c = p - b * C;
+  const float dp = d[p], bb = bias[c];
+  const int64_t plane = (int64_t)p * W2 * W2;
+  const int R0 = 2 * iy0 - 2, C0 = 2 * ix0 - 2;                        // go tile origin
+  constexpr int GN = UB_GY * UB_GX, GIT = (GN + 255) / 256;
+  float gv[GIT], ov[GIT];
+#pragma unroll
+  for (int it = 0; it < GIT; ++it) {
+    const int k = min(it * 256 + (int)threadIdx.x, GN - 1);
+    const int r = k / UB_GX, q = k - r * UB_GX;
+    const int64_t a = plane + (int64_t)min(max(R0 + r, 0), W2 - 1) * W2 + min(max(C0 + q, 0), W2 - 1);
+    gv[it] = g[a];
+    ov[it] = o[a];
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int it = 0; it < GIT; ++it) {
+    const int k = it * 256 + threadIdx.x;
+    const int r = k / UB_GX, q = k - r * UB_GX;
+    const int Y = R0 + r, X = C0 + q;
+    const bool in = k < GN && Y >= 0 && Y < W2 && X >= 0 && X < W2;
+    const float gz = gv[it] * gain * act_slope(ov[it], dp, bb);
+    const bool own = in && r >= 2 && r < 2 + 2 * UB_TY && q >= 2 && q < 2 + 2 * UB_TX;
+    acc += own ? gz * ov[it] : 0.f;
+    if (k < GN) Gs[r][q] = in ? gz * dp : 0.f;
+  }
+  __syncthreads();
+  // gt rows 2 iy0 .. 2 iy0 + 16, cols 2 ix0 .. 2 ix0 + 64 (fir_up_bwd_kernel's sums)
+  for (int k = threadIdx.x; k < UB_RY * UB_RX; k += 256) {
+    const int rr = k / UB_RX, cc = k - rr * UB_RX;
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float h = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h += k4(q) * Gs[rr + 3 - a][cc + 3 - q];
+      s += k4(a) * h;
+    }
+    Rs[rr][cc] = s * (1.f / 16.f);
+  }
+  // dd: block sum of the owned gz * o
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(dd + p, (part[0] + part[1]) + (part[2] + part[3]));
+  // dP[tap][iy][ix] = gt[2 iy + ky][2 ix + kx]
+  const int lx = threadIdx.x % UB_TX, ly = threadIdx.x / UB_TX;
+  const int64_t nn = (int64_t)n * n;
+  float* out = dP + ((int64_t)b * 9 * C + c) * nn + (int64_t)(iy0 + ly) * n + ix0 + lx;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) out[(ky * 3 + kx) * C * nn] = Rs[2 * ly + ky][2 * lx + kx];
 }
 
 // Its adjoint's operand (the data gradient of the transposed convolution is W9^T dP): gt
@@ -896,6 +982,21 @@ int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const fl
   up_fir_act_kernel<<<dim3((unsigned)((W2 / UF_TY) * (W2 / UF_TX)), (unsigned)(B * C)), 256, 0,
                       (hipStream_t)stream>>>(P, d, bias, (float4*)o, (float4*)y, C, n, gain);
   NFI_CHECK_LAUNCH("up_fir_act_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
+                                     float* dd, int32_t B, int32_t C, int32_t n, float gain, void* stream) {
+  NFI_REQUIRE(g && o && d && bias && dP && dd, "syn_up_conv_act_backward: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && n > 0 && n % UB_TX == 0, "syn_up_conv_act_backward: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(dd, 0, sizeof(float) * B * C, st) != hipSuccess) {
+    nfi::set_error("syn_up_conv_act_backward: memset failed");
+    return NFI_ELAUNCH;
+  }
+  up_bwd_fused_kernel<<<dim3((unsigned)((n / UB_TY) * (n / UB_TX)), (unsigned)(B * C)), 256, 0, st>>>(
+      g, o, d, bias, dP, dd, C, n, gain);
+  NFI_CHECK_LAUNCH("up_bwd_fused_kernel");
   return NFI_OK;
 }
 

@@ -6,7 +6,12 @@ the inversion (run.py:630-632), so biases never receive gradients (asking for on
   act        lrelu(gain*(o*d[b,c] + bias[c]))   stylegan.py:145, 348-356 (demodulation epilogue)
   fir_up_act FIR(t) then act                    stylegan.py:99-103 + the epilogue (up layers)
   up_add     upsample2d(img) + c + bias[c]      stylegan.py:69-73, 380-381, 428-433 (skip image)
+  up_conv    conv_transpose2d(x, w^T, stride 2)  stylegan.py:99-101: one GEMM over the 9 taps + scatter
+  up_conv_act  fir_up_act(up_conv(x, w))         the up layer tail fused (2n >= 64), fused backward
+  modulated_conv1x1  conv2d(x * s, w 1x1)        stylegan.py:363-384 (to-planes) as one batched GEMM
   vgg_epilogue relu(x + bias[c]) (+ 2x2 max pool) LPIPS VGG16 trunk (lpips 0.1 via metrics.py:107)
+  lpips_head   the LPIPS distance of one layer    metrics.py:130-146
+  aug_sample   the 'vgg' loss's 15 augmented copies (run.py:720-767), gathered adjoint
 """
 
 from __future__ import annotations
@@ -191,14 +196,18 @@ class _UpConvAct(torch.autograd.Function):
         B, Ci, Co, n = ctx.shape
         g = g.contiguous()
         dev = _stream(o.device)
-        go = torch.empty_like(o)
         dd = torch.empty_like(d)
-        _call('nfi_syn_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(go), _p(dd), B * Co, Co,
-              4 * n * n, ctypes.c_float(ctx.gain), dev)
-        gt = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
-        _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * Co, n, dev)
         dP = torch.empty((B, 9 * Co, n * n), device=o.device, dtype=o.dtype)
-        _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, dev)
+        if n % 32 == 0:       # epilogue backward + FIR adjoint + tap gather in one pass
+            _call('nfi_syn_up_conv_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(dP), _p(dd), B, Co, n,
+                  ctypes.c_float(ctx.gain), dev)
+        else:
+            go = torch.empty_like(o)
+            _call('nfi_syn_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(go), _p(dd), B * Co, Co,
+                  4 * n * n, ctypes.c_float(ctx.gain), dev)
+            gt = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
+            _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * Co, n, dev)
+            _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, dev)
         gx = torch.matmul(W9t, dP).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
         return gx, None, None, dd, None, None
 
