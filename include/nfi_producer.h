@@ -84,6 +84,21 @@ int32_t nfi_syn_up_add_forward(const float* img, const float* c, const float* bi
  * pad 1; stylegan.py:79-83). */
 int32_t nfi_syn_up_backward(const float* g, float* gimg, int32_t P, int32_t n, void* stream);
 
+/* The skip path with channel-contiguous layouts: each tensor [B][C][h][w] is addressed by float
+ * strides {b, q, t}: element (b, c, y, x) at b*sb + (c/32)*sq + (y*w + x)*st + c%32 — channels-last
+ * [B][h][w][C] has sq = 32, st = C; the renderer's texel-major planes [B][C/32][h][w][32] have
+ * sq = h*w*32, st = 32.  img (NULL: none) [B][C][n][n], c and out [B][C][2n][2n]; the same sums
+ * as nfi_syn_up_add_forward.  The synthesis network's skip image runs channels-last and its last
+ * image is written texel-major: the renderer reads it with no conversion pass.  C % 4 == 0, all
+ * strides multiples of 4. */
+int32_t nfi_syn_up_add_forward_strided(const float* img, const int64_t* img_strides, const float* c,
+                                       const int64_t* c_strides, const float* bias, float* out,
+                                       const int64_t* out_strides, int32_t B, int32_t C, int32_t n, void* stream);
+
+/* Adjoint of upsample2d with the same strided layouts: g [B][C][2n][2n] -> gimg [B][C][n][n]. */
+int32_t nfi_syn_up_backward_strided(const float* g, const int64_t* g_strides, float* gimg, const int64_t* gimg_strides,
+                                    int32_t B, int32_t C, int32_t n, void* stream);
+
 /* Backward of x * s[p] (stylegan.py:130 modulation): gx = g * s[p] (gx may be NULL),
  * ds[p] = sum_hw g * x (overwritten).  HW % 4 == 0. */
 int32_t nfi_syn_scale_backward(const float* g, const float* x, const float* s, float* gx,

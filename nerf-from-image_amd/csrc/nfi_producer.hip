@@ -458,6 +458,110 @@ __global__ void __launch_bounds__(256) up_add_kernel(const float* __restrict__ i
                        acc[2] * inv + (cv.z + b), acc[3] * inv + (cv.w + b));
 }
 
+// The same with channel-contiguous layouts (each tensor addressed by float4 strides: element
+// (b, c, y, x) at b*sb + (c/32)*sq + (y*w + x)*st + c%32 floats, sq = 32 and st = C for
+// channels-last [B][h][w][C], sq = h*w*32 and st = 32 for the renderer's texel-major planes
+// [B][C/32][h][w][32]): the skip-image chain runs channels-last and its last image is written
+// texel-major, the renderer's layout, with no conversion pass.  One thread per output pixel and
+// 4 channels, up_add_kernel's arithmetic (C % 4 == 0).
+struct Str4 {
+  long long b, q, t;   // float4 units
+};
+__device__ __forceinline__ long long str4_at(const Str4& s, int b, int c4, long long pix) {
+  return b * s.b + (c4 >> 3) * s.q + pix * s.t + (c4 & 7);
+}
+__global__ void __launch_bounds__(256) up_add_str_kernel(const float4* __restrict__ img, Str4 si,
+                                                         const float4* __restrict__ cc, Str4 sc,
+                                                         const float4* __restrict__ bias,
+                                                         float4* __restrict__ out, Str4 so, int64_t total4, int C4,
+                                                         int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int W2 = 2 * n;
+  const int64_t pix = i / C4;
+  const int c4 = (int)(i - pix * C4);
+  const int64_t per = (int64_t)W2 * W2;
+  const int b = (int)(pix / per);
+  const int rem = (int)(pix - (int64_t)b * per);
+  const int Y = rem / W2, X = rem - Y * W2;
+  const float4 bv = bias[c4];
+  const float4 cv = cc[str4_at(sc, b, c4, rem)];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (img) {
+    const int q = Y >> 1;
+    const int r0 = (Y & 1) ? q : q - 1;
+    const float w0 = (Y & 1) ? 3.f : 1.f, w1 = (Y & 1) ? 1.f : 3.f;
+    const int mm = X >> 1;
+    const int ca = (X & 1) ? mm : mm - 1;                 // columns ca, ca + 1
+    float4 v[2][2];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = r0 + rr, col = ca + j;
+        const float4 t = img[str4_at(si, b, c4, (long long)min(max(row, 0), n - 1) * n + min(max(col, 0), n - 1))];
+        const bool ok = row >= 0 && row < n && col >= 0 && col < n;
+        v[rr][j] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const float wr = rr == 0 ? w0 : w1;
+      // up_add_kernel: even X: (v[m-1] + 3 v[m]), odd X: (3 v[m] + v[m+1])
+#define NFI_UPC(F) acc.F += wr * ((X & 1) ? (3.f * v[rr][0].F + v[rr][1].F) : (v[rr][0].F + 3.f * v[rr][1].F));
+      NFI_UPC(x) NFI_UPC(y) NFI_UPC(z) NFI_UPC(w)
+#undef NFI_UPC
+    }
+  }
+  const float inv = 1.f / 16.f;
+  out[str4_at(so, b, c4, rem)] = make_float4(acc.x * inv + (cv.x + bv.x), acc.y * inv + (cv.y + bv.y),
+                                             acc.z * inv + (cv.z + bv.z), acc.w * inv + (cv.w + bv.w));
+}
+
+// up_bwd_kernel with the same strided layouts: g [B][C][2n][2n] -> gimg [B][C][n][n], 4 channels a thread
+__global__ void __launch_bounds__(256) up_bwd_str_kernel(const float4* __restrict__ g, Str4 sg,
+                                                         float4* __restrict__ gimg, Str4 sr, int64_t total4, int C4,
+                                                         int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int W2 = 2 * n;
+  const int64_t pix = i / C4;
+  const int c4 = (int)(i - pix * C4);
+  const int64_t nn = (int64_t)n * n;
+  const int b = (int)(pix / nn);
+  const int rem = (int)(pix - (int64_t)b * nn);
+  const int q = rem / n, m = rem - q * n;
+  float4 gv[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = min(max(2 * q - 1 + a, 0), W2 - 1);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+      gv[a][bb] = g[str4_at(sg, b, c4, (long long)row * W2 + min(max(2 * m - 1 + bb, 0), W2 - 1))];
+  }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int row = 2 * q - 1 + a;
+    float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int col = 2 * m - 1 + bb;
+      const bool ok = col >= 0 && col < W2;
+      h.x += k4(bb) * (ok ? gv[a][bb].x : 0.f);
+      h.y += k4(bb) * (ok ? gv[a][bb].y : 0.f);
+      h.z += k4(bb) * (ok ? gv[a][bb].z : 0.f);
+      h.w += k4(bb) * (ok ? gv[a][bb].w : 0.f);
+    }
+    const bool rok = row >= 0 && row < W2;
+    acc.x += rok ? k4(a) * h.x : 0.f;
+    acc.y += rok ? k4(a) * h.y : 0.f;
+    acc.z += rok ? k4(a) * h.z : 0.f;
+    acc.w += rok ? k4(a) * h.w : 0.f;
+  }
+  const float inv = 1.f / 16.f;
+  gimg[str4_at(sr, b, c4, rem)] = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+}
+
 // gimg[q][m] = sum over rows {2q-1:1, 2q:3, 2q+1:3, 2q+2:1} x cols (same) / 16
 __global__ void __launch_bounds__(256) up_bwd_kernel(const float* __restrict__ g,
                                                      float* __restrict__ gimg, int64_t total,
@@ -1025,6 +1129,43 @@ int32_t nfi_syn_up_add_forward(const float* img, const float* c, const float* bi
   up_add_kernel<<<blocks(n4), 256, 0, (hipStream_t)stream>>>(img, (const float4*)c, bias,
                                                               (float4*)out, n4, C, n);
   NFI_CHECK_LAUNCH("up_add_kernel");
+  return NFI_OK;
+}
+
+static int str4_of(const int64_t* s, Str4& o) {
+  // float strides (b, q, t) -> float4 units; every one a multiple of 4 floats
+  if (s[0] % 4 || s[1] % 4 || s[2] % 4) return 0;
+  o = Str4{s[0] / 4, s[1] / 4, s[2] / 4};
+  return 1;
+}
+
+int32_t nfi_syn_up_add_forward_strided(const float* img, const int64_t* img_strides, const float* c,
+                                       const int64_t* c_strides, const float* bias, float* out,
+                                       const int64_t* out_strides, int32_t B, int32_t C, int32_t n, void* stream) {
+  NFI_REQUIRE(c && bias && out && c_strides && out_strides && (!img || img_strides),
+              "syn_up_add_forward_strided: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && C % 4 == 0 && n >= 1, "syn_up_add_forward_strided: bad shape");
+  Str4 si{0, 0, 0}, sc, so;
+  NFI_REQUIRE((!img || str4_of(img_strides, si)) && str4_of(c_strides, sc) && str4_of(out_strides, so),
+              "syn_up_add_forward_strided: strides must be multiples of 4 floats");
+  const int64_t total4 = (int64_t)B * (2 * n) * (2 * n) * (C / 4);
+  up_add_str_kernel<<<blocks(total4), 256, 0, (hipStream_t)stream>>>(
+      (const float4*)img, si, (const float4*)c, sc, (const float4*)bias, (float4*)out, so, total4, C / 4, n);
+  NFI_CHECK_LAUNCH("up_add_str_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_up_backward_strided(const float* g, const int64_t* g_strides, float* gimg, const int64_t* gimg_strides,
+                                    int32_t B, int32_t C, int32_t n, void* stream) {
+  NFI_REQUIRE(g && gimg && g_strides && gimg_strides && B > 0 && C > 0 && C % 4 == 0 && n >= 1,
+              "syn_up_backward_strided: bad args");
+  Str4 sg, sr;
+  NFI_REQUIRE(str4_of(g_strides, sg) && str4_of(gimg_strides, sr),
+              "syn_up_backward_strided: strides must be multiples of 4 floats");
+  const int64_t total4 = (int64_t)B * n * n * (C / 4);
+  up_bwd_str_kernel<<<blocks(total4), 256, 0, (hipStream_t)stream>>>((const float4*)g, sg, (float4*)gimg, sr,
+                                                                    total4, C / 4, n);
+  NFI_CHECK_LAUNCH("up_bwd_str_kernel");
   return NFI_OK;
 }
 

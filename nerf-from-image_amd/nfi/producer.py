@@ -165,11 +165,14 @@ class ToPlanes(nn.Module):
         self.weight_gain = 1.0 / math.sqrt(in_ch)
 
     backend = 'hip'
+    out_layout = 'nhwc'     # 'hip' backend: the last resolution's layer is set to 'planes'
 
     def forward(self, x, w, pre=None):
         styles = self.affine(w) * self.weight_gain if pre is None else pre
         if self.backend == 'hip':
-            return _hip().modulated_conv1x1(x, styles, self.weight)       # bias added in up_add
+            # channels-last (the skip-image chain's layout: its last image is the renderer's
+            # texel-major planes, no conversion pass); bias added in up_add
+            return _hip().modulated_conv1x1(x, styles, self.weight, layout=self.out_layout)
         x = F.conv2d(x * styles[:, :, None, None], self.weight)
         return x + self.bias[None, :, None, None]
 
@@ -224,6 +227,9 @@ class SynthesisNetwork(nn.Module):
             setattr(self, f'b{r}', blk)
             self.num_ws += blk.num_conv
         self.num_ws += 1   # the last block's toRGB
+        # the last image is the tri-planes: written texel-major ([b, 3, 32, R, R] in the renderer's
+        # [b, 3, R, R, 32] storage, 'hip' backend), so render() reads it with no conversion pass
+        getattr(self, f'b{self.resolutions[-1]}').torgb.out_layout = 'planes'
 
     def forward(self, ws, noise_mode: str = 'const'):
         # ws [b, num_ws, w_dim] or its rows (a sequence of [b, w_dim]); the rows are split once
@@ -429,6 +435,7 @@ class InversionGenerator(nn.Module):
         return self
 
     def planes_and_palette(self, ws):
-        palette = self.texture_mapper(ws[:, 14])
-        planes = self.synthesis_network(ws[:, :14])
+        w_syn, w_tex = ws.split([14, ws.shape[1] - 14], dim=1)    # one split (its backward is one cat)
+        palette = self.texture_mapper(w_tex[:, 0])
+        planes = self.synthesis_network(w_syn)
         return planes.view(ws.shape[0], 3, 32, planes.shape[-2], planes.shape[-1]), palette

@@ -227,12 +227,18 @@ def up_conv_act(x, w, d, bias, gain: float):
 
 class _ModConv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, s, Wf, Wt):
+    def forward(ctx, x, s, Wf, Wt, layout: str):
         x = x.contiguous()
         s = s.contiguous()
         B, C, H, W = x.shape
         O = Wf.shape[0]
-        y = torch.bmm(Wf[None] * s[:, None, :], x.view(B, C, H * W)).view(B, O, H, W)
+        Wm = Wf[None] * s[:, None, :]                                       # [B, O, C]
+        if layout != 'nchw':  # y^T = x^T Wm^T: [B, HW, O], i.e. [B, O, H, W] in channels-last strides
+            y = torch.bmm(x.view(B, C, H * W).transpose(1, 2), Wm.transpose(1, 2))
+            y = (y.view(B, H, W, O).permute(0, 3, 1, 2) if layout == 'nhwc'
+                 else y.view(B, H, W, O // 32, 32).permute(0, 3, 4, 1, 2))      # 'planes': [B, O/32, 32, H, W]
+        else:
+            y = torch.bmm(Wm, x.view(B, C, H * W)).view(B, O, H, W)
         ctx.save_for_backward(x, s, Wt)
         return y
 
@@ -240,20 +246,32 @@ class _ModConv1x1(torch.autograd.Function):
     def backward(ctx, gy):
         x, s, Wt = ctx.saved_tensors
         B, C, H, W = x.shape
-        gxs = torch.matmul(Wt, gy.reshape(B, -1, H * W))                  # d(x * s) [B, C, HW]
+        if gy.dim() == 5:     # texel-major planes [B, Q, 32, H, W]: one product per plane, accumulated
+            gxs = None
+            for q in range(gy.shape[1]):
+                gq = gy[:, q].reshape(B, 32, H * W)
+                Wq = Wt[:, 32 * q:32 * (q + 1)]
+                gxs = torch.matmul(Wq, gq) if gxs is None else gxs.baddbmm_(Wq.expand(B, -1, -1), gq)
+        elif gy.is_contiguous():
+            gxs = torch.matmul(Wt, gy.view(B, -1, H * W))
+        else:                 # channels-last: [B, HW, O] seen as [B, O, HW] (a transposed operand, no copy)
+            gxs = torch.matmul(Wt, gy.permute(0, 2, 3, 1).reshape(B, H * W, -1).transpose(1, 2))
+        # gxs = d(x * s) [B, C, HW]
         gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
         _call('nfi_syn_scale_backward', _p(gxs), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W,
               _stream(x.device))
-        return gx, ds, None, None
+        return gx, ds, None, None, None
 
 
-def modulated_conv1x1(x, s, weight):
+def modulated_conv1x1(x, s, weight, layout: str = 'nchw'):
     """F.conv2d(x * s[:, :, None, None], weight) for a frozen 1x1 weight [O, C, 1, 1] (the toRGB /
     to-planes layers, stylegan.py:363-384): the modulation goes into a per-image weight (W * s_b,
     [B, O, C]: O = 96 rows, far smaller than x) and the layer is one batched GEMM; the backward is
-    W^T dy (one GEMM) and nfi_syn_scale_backward (d x = s * that, d s = sum x * that).  A weight that
-    takes gradients goes to MIOpen."""
+    W^T dy (one GEMM) and nfi_syn_scale_backward (d x = s * that, d s = sum x * that).
+    layout 'nhwc' returns [B, O, H, W] in channels-last strides (the skip-image chain's layout);
+    'planes' returns it as [B, O/32, 32, H, W] (the last layer's: up_add then writes the renderer's
+    texel-major planes).  A weight that takes gradients goes to MIOpen."""
     _require_device(x, s, weight)
     if torch.is_grad_enabled() and weight.requires_grad:
         return F.conv2d(x * s[:, :, None, None], weight)
@@ -264,7 +282,9 @@ def modulated_conv1x1(x, s, weight):
             Wf = weight.detach().reshape(weight.shape[0], -1).contiguous()
             hit = (key, (Wf, Wf.t().contiguous()))
         weight._nfi_1x1 = hit
-    return _ModConv1x1.apply(x, s, *hit[1])
+    if layout not in ('nchw', 'nhwc', 'planes') or (layout == 'planes' and weight.shape[0] % 32):
+        raise ValueError(f'modulated_conv1x1: layout {layout!r} for {weight.shape[0]} outputs')
+    return _ModConv1x1.apply(x, s, *hit[1], layout)
 
 
 class _AugSample(torch.autograd.Function):
@@ -301,6 +321,65 @@ def aug_sample(img, grid, copies: int, white_background: bool = False):
     if img.shape[-1] != 3 or grid.shape[0] != img.shape[0] * copies or grid.shape[-1] != 2:
         raise ValueError(f'aug_sample: img {tuple(img.shape)} / grid {tuple(grid.shape)} / copies {copies}')
     return _AugSample.apply(img, grid.detach(), copies, 1.0 if white_background else 0.0)
+
+
+def _str3(t):
+    """(b, q, t) float strides of a channel-contiguous [B, C, h, w] (channels-last) or
+    [B, C/32, 32, h, w] (texel-major planes) tensor, as the strided C-ABI takes them; None if t is
+    neither."""
+    if t.dim() == 4 and t.stride(1) == 1 and t.stride(2) == t.shape[3] * t.stride(3):
+        return (ctypes.c_int64 * 3)(t.stride(0), 32, t.stride(3))
+    if t.dim() == 5 and t.shape[2] == 32 and t.stride(2) == 1 and t.stride(3) == t.shape[4] * t.stride(4):
+        return (ctypes.c_int64 * 3)(t.stride(0), t.stride(1), t.stride(4))
+    return None
+
+
+def _conform(t):
+    """t in a layout _str3 accepts (a copy only if it is in neither)."""
+    if _str3(t) is not None:
+        return t
+    if t.dim() == 4:
+        return t.contiguous(memory_format=torch.channels_last)
+    return t.permute(0, 1, 3, 4, 2).contiguous().permute(0, 1, 4, 2, 3)
+
+
+def _texel_major(shape, dev, dtype):
+    """[B, Q, 32, h, w] stored as [B, Q, h, w, 32] (the renderer's plane layout)."""
+    B, Q, _, h, w = shape
+    return torch.empty((B, Q, h, w, 32), device=dev, dtype=dtype).permute(0, 1, 4, 2, 3)
+
+
+class _UpAddStrided(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, c, bias):
+        _require_device(img, c, bias)
+        _frozen(bias)
+        c = _conform(c)
+        B = c.shape[0]
+        C = c.shape[1] * (c.shape[2] if c.dim() == 5 else 1)
+        H = c.shape[-2]
+        n = H // 2
+        if img is not None:
+            img = img.contiguous(memory_format=torch.channels_last)
+            assert img.shape == (B, C, n, n), (img.shape, c.shape)
+        # a 5-d c (the last layer's to-planes output) -> texel-major planes; else channels-last
+        out = (_texel_major(c.shape, c.device, c.dtype) if c.dim() == 5
+               else torch.empty_like(c, memory_format=torch.channels_last))
+        _call('nfi_syn_up_add_forward_strided', _p(img), None if img is None else _str3(img), _p(c), _str3(c),
+              _p(bias.contiguous()), _p(out), _str3(out), B, C, n, _stream(c.device))
+        ctx.has_img = img is not None
+        ctx.shape = (B, C, n)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        gimg = None
+        g = _conform(g)
+        if ctx.has_img and ctx.needs_input_grad[0]:
+            B, C, n = ctx.shape
+            gimg = torch.empty((B, C, n, n), device=g.device, dtype=g.dtype, memory_format=torch.channels_last)
+            _call('nfi_syn_up_backward_strided', _p(g), _str3(g), _p(gimg), _str3(gimg), B, C, n, _stream(g.device))
+        return gimg, g, None
 
 
 class _UpAdd(torch.autograd.Function):
@@ -413,4 +492,10 @@ def fir_up_act(t, d, bias, gain: float):
 
 
 def up_add(img, c, bias):
+    """upsample2d(img) + c + bias (stylegan.py:69-73, 380-381, 428-433): NCHW; channels-last when c
+    is; texel-major planes [B, C/32, 32, 2n, 2n] (the renderer's layout) when c is 5-d
+    (nfi_syn_up_add_forward_strided)."""
+    if c.dim() == 5 or (c.is_contiguous(memory_format=torch.channels_last) and not c.is_contiguous()
+                        and c.shape[1] % 4 == 0):
+        return _UpAddStrided.apply(img, c, bias)
     return _UpAdd.apply(img, c, bias)

@@ -121,7 +121,8 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
         ws = gen.mapping_network(c, None)
     if nattn:                           # generator.py:451-462
         assert ws.shape[1] == 15
-        w_tex, w_syn = ws[:, 14], ws[:, :14]
+        w_syn, w_tex = ws.split([14, 1], dim=1)     # one split (its backward is one cat)
+        w_tex = w_tex[:, 0]
         if 'attention_values' in extra_model_inputs:
             palette = extra_model_inputs['attention_values']
         else:

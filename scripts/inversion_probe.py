@@ -22,6 +22,10 @@ def run(B, loss, steps=10, cl=False, graph=False, overlap=True):
     batch = bench.make_inputs(cfg, dev, 1)
     torch.manual_seed(4321)
     gen = producer.InversionGenerator(scene_range=1.4).to(dev).requires_grad_(False)
+    if os.environ.get('NFI_PLANES_LAYOUT'):    # A/B: 'nchw' = channel-major planes (converted by render)
+        for m in gen.modules():
+            if isinstance(m, producer.ToPlanes):
+                m.out_layout = os.environ['NFI_PLANES_LAYOUT']
     w_avg = gen.mapping_network.get_average_w(generator=torch.Generator().manual_seed(7))
     target = torch.tanh(torch.randn((B, 128, 128, 3), device=dev))
     net = lpips.LPIPS().to(dev) if loss == 'vgg' else None

@@ -170,6 +170,52 @@ def test_up_add(B, C, n, with_img):
         _close(img.grad, irf.grad)
 
 
+@pytest.mark.parametrize('B,C,n', [(2, 96, 2), (1, 96, 16), (2, 8, 64)])
+@pytest.mark.parametrize('with_img', [True, False])
+def test_up_add_channels_last(B, C, n, with_img):
+    """The channels-last skip path (the producer's texel-major planes) == the NCHW one, values and
+    gradients, and the 1x1 layer's channels-last output == its NCHW output."""
+    img = _rand(B, C, n, n, seed=28).requires_grad_() if with_img else None
+    c = _rand(B, C, 2 * n, 2 * n, seed=29).requires_grad_()
+    bias = 0.3 * _rand(C, seed=30)
+    g = _rand(B, C, 2 * n, 2 * n, seed=31)
+    out = producer_ops.up_add(img, c, bias)
+    out.backward(g)
+    il = img.detach().to(memory_format=torch.channels_last).requires_grad_() if with_img else None
+    cl = c.detach().to(memory_format=torch.channels_last).requires_grad_()
+    out_l = producer_ops.up_add(il, cl, bias)
+    assert out_l.is_contiguous(memory_format=torch.channels_last)
+    out_l.backward(g.to(memory_format=torch.channels_last))
+    _close(out_l.detach(), out.detach(), rel=1e-7)
+    _close(cl.grad, c.grad, rel=1e-7)
+    if with_img:
+        _close(il.grad, img.grad, rel=1e-7)
+    x = _rand(B, 16, 2 * n, 2 * n, seed=32)
+    s = _rand(B, 16, seed=33)
+    w = _rand(C, 16, 1, 1, seed=34)
+    y0 = producer_ops.modulated_conv1x1(x, s, w)
+    y1 = producer_ops.modulated_conv1x1(x, s, w, layout='nhwc')
+    assert y1.is_contiguous(memory_format=torch.channels_last)
+    _close(y1, y0, rel=1e-6)
+    if C % 32 == 0:
+        # the last layer: to-planes output as [B, C/32, 32, H, W] -> up_add writes texel-major
+        # planes ([B, C/32, H, W, 32] storage); values and gradients as the NCHW chain
+        xs = x.clone().requires_grad_()
+        ss = s.clone().requires_grad_()
+        y5 = producer_ops.modulated_conv1x1(xs, ss, w, layout='planes')
+        p5 = producer_ops.up_add(il.detach().requires_grad_() if with_img else None, y5, bias)
+        assert p5.dim() == 5 and p5.permute(0, 1, 3, 4, 2).is_contiguous()
+        x0, s0 = x.clone().requires_grad_(), s.clone().requires_grad_()
+        i0 = img.detach().clone().requires_grad_() if with_img else None
+        p0 = producer_ops.up_add(i0, producer_ops.modulated_conv1x1(x0, s0, w), bias)
+        _close(p5.reshape(p0.shape), p0.detach(), rel=1e-6)
+        g5 = g.view(B, C // 32, 32, 2 * n, 2 * n).permute(0, 1, 3, 4, 2).contiguous().permute(0, 1, 4, 2, 3)
+        p5.backward(g5)
+        p0.backward(g)
+        _close(xs.grad, x0.grad, rel=1e-6)
+        _close(ss.grad, s0.grad, rel=1e-5)
+
+
 def test_backends_agree_on_gpu():
     """Full producer: 'hip' (Winograd F(4,3) 3x3 convolutions, fused epilogues) and 'torch' (the
     reference's op sequence, fp32) against the same op sequence in float64 on the device.  d ws
