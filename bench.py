@@ -46,7 +46,10 @@ TAP_BYTES = 3 * 4 * 32 * 4  # 1,536 B per sample per tap pass
 def make_inputs(cfg, dev, seed):
     from nfi.synthetic import inversion_batch
     sr, wbg, flipped, B, H, S, pose, bwd = cfg
-    return inversion_batch(B, H, H, S, 256, sr, seed, flipped=flipped, device=dev)
+    # planes in the renderer's texel-major storage: what the producer (InversionGenerator) emits,
+    # so the timed path is the inversion step's; channel-major callers pay one conversion pass each
+    # way, reported separately as channel_major_conversion_ms
+    return inversion_batch(B, H, H, S, 256, sr, seed, flipped=flipped, device=dev, texel_major=True)
 
 
 def run_step(nfi, batch, cfg, backward: bool):
@@ -63,6 +66,26 @@ def run_step(nfi, batch, cfg, backward: bool):
         loss = (rgb * batch['g_rgb']).sum() + (mask * batch['g_mask']).sum()
         loss.backward()
     return rgb
+
+
+def conversion_ms(planes, ops, reps=5):
+    """ms per step a caller holding channel-major [B,3,32,R,R] planes would add: the texel-major
+    copy in the forward and the gradient's copy back (planes_t2c / planes_c2t)."""
+    cm = planes.detach().contiguous().requires_grad_()
+    g = torch.ones((cm.shape[0], 3, cm.shape[3], cm.shape[4], 32), device=cm.device)
+
+    def once():
+        cm.grad = None
+        ops.planes_texel_major(cm).backward(g)
+    once()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        once()
+    e1.record()
+    torch.cuda.synchronize()
+    return round(e0.elapsed_time(e1) / reps, 4)
 
 
 def cpu_baseline(args):
@@ -292,6 +315,7 @@ def main():
 
     samples_per_step = B * H * H * 2 * S
     value = world * samples_per_step * args.steps / elapsed / 1e6
+    conv_ms = conversion_ms(batch['field'].planes, ops)
     ms_per_step = elapsed / args.steps * 1e3
 
     # roofline of the dominant stage (DESIGN.md "Kernels and their rooflines"):
@@ -361,7 +385,9 @@ def main():
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
         'config': {'workload': args.config, 'global_batch': B * world, 'resolution': H,
                    'samples_per_ray': f'{S}+{S}', 'plane_res': 256, 'pose_grad': pose,
-                   'backward': bwd, 'parallelism': f'dp{world} (one process per GPU, no collective)'},
+                   'backward': bwd, 'parallelism': f'dp{world} (one process per GPU, no collective)',
+                   'planes_layout': 'texel-major [B,3,R,R,32] storage (the producer\'s native output)'},
+        'channel_major_conversion_ms': conv_ms,
         'renderer_s_per_image_30step': round(30 * ms_per_step / 1e3 / B, 5),
         'roofline': roof,
     }

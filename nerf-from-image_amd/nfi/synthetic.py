@@ -16,10 +16,14 @@ from .inversion import pose_to_matrix
 from .render import TriplaneField
 
 
-def inversion_batch(B, H, W, S, R, scene_range, seed, flipped=True, device='cuda'):
+def inversion_batch(B, H, W, S, R, scene_range, seed, flipped=True, device='cuda', texel_major=False):
+    """texel_major: the planes [B,3,32,R,R] held in [B,3,R,R,32] storage (same values) — the layout
+    InversionGenerator's 'hip' backend emits and the renderer reads with no conversion pass."""
     g = torch.Generator(device=device).manual_seed(seed)
     dev = torch.device(device)
     planes = 1.87 * torch.randn((B, 3, 32, R, R), generator=g, device=dev)
+    if texel_major:
+        planes = planes.permute(0, 1, 3, 4, 2).contiguous().permute(0, 1, 4, 2, 3)
     w1 = torch.randn((64, 32), generator=g, device=dev)
     w2 = torch.randn((11, 64), generator=g, device=dev)
     b1 = torch.zeros(64, device=dev)
