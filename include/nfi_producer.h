@@ -118,6 +118,17 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
                                 const float* inv0, const float* inv1, float* gf0, int32_t N,
                                 int32_t C, int32_t HW, void* stream);
 
+/* The LPIPS trunk's first layer (vgg16.features[0:2], metrics.py:107): x [N,3,H,W] -> y = relu(conv3x3(x,
+ * w [Co,3,3,3], padding 1) + bias[co]) [N,Co,H,W], a direct convolution with the epilogue (27 products
+ * per output: bound by writing y).  W % 4 == 0. */
+int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
+                              int32_t H, int32_t W, void* stream);
+
+/* Its backward to the image: gx [N,3,H,W] = conv_transpose(gy * (y > 0), w) (threshold_backward then
+ * the data gradient; overwritten).  H % 16 == 0, W % 64 == 0. */
+int32_t nfi_vgg_first_backward(const float* gy, const float* y, const float* w, float* gx, int32_t N, int32_t Co,
+                               int32_t H, int32_t W, void* stream);
+
 /* LPIPS VGG16 block epilogue (torchvision vgg16.features[:30] as lpips 0.1 runs it, metrics.py:107):
  * x [P, H, W] = a bias-free 3x3 convolution's output (P = N*C planes) -> y = relu(x + bias[c]);
  * when `pooled` is not NULL also pooled [P, H/2, W/2] = MaxPool2d(2, 2)(y).  Replaces the bias

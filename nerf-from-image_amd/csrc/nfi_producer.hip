@@ -801,6 +801,126 @@ __global__ void __launch_bounds__(64 * LP_WAVES) lpips_bwd_regs_kernel(const flo
 }
 
 // ---------------------------------------------------------------------------------------
+// The LPIPS trunk's first layer (vgg16.features[0:2]: 3 -> Co channels, 3x3, padding 1, + bias,
+// ReLU) as a direct convolution with the epilogue: K = 27 products per output, so the layer is
+// bound by writing its Co-channel output — one pass, instead of a library convolution (~17
+// TFLOP/s on this shape) plus the epilogue pass.  One thread per 4 consecutive pixels of one row:
+// the 3 x 3 x 6 input window (zero padding by selects), Co float4 stores.  The weights are
+// wave-uniform (scalar loads).
+// Backward: gx = conv_transpose(gy * (y > 0)) (threshold_backward then the data gradient), one
+// workgroup per 16 x 64 pixel block: the masked gradient of FB channels at a time is staged in
+// LDS with a 1-pixel halo, each thread accumulates its 4 pixels x 3 input channels.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float4* __restrict__ y,
+                                                            int64_t total, int Co, int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int W4 = W / 4;
+  const int64_t row = i / W4;                // n * H + yy
+  const int x0 = (int)(i - row * W4) * 4;
+  const int n = (int)(row / H), yy = (int)(row - (int64_t)n * H);
+  float v[3][3][6];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float* xc = x + ((int64_t)n * 3 + c) * H * W;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int ry = yy - 1 + r;
+      const float* xr = xc + (int64_t)min(max(ry, 0), H - 1) * W;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int cx = x0 - 1 + j;
+        const float t = xr[min(max(cx, 0), W - 1)];
+        v[c][r][j] = (ry >= 0 && ry < H && cx >= 0 && cx < W) ? t : 0.f;
+      }
+    }
+  }
+  float4* yo = y + (((int64_t)n * Co) * H + yy) * W4 + x0 / 4;
+  const int64_t plane4 = (int64_t)H * W4;
+  for (int co = 0; co < Co; ++co) {
+    const float* wc = w + co * 27;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float wv = wc[c * 9 + r * 3 + kx];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) a[k] = fmaf(wv, v[c][r][k + kx], a[k]);
+        }
+    const float b = bias[co];
+    yo[co * plane4] = make_float4(fmaxf(a[0] + b, 0.f), fmaxf(a[1] + b, 0.f), fmaxf(a[2] + b, 0.f),
+                                  fmaxf(a[3] + b, 0.f));
+  }
+}
+
+constexpr int VF_TY = 16, VF_TX = 64, VF_FB = 4;   // pixel block, channels per LDS stage
+__global__ void __launch_bounds__(256) vgg_first_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                                                            const float* __restrict__ w, float* __restrict__ gx,
+                                                            int Co, int H, int W) {
+  __shared__ float M[VF_FB][VF_TY + 2][VF_TX + 3];
+  const int tiles_x = W / VF_TX;
+  const int Y0 = (blockIdx.x / tiles_x) * VF_TY, X0 = (blockIdx.x % tiles_x) * VF_TX;
+  const int n = blockIdx.y;
+  const int ty = threadIdx.x / (VF_TX / 4), tx4 = (threadIdx.x % (VF_TX / 4)) * 4;
+  const int64_t HW = (int64_t)H * W;
+  float acc[3][4] = {};
+  constexpr int SN = VF_FB * (VF_TY + 2) * (VF_TX + 2), SIT = (SN + 255) / 256;
+  for (int c0 = 0; c0 < Co; c0 += VF_FB) {
+    // stage m = gy * (y > 0) of channels c0 .. c0+FB-1 over rows Y0-1 .. Y0+16, cols X0-1 .. X0+64
+    float gv[SIT], yv[SIT];
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int k = min(it * 256 + (int)threadIdx.x, SN - 1);
+      const int f = k / ((VF_TY + 2) * (VF_TX + 2)), rem = k - f * ((VF_TY + 2) * (VF_TX + 2));
+      const int r = rem / (VF_TX + 2), q = rem - r * (VF_TX + 2);
+      const int Y = min(max(Y0 - 1 + r, 0), H - 1), X = min(max(X0 - 1 + q, 0), W - 1);
+      const int64_t a = ((int64_t)n * Co + min(c0 + f, Co - 1)) * HW + (int64_t)Y * W + X;
+      gv[it] = gy[a];
+      yv[it] = y[a];
+    }
+    __syncthreads();   // the previous stage's reads are done
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int k = it * 256 + threadIdx.x;
+      if (k < SN) {
+        const int f = k / ((VF_TY + 2) * (VF_TX + 2)), rem = k - f * ((VF_TY + 2) * (VF_TX + 2));
+        const int r = rem / (VF_TX + 2), q = rem - r * (VF_TX + 2);
+        const int Y = Y0 - 1 + r, X = X0 - 1 + q;
+        const bool in = Y >= 0 && Y < H && X >= 0 && X < W && c0 + f < Co;
+        M[f][r][q] = (in && yv[it] > 0.f) ? gv[it] : 0.f;
+      }
+    }
+    __syncthreads();
+    for (int f = 0; f < VF_FB && c0 + f < Co; ++f) {
+      const float* wc = w + (c0 + f) * 27;
+      // gx[ci][Y][X] += w[co][ci][ky][kx] * m[co][Y+1-ky][X+1-kx]
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        float mv[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) mv[j] = M[f][ty + 2 - ky][tx4 + j];   // X + 1 - kx - (X0 - 1) = tx4 + 2 - kx + k
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int ci = 0; ci < 3; ++ci) {
+            const float wv = wc[ci * 9 + ky * 3 + kx];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[ci][k] = fmaf(wv, mv[k + 2 - kx], acc[ci][k]);
+          }
+      }
+    }
+  }
+#pragma unroll
+  for (int ci = 0; ci < 3; ++ci)
+    *reinterpret_cast<float4*>(gx + ((int64_t)n * 3 + ci) * HW + (int64_t)(Y0 + ty) * W + X0 + tx4) =
+        make_float4(acc[ci][0], acc[ci][1], acc[ci][2], acc[ci][3]);
+}
+
+// ---------------------------------------------------------------------------------------
 // VGG16 block epilogue of the LPIPS trunk (torchvision vgg16.features as lpips 0.1 runs it):
 // conv output x (MIOpen, no bias) -> y = ReLU(x + bias[c]) and, before a MaxPool2d(2, 2), the
 // pooled map m = max over each 2x2 window of y, in one pass (torch: bias add, relu, max_pool2d =
@@ -1230,6 +1350,26 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
     default: lpips_bwd_kernel<<<blocks((int64_t)N * HW), 256, 0, st>>>(g, f0, f1, w, inv0, inv1, gf0, N, C, HW);
   }
   NFI_CHECK_LAUNCH("lpips_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
+                              int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(x && w && bias && y, "vgg_first_forward: null pointer");
+  NFI_REQUIRE(N > 0 && Co > 0 && H > 0 && W > 0 && W % 4 == 0, "vgg_first_forward: bad shape");
+  const int64_t total = (int64_t)N * H * (W / 4);
+  vgg_first_fwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(x, w, bias, (float4*)y, total, Co, H, W);
+  NFI_CHECK_LAUNCH("vgg_first_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_vgg_first_backward(const float* gy, const float* y, const float* w, float* gx, int32_t N, int32_t Co,
+                               int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(gy && y && w && gx, "vgg_first_backward: null pointer");
+  NFI_REQUIRE(N > 0 && Co > 0 && H % VF_TY == 0 && W % VF_TX == 0, "vgg_first_backward: bad shape");
+  vgg_first_bwd_kernel<<<dim3((unsigned)((H / VF_TY) * (W / VF_TX)), (unsigned)N), 256, 0, (hipStream_t)stream>>>(
+      gy, y, w, gx, Co, H, W);
+  NFI_CHECK_LAUNCH("vgg_first_bwd_kernel");
   return NFI_OK;
 }
 

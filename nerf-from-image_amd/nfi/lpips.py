@@ -72,6 +72,12 @@ class VGG16Features(nn.Module):
                     out.append(y)
                 i += 3 if pool else 2
                 continue
+            if i == 0 and not pool and producer_ops.vgg_first_applicable(x, conv.weight):
+                x = producer_ops.vgg_first(x, conv.weight, conv.bias)     # conv1_1 + ReLU, one pass
+                if i + 1 in TAPS:
+                    out.append(x)
+                i += 2
+                continue
             z = F.conv2d(x, conv.weight, None, 1, 1)
             if z.shape[-1] % 4 == 0 and not (pool and z.shape[-2] % 2):
                 r = producer_ops.vgg_epilogue(z, conv.bias, pool)

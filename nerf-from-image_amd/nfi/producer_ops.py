@@ -468,6 +468,43 @@ class _VggEpilogue(torch.autograd.Function):
         return gx, None, None
 
 
+class _VggFirst(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        x = x.contiguous()
+        N, _, H, W = x.shape
+        Co = w.shape[0]
+        y = torch.empty((N, Co, H, W), device=x.device, dtype=x.dtype)
+        wd = w.detach().contiguous()
+        _call('nfi_vgg_first_forward', _p(x), _p(wd), _p(bias.detach().contiguous()), _p(y), N, Co, H, W,
+              _stream(x.device))
+        ctx.save_for_backward(y, wd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        y, wd = ctx.saved_tensors
+        N, Co, H, W = y.shape
+        gx = torch.empty((N, 3, H, W), device=y.device, dtype=y.dtype)
+        _call('nfi_vgg_first_backward', _p(gy.contiguous()), _p(y), _p(wd), _p(gx), N, Co, H, W,
+              _stream(y.device))
+        return gx, None, None
+
+
+def vgg_first_applicable(x, w) -> bool:
+    return (x.dim() == 4 and x.shape[1] == 3 and tuple(w.shape[1:]) == (3, 3, 3) and x.shape[-2] % 16 == 0
+            and x.shape[-1] % 64 == 0 and not (torch.is_grad_enabled() and w.requires_grad))
+
+
+def vgg_first(x, w, bias):
+    """relu(conv2d(x, w, bias, padding=1)) for the LPIPS trunk's 3-channel first layer
+    (vgg16.features[0:2]): one direct-convolution pass with the epilogue each way
+    (nfi_vgg_first_forward / _backward); frozen weights (the LPIPS net is not trained)."""
+    _require_device(x, w, bias)
+    _frozen(bias)
+    return _VggFirst.apply(x, w, bias)
+
+
 def vgg_epilogue(x, bias, pool: bool = False):
     """relu(x + bias[c]) of a bias-free conv output x; with pool=True also returns MaxPool2d(2, 2)
     of it: (y, pooled).  One HIP pass each way (nfi_vgg_bias_relu_forward / nfi_vgg_relu_backward)."""

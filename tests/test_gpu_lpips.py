@@ -150,6 +150,29 @@ def test_aug_sample_matches_grid_sample(B, H, W, white, scale):
     assert gerr <= max(1e-6 * float(gr.abs().max()), 4 * gerr32), (gerr, gerr32)
 
 
+@pytest.mark.parametrize('N,Co,H,W', [(2, 64, 16, 64), (3, 64, 32, 128), (1, 8, 48, 64)])
+def test_vgg_first_layer(N, Co, H, W):
+    """The fused first VGG layer (direct 3x3 conv + bias + ReLU; backward threshold + data gradient)
+    against fp64 torch: within 4x the fp32 torch formulation's own error (floor 1e-6 of the max)."""
+    g = torch.Generator(device=DEV).manual_seed(N * H + Co)
+    x = torch.randn((N, 3, H, W), device=DEV, generator=g).requires_grad_()
+    w = torch.randn((Co, 3, 3, 3), device=DEV, generator=g) * 0.3
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=g)
+    y = producer_ops.vgg_first(x, w, b)
+    y.backward(gy)
+    x64 = x.detach().double().requires_grad_()
+    y64 = torch.relu(torch.nn.functional.conv2d(x64, w.double(), b.double(), padding=1))
+    y64.backward(gy.double())
+    x32 = x.detach().clone().requires_grad_()
+    y32 = torch.relu(torch.nn.functional.conv2d(x32, w, b, padding=1))
+    y32.backward(gy)
+    for got, ref, r32 in ((y.detach(), y64.detach(), y32.detach()), (x.grad, x64.grad, x32.grad)):
+        m = float(ref.abs().max())
+        err, err32 = float((got.double() - ref).abs().max()), float((r32.double() - ref).abs().max())
+        assert err <= max(1e-6 * m, 4 * err32), (err, err32, m)
+
+
 def test_vgg_target_on_side_stream_matches_inline():
     """The target half of the 'vgg' loss (grid + target features) computed on a side stream gives
     the inline loss and gradient (same device draws, same kernels); the inversion
