@@ -167,6 +167,13 @@ int32_t nfi_wino_input_transform_scaled(const float* x, const float* scale, floa
 int32_t nfi_wino_output_transform(const float* M, const float* bias, float* y, float* pooled, int32_t N,
                                   int32_t Co, int32_t H, int32_t W, void* stream);
 
+/* The data gradient of a modulated convolution conv(x * scale) finished in the output transform:
+ * M [36,C,P] = the data-gradient products (d(x * scale) in the Winograd domain) -> gx [N,C,H,W] =
+ * that * scale[n][c] (gx may be NULL) and ds [N,C] = sum_hw that * x (overwritten) — the
+ * modulation backward (nfi_syn_scale_backward) without the intermediate. */
+int32_t nfi_wino_output_transform_scaled_grad(const float* M, const float* x, const float* scale, float* gx,
+                                              float* ds, int32_t N, int32_t C, int32_t H, int32_t W, void* stream);
+
 /* The fused layer: input transform, the 36 products on the matrix cores (v_mfma_f32_16x16x4_f32,
  * accumulators resident for a 32-tile x 32-channel block) and the output transform in one kernel,
  * same epilogue contract as nfi_wino_output_transform.  Ua = nfi_wino_pack_weights(U) (the

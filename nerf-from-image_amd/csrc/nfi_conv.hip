@@ -234,6 +234,65 @@ __global__ void __launch_bounds__(256) output_kernel(const float* __restrict__ M
   }
 }
 
+// The data gradient of a modulated convolution (conv(x * s)) finished in the output transform:
+// g' = the transform of M (d(x * s)), gx = g' s[n][c] and ds[n][c] += sum g' x — the scale
+// backward (nfi_syn_scale_backward) without g' in memory.  ds zeroed by the caller; a wave whose
+// tiles are all in one image adds one atomic, else one per lane.
+__global__ void __launch_bounds__(256) output_scaled_kernel(const float* __restrict__ M, const float* __restrict__ x,
+                                                            const float* __restrict__ sc, float* __restrict__ gx,
+                                                            float* __restrict__ ds, int C, int H, int W, int TW, int T,
+                                                            int64_t P) {
+  const int64_t p0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  const bool live = p0 < P;
+  const int64_t p = live ? p0 : P - 1;
+  const int n = (int)(p / T);
+  const int t = (int)(p - (int64_t)n * T);
+  const int ty = t / TW, tx = t - ty * TW;
+  const int64_t plane = (int64_t)C * P;
+  const float* src = M + (int64_t)c * P + p;
+  float m[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) m[r][j] = ld_stream(src + (r * 6 + j) * plane);
+  const int64_t off = (((int64_t)n * C + c) * H + 4 * ty) * W + 4 * tx;
+  float4 xv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const float4*>(x + off + (int64_t)r * W);
+  float s[4][6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float col[6], o[4];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) col[r] = m[r][j];
+    at_col(col, o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[r][j] = o[r];
+  }
+  float o[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) at_col(s[r], o[r]);
+  const float sv = sc[(int64_t)n * C + c];
+  float acc = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    acc += (o[r][0] * xv[r].x + o[r][1] * xv[r].y) + (o[r][2] * xv[r].z + o[r][3] * xv[r].w);
+    if (live && gx)
+      *reinterpret_cast<float4*>(gx + off + (int64_t)r * W) =
+          make_float4(o[r][0] * sv, o[r][1] * sv, o[r][2] * sv, o[r][3] * sv);
+  }
+  acc = live ? acc : 0.f;
+  const int n0 = __shfl(n, 0), n63 = __shfl(n, 63);
+  if (n0 == n63) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d);
+    if ((threadIdx.x & 63) == 0) atomicAdd(ds + (int64_t)n * C + c, acc);
+  } else if (live) {
+    atomicAdd(ds + (int64_t)n * C + c, acc);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Fused layer: input transform, the 36 products and the output transform in one kernel, so V
 // and M never leave the chip (the unfused path writes and re-reads 2.25x the input and the
@@ -513,6 +572,25 @@ int32_t nfi_wino_output_transform(const float* M, const float* bias, float* y, f
   hipLaunchKernelGGL(output_kernel, dim3((unsigned)((P + 255) / 256), Co), dim3(256), 0,
                      (hipStream_t)stream, M, bias, y, pooled, Co, H, W, TW, T, P, bias ? 1 : 0);
   NFI_CHECK_LAUNCH("wino output_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_wino_output_transform_scaled_grad(const float* M, const float* x, const float* scale, float* gx,
+                                              float* ds, int32_t N, int32_t C, int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(M && x && scale && ds, "wino_output_transform_scaled_grad: null pointer");
+  NFI_REQUIRE(N > 0 && C > 0 && C <= 65535 && H >= 4 && W >= 4 && H % 4 == 0 && W % 4 == 0,
+              "wino_output_transform_scaled_grad: bad shape (H, W multiples of 4)");
+  NFI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)gx & 15) == 0, "wino_output_transform_scaled_grad: misaligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(ds, 0, sizeof(float) * N * C, st) != hipSuccess) {
+    nfi::set_error("wino_output_transform_scaled_grad: memset failed");
+    return NFI_ELAUNCH;
+  }
+  const int TW = W / 4, T = (H / 4) * TW;
+  const int64_t P = (int64_t)N * T;
+  hipLaunchKernelGGL(output_scaled_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0, st, M, x, scale, gx,
+                     ds, C, H, W, TW, T, P);
+  NFI_CHECK_LAUNCH("wino output_scaled_kernel");
   return NFI_OK;
 }
 

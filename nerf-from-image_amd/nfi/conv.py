@@ -160,11 +160,24 @@ class _ModConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, s = ctx.saved_tensors
-        gxs = _dgrad(g.contiguous(), ctx)
+        g = g.contiguous()
         B, C, H, W = x.shape
         gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
-        _call('nfi_syn_scale_backward', _p(gxs), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W, _stream(x.device))
+        st = _stream(x.device)
+        Co = g.shape[1]
+        Ut, Uta = ctx.Ut
+        if DGRAD and not (FUSED and Uta is not None and Co <= FUSED_MAX_CI):
+            # three-pass data gradient, the scale backward in its output transform
+            P = B * (H // 4) * (W // 4)
+            V = torch.empty((36, Co, P), device=g.device)
+            _call('nfi_wino_input_transform_scaled', _p(g), None, _p(V), B, Co, H, W, st)
+            M = torch.bmm(Ut, V)
+            del V
+            _call('nfi_wino_output_transform_scaled_grad', _p(M), _p(x), _p(s), _p(gx), _p(ds), B, C, H, W, st)
+            return gx, ds, None
+        gxs = _dgrad(g, ctx)
+        _call('nfi_syn_scale_backward', _p(gxs), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W, st)
         return gx, ds, None
 
 

@@ -36,6 +36,16 @@ class Count(TorchDispatchMode):
                 if '/nfi/' in fr.filename or fr.filename.endswith('bench.py'):
                     where = f'{os.path.basename(fr.filename)}:{fr.lineno} {fr.name}'
                     break
+            if where == '?':        # backward: the forward line that created the running node
+                node = torch._C._current_autograd_node()
+                tb = None if node is None else node.metadata.get('traceback_')
+                if tb:
+                    lines = [ln for ln in ''.join(tb).split('\n') if '/nfi/' in ln]
+                    if lines:
+                        last = lines[-1].strip()
+                        where = 'bwd ' + type(node).__name__ + ' <- ' + last.split('/nfi/')[-1]
+                else:
+                    where = 'bwd ' + (type(node).__name__ if node is not None else '?')
             self.c[(where, name)] += 1
         return func(*args, **(kwargs or {}))
 
@@ -57,12 +67,12 @@ def main():
     inversion.invert(gen, target, batch['cam'], batch['focal'], w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     icfg.steps = 3
-    with Count() as m:
+    with torch.autograd.detect_anomaly(check_nan=False), Count() as m:
         inversion.invert(gen, target, batch['cam'], batch['focal'], w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     tot = sum(m.c.values())
     print(f'{tot / icfg.steps:.0f} ops per step (3 steps incl. setup)')
-    for (where, name), n in m.c.most_common(90):
+    for (where, name), n in m.c.most_common(120):
         print(f'{n / icfg.steps:6.1f}  {name:40s} {where}')
 
 

@@ -122,7 +122,7 @@ def test_trainable_weight_takes_the_library_path():
         conv.vgg_block(x, w, torch.zeros(16, device=DEV), False)
 
 
-@pytest.mark.parametrize('N,C,Co,H', [(2, 128, 96, 16), (4, 512, 512, 4), (3, 16, 32, 8)])
+@pytest.mark.parametrize('N,C,Co,H', [(2, 128, 96, 16), (4, 512, 512, 4), (3, 16, 32, 8), (2, 64, 128, 32), (1, 128, 128, 64)])
 def test_modulated_conv(N, C, Co, H):
     """conv2d(x * s, w) with the modulation folded into the input transform, against the fp64
     formulation: output, d x and d s (the synthesis layers' style gradient)."""
