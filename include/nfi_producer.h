@@ -161,6 +161,11 @@ int32_t nfi_wino_input_transform(const float* x, float* V, int32_t N, int32_t C,
 int32_t nfi_wino_input_transform_scaled(const float* x, const float* scale, float* V, int32_t N, int32_t C,
                                         int32_t H, int32_t W, void* stream);
 
+/* The transform of (y > 0) * g (threshold_backward of a ReLU output y, then the data-gradient
+ * Winograd's input transform): g, y [N,C,H,W] -> V [36,C,P] without the masked gradient in memory. */
+int32_t nfi_wino_input_transform_relu_grad(const float* g, const float* y, float* V, int32_t N, int32_t C, int32_t H,
+                                           int32_t W, void* stream);
+
 /* M [36,Co,P] -> y [N,Co,H,W].  bias == NULL: y = the convolution.  bias != NULL: y =
  * relu(conv + bias[co]) (the LPIPS VGG16 block epilogue, as nfi_vgg_bias_relu_forward) and, when
  * pooled != NULL, pooled [N,Co,H/2,W/2] = MaxPool2d(2, 2)(y). */

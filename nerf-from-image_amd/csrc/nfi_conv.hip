@@ -139,8 +139,8 @@ __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ w
 // modulation of the synthesis layers, stylegan.py:130, applied to the input of the convolution;
 // the transform is linear, so the per-(image, channel) factor multiplies the 36 outputs)
 __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x, const float* __restrict__ scale,
-                                                    float* __restrict__ V, int C, int H, int W, int TW, int T,
-                                                    int64_t P) {
+                                                    const float* __restrict__ mask, float* __restrict__ V, int C,
+                                                    int H, int W, int TW, int T, int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c = blockIdx.y;
   if (p >= P) return;
@@ -150,6 +150,14 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
   const float* xp = x + ((int64_t)n * C + c) * H * W;
   float d[6][6];
   load_patch(xp, H, W, ty, tx, true, d);
+  if (mask != nullptr) {   // threshold_backward: x is a ReLU output's gradient, mask that output
+    float mk[6][6];
+    load_patch(mask + ((int64_t)n * C + c) * H * W, H, W, ty, tx, true, mk);
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) d[r][j] = mk[r][j] > 0.f ? d[r][j] : 0.f;
+  }
   if (scale != nullptr) {
     const float sc = scale[(int64_t)n * C + c];
 #pragma unroll
@@ -549,7 +557,21 @@ int32_t nfi_wino_input_transform_scaled(const float* x, const float* scale, floa
   const int TW = W / 4, T = (H / 4) * TW;
   const int64_t P = (int64_t)N * T;
   hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
-                     (hipStream_t)stream, x, scale, V, C, H, W, TW, T, P);
+                     (hipStream_t)stream, x, scale, nullptr, V, C, H, W, TW, T, P);
+  NFI_CHECK_LAUNCH("wino input_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_wino_input_transform_relu_grad(const float* g, const float* y, float* V, int32_t N, int32_t C, int32_t H,
+                                           int32_t W, void* stream) {
+  NFI_REQUIRE(g && y && V, "wino_input_transform_relu_grad: null pointer");
+  NFI_REQUIRE(N > 0 && C > 0 && C <= 65535 && H >= 4 && W >= 4 && H % 4 == 0 && W % 4 == 0,
+              "wino_input_transform_relu_grad: bad shape (H, W multiples of 4)");
+  NFI_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)y & 15) == 0, "wino_input_transform_relu_grad: misaligned");
+  const int TW = W / 4, T = (H / 4) * TW;
+  const int64_t P = (int64_t)N * T;
+  hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
+                     (hipStream_t)stream, g, nullptr, y, V, C, H, W, TW, T, P);
   NFI_CHECK_LAUNCH("wino input_kernel");
   return NFI_OK;
 }

@@ -40,6 +40,9 @@ FUSED = True          # one fused kernel per layer (nfi_wino_conv_fused) for lay
 # (LPIPS 64->64 @128^2: 0.50 vs 0.68 ms) — and loses on the deeper ones (512->512 @16^2: 0.37 vs
 # 0.21 ms); scripts/wino_layers.py.
 FUSED_MAX_CI = 64
+# the VGG blocks' ReLU threshold_backward inside the data gradient's input transform (no pool
+# gradient; three-pass layers)
+RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
 
 
 def _p(t):
@@ -203,9 +206,22 @@ class _VggBlock(torch.autograd.Function):
         if gy is None and gm is None:
             return None, None, None, None
         N, C, H, W = y.shape
-        gz = torch.empty_like(y)
         gy = None if gy is None else gy.contiguous()
         gm = None if gm is None else gm.contiguous()
+        Ut, Uta = ctx.Ut
+        if RELU_IN_TRANSFORM and gm is None and DGRAD and not (FUSED and Uta is not None and C <= FUSED_MAX_CI):
+            # no pool gradient: the ReLU threshold inside the data gradient's input transform
+            st = _stream(y.device)
+            P = N * (H // 4) * (W // 4)
+            V = torch.empty((36, C, P), device=y.device)
+            _call('nfi_wino_input_transform_relu_grad', _p(gy), _p(y), _p(V), N, C, H, W, st)
+            M = torch.bmm(Ut, V)
+            del V
+            Ci = Ut.shape[1]
+            gx = torch.empty((N, Ci, H, W), device=y.device)
+            _call('nfi_wino_output_transform', _p(M), None, _p(gx), None, N, Ci, H, W, st)
+            return gx, None, None, None
+        gz = torch.empty_like(y)
         _call('nfi_vgg_relu_backward', _p(gy), _p(gm), _p(y), _p(gz), N * C, H, W, _stream(y.device))
         return _dgrad(gz, ctx), None, None, None
 
