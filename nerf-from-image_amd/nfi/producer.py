@@ -381,16 +381,45 @@ class PaletteMapper(nn.Module):
         self.fc5 = EqualizedLinear(hidden, hidden)
         self.fc_values = EqualizedLinear(hidden, num_values * 3)
 
+    backend = 'hip'
+
     def forward(self, c):
         scale = SQRT2 / 2
         x = self.const.expand(c.shape[0], -1)
+        cond = self._conditions(c) if self.backend == 'hip' else None
         for pair in ((1, 2), (3, 4)):
             shortcut = x
             for i in pair:
-                x = F.leaky_relu(getattr(self, f'norm{i}')(getattr(self, f'fc{i}')(x), c), 0.2)
+                h = getattr(self, f'fc{i}')(x)
+                if cond is None:
+                    x = F.leaky_relu(getattr(self, f'norm{i}')(h, c), 0.2)
+                else:        # (1 + gamma_i(c)) and beta_i(c) from the one batched projection
+                    g1, b = cond[2 * (i - 1)], cond[2 * (i - 1) + 1]
+                    x = F.leaky_relu(torch.addcmul(b, g1, F.layer_norm(h, (h.shape[-1],))), 0.2)
             x = (x + shortcut) * scale
         x = F.leaky_relu(self.fc5(x), 0.2)
         return wide_sigmoid_rescaled(self.fc_values(x).view(-1, self.num_values, 3))
+
+    def _conditions(self, c):
+        """The 4 conditional norms' (1 + gamma_i(c), beta_i(c)) (generator.py:42-60) as ONE
+        [b,512] x [512, 8*512] product over the stacked gain-scaled weights (the +1 folded into
+        gamma's bias), split into 8 views: 1 GEMM and one concatenated gradient instead of 8 GEMMs,
+        4 adds and 8 accumulated gradients (frozen weights: built once per parameter version)."""
+        norms = [getattr(self, f'norm{i}') for i in range(1, 5)]
+        params = []
+        for n in norms:
+            params += [n.fc_gamma.weight, n.fc_gamma.bias, n.fc_beta.weight, n.fc_beta.bias]
+
+        def build():
+            ws, bs = [], []
+            for n in norms:
+                for lin, one in ((n.fc_gamma, 1.0), (n.fc_beta, 0.0)):
+                    ws.append(lin.weight * lin.weight_gain)
+                    bs.append(lin.bias * lin.bias_gain + one)
+            return torch.cat(ws, 0), torch.cat(bs, 0)
+
+        W, b = frozen_value(self, 'conditions', build, *params)
+        return F.linear(c, W, b).split(norms[0].ch, dim=1)
 
 
 class Decoder(nn.Module):
@@ -432,6 +461,7 @@ class InversionGenerator(nn.Module):
         for m in self.synthesis_network.modules():
             if isinstance(m, (ModulatedConv, ToPlanes, SynthesisBlock)):
                 m.backend = backend
+        self.texture_mapper.backend = backend
         return self
 
     def planes_and_palette(self, ws):
