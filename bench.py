@@ -63,8 +63,8 @@ def run_step(nfi, batch, cfg, backward: bool):
     with torch.enable_grad() if backward else torch.no_grad():
         rgb, depth, mask, _, _, _ = nfi.render(f, H, H, cam, focal, None, None, None, S, randomize=True)
     if backward:
-        loss = (rgb * batch['g_rgb']).sum() + (mask * batch['g_mask']).sum()
-        loss.backward()
+        # the upstream gradients of a loss sum(rgb * g_rgb) + sum(mask * g_mask), handed in directly
+        torch.autograd.backward([rgb, mask], [batch['g_rgb'], batch['g_mask']])
     return rgb
 
 

@@ -69,8 +69,8 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
 
 __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, float* __restrict__ ro,
                                                        float* __restrict__ rd, float* __restrict__ nearp,
-                                                       float* __restrict__ farp, uint32_t* __restrict__ ws,
-                                                       int* __restrict__ hitflag) {
+                                                       float* __restrict__ farp, uint32_t* __restrict__ part,
+                                                       uint8_t* __restrict__ hitflag) {
   const int HW = c.H * c.W;
   const long long n = (long long)c.B * HW;
   const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -130,7 +130,9 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
     farp[r] = fr;
     hitflag[r] = hit ? 1 : 0;
   }
-  // min near / max far over hits of the whole call (nerf_utils.py:260-261)
+  // min near / max far over hits of the whole call (nerf_utils.py:260-261): this block's pair of
+  // keys to part[2 block], combined by rays_fix_kernel (no contended atomics on one address)
+  __shared__ uint32_t red[2][4];
   uint32_t kmin = hit ? fkey(nr) : 0xFFFFFFFFu;
   uint32_t kmax = hit ? fkey(fr) : 0u;
   for (int o = 32; o > 0; o >>= 1) {
@@ -138,21 +140,47 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
     kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
   }
   if ((threadIdx.x & 63) == 0) {
-    if (kmin != 0xFFFFFFFFu) atomicMin(ws + 0, kmin);
-    if (kmax != 0u) atomicMax(ws + 1, kmax);
+    red[0][threadIdx.x >> 6] = kmin;
+    red[1][threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+    part[2 * blockIdx.x + 1] = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
   }
 }
 
 __global__ void __launch_bounds__(256) rays_fix_kernel(long long n, float* __restrict__ nearp,
                                                        float* __restrict__ farp,
-                                                       const uint32_t* __restrict__ ws,
-                                                       const int* __restrict__ hitflag) {
+                                                       const uint32_t* __restrict__ part, int nparts,
+                                                       const uint8_t* __restrict__ hitflag) {
+  __shared__ uint32_t red[2][4];
   const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
+  const bool live = r < n;
+  const bool miss = live && !hitflag[r];
+  uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+  if (__syncthreads_or(miss)) {     // a ray of this block missed the box: the call's min / max
+    for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
+      kmin = min(kmin, part[2 * i]);
+      kmax = max(kmax, part[2 * i + 1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+      kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = kmin;
+      red[1][threadIdx.x >> 6] = kmax;
+    }
+    __syncthreads();
+    kmin = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+    kmax = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+  }
+  if (!live) return;
   float nr = nearp[r], fr = farp[r];
-  if (!hitflag[r]) {
-    nr = fdecode(ws[0]);
-    fr = fdecode(ws[1]);
+  if (miss) {
+    nr = fdecode(kmin);
+    fr = fdecode(kmax);
   }
   nr = fmaxf(nr, 0.1f);   // clamp_(min=0.1)  (nerf_utils.py:264-265)
   fr = fmaxf(fr, 0.1f);
@@ -377,14 +405,14 @@ int32_t nfi_rays_forward(const nfi_camera* cam, float scene_range, float* ro, fl
   NFI_REQUIRE(scene_range > 0.f && std::isfinite(scene_range), "rays_forward: bad scene_range");
   hipStream_t s = (hipStream_t)stream;
   const long long n = (long long)cam->B * cam->H * cam->W;
-  // ws layout: [0]=min-key, [1]=max-key, [2..] = per-ray hit flags (int)
-  NFI_REQUIRE(hipMemsetAsync(ws, 0xFF, 4, s) == hipSuccess && hipMemsetAsync(ws + 1, 0, 4, s) == hipSuccess,
-              "rays_forward: hipMemsetAsync failed");
+  // ws layout (within the documented 2 + B*H*W words): [0, 2 blocks) = per-block (min, max) keys,
+  // then one hit byte per ray
   const int blocks = (int)((n + 255) / 256);
-  int* hit = reinterpret_cast<int*>(ws + 2);
-  rays_fwd_kernel<<<blocks, 256, 0, s>>>(*cam, scene_range, ro, rd, near_, far_, ws, hit);
+  uint32_t* part = ws;
+  uint8_t* hit = reinterpret_cast<uint8_t*>(ws + 2 * (long long)blocks);
+  rays_fwd_kernel<<<blocks, 256, 0, s>>>(*cam, scene_range, ro, rd, near_, far_, part, hit);
   NFI_CHECK_LAUNCH("rays_fwd_kernel");
-  rays_fix_kernel<<<blocks, 256, 0, s>>>(n, near_, far_, ws, hit);
+  rays_fix_kernel<<<blocks, 256, 0, s>>>(n, near_, far_, part, blocks, hit);
   NFI_CHECK_LAUNCH("rays_fix_kernel");
   return NFI_OK;
 }
