@@ -285,7 +285,16 @@ __global__ void __launch_bounds__(256) segsum_pass1(const float* __restrict__ in
   const int k = tid % K, s = tid / K;
   float acc = 0.f;
   if (s < per) {
-    for (int m = m0 + s; m < m1; m += per) acc += in[((long long)b * M + m) * K + k];
+    // 8 independent partial sums: 8 loads in flight per thread (the grid is only 64 x B blocks)
+    float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* src = in + (long long)b * M * K + k;
+    int m = m0 + s;
+    for (; m + 7 * per < m1; m += 8 * per) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a8[u] += src[(long long)(m + u * per) * K];
+    }
+    for (; m < m1; m += per) a8[0] += src[(long long)m * K];
+    acc = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
   }
   red[tid] = acc;
   __syncthreads();
