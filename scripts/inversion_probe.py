@@ -52,7 +52,7 @@ if os.environ.get('NFI_BLAS'):         # A/B of the BLAS backend behind torch.bm
 
 if __name__ == '__main__':
     if len(sys.argv) > 1:          # python scripts/inversion_probe.py B loss steps
-        run(int(sys.argv[1]), sys.argv[2], steps=int(sys.argv[3]))
+        run(int(sys.argv[1]), sys.argv[2], steps=int(sys.argv[3]), graph=os.environ.get('NFI_GRAPH') == '1')
         sys.exit(0)
     for loss in ('l1', 'vgg'):
         for graph in (False, True):
