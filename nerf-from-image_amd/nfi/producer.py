@@ -300,18 +300,50 @@ class SynthesisNetwork(nn.Module):
         At, bias, W2t, rows, conv_ids = frozen_value(self, 'style_bank', build, *params)
         S = torch.baddbmm(bias, ws.index_select(1, rows).transpose(0, 1), At)        # [L, b, cmax]
         D = (torch.bmm(S.index_select(0, conv_ids).square(), W2t) + 1e-8).rsqrt()   # [Lc, b, omax]
-        styles, dcoefs = S.unbind(0), iter(D.unbind(0))
-        out = []
-        for (m, _, conv), s in zip(layers, styles):
-            n = m.affine.weight.shape[0]
-            s = s if n == s.shape[1] else s[:, :n]
-            if conv:
-                d = next(dcoefs)
-                o = m.weight.shape[0]
-                out.append((s, d if o == d.shape[1] else d[:, :o]))
-            else:
-                out.append(s)
-        return out
+        b = ws.shape[0]
+        s_w = [m.affine.weight.shape[0] for m, _, _ in layers]
+        d_w = [m.weight.shape[0] for m, _, c in layers if c]
+        styles = _PackRows.apply(S, _pack_index(self, 'styles', S.shape, s_w, S.device), b, s_w)
+        dcoefs = iter(_PackRows.apply(D, _pack_index(self, 'dcoefs', D.shape, d_w, D.device), b, d_w))
+        return [(s, next(dcoefs)) if conv else s for (m, _, conv), s in zip(layers, styles)]
+
+
+def _pack_index(mod, key, shape, widths, dev):
+    """Flat positions in a padded [L, b, W] stack of each layer's [b, n_l] block, in layer order
+    (built once per shape on the device: no host copy inside a step)."""
+    cache = mod.__dict__.setdefault('_pack_cache', {})
+    k = (key, tuple(shape), tuple(widths), dev)
+    idx = cache.get(k)
+    if idx is None:
+        L, b, W = shape
+        idx = torch.cat([(l * b * W + torch.arange(b)[:, None] * W + torch.arange(n)[None, :]).reshape(-1)
+                         for l, n in enumerate(widths)]).to(dev)
+        cache[k] = idx
+    return idx
+
+
+class _PackRows(torch.autograd.Function):
+    """A padded [L, b, W] stack -> its L blocks [b, n_l] as contiguous tensors (views of one packed
+    buffer): one gather forward; backward one concatenation of the gradients and one index_copy
+    into the zero-padded stack (instead of a copy per sliced layer forward and a zero-fill + copy
+    per layer backward)."""
+
+    @staticmethod
+    def forward(ctx, X, idx, b, widths):
+        flat = X.reshape(-1).index_select(0, idx)
+        ctx.save_for_backward(idx)
+        ctx.shape, ctx.b, ctx.widths = X.shape, b, widths
+        return tuple(t.view(b, n) for t, n in zip(flat.split([b * n for n in widths]), widths))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        idx, = ctx.saved_tensors
+        b = ctx.b
+        flat = torch.cat([(g if g is not None else idx.new_zeros((b, n), dtype=torch.float32)).reshape(-1)
+                          for g, n in zip(grads, ctx.widths)])
+        G = flat.new_zeros(ctx.shape).view(-1)
+        G.index_copy_(0, idx, flat)
+        return G.view(ctx.shape), None, None, None
 
 
 class MappingNetwork(nn.Module):
