@@ -199,7 +199,10 @@ int32_t nfi_aug_sample_forward(const float* img, const float* grid, float* out, 
                                int32_t W, int32_t Ho, int32_t Wo, float shift, void* stream);
 
 /* Its adjoint summed over the K copies: gout [B*K][3][Ho][Wo] -> gimg [B][H][W][3] (overwritten),
- * gathered per input pixel (no atomics; grid_sampler_2d_backward's weights). */
+ * gathered per input pixel (no atomics; grid_sampler_2d_backward's weights).  Each copy's grid
+ * must be an affine function of the output pixel (F.affine_grid, as augment_impl builds it): the
+ * output pixels that sample an input pixel are enumerated in the preimage of its neighbourhood
+ * under that map (read off the grid's corners), so a non-affine grid would lose contributions. */
 int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gimg, int32_t B, int32_t K, int32_t H,
                                 int32_t W, int32_t Ho, int32_t Wo, void* stream);
 

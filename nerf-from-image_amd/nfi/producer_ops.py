@@ -316,7 +316,9 @@ def aug_sample(img, grid, copies: int, white_background: bool = False):
     last, as rendered) -> [B*copies, 3, Ho, Wo] = grid_sample(img[b] (- 1), grid[b*copies + k],
     bilinear, zeros, align_corners=False) (+ 1 on white backgrounds), without materializing the
     expanded copies; the backward gathers each input pixel's share from all copies (no atomics,
-    nfi_aug_sample_backward) into d img [B, H, W, 3]."""
+    nfi_aug_sample_backward) into d img [B, H, W, 3].  Each copy's grid must be affine in the
+    output pixel (F.affine_grid, as inversion.augment_grid builds it): the adjoint enumerates the
+    preimage of each input pixel's neighbourhood under that map."""
     _require_device(img, grid)
     if img.shape[-1] != 3 or grid.shape[0] != img.shape[0] * copies or grid.shape[-1] != 2:
         raise ValueError(f'aug_sample: img {tuple(img.shape)} / grid {tuple(grid.shape)} / copies {copies}')
