@@ -13,6 +13,7 @@
  *   LPIPS distance head      metrics.py:130-146 (lpips 0.1) normalise, difference, lin, mean
  *   LPIPS VGG16 epilogue     bias + ReLU (+ 2x2 max pool) after each trunk convolution
  *   LPIPS augmented copies   run.py:720-767 (grid_sample of 15 affine copies, gathered adjoint)
+ *   LPIPS first layer        vgg16.features[0:2]: direct 3x3 conv + bias + ReLU, one pass each way
  *
  * Tensors are NCHW float32, contiguous; "planes" P = B*C images of one channel; per-plane
  * scales `d` have P entries ([B,C] row-major), per-channel biases C entries.  `stream` is a
