@@ -1238,8 +1238,14 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
 
   const int i = e * 64 + l;
   const bool v = i < N;
-  const float te = v ? a.t_saved[r * N + i] : R.near_;
-  const int ei = v ? (int)a.perm[r * N + i] : 0;
+  // every per-sample load is issued at a clamped valid index and masked by a select afterwards
+  // (a lane-guarded load becomes an exec-mask branch with a vmcnt(0) wait after it)
+  const long long ic = r * N + min(i, N - 1);
+  const float t_ld = a.t_saved[ic];
+  const int p_ld = (int)a.perm[ic];
+  const float gs_ld = g.gsig[ic], w_ld = g.wts[ic];
+  const float te = v ? t_ld : R.near_;
+  const int ei = v ? p_ld : 0;
   float pmask;
   {
     PointP P;
@@ -1258,14 +1264,17 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     for (int sb = 0; sb < 4; ++sb) eis[sb] = __shfl(ei, 16 * sb + j);
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
-      const int ip = e * 64 + 16 * sb + j;
-      xa[sb] = f4v{0.f, 0.f, 0.f, 0.f};
-      xb[sb] = xa[sb];
-      if (ip < N) {
-        const float* xr = a.x_saved + (r * N + eis[sb]) * NC + 8 * q;
-        xa[sb] = ld4(xr);
-        xb[sb] = ld4(xr + 4);
-      }
+      // (points past N have ei = 0: row 0 of this ray is loaded and zeroed by the select)
+      const float* xr = a.x_saved + (r * N + eis[sb]) * NC + 8 * q;
+      xa[sb] = ld4(xr);
+      xb[sb] = ld4(xr + 4);
+    }
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const bool vp = e * 64 + 16 * sb + j < N;
+      const f4v z{0.f, 0.f, 0.f, 0.f};
+      xa[sb] = vp ? xa[sb] : z;
+      xb[sb] = vp ? xb[sb] : z;
     }
   }
   NFI_STAMP(17)
@@ -1274,7 +1283,9 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
   {
     const float* ys = a.y_saved + r * NOUT * N + ei;
 #pragma unroll
-    for (int k = 0; k < NOUT; ++k) y[k] = v ? ys[k * N] : 0.f;
+    for (int k = 0; k < NOUT; ++k) y[k] = ys[k * N];
+#pragma unroll
+    for (int k = 0; k < NOUT; ++k) y[k] = v ? y[k] : 0.f;
   }
   float gy[NO];
   float y11[NO];
@@ -1288,7 +1299,7 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     Head h;
     const int heads = VARIANT ? a.field.heads : 0;
     head_forward(y11, pmask, a.field.inv_alpha, a.field.beta, pal, heads, h);
-    const float gs = v ? g.gsig[r * N + i] : 0.f;
+    const float gs = v ? gs_ld : 0.f;
     if (heads & NFI_HEAD_NERF_DENSITY) {
       // sigma -> d: softplus_backward of d - 1 (ATen: z > 20 ? g : g * e^z / (e^z + 1)), :637-641
       const float z = fsub(y11[0], 1.f);
@@ -1303,7 +1314,7 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
       const float gcdf = (gs * a.field.inv_alpha) * (1.f - pmask);
       gy[0] = -(((gcdf * 0.5f * sgn) * ex2 / a.field.beta) * sgn);
     }
-    const float w = v ? g.wts[r * N + i] : 0.f;
+    const float w = v ? w_ld : 0.f;
     const float gc0 = w * gr0, gc1 = w * gr1, gc2 = w * gr2;
     if (heads & NFI_HEAD_RGB_SIGMOID) {
       // rgb -> features: (g * 2.004) * (1 - s) * s  (sigmoid backward), no palette
