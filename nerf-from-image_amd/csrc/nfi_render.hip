@@ -1602,6 +1602,9 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 #ifndef NFI_TILE_DBUF
 #define NFI_TILE_DBUF 0   // 1: two batches of rows in registers at occupancy 3 (measured 2.64 vs 2.28 ms)
 #endif
+#ifndef NFI_TILE_COALESCED
+#define NFI_TILE_COALESCED 1   // 0: each lane loads its own entry's whole row (8 b128 loads, 56 rows each)
+#endif
 constexpr int BATCH = 56;
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
@@ -1721,7 +1724,10 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       int cur = 0;
       float a0 = 0.f, a1 = 0.f;
       const cint4_p L = (cint4_p)A.list;
-      float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
+      float4 r0, r1, r2, r3, r4, r5, r6;   // named (an array here is not promoted to registers)
+#if NFI_TILE_DBUF || !NFI_TILE_COALESCED
+      float4 r7;
+#endif
 #define NFI_LOAD_ROW(P, REC)                                                                     \
   {                                                                                              \
     const float4* src_ = reinterpret_cast<const float4*>(A.gfeat + (long long)(REC).x * NC);     \
@@ -1788,6 +1794,55 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         if (bb + BATCH >= b1) break;
         NFI_BATCH(bb + BATCH, s, vrecb, 2 * BATCH)
       }
+#elif NFI_TILE_COALESCED
+      // Rows loaded coalesced: lane l holds float4 (l & 7) of entry 8j + (l >> 3), j = 0..6 (the
+      // entry's row index comes from its lane's record by ds_bpermute): each b128 load reads 8
+      // whole 128-B rows instead of one 16-B piece of 56 different rows.
+#define NFI_LD1(J, V, SX)                                                                            \
+  {                                                                                                  \
+    const int row_ = __shfl((SX), 8 * (J) + (l >> 3));                                              \
+    V = *reinterpret_cast<const float4*>(A.gfeat + (long long)row_ * NC + 4 * (l & 7));             \
+  }
+#define NFI_LOAD_ROWC(REC)                                                                           \
+  {                                                                                                  \
+    const int sx_ = (REC).x;                                                                         \
+    NFI_LD1(0, r0, sx_) NFI_LD1(1, r1, sx_) NFI_LD1(2, r2, sx_) NFI_LD1(3, r3, sx_)                  \
+    NFI_LD1(4, r4, sx_) NFI_LD1(5, r5, sx_) NFI_LD1(6, r6, sx_)                                      \
+  }
+#define NFI_ST1(J, V)                                                                                \
+  {                                                                                                  \
+    const int e_ = 8 * (J) + (l >> 3);                                                               \
+    *reinterpret_cast<float4*>(G + e_ * XS + 4 * (l & 7)) = e_ < n ? V : make_float4(0.f, 0.f, 0.f, 0.f); \
+  }
+#define NFI_BATCHC(BASE, VREC, AHEAD)                                                                \
+  {                                                                                                  \
+    const int base_ = (BASE);                                                                        \
+    const int n = min(BATCH, b1 - base_);                                                            \
+    NFI_ST1(0, r0) NFI_ST1(1, r1) NFI_ST1(2, r2) NFI_ST1(3, r3) NFI_ST1(4, r4) NFI_ST1(5, r5)        \
+    NFI_ST1(6, r6)                                                                                   \
+    wave_lds_sync();                                                                                 \
+    if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
+    VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];                                                 \
+    NFI_LOAD_ROWC(VREC)                                                                              \
+    NFI_STAMP(24)                                                                                    \
+    iv4 ra[8], rb[8];                                                                                \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];                             \
+    for (int u = 0; u < n; u += 16) {                                                                \
+      NFI_STEP(u, ra, rb)                                                                            \
+      if (u + 8 >= n) break;                                                                         \
+      NFI_STEP(u + 8, rb, ra)                                                                        \
+    }                                                                                                \
+    wave_lds_sync();                                                                                 \
+    NFI_STAMP(25)                                                                                    \
+  }
+      static_assert(BATCH == 56, "7 coalesced row loads of 8 entries per batch");
+      int4 vrec = A.list[min(b0 + l, b1 - 1)];
+      NFI_LOAD_ROWC(vrec)
+      for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
+#undef NFI_BATCHC
+#undef NFI_ST1
+#undef NFI_LOAD_ROWC
+#undef NFI_LD1
 #else
       int4 vrec = A.list[min(b0 + l, b1 - 1)];
       NFI_LOAD_ROW(r, vrec)
