@@ -1605,14 +1605,18 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 #ifndef NFI_TILE_COALESCED
 #define NFI_TILE_COALESCED 1   // 0: each lane loads its own entry's whole row (8 b128 loads, 56 rows each)
 #endif
-constexpr int BATCH = 56;
+#ifndef NFI_TILE_BATCH
+#define NFI_TILE_BATCH 56
+#endif
+constexpr int BATCH = NFI_TILE_BATCH;
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 __device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
 // the tile's 8x5 plane texels x 32 channels (pose gradients), texel rows of XS floats (per-lane
 // b128 reads of different texels conflict only for texels 16 slots apart)
 constexpr int TEXF = TTX * TTY * XS;            // 1,440 floats
-constexpr int TILE_LDS = 4 * TROWS + TEXF;      // 40,320 B: 4 workgroups per CU
+// (the wave images are dumped over the stages and texels at the end of a chunk: >= 4 x 2,048)
+constexpr int TILE_LDS = (4 * TROWS + TEXF > 4 * 2048) ? 4 * TROWS + TEXF : 4 * 2048;   // 38,016 B at BATCH 56
 
 // img[slot] += a0, img[slot + 1] += a1 for a wave-uniform slot: M0-indexed source AND
 // destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
@@ -1724,9 +1728,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       int cur = 0;
       float a0 = 0.f, a1 = 0.f;
       const cint4_p L = (cint4_p)A.list;
-      float4 r0, r1, r2, r3, r4, r5, r6;   // named (an array here is not promoted to registers)
 #if NFI_TILE_DBUF || !NFI_TILE_COALESCED
-      float4 r7;
+      float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
 #endif
 #define NFI_LOAD_ROW(P, REC)                                                                     \
   {                                                                                              \
@@ -1806,8 +1809,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #define NFI_LOAD_ROWC(REC)                                                                           \
   {                                                                                                  \
     const int sx_ = (REC).x;                                                                         \
-    NFI_LD1(0, r0, sx_) NFI_LD1(1, r1, sx_) NFI_LD1(2, r2, sx_) NFI_LD1(3, r3, sx_)                  \
-    NFI_LD1(4, r4, sx_) NFI_LD1(5, r5, sx_) NFI_LD1(6, r6, sx_)                                      \
+    _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_LD1(j, rc[j], sx_)                     \
   }
 #define NFI_ST1(J, V)                                                                                \
   {                                                                                                  \
@@ -1818,8 +1820,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
   {                                                                                                  \
     const int base_ = (BASE);                                                                        \
     const int n = min(BATCH, b1 - base_);                                                            \
-    NFI_ST1(0, r0) NFI_ST1(1, r1) NFI_ST1(2, r2) NFI_ST1(3, r3) NFI_ST1(4, r4) NFI_ST1(5, r5)        \
-    NFI_ST1(6, r6)                                                                                   \
+    _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_ST1(j, rc[j])                         \
     wave_lds_sync();                                                                                 \
     if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
     VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];                                                 \
@@ -1835,7 +1836,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     wave_lds_sync();                                                                                 \
     NFI_STAMP(25)                                                                                    \
   }
-      static_assert(BATCH == 56, "7 coalesced row loads of 8 entries per batch");
+      static_assert(BATCH % 8 == 0, "coalesced row loads of 8 entries each");
+      float4 rc[BATCH / 8];
       int4 vrec = A.list[min(b0 + l, b1 - 1)];
       NFI_LOAD_ROWC(vrec)
       for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
@@ -2091,7 +2093,10 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
 
 // d planes and the per-(sample, plane) grid gradients of the pose path, one workgroup per tile
 // chunk (the grid is sized for a bound on the chunk count; blocks past meta[0] exit at once).
-__global__ void __launch_bounds__(256, NFI_TILE_DBUF ? 3 : 4) tile_kernel(TileArgs A) {
+#ifndef NFI_TILE_OCC
+#define NFI_TILE_OCC (NFI_TILE_DBUF ? 3 : 4)
+#endif
+__global__ void __launch_bounds__(256, NFI_TILE_OCC) tile_kernel(TileArgs A) {
   __shared__ __attribute__((aligned(16))) float lds[TILE_LDS];
   if ((long long)blockIdx.x >= A.meta[0]) return;
   tile_chunk(A, lds, (int)blockIdx.x);
