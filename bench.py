@@ -246,7 +246,7 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
                                    'package offline)' if net is not None else ''),
             'loss_first_last': [round(res.losses[0], 5), round(res.losses[-1], 5)],
             'producer': 'StyleGAN2 synthesis 256^2x96 + AttentionMapper, fp32: 3x3 convs Winograd F(4,3) '
-                        '(nfi HIP transforms + hipBLASLt batched GEMM), transposed convs MIOpen, '
+                        '(nfi HIP transforms + hipBLASLt batched GEMM), up-sampling convs as one 9-tap GEMM + HIP FIR, '
                         'epilogues/FIR/skip/modulation-backward nfi HIP',
             'renderer': 'nfi HIP fwd+bwd',
             'step_replay': ('HIP graph of the whole step (captured in the warm-up batch, reused)'

@@ -17,6 +17,7 @@ SHAPES = [(2, 16, 24, 8, 8), (3, 64, 64, 16, 12), (2, 128, 96, 32, 32), (1, 512,
 
 
 def _err(a, ref):
+    ref = ref.detach()
     return float((a.detach().double().cpu() - ref).abs().max() / ref.abs().max())
 
 
