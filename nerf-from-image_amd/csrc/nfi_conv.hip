@@ -391,6 +391,10 @@ __device__ __forceinline__ void emit_tile(float (&m)[6][6], float b, int mode, f
   }
 }
 
+#ifndef NFI_WINO_ADEPTH
+#define NFI_WINO_ADEPTH 3   // 1: the previous one-product-ahead A loads
+#endif
+
 // grid (ceil(P / FP), CoP / FC), 256 threads, one workgroup per CU (occupancy 1: 288
 // accumulator registers per lane, the next chunk's A operands and patch prefetched a whole
 // chunk ahead).  Ci % FK == 0.
@@ -447,9 +451,15 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const float* __restrict__
   };
 
   float d[6][6];
-  float an[HB][2];
+  // A operands AD products ahead (ring slot = product index % AD; 9 % AD == 0 keeps the slot of
+  // product (c, xl) a compile-time xl % AD): an L2 round trip under load outlasts one product's
+  // 16 MFMAs, and at occupancy 1 no other wave covers it
+  constexpr int AD = NFI_WINO_ADEPTH;
+  static_assert(9 % AD == 0, "A-operand prefetch depth divides the 9 products of a wave");
+  float an[AD][HB][2];
   load_patch(xs, H, W, sty, stx, pvalid, d);
-  load_a(0, 0, an);
+#pragma unroll
+  for (int u = 0; u < AD; ++u) load_a(u, 0, an[u]);
   stage_patch(d, vdst);
   __syncthreads();
   for (int c = 0; c < nk; ++c) {
@@ -469,20 +479,19 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const float* __restrict__
 #pragma unroll
       for (int h = 0; h < HB; ++h)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) a[h][s2] = an[h][s2];
+        for (int s2 = 0; s2 < 2; ++s2) a[h][s2] = an[xl % AD][h][s2];
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int g = 0; g < 2; ++g) b[s2][g] = bn[s2][g];
+      if (xl + AD < 9) load_a(xl + AD, c, an[xl % AD]);
+      else if (c + 1 < nk) load_a(xl + AD - 9, c + 1, an[xl % AD]);
       if (xl + 1 < 9) {
-        load_a(xl + 1, c, an);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int g = 0; g < 2; ++g)
             bn[s2][g] = V[((xi + 1) * FK + 4 * s2 + kk) * FP + ((16 * g + cc + 16 * (kk & 1)) & 31)];
-      } else if (c + 1 < nk) {
-        load_a(0, c + 1, an);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)

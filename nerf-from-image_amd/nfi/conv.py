@@ -35,11 +35,12 @@ FOLD_SCALE = os.environ.get('NFI_FOLD_SCALE', '1') == '1'   # modulation folded 
 FUSED = True          # one fused kernel per layer (nfi_wino_conv_fused) for layers with Ci % 8 == 0
                       # and Ci <= FUSED_MAX_CI; else the three-pass form (transforms + hipBLASLt GEMM)
 # The fused kernel keeps V and M on chip but its 36-way split accumulators leave small per-product
-# tiles: 39-53 TFLOP/s of Winograd products on MI355X vs 100-137 for hipBLASLt's batched GEMM.  It
+# tiles: 46-64 TFLOP/s of Winograd products on MI355X vs 100-137 for hipBLASLt's batched GEMM.  It
 # wins where the three-pass form's HBM round trips dominate — the 64-channel, large-map layers
-# (LPIPS 64->64 @128^2: 0.50 vs 0.68 ms) — and loses on the deeper ones (512->512 @16^2: 0.37 vs
+# (LPIPS 64->64 @128^2: 0.42 vs 0.68 ms; Ci = 128 is a per-layer tie that loses over the step:
+# NFI_FUSED_MAX_CI=128 measured 18.9 vs 18.8 ms) — and loses on the deeper ones (512->512 @16^2: 0.32 vs
 # 0.21 ms); scripts/wino_layers.py.
-FUSED_MAX_CI = 64
+FUSED_MAX_CI = int(os.environ.get('NFI_FUSED_MAX_CI', '64'))
 # the VGG blocks' ReLU threshold_backward inside the data gradient's input transform (no pool
 # gradient; three-pass layers)
 RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
