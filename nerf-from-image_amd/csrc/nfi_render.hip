@@ -372,7 +372,7 @@ __device__ __forceinline__ f4v layer1(f4v ta, f4v tb, f4v b, f4v xa, f4v xb) {
 
 // Decoder forward for the points of the wave's X tile (LDS, rows of XS floats); returns point
 // l's NOUT outputs.  The tile is reused as scratch (callers re-sync before writing it).
-template <int NOUT>
+template <int NOUT, bool PREFETCH>
 __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, float* __restrict__ X,
                                                  float y[NOUT]) {
   using L = DecL<NOUT>;
@@ -389,12 +389,10 @@ __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, 
   for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) Y[ob][sb] = f4v{0.f, 0.f, 0.f, 0.f};
-#ifndef NFI_MLP_PREFETCH
-#define NFI_MLP_PREFETCH 1
-#endif
-#if NFI_MLP_PREFETCH
+  if constexpr (PREFETCH) {
   // operand tables of hidden block hb + 1 are loaded while block hb runs (L1/L2 round trips
-  // otherwise serialise with the MFMA chains: 16 more VGPRs, within occupancy 3)
+  // otherwise serialise with the MFMA chains: 16 more VGPRs — used by the occupancy-2 kernels;
+  // the inversion forward runs at occupancy 4 without them, render_fwd_kernel)
   f4v ta = ld4(dec + L::DT1 + l * 8), tb = ld4(dec + L::DT1 + l * 8 + 4);
   f4v b = ld4(dec + L::DB1 + l * 4);
   f4v t2[NOB];
@@ -430,7 +428,7 @@ __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, 
 #pragma unroll
     for (int ob = 0; ob < NOB; ++ob) t2[ob] = nt2[ob];
   }
-#else
+  } else {
 #pragma unroll
   for (int hb = 0; hb < 4; ++hb) {
     const f4v ta = ld4(dec + L::DT1 + (hb * 64 + l) * 8), tb = ld4(dec + L::DT1 + (hb * 64 + l) * 8 + 4);
@@ -447,7 +445,7 @@ __device__ __forceinline__ void mlp_forward_tile(const float* __restrict__ dec, 
       }
     }
   }
-#endif
+  }
   // lane (j, q) holds outputs 16ob + 4q..4q+3 of point 16sb + j: transpose through the tile
   // (outputs past NOUT's last quad are not stored: 33 outputs use columns 0..35 of the XS = 36 row)
   wave_lds_sync();
@@ -698,7 +696,7 @@ __device__ __forceinline__ void load_ray(const nfi_render_args& a, long long r, 
 }
 
 // Evaluate the field at the (up to 64) points t (one per lane; lanes >= npts ignored).
-template <int NOUT>
+template <int NOUT, bool MLP_PREFETCH>
 __device__ __forceinline__ void field_eval(const nfi_render_args& a, const PlaneView& pv, const RayCtx& R,
                                            float t, int npts, float* __restrict__ X, float& sigma,
                                            float rgb[3], int eval_base NFI_STAMP_PARAM) {
@@ -718,7 +716,7 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   }
   NFI_STAMP(1)
   float y[NOUT];
-  mlp_forward_tile<NOUT>(a.field.dec, X, y);
+  mlp_forward_tile<NOUT, MLP_PREFETCH>(a.field.dec, X, y);
   NFI_STAMP(2)
   if (a.y_saved && lane_id() < npts) {     // (no saved state in forward-only calls)
     const int N = a.fine ? 2 * a.S : a.S;
@@ -774,12 +772,16 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 // ---------------------------------------------------------------------------------------
 // Forward kernel.  SPL = coarse samples per lane (S <= 64*SPL), NPL = merged per lane.
 // ---------------------------------------------------------------------------------------
+// The inversion-sized kernels (<= 128 merged samples, 11 outputs) run at occupancy 4: 128 VGPRs
+// with the decoder tables loaded at their use (4 VGPRs spill, outside the loops); with the
+// tables prefetched a hidden block ahead they need 147 (occupancy 3): forward 2.39 vs 2.51 ms.
 #ifndef NFI_FWD_OCC
-#define NFI_FWD_OCC 3
+#define NFI_FWD_OCC 4
 #endif
 template <int SPL, int NPL, bool FINE, int NOUT>
 __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NFI_FWD_OCC : 2)
     render_fwd_kernel(nfi_render_args a) {
+  constexpr bool MLP_PF = !(NPL <= 2 && SPL <= 2 && NOUT == NO && NFI_FWD_OCC >= 4);
   constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
   // per-wave LDS: the X tile; the merge / sample_pdf arrays alias it (they are live only
   // outside field_eval), which keeps a workgroup at 36 KiB
@@ -824,7 +826,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NF
     tc[e] = t;
     sc[e] = 0.f;
     cc[e][0] = cc[e][1] = cc[e][2] = 0.f;
-    if (e * 64 < S) field_eval<NOUT>(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64 NFI_STAMP_ARG);
+    if (e * 64 < S) field_eval<NOUT, MLP_PF>(a, pv, R, t, min(64, S - e * 64), X, sc[e], cc[e], e * 64 NFI_STAMP_ARG);
   }
 
   if constexpr (FINE) {
@@ -930,7 +932,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NF
     for (int e = 0; e < SPL; ++e) {
       sf[e] = 0.f;
       cf[e][0] = cf[e][1] = cf[e][2] = 0.f;
-      if (e * 64 < S) field_eval<NOUT>(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64 NFI_STAMP_ARG);
+      if (e * 64 < S) field_eval<NOUT, MLP_PF>(a, pv, R, tf[e], min(64, S - e * 64), X, sf[e], cf[e], S + e * 64 NFI_STAMP_ARG);
     }
     // ---- merge: stable sort of cat(z_coarse, z_fine) (run.py:283-288, 312-319) ----
 #pragma unroll
