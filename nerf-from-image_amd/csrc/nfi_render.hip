@@ -778,10 +778,15 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 #ifndef NFI_FWD_OCC
 #define NFI_FWD_OCC 4
 #endif
+#ifndef NFI_FWD_OCC4
+#define NFI_FWD_OCC4 3   // the 256-merged-sample kernel (imagenet_256)
+#endif
 template <int SPL, int NPL, bool FINE, int NOUT>
-__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NFI_FWD_OCC : 2)
+__global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NFI_FWD_OCC
+                                       : ((NPL <= 4 && SPL <= 2 && NOUT == NO) ? NFI_FWD_OCC4 : 2))
     render_fwd_kernel(nfi_render_args a) {
-  constexpr bool MLP_PF = !(NPL <= 2 && SPL <= 2 && NOUT == NO && NFI_FWD_OCC >= 4);
+  constexpr bool MLP_PF = !(NOUT == NO && SPL <= 2 &&
+                            ((NPL <= 2 && NFI_FWD_OCC >= 4) || (NPL <= 4 && NFI_FWD_OCC4 >= 3)));
   constexpr int SMAX = 64 * SPL, NMAX = 64 * NPL;
   // per-wave LDS: the X tile; the merge / sample_pdf arrays alias it (they are live only
   // outside field_eval), which keeps a workgroup at 36 KiB
