@@ -1609,6 +1609,9 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 #ifndef NFI_TILE_DBUF
 #define NFI_TILE_DBUF 0   // 1: two batches of rows in registers at occupancy 3 (measured 2.64 vs 2.28 ms)
 #endif
+#ifndef NFI_TILE_REC2
+#define NFI_TILE_REC2 1   // records loaded two batches ahead (coalesced form)
+#endif
 #ifndef NFI_TILE_COALESCED
 #define NFI_TILE_COALESCED 1   // 0: each lane loads its own entry's whole row (8 b128 loads, 56 rows each)
 #endif
@@ -1823,6 +1826,13 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int e_ = 8 * (J) + (l >> 3);                                                               \
     *reinterpret_cast<float4*>(G + e_ * XS + 4 * (l & 7)) = e_ < n ? V : make_float4(0.f, 0.f, 0.f, 0.f); \
   }
+#if NFI_TILE_REC2
+#define NFI_NEXT_REC(VREC, AHEAD)                                                                    \
+    VREC = vnext;                                                                                    \
+    vnext = A.list[min(base_ + 2 * (AHEAD) + l, b1 - 1)];
+#else
+#define NFI_NEXT_REC(VREC, AHEAD) VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];
+#endif
 #define NFI_BATCHC(BASE, VREC, AHEAD)                                                                \
   {                                                                                                  \
     const int base_ = (BASE);                                                                        \
@@ -1830,7 +1840,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_ST1(j, rc[j])                         \
     wave_lds_sync();                                                                                 \
     if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
-    VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];                                                 \
+    NFI_NEXT_REC(VREC, AHEAD)                                                                        \
     NFI_LOAD_ROWC(VREC)                                                                              \
     NFI_STAMP(24)                                                                                    \
     iv4 ra[8], rb[8];                                                                                \
@@ -1846,9 +1856,15 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       static_assert(BATCH % 8 == 0, "coalesced row loads of 8 entries each");
       float4 rc[BATCH / 8];
       int4 vrec = A.list[min(b0 + l, b1 - 1)];
+#if NFI_TILE_REC2
+      // the next batch's records are already in registers when its rows are issued (the row
+      // loads do not wait a record round trip)
+      int4 vnext = A.list[min(b0 + BATCH + l, b1 - 1)];
+#endif
       NFI_LOAD_ROWC(vrec)
       for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
 #undef NFI_BATCHC
+#undef NFI_NEXT_REC
 #undef NFI_ST1
 #undef NFI_LOAD_ROWC
 #undef NFI_LD1
