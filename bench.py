@@ -88,6 +88,36 @@ def conversion_ms(planes, ops, reps=5):
     return round(e0.elapsed_time(e1) / reps, 4)
 
 
+def cpu_model() -> str:
+    """lscpu's 'Model name' (the /proc/cpuinfo model name when lscpu is absent)."""
+    import subprocess
+    try:
+        out = subprocess.run(['lscpu'], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.strip().startswith('Model name'):
+                return line.split(':', 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None when unlimited / unreadable."""
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == 'max' else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args):
     """The CPU oracle (oracle/render_oracle.py, the reference's op graph in PyTorch) timed on this
     host's cores on a bounded sample of the same workload: ONE 128x128 image, 64+64 samples,
@@ -95,11 +125,12 @@ def cpu_baseline(args):
     from oracle import render_oracle as orc
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     from gpu_helpers import synthetic_inputs
+    # SURVEY §8(d) CPU-baseline plan: every core of this process's affinity set
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
+    cores = max(1, cores)
     torch.set_num_threads(cores)
     H = args.cpu_res
     inp, meta = synthetic_inputs(B=1, H=H, W=H, S=64, R=256, scene_range=1.4, seed=0)
@@ -121,18 +152,13 @@ def cpu_baseline(args):
         times.append(time.perf_counter() - t0)
     t = sorted(times)[len(times) // 2]
     samples = H * H * 128
-    model = ''
-    try:
-        with open('/proc/cpuinfo') as fh:
-            for line in fh:
-                if line.startswith('model name'):
-                    model = line.split(':', 1)[1].strip()
-                    break
-    except OSError:
-        pass
+    model = cpu_model()
     out = {'value': samples / t / 1e6, 'unit': 'Msamples/s', 'cores': cores, 'kind': 'port',
            'sample': f'1 image {H}x{H}, 64+64 samples/ray, fwd+bwd (planes, palette, pose grads), '
-                     f'median of {args.cpu_reps} after 1 warm-up; {model or platform.processor()}',
+                     f'median of {args.cpu_reps} after 1 warm-up; torch.set_num_threads({cores}) = '
+                     f'len(sched_getaffinity); {model}',
+           'cpu_model': model, 'cgroup_cpu_quota': cgroup_cpu_quota(),
+           'reps_seconds': [round(x, 3) for x in times],
            'seconds_per_image_step': t}
     if not args.no_inversion:
         inv = cpu_inversion_step(inp, H, args.inv_loss.split(','))
@@ -187,19 +213,22 @@ def max_over_ranks(x: float, dev) -> float:
     return float(t.item())
 
 
-def inversion_leg(args, dev, cfg, batch, world, loss):
+def inversion_leg(args, dev, cfg, world, loss):
     """BASELINE.json's second number: seconds per image of the 30-step inversion (run.py:1960-2310,
-    pose optimised): per step the producer (synthesis network + AttentionMapper: convolutions on
-    MIOpen, the rest in the fused HIP kernels, fp32) forward, the HIP render fwd+bwd, the loss
-    ('vgg' = the reference default --inv_loss: LPIPS-VGG over the image + 15 augmented copies,
-    random weights since none ship offline; or 'l1'), the backward to the latent and pose, Adam.
-    Random-init generator (no checkpoint offline), z_avg from the mapping network, the first
-    --inv-batch (default 4 = BASELINE configs[3]'s 32 images over 8 GPUs) cameras of the
-    renderer leg, a synthetic target image.  Timed like the renderer leg (barrier +
-    synchronize around exactly --inv-steps steps, max over ranks)."""
-    from nfi import inversion, lpips, ops, producer
+    pose optimised), BASELINE configs[3]: a global batch of --inv-batch images per GPU (4: 32 over 8
+    GPUs) split over the ranks by nfi.parallel.invert_sharded (DataParallel's torch.chunk,
+    run.py:636-640, 1757; every rank holds the whole batch's targets and cameras, inverts its
+    chunk, and the per-image results are all_gathered — over RCCL under torchrun).  Per step the
+    producer (synthesis network + AttentionMapper, fp32), the HIP render fwd+bwd, the loss ('vgg' =
+    the reference default --inv_loss: LPIPS-VGG over the image + 15 augmented copies, random
+    weights since none ship offline; or 'l1'), the backward to the latent and pose, Adam.
+    Random-init generator (no checkpoint offline), z_avg from the mapping network, seeded cameras
+    (nfi.synthetic.cameras), a synthetic target image.  Timed like the renderer leg (barrier +
+    synchronize around exactly --inv-steps steps, max over ranks); the final all_gather of the
+    results is inside the timed region."""
+    from nfi import inversion, lpips, ops, parallel, producer, synthetic
     sr, wbg, flipped, _, H, S, pose, bwd = cfg
-    B = args.inv_batch              # BASELINE configs[3]: batch 32 over 8 GPUs = 4 per GPU
+    B = args.inv_batch * world      # the global step batch
     torch.manual_seed(4321)
     gen = producer.InversionGenerator(scene_range=sr).to(dev)
     with torch.no_grad():
@@ -208,27 +237,29 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
     w_avg = gen.mapping_network.get_average_w(generator=torch.Generator().manual_seed(7))
     g = torch.Generator(device=dev).manual_seed(99)
     target = torch.tanh(torch.randn((B, H, H, 3), generator=g, device=dev))
+    cam, focal = synthetic.cameras(B, sr, 4321, flipped=flipped, device=dev)
     icfg = inversion.InversionConfig(steps=2, resolution=H, samples=S, loss=loss,
                                      camera_flipped=flipped, white_background=wbg,
                                      graph=args.inv_graph)
     net = lpips.LPIPS().to(dev) if loss in inversion.VGG_LOSSES else None
-    cam, focal = batch['cam'][:B].detach(), batch['focal'][:B].detach()
     # warm-up: library plans (MIOpen / hipBLASLt), frozen-weight caches, and the step's HIP graph
     # (captured after inversion.EAGER_STEPS eager steps; the timed batch reuses it, as every later
-    # batch of a run does).  The renderer's share is timed with HIP events on the eager steps.
+    # batch of a run does)
     icfg.steps = inversion.EAGER_STEPS + 1 if icfg.graph else 2
+    parallel.invert_sharded(gen, target, cam, focal, w_avg, icfg, lpips_net=net)
+    # the renderer's share: HIP events over one further eager step (first-launch costs excluded)
     ops.KERNEL_TIMERS = {}
-    inversion.invert(gen, target, cam, focal, w_avg, icfg, lpips_net=net)
+    icfg.steps = 1
+    parallel.invert_sharded(gen, target, cam, focal, w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
-    eager = max(1, len(timers.get('render_fwd', [])))
-    render_ms = sum(a.elapsed_time(b) for v in timers.values() for a, b in v) / eager
+    render_ms = sum(a.elapsed_time(b) for v in timers.values() for a, b in v)
     icfg.steps = args.inv_steps
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = inversion.invert(gen, target, cam, focal, w_avg, icfg, lpips_net=net)
+    res = parallel.invert_sharded(gen, target, cam, focal, w_avg, icfg, lpips_net=net)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -236,12 +267,15 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
     step_ms = elapsed / icfg.steps * 1e3
-    # s/image of a 30-step inversion (run.py:1829-1830: checkpoint_steps [0, 30] by default): all ranks together
-    # finish B * world images per `elapsed` for icfg.steps steps
-    return {'s_per_image': round(elapsed * 30 / icfg.steps / (B * world), 5), 'steps': icfg.steps,
-            'images': B * world, 'images_per_gpu': B, 'seconds': round(elapsed, 4), 'ms_per_step': round(step_ms, 3),
+    # s/image of a 30-step inversion (run.py:1829-1830: checkpoint_steps [0, 30] by default): all ranks
+    # together finish the B-image batch in `elapsed` for icfg.steps steps
+    return {'s_per_image': round(elapsed * 30 / icfg.steps / B, 5), 'steps': icfg.steps,
+            'images': B, 'images_per_gpu': args.inv_batch, 'seconds': round(elapsed, 4),
+            'ms_per_step': round(step_ms, 3),
             'render_ms_per_step': round(render_ms, 3),
             'rest_ms_per_step': round(step_ms - render_ms, 3),
+            'sharding': f'nfi.parallel.invert_sharded: {B} images over {world} rank(s), torch.chunk, '
+                        f'results all_gathered ({dist.get_backend() if world > 1 else "single process"})',
             'loss': loss + (' (LPIPS-VGG, random weights, 16 copies; parity unpinned: no lpips weights or '
                                    'package offline)' if net is not None else ''),
             'loss_first_last': [round(res.losses[0], 5), round(res.losses[-1], 5)],
@@ -253,6 +287,41 @@ def inversion_leg(args, dev, cfg, batch, world, loss):
                             if icfg.graph else 'eager launches')}
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without torchrun (WORLD_SIZE unset): start N rank processes of
+    this script, one per GPU, torchrun-style (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), before
+    anything here touches the GPU, wait for them and return the worst exit code.  Refuses when
+    the node has fewer devices than ranks (RCCL needs one GPU per rank): it never reports a run
+    of fewer GPUs under n_gpus N."""
+    import subprocess
+    backend = os.environ.get('NFI_BENCH_DIST', 'nccl')
+    ndev = torch.cuda.device_count()     # counting devices does not initialise the GPU
+    if backend == 'nccl' and ndev < n:
+        sys.stderr.write(f'bench.py: --gpus {n} needs {n} visible GPUs, found {ndev}\n')
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        sys.stderr.write(f'bench.py: rank exit codes {rcs}\n')
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -260,9 +329,10 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='p3d_fwdbwd', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-reps', type=int, default=2)
+    ap.add_argument('--cpu-reps', type=int, default=3)
     ap.add_argument('--cpu-res', type=int, default=128)
     ap.add_argument('--no-inversion', action='store_true')
+    ap.add_argument('--no-configs', action='store_true', help='time only --config (no other configs[] sub-objects)')
     ap.add_argument('--inv-steps', type=int, default=30)
     ap.add_argument('--inv-batch', type=int, default=4, help='images per GPU in the inversion leg')
     ap.add_argument('--inv-graph', action='store_true',
@@ -271,7 +341,13 @@ def main():
                     help="comma list; the first is reported as inversion_s_per_image")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        ap.error(f'--gpus {args.gpus} but WORLD_SIZE={world} (launch one rank per GPU)')
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     # NFI_BENCH_DIST=gloo rehearses the N-rank path on a box with fewer GPUs than ranks (ranks
@@ -286,12 +362,65 @@ def main():
 
     import nfi
     from nfi import ops
-    cfg = CONFIGS[args.config]
+    out = measure(args.config, args, nfi, ops, dev, world, rank, headline=True)
+    sr, wbg, flipped, B, H, S, pose, bwd = CONFIGS[args.config]
+    if args.config == 'p3d_fwdbwd' and not args.no_configs:
+        # the other single-GPU configurations of BASELINE.json, each its own timed loop (parity-test
+        # cases too; the headline stays p3d_fwdbwd)
+        out['configs'] = {name: measure(name, args, nfi, ops, dev, world, rank, headline=False)
+                          for name in ('p3d_fwd', 'shapenet_fwdbwd', 'imagenet_256')}
+    if bwd and not args.no_inversion:
+        for k, loss in enumerate(args.inv_loss.split(',')):
+            leg = inversion_leg(args, dev, CONFIGS[args.config], world, loss)
+            out['inversion' if k == 0 else f'inversion_{loss}'] = leg
+            if k == 0:
+                out['inversion_s_per_image'] = leg['s_per_image']
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(args)
+        out['cpu_baseline'] = cb
+        out['speedup_vs_cpu'] = round(out['value'] / cb['value'], 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# fp32 FLOPs per sample: forward 6,450 (5,504 of them the decoder on MFMA); field
+# backward 5,700 (5,504 MFMA); tile pass 768 per tap pass (d planes; + 768 for the grid gradients)
+FLOPS = {'render_fwd': (6450, 5504), 'bwd_bins': (0, 0), 'bwd_field': (5700, 5504)}
+KERNEL_OF = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
+             'bwd_tiles': 'tile_kernel', 'bwd_bins': 'scan_blocks_kernel'}
+# gather ceiling (MI355X_MICROARCH.md, 'Indexed rows: gather into LDS'): rows shared by every
+# workgroup, served by the XCD's L2, 16.8-18.8 TB/s chip-wide (the table's upper figure)
+GATHER_CEILING_GBS = 18800.0
+
+
+def hbm_model(name, pose, bwd, H, S):
+    """Algorithmic HBM bytes per sample of each launch: the bytes this design must
+    stream through HBM — planes once per image and tap pass (25.17 MB = 12 B per sample at
+    128^2 x 128), the per-sample state the forward saves for the backward, the backward's
+    streamed rows and records; per-ray I/O is < 0.5 B per sample."""
+    plane = 3 * 32 * 256 * 256 * 4 / (H * H * 2 * S)
+    return {
+        # planes + saved state written (t, sigma 8 B, rgb 12, decoder outputs 44, inputs 128, perm 2)
+        'render_fwd': plane + (194 if bwd else 0),
+        'bwd_bins': 12.0,
+        # saved state read (194) + feature-gradient row written (128) + 3 entry records (48) + 8
+        'bwd_field': 194 + 128 + 48 + 8,
+        # d planes written once + (pose) the tile texels read once + each sample's gradient row and records
+        'bwd_tiles': plane * (2 if pose else 1) + 128 + 48 + (24 if pose else 0),
+    }[name]
+
+
+def measure(name, args, nfi, ops, dev, world, rank, headline):
+    """One configuration's timed loop: --warmup untimed steps, then exactly --steps steps bracketed
+    by barrier + synchronize, max over ranks; per-stage HIP-event times on the launch streams."""
+    cfg = CONFIGS[name]
     sr, wbg, flipped, B, H, S, pose, bwd = cfg
     nfi.configure(scene_range=sr, white_background=wbg, fine_sampling=True)
     batch = make_inputs(cfg, dev, seed=1234 + rank)
-
-    for _ in range(args.warmup):
+    steps = args.steps if headline else max(3, min(args.steps, 10))
+    for _ in range(args.warmup if headline else 2):
         run_step(nfi, batch, cfg, bwd)
     torch.cuda.synchronize()
     ops.KERNEL_TIMERS = {}
@@ -299,112 +428,101 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         run_step(nfi, batch, cfg, bwd)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     timers, ops.KERNEL_TIMERS = ops.KERNEL_TIMERS, None
-    # ms per step of each stage: the sum of its launches (the backward runs each stage once per
-    # image half, ops.BACKWARD_PIPELINE; the halves' tile passes overlap the field backward)
-    kern = {k: sum(a.elapsed_time(b) for a, b in v) / args.steps for k, v in timers.items()}
-    launches = {k: len(v) / args.steps for k, v in timers.items()}
+    # ms per step of each stage: the sum of its launches
+    kern = {k: sum(a.elapsed_time(b) for a, b in v) / steps for k, v in timers.items()}
+    launches = {k: len(v) / steps for k, v in timers.items()}
     if world > 1:
         elapsed = max_over_ranks(elapsed, dev)
-
     samples_per_step = B * H * H * 2 * S
-    value = world * samples_per_step * args.steps / elapsed / 1e6
-    conv_ms = conversion_ms(batch['field'].planes, ops)
-    ms_per_step = elapsed / args.steps * 1e3
+    value = world * samples_per_step * steps / elapsed / 1e6
+    ms_per_step = elapsed / steps * 1e3
+    conv_ms = conversion_ms(batch['field'].planes, ops) if headline else None
+    del batch
+    torch.cuda.empty_cache()
 
-    # roofline of the dominant stage (DESIGN.md "Kernels and their rooflines"):
-    # algorithmic tap bytes per sample — forward 1,536 B; backward d-planes scatter 1,536 B plus the
-    # pose re-gather 1,536 B (both in the bwd_tiles launch); the field backward touches no taps
-    # (its streamed per-sample state is ~380 B) — and fp32 FLOPs per sample (forward 6,450,
-    # field backward 5,700 of which 5,504 on MFMA, tiles 768 + 768).  Taps are served largely by
-    # L2 / Infinity Cache, so the tap rate can exceed the HBM peak: 'traffic' (rocprofv3 PMC) is
-    # what actually crossed HBM per launch.
-    model = {
-        'render_fwd': (TAP_BYTES + (194 if bwd else 0), 6450),   # + saved state when a backward follows
-        'bwd_bins': (12, 0),
-        'bwd_field': (380, 5700),
-        'bwd_tiles': (TAP_BYTES * (2 if pose else 1) + 48 + 3 * 128, 768 * (2 if pose else 1)),
-    }
-    plane_bytes = 3 * 32 * 256 * 256 * 4 / (H * H * 2 * S)       # per sample, one pass over the planes
-    compulsory = {'render_fwd': plane_bytes, 'bwd_bins': 0.0, 'bwd_field': 0.0,
-                  'bwd_tiles': plane_bytes * (2 if pose else 1)}
-    compulsory = {k: round(v, 3) for k, v in compulsory.items()}
-    kernel_of = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
-                 'bwd_tiles': 'tile_kernel', 'bwd_bins': 'scan_blocks_kernel'}
-    dom = max(kern, key=kern.get)
-    sec = kern[dom] * 1e-3
-    achieved = samples_per_step * model[dom][0] / sec / 1e9
-    # measured HBM bytes of the dominant kernel from the committed rocprofv3 counter passes, used
-    # only when they were collected from the kernel sources this run executes (source digest)
+    tap = {'render_fwd': TAP_BYTES, 'bwd_bins': 0, 'bwd_field': 0,
+           'bwd_tiles': TAP_BYTES * (2 if pose else 1)}
+    flops = dict(FLOPS, bwd_tiles=(768 * (2 if pose else 1), 0))
+    stages = {}
+    for k, v in kern.items():
+        if k not in tap:
+            continue
+        sec = v * 1e-3 / launches[k]
+        per_launch = samples_per_step / launches[k]
+        stages[k] = {'ms': round(v, 4), 'launches_per_step': launches[k],
+                     'hbm_model_bytes_per_sample': round(hbm_model(k, pose, bwd, H, S), 1),
+                     'hbm_model_GBps': round(per_launch * hbm_model(k, pose, bwd, H, S) / sec / 1e9, 1),
+                     'tap_rate_GBps': round(per_launch * tap[k] / sec / 1e9, 1),
+                     'fp32_TFLOPs': round(per_launch * flops[k][0] / sec / 1e12, 2),
+                     'mfma_TFLOPs': round(per_launch * flops[k][1] / sec / 1e12, 2)}
+    res = {'metric': (f'Msamples/sec fwd+bwd ({H}^2, {S}+{S} samples/ray)' if bwd
+                      else f'Msamples/sec fwd ({H}^2, {S}+{S} samples/ray)'),
+           'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': steps,
+           'warmup': args.warmup if headline else 2, 'ms_per_step': round(ms_per_step, 4),
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+           'data': 'synthetic',
+           'config': {'workload': name, 'global_batch': B * world, 'resolution': H,
+                      'samples_per_ray': f'{S}+{S}', 'plane_res': 256, 'pose_grad': pose,
+                      'backward': bwd, 'white_background': wbg, 'scene_range': sr,
+                      'parallelism': f'dp{world} (one process per GPU, no collective)',
+                      'planes_layout': 'texel-major [B,3,R,R,32] storage (the producer\'s native output)'},
+           'renderer_s_per_image_30step': round(30 * ms_per_step / 1e3 / B, 5),
+           'stages': stages}
+    if not headline:
+        for key in ('metric', 'unit', 'n_gpus', 'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data'):
+            res.pop(key)
+        return res
+    res['channel_major_conversion_ms'] = conv_ms
+
+    # roofline of the dominant launch (the longest HIP-event-timed stage)
+    dom = max(stages, key=lambda k: stages[k]['ms'] / stages[k]['launches_per_step'])
+    st = stages[dom]
+    sec = st['ms'] * 1e-3 / st['launches_per_step']
+    per_launch = samples_per_step / st['launches_per_step']
     traffic, traffic_src = None, 'none'
     try:
         from nfi.build import source_digest
         with open(os.path.join(ROOT, 'profiles', 'latest_counters.json')) as fh:
             cj = json.load(fh)
-        ctr = cj['kernels'].get(kernel_of[dom])
+        ctr = cj['kernels'].get(KERNEL_OF[dom])
         if cj.get('source_digest') != source_digest():
             traffic_src = f"stale ({cj.get('tag')}: counters of other kernel sources; not used)"
-        elif ctr is not None and args.config == 'p3d_fwdbwd' and B == 8:
+        elif ctr is not None and name == cj.get('config', 'p3d_fwdbwd') and B == cj.get('batch', 8):
             traffic = round(ctr['hbm_bytes_corrected'] / 1e9, 3)
-            traffic_src = f"profiles/latest_counters.json ({cj.get('tag')}, source digest {cj['source_digest']})"
+            traffic_src = (f"profiles/latest_counters.json ({cj.get('tag')}, source digest {cj['source_digest']}): "
+                           f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes")
     except (OSError, ValueError, KeyError):
         pass
-    stages = {k: {'ms': round(v, 4), 'launches_per_step': launches[k],
-                  'tap_GBps': round(samples_per_step * model[k][0] / (v * 1e-3) / 1e9, 1),
-                  'fp32_TFLOPs': round(samples_per_step * model[k][1] / (v * 1e-3) / 1e12, 2)}
-              for k, v in kern.items() if k in model}
-    roof = {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-            # 'achieved' / 'frac' count SURVEY §8(d)'s algorithmic TAP bytes (1,536 B per sample and
-            # tap pass), most of which L2 / the Infinity Cache serve: a tap rate, which exceeds the
-            # HBM peak; the HBM-side fraction is hbm_frac_measured (PMC counters)
-            'frac_basis': 'algorithmic tap bytes (SURVEY 8d) / HBM peak: a cache-served tap rate, not HBM traffic',
-            'traffic': traffic, 'traffic_unit': 'GB per launch (rocprofv3 FETCH_SIZEx2+WRITE_SIZE)',
-            'traffic_source': traffic_src,
-            'bytes_per_sample': model[dom][0],
-            'hbm_frac_measured': (round(traffic * launches[dom] / sec / HBM_PEAK_GBS, 4) if traffic else None),
-            # SURVEY §8(d)'s compulsory bytes: the planes once per image and pass (25.17 MB = 12 B per
-            # sample at 128^2 x 128) — read by render_fwd; the tile pass writes d planes (and, with
-            # pose gradients, reads each tile's texels): 12 or 24 B per sample
-            'compulsory_bytes_per_sample': compulsory[dom],
-            'compulsory_frac': round(samples_per_step * compulsory[dom] / sec / 1e9 / HBM_PEAK_GBS, 4),
-            'fp32_TFLOPs': stages[dom]['fp32_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
-            'stages': stages}
-
-    out = {
-        'metric': (f'Msamples/sec fwd+bwd ({H}^2, {S}+{S} samples/ray)' if bwd
-                   else f'Msamples/sec fwd ({H}^2, {S}+{S} samples/ray)'),
-        'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps,
-        'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-        'config': {'workload': args.config, 'global_batch': B * world, 'resolution': H,
-                   'samples_per_ray': f'{S}+{S}', 'plane_res': 256, 'pose_grad': pose,
-                   'backward': bwd, 'parallelism': f'dp{world} (one process per GPU, no collective)',
-                   'planes_layout': 'texel-major [B,3,R,R,32] storage (the producer\'s native output)'},
-        'channel_major_conversion_ms': conv_ms,
-        'renderer_s_per_image_30step': round(30 * ms_per_step / 1e3 / B, 5),
-        'roofline': roof,
+    model_bytes = per_launch * hbm_model(dom, pose, bwd, H, S)
+    if traffic is not None:
+        achieved, basis = traffic * 1e9 / sec / 1e9, 'measured HBM bytes per launch (traffic) / HIP-event launch time'
+    else:
+        achieved, basis = model_bytes / sec / 1e9, ('algorithmic HBM stream bytes per launch '
+                                                    '(DESIGN.md §3 model) / HIP-event launch time')
+    res['roofline'] = {
+        'bound': 'hbm', 'kernel': KERNEL_OF[dom], 'stage': dom,
+        'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': round(achieved / HBM_PEAK_GBS, 4), 'frac_basis': basis,
+        'traffic': traffic, 'traffic_unit': 'GB per launch', 'traffic_source': traffic_src,
+        'launch_ms': round(sec * 1e3, 4),
+        'hbm_model_bytes_per_sample': round(hbm_model(dom, pose, bwd, H, S), 1),
+        'hbm_model_frac': round(model_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
+        # SURVEY §8(d)'s tap bytes (1,536 B per sample and tap pass), served mostly by L2 / the
+        # Infinity Cache: a rate against the guide's L2 gather ceiling, not against HBM
+        'tap_rate_GBps': st['tap_rate_GBps'],
+        'gather_ceiling_GBps': GATHER_CEILING_GBS,
+        'gather_ceiling_frac': round(st['tap_rate_GBps'] / GATHER_CEILING_GBS, 4),
+        'fp32_TFLOPs': st['fp32_TFLOPs'], 'mfma_TFLOPs': st['mfma_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
+        'mfma_frac': round(st['mfma_TFLOPs'] / 157.3, 4),
     }
-    if bwd and not args.no_inversion:
-        for k, loss in enumerate(args.inv_loss.split(',')):
-            leg = inversion_leg(args, dev, cfg, batch, world, loss)
-            out['inversion' if k == 0 else f'inversion_{loss}'] = leg
-            if k == 0:
-                out['inversion_s_per_image'] = leg['s_per_image']
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args)
-        out['cpu_baseline'] = cb
-        out['speedup_vs_cpu'] = round(value / cb['value'], 1)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return res
 
 
 if __name__ == '__main__':

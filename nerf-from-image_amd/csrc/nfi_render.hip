@@ -1670,8 +1670,11 @@ __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1
       "v_add_f32 v41, v41, %3\n\t"
       "s_set_gpr_idx_off"
       : "+{v[40:71]}"(img)
-      : "s"(slot), "v"(a0), "v"(a1));   // (M0, which the index goes through, is reserved:
-                                         //  the compiler re-initializes it before any use)
+      : "s"(slot), "v"(a0), "v"(a1)
+      : "m0");   // s_set_gpr_idx_on writes the index into M0.  M0 is reserved in LLVM's AMDGPU
+                 // backend (hence the compiler's note on this clobber): it materialises M0 right
+                 // before each instruction that reads it and keeps nothing live in it across
+                 // statements (this file's code uses M0 nowhere else: checked in the ISA dump)
 }
 
 // One entry: run-merge into (a0, a1) while the cell repeats, else flush to the image.

@@ -366,7 +366,9 @@ class _State:
         self.opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas, capturable=capturable)
         self.target = target_img[..., :3]
         if capturable:
-            self.target = self.target.contiguous()
+            # a private static buffer: later batches are copied into it (load), which must never
+            # overwrite the caller's first target image
+            self.target = self.target.clone(memory_format=torch.contiguous_format)
         self.center, self.bbox = center, bbox
         # the prediction-independent half of the 'vgg' losses (augmentation grid, LPIPS features
         # of the target and its copies) runs on a side stream, concurrently with the producer and

@@ -166,6 +166,17 @@ def _check_frozen(f: TriplaneField):
                 raise NotImplementedError(
                     f'decoder parameter {name} requires grad: nfi differentiates the inversion '
                     f'path, where the generator is frozen (run.py:630-632); call requires_grad_(False)')
+        # the view-direction mapper's output layer is packed into the kernels' head (its trunk
+        # stays an autograd module): a trainable output layer would silently get no gradient
+        vm = f.viewdir_mapper
+        if vm is not None:
+            for name in ('weight', 'bias'):
+                p = getattr(getattr(vm, 'output', None), name, None)
+                if p is not None and p.requires_grad:
+                    raise NotImplementedError(
+                        f'viewdir_mapper.output.{name} requires grad: the kernels take the mapper\'s '
+                        f'output layer as a frozen head (its trunk may train); call '
+                        f'viewdir_mapper.output.requires_grad_(False)')
 
 
 def render(target_model, height, width, tform_cam2world, focal_length, center, bbox, model_input,

@@ -162,13 +162,17 @@ def evaluate(report: dict, it: int, generator, params, target_img, resolution: i
     from .render import render
     z_, z0_, t2_, s_, q_ = params
     item = report[it]
+
+    def snap(t):
+        # a copy even on the host (.cpu() of a CPU tensor is the live parameter Adam keeps updating)
+        return t.detach().to('cpu', copy=True)
     ws = z_.detach() * gain_z
-    item['ws'].append(ws.cpu())
+    item['ws'].append(snap(ws))
     if z0_ is not None:
-        item['z0'].append(z0_.detach().cpu())
-    item['R'].append(q_.detach().cpu())
-    item['s'].append(s_.detach().cpu())
-    item['t2'].append(t2_.detach().cpu())
+        item['z0'].append(snap(z0_))
+    item['R'].append(snap(q_))
+    item['s'].append(snap(s_))
+    item['t2'].append(snap(t2_))
     cam, focal = pose_to_matrix(None if z0_ is None else z0_.detach(), t2_.detach(), s_.detach(),
                                 F.normalize(q_.detach(), dim=-1), camera_flipped)
     if ws.shape[1] == 1:
@@ -189,15 +193,41 @@ def evaluate(report: dict, it: int, generator, params, target_img, resolution: i
     return rgb
 
 
+def _gather_report_rows(report: dict, it: int, local: dict):
+    """Append to report[it] the per-image rows every rank recorded for its chunk of the batch,
+    in rank (= batch) order.  The rows are a few KB per image of CPU tensors (ws is the largest,
+    30 KB), so they travel as objects; ranks with an empty chunk send nothing."""
+    import torch.distributed as dist
+    rows = {k: torch.cat(v, dim=0) for k, v in local.items() if len(v)}
+    every = [None] * dist.get_world_size()
+    dist.all_gather_object(every, rows)
+    for k in REPORT_KEYS:
+        parts = [r[k] for r in every if k in r]
+        if parts:
+            report[it][k].append(torch.cat(parts, dim=0))
+
+
 def run(generator, images, cams, focals, w_init, cfg, test_bs: int, report_path: str,
         steps: Optional[list] = None, lpips_net=None, gt_cams=None, has_mask: bool = False,
-        log=print, save_every: int = 512, render_fn=None):
+        log=print, save_every: int = 512, render_fn=None, uniforms=None, distributed: Optional[bool] = None):
     """The batch loop of run.py:1872-2336 over a set of target images: resume from
     `report_path` (report_checkpoint.pth) if present, invert `test_bs` images at a time
     (falling back to 1 for a short tail, run.py:1879), evaluate at the checkpoint steps, log the
-    s/img line, checkpoint every `save_every` images.  Returns the consolidated report."""
+    s/img line, checkpoint every `save_every` images.  Returns the consolidated report.
+
+    Under torch.distributed (`distributed` None = whenever a process group of >1 ranks exists)
+    `test_bs` is the GLOBAL batch, as the reference's `batch_size // 4 * len(gpu_ids)`
+    (run.py:1757): every rank calls run() with the same arguments, each batch is split over the
+    ranks by nfi.parallel.invert_sharded (DataParallel's torch.chunk), each rank evaluates its own
+    images, and the per-image report rows are gathered in batch order, so every rank returns the
+    same report as one process inverting the whole batch.  Rank 0 alone logs and writes the
+    report checkpoint.  `uniforms(idx, it) -> (u_coarse, u_fine)` injects the renderer's draws
+    of batch `idx` (tests)."""
     import time as _time
     from .inversion import invert
+    from .parallel import invert_sharded, world
+    rank, ws = world()
+    sharded = ws > 1 if distributed is None else distributed
     steps = steps or checkpoint_steps(cfg.steps, cfg.gain_z)
     cfg.steps = max(steps)
     report, idx = new_report(steps), 0
@@ -212,17 +242,32 @@ def run(generator, images, cams, focals, w_init, cfg, test_bs: int, report_path:
         sl = slice(idx, idx + test_bs)
         tgt = images[sl]
         gt = None if gt_cams is None else gt_cams[sl]
+        unif = None if uniforms is None else (lambda it, i0=idx: uniforms(i0, it))
 
-        def on_checkpoint(it, params, tgt=tgt, gt=gt, sl=sl):
-            evaluate(report, it, generator, params, tgt, cfg.resolution, cfg.samples,
-                     cfg.camera_flipped, gain_z=cfg.gain_z, lpips_net=lpips_net,
-                     gt_cam2world=gt, has_mask=has_mask, render_fn=render_fn)
+        def on_checkpoint(it, params, tgt=tgt, gt=gt, chunk=None):
+            if chunk is None:
+                evaluate(report, it, generator, params, tgt, cfg.resolution, cfg.samples,
+                         cfg.camera_flipped, gain_z=cfg.gain_z, lpips_net=lpips_net,
+                         gt_cam2world=gt, has_mask=has_mask, render_fn=render_fn)
+                return
+            a, e = chunk
+            local = new_report([it])
+            if params is not None:
+                evaluate(local, it, generator, params, tgt[a:e], cfg.resolution, cfg.samples,
+                         cfg.camera_flipped, gain_z=cfg.gain_z, lpips_net=lpips_net,
+                         gt_cam2world=None if gt is None else gt[a:e], has_mask=has_mask, render_fn=render_fn)
+            _gather_report_rows(report, it, local[it])
 
-        invert(generator, tgt, cams[sl], None if focals is None else focals[sl], w_init, cfg,
-               lpips_net=lpips_net, checkpoints=steps, on_checkpoint=on_checkpoint,
-               render_fn=render_fn)
+        foc = None if focals is None else focals[sl]
+        if sharded:
+            invert_sharded(generator, tgt, cams[sl], foc, w_init, cfg, uniforms=unif, lpips_net=lpips_net,
+                           render_fn=render_fn, checkpoints=steps, on_checkpoint=on_checkpoint)
+        else:
+            invert(generator, tgt, cams[sl], foc, w_init, cfg, uniforms=unif, lpips_net=lpips_net,
+                   checkpoints=steps, on_checkpoint=on_checkpoint, render_fn=render_fn)
         idx += test_bs
-        log(batch_line(idx, n, _time.time() - t1, test_bs))
-        if idx % save_every == 0:
-            save_checkpoint(report_path, report, idx, test_bs)
+        if rank == 0:
+            log(batch_line(idx, n, _time.time() - t1, test_bs))
+            if idx % save_every == 0:
+                save_checkpoint(report_path, report, idx, test_bs)
     return consolidate(report)

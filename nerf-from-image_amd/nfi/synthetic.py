@@ -41,3 +41,17 @@ def inversion_batch(B, H, W, S, R, scene_range, seed, flipped=True, device='cuda
     return {'field': field, 'cam': cam, 'focal': focal,
             'g_rgb': torch.randn((B, H, W, 3), generator=g, device=dev),
             'g_mask': torch.randn((B, H, W), generator=g, device=dev)}
+
+
+def cameras(B, scene_range, seed, flipped=True, device='cuda'):
+    """B seeded cameras of inversion_batch's distribution (random unit quaternion, small t2,
+    focal 1.859 at 3.3*scene_range) from their own stream: every rank of a sharded run draws the
+    same whole-batch cameras -> (cam2world [B,4,4], focal [B])."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    dev = torch.device(device)
+    q = F.normalize(torch.randn((B, 4), generator=g, device=dev), dim=-1)
+    t2 = 0.05 * torch.randn((B, 2), generator=g, device=dev)
+    f = 2 * 1.859
+    s = torch.full((B,), f / (3.3 * scene_range), device=dev)
+    z0 = torch.full((B,), math.log(f - 1), device=dev)
+    return pose_to_matrix(z0, t2, s, q, flipped)

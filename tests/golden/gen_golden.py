@@ -87,7 +87,8 @@ def make_cameras(b, scene_range, flipped, seed, ortho=False):
 
 def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, randomize,
                 force_no_cam_grad=False, ortho=False, with_bbox=False, with_center=False,
-                attention_values=10, use_sdf=True, render_file='run.py', use_viewdir=False):
+                attention_values=10, use_sdf=True, render_file='run.py', use_viewdir=False,
+                inside=False):
     torch.manual_seed(1000 + seed)
     gen = generator.Generator(512, scene_range, attention_values=attention_values, use_sdf=use_sdf,
                               use_viewdir=use_viewdir, disable_stylegan_noise=True)
@@ -109,6 +110,16 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
     gen.synthesis_network = PlanesLeaf(planes)
     palette = generator.wide_sigmoid_rescaled(torch.randn(b, 10, 3)).detach().requires_grad_()
     cam, focal = make_cameras(b, scene_range, flipped, seed, ortho=ortho)
+    if inside:
+        # nerf_utils.py:264-270: image 0's camera sits INSIDE the scene box (0.6 scene_range from
+        # the centre, looking at it: near < 0 -> clamped to 0.1); image 1's camera is turned away
+        # from the box (rotated 180 degrees about its y axis: the box lies behind it on every ray's
+        # line, near and far < 0 -> both 0.1 -> far = near + 1e-3)
+        cam = cam.detach().clone()
+        t = cam[0, :3, 3]
+        cam[0, :3, 3] = t * (0.6 * scene_range / float(t.norm()))
+        cam[1, :3, 0] = -cam[1, :3, 0]
+        cam[1, :3, 2] = -cam[1, :3, 2]
     cam = cam.detach().requires_grad_(not force_no_cam_grad)
     if focal is not None:
         focal = focal.detach().requires_grad_(not force_no_cam_grad)
@@ -456,6 +467,12 @@ def viewdir_cases():
                 flipped=False, randomize=False, attention_values=0, use_viewdir=True)
 
 
+def near_far_clamp_cases():
+    """near/far clamps (nerf_utils.py:264-270): a camera inside the box, one facing away from it."""
+    render_case('inside', 7, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=False,
+                flipped=True, randomize=True, inside=True)
+
+
 SDF_SHIFT = 0.0
 
 
@@ -483,6 +500,7 @@ if __name__ == '__main__':
     # perspective with bbox + center (nerf_utils.py:43-56; eval_*_persp.py callers)
     render_case('persp_center_bbox', 3, b=2, H=8, W=12, S=8, R=8, scene_range=1.4,
                 white_bg=False, flipped=True, randomize=True, with_bbox=True, with_center=True)
+    near_far_clamp_cases()
     field_variant_cases()
     viewdir_cases()
     zbuffer_cases()

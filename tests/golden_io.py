@@ -6,7 +6,7 @@ import numpy as np
 import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
-RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox']
+RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox', 'inside']
 VARIANT_CASES = ['rgbhead', 'nerfdensity', 'nerf_rgbhead']   # attention_values 0 / use_sdf False
 VIEWDIR_CASES = ['viewdir', 'viewdir_rgbhead']               # --use_viewdir
 ZBUFFER_CASES = ['zbuffer']        # eval_nusc_persp.py's render copy (z-buffer depth)

@@ -91,3 +91,53 @@ def test_backward_image_halves_match(full):
     assert torch.equal(a['d_palette'], b['d_palette'])
     for k in ('d_planes', 'd_cam', 'd_focal'):
         assert rel_l2(b[k], a[k]) < 1e-5, k
+
+
+def _render_shapenet(inp, meta, sl, g_rgb, g_mask):
+    """BASELINE configs[2]'s render: shapenet_chairs setting (scene_range 0.55, white background,
+    camera not flipped), deterministic sampling, pose frozen (loaders.py:123 forces
+    --inv_no_optimize_pose: force_no_cam_grad), gradients to planes and palette only."""
+    nfi.configure(scene_range=0.55, white_background=True, fine_sampling=True)
+    planes = inp['planes'][sl].to(DEV).requires_grad_()
+    pal = inp['palette'][sl].to(DEV).requires_grad_()
+    f = nfi.TriplaneField(planes=planes, palette=pal, w1=inp['w1'].to(DEV), b1=inp['b1'].to(DEV),
+                          w2=inp['w2'].to(DEV), b2=inp['b2'].to(DEV), alpha=1.0, beta=0.1)
+    rgb, depth, mask, _, _, _ = nfi.render(f, int(meta['H']), int(meta['W']), inp['cam'][sl].to(DEV),
+                                           inp['focal'][sl].to(DEV), None, None, None, int(meta['S']),
+                                           randomize=False, force_no_cam_grad=True)
+    loss = (rgb * g_rgb[sl]).sum() + (mask * g_mask[sl]).sum()
+    loss.backward()
+    nfi.configure(white_background=False)
+    return {'rgb': rgb.detach(), 'depth': depth.detach(), 'mask': mask.detach(), 'd_planes': planes.grad,
+            'd_palette': pal.grad}
+
+
+def test_shapenet_config_full_size():
+    """configs[2] at full size (B=16, 128^2, 64+64, R=256): the batch render equals each image
+    rendered alone (rays, samples and gradients are per image; the only batch coupling, the
+    min/max near/far of missed rays, cannot change their zero weights): rgb / depth / mask and
+    d palette bit for bit, d planes to summation order; repeat renders are deterministic; white-
+    background bounds (rgb = sum w c + 1 - mask)."""
+    B = 16
+    inp, meta = synthetic_inputs(B=B, H=128, W=128, S=64, R=256, scene_range=0.55, seed=91,
+                                 flipped=False, white_bg=True, randomize=False)
+    g = torch.Generator().manual_seed(17)
+    g_rgb = torch.randn(B, 128, 128, 3, generator=g).to(DEV)
+    g_mask = torch.randn(B, 128, 128, generator=g).to(DEV)
+    full = _render_shapenet(inp, meta, slice(0, B), g_rgb, g_mask)
+    again = _render_shapenet(inp, meta, slice(0, B), g_rgb, g_mask)
+    for k in ('rgb', 'depth', 'mask', 'd_palette'):
+        assert torch.equal(full[k], again[k]), k
+    assert rel_l2(full['d_planes'], again['d_planes']) < 1e-6
+    m = full['mask']
+    assert float(m.min()) >= 0.0 and float(m.max()) <= 1.0 + 1e-6
+    assert 0.05 < float(m.mean()) < 0.95                       # neither empty nor opaque everywhere
+    pal_max = float(inp['palette'].abs().max())
+    bound = pal_max * m + (1 - m)
+    assert bool((full['rgb'].abs() <= bound[..., None] * (1 + 1e-5) + 1e-6).all())
+    assert float(full['depth'].min()) >= 0.0
+    for k in (0, 7, 15):
+        one = _render_shapenet(inp, meta, slice(k, k + 1), g_rgb, g_mask)
+        for key in ('rgb', 'depth', 'mask', 'd_palette'):
+            assert torch.equal(one[key][0], full[key][k]), (k, key)
+        assert rel_l2(one['d_planes'][0], full['d_planes'][k]) < 1e-6, k

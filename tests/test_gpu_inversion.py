@@ -141,12 +141,16 @@ def test_graph_reused_by_the_next_batch():
     renderer's sampling noise (1e-2 relative), the same descent."""
     gen, d, cfg, target, net = _graph_case('l1')
     inversion._GRAPHS.clear()
+    t2 = target.flip(1).contiguous()                 # the second batch's target, built once
+    target0, t20 = target.clone(), t2.clone()
     _run(gen, d, cfg, target, net, graph=True, seed=3)                 # captures
     key_graphs = [e['graph'] for e in inversion._GRAPHS.values()]
     assert len(key_graphs) == 1 and key_graphs[0] is not None
-    second = _run(gen, d, cfg, target.flip(1).contiguous(), net, graph=True, seed=5, w_shift=0.01)
+    second = _run(gen, d, cfg, t2, net, graph=True, seed=5, w_shift=0.01)
     assert [e['graph'] for e in inversion._GRAPHS.values()] == key_graphs   # reused, not recaptured
-    ref = _run(gen, d, cfg, target.flip(1).contiguous(), net, graph=False, seed=5, w_shift=0.01)
+    # the graph's static target is a private buffer: loading batch 2 leaves the caller's tensors alone
+    assert torch.equal(target, target0) and torch.equal(t2, t20)
+    ref = _run(gen, d, cfg, t2, net, graph=False, seed=5, w_shift=0.01)
     torch.testing.assert_close(torch.tensor(second.losses), torch.tensor(ref.losses), rtol=1e-2, atol=0)
     assert second.losses[-1] < second.losses[0] and ref.losses[-1] < ref.losses[0]
     inversion._GRAPHS.clear()

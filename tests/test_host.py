@@ -78,6 +78,41 @@ def test_frozen_decoder_required():
         nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
 
 
+def test_trainable_viewdir_output_layer_refused():
+    """The view-direction mapper's output layer is packed into the kernels' head: a trainable one
+    would get no gradient, so render() refuses it (the trunk may still train)."""
+    from nfi.viewdir import ViewDirectionMapper
+    f = _field()
+    f.viewdir_mapper = ViewDirectionMapper(10)
+    f.viewdir_mapper.requires_grad_(False)
+    f.viewdir_mapper.output.weight.requires_grad_()
+    nfi.configure(use_viewdir=True)
+    try:
+        with pytest.raises(NotImplementedError, match='viewdir_mapper.output.weight'):
+            nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)
+        f.viewdir_mapper.output.weight.requires_grad_(False)
+        with torch.no_grad(), pytest.raises(RuntimeError, match='HIP devices only'):
+            f.viewdir_mapper.output.weight.requires_grad_()
+            nfi.render(f, 8, 8, torch.eye(4)[None], torch.ones(1), None, None, None, 32)   # no_grad: allowed
+    finally:
+        nfi.configure(use_viewdir=False)
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """bench.py --gpus N without torchrun starts N rank processes itself, and refuses (before any
+    GPU work) when fewer than N GPUs are visible: it never reports a smaller run under n_gpus N."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '1'],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert 'needs 2 visible GPUs' in r.stderr
+    assert r.stdout.strip() == ''
+
+
 def test_planes_shape_checked():
     with pytest.raises(RuntimeError):
         ops.planes_texel_major(torch.zeros(1, 3, 32, 8, 8))
