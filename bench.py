@@ -88,6 +88,12 @@ def conversion_ms(planes, ops, reps=5):
     return round(e0.elapsed_time(e1) / reps, 4)
 
 
+def progress(msg: str):
+    """A progress line on stderr (the JSON result alone goes to stdout)."""
+    sys.stderr.write(f'[bench {time.strftime("%H:%M:%S")}] {msg}\n')
+    sys.stderr.flush()
+
+
 def cpu_model() -> str:
     """lscpu's 'Model name' (the /proc/cpuinfo model name when lscpu is absent)."""
     import subprocess
@@ -125,13 +131,20 @@ def cpu_baseline(args):
     from oracle import render_oracle as orc
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     from gpu_helpers import synthetic_inputs
-    # SURVEY §8(d) CPU-baseline plan: every core of this process's affinity set
+    # SURVEY §8(d) CPU-baseline plan: every core this process may run on — its affinity set,
+    # capped by the cgroup CPU quota where one is set (a GPU box grants each GPU's job a share of
+    # the host: its affinity lists the whole machine, and threads beyond the quota only time-slice)
     try:
-        cores = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, cores)
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()
+    share = int(math.ceil(quota)) if quota else None
+    if share is None and os.environ.get('OMP_NUM_THREADS', '').isdigit():
+        share = int(os.environ['OMP_NUM_THREADS'])     # the box's per-job CPU share when no quota is visible
+    cores = max(1, min(affinity, share) if share else affinity)
     torch.set_num_threads(cores)
+    progress(f'cpu baseline: {cores} threads (affinity {affinity}, cgroup quota {quota})')
     H = args.cpu_res
     inp, meta = synthetic_inputs(B=1, H=H, W=H, S=64, R=256, scene_range=1.4, seed=0)
     field = orc.Field(planes=inp['planes'].clone().requires_grad_(), w1=inp['w1'], b1=inp['b1'],
@@ -146,17 +159,20 @@ def cpu_baseline(args):
 
     once()  # warm-up
     times = []
-    for _ in range(args.cpu_reps):
+    for k in range(args.cpu_reps):
         t0 = time.perf_counter()
         once()
         times.append(time.perf_counter() - t0)
+        progress(f'cpu baseline rep {k}: {times[-1]:.2f} s')
     t = sorted(times)[len(times) // 2]
     samples = H * H * 128
     model = cpu_model()
     out = {'value': samples / t / 1e6, 'unit': 'Msamples/s', 'cores': cores, 'kind': 'port',
            'sample': f'1 image {H}x{H}, 64+64 samples/ray, fwd+bwd (planes, palette, pose grads), '
                      f'median of {args.cpu_reps} after 1 warm-up; torch.set_num_threads({cores}) = '
-                     f'len(sched_getaffinity); {model}',
+                     f'min(len(sched_getaffinity) {affinity}, the CPU share granted: cgroup quota {quota} / '
+                     f'OMP_NUM_THREADS {os.environ.get("OMP_NUM_THREADS")}); {model}',
+           'affinity_cpus': affinity,
            'cpu_model': model, 'cgroup_cpu_quota': cgroup_cpu_quota(),
            'reps_seconds': [round(x, 3) for x in times],
            'seconds_per_image_step': t}
@@ -194,6 +210,7 @@ def cpu_inversion_step(inp, H, loss_kinds):
 
     res = {}
     for loss in loss_kinds:
+        progress(f'cpu inversion step ({loss})')
         cfg = inversion.InversionConfig(steps=1, resolution=H, samples=64, loss=loss, camera_flipped=True)
         net = lpips.LPIPS(backend='torch') if loss in inversion.VGG_LOSSES else None
         inversion.invert(gen, target, inp['cam'], inp['focal'], w_avg, cfg, render_fn=render_fn, lpips_net=net)
@@ -228,6 +245,7 @@ def inversion_leg(args, dev, cfg, world, loss):
     results is inside the timed region."""
     from nfi import inversion, lpips, ops, parallel, producer, synthetic
     sr, wbg, flipped, _, H, S, pose, bwd = cfg
+    progress(f'inversion leg ({loss})')
     B = args.inv_batch * world      # the global step batch
     torch.manual_seed(4321)
     gen = producer.InversionGenerator(scene_range=sr).to(dev)
@@ -417,6 +435,7 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
     by barrier + synchronize, max over ranks; per-stage HIP-event times on the launch streams."""
     cfg = CONFIGS[name]
     sr, wbg, flipped, B, H, S, pose, bwd = cfg
+    progress(f'config {name}')
     nfi.configure(scene_range=sr, white_background=wbg, fine_sampling=True)
     batch = make_inputs(cfg, dev, seed=1234 + rank)
     steps = args.steps if headline else max(3, min(args.steps, 10))

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 11
+#define NFI_ABI_VERSION 12
 #define NFI_DEC_SIZE 7184   /* floats in the packed decoder buffer (11 outputs) */
 #define NFI_DEC_SIZE_VIEWDIR 11312 /* ... with the view-direction mapper (33 outputs) */
 
@@ -203,6 +203,58 @@ int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args
  * 2 = per-tile d planes accumulation + grid gradients, then d rays. */
 int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_grad_args* g, int32_t stage,
                                   void* stream);
+
+/* ---- Per-stage seams: the reference's nerf_utils functions and the sampler
+ * closure as launches of their own, for a caller that uses one of them without render().
+ * Same conventions (device pointers, caller's stream, no allocation). */
+
+/* compute_near_far_planes (lib/nerf_utils.py:227-275) on n rays ro, rd [n,3] (directions taken as
+ * given): slab test against [-scene_range, scene_range]^3; rays that miss get the min near / max far
+ * of the hits of the call (:260-261); near, far clamped to >= 0.1, far >= near + 1e-3 (:264-270).
+ * ws: nfi_near_far_workspace_bytes(n) bytes of device scratch.  No ray hitting the box: the
+ * reference raises (min() of an empty tensor); here near = 0.1, far = 0.101. */
+int64_t nfi_near_far_workspace_bytes(int64_t n);
+int32_t nfi_near_far(const float* ro, const float* rd, int64_t n, float scene_range, float* near_, float* far_,
+                     void* ws, void* stream);
+
+/* sample_pdf (lib/nerf_utils.py:185-224): bins [n,nbins], weights [n,nbins-1] -> out [n,num_samples]
+ * (2 <= nbins <= 1024).  deterministic: u = linspace(0, 1, num_samples); else u [n,num_samples] if
+ * given (the reference's torch.rand draws), or a Philox-4x32-10 stream of (seed, offset).  No
+ * gradient (the reference samples under no_grad, run.py:259-281). */
+int32_t nfi_sample_pdf(const float* bins, const float* weights, int64_t n, int32_t nbins, int32_t num_samples,
+                       int32_t deterministic, const float* u, uint64_t seed, uint64_t offset, float* out,
+                       void* stream);
+
+/* render_volume_density (lib/nerf_utils.py:125-163, with cumprod_exclusive :20-25) on n rays of
+ * N samples (1 <= N <= 1024): sigma [n,N], rgb [n,N,3], rd [n,3] (distances are scaled by ||rd||),
+ * t [n,N] depth values -> rgb_map [n,3] (+ 1 - mask if white_bg), depth [n] (detached weights),
+ * mask [n], and the weights [n,N] if `weights` is not NULL (for the normal / semantic maps a caller
+ * builds on them, :150-157).  Backward: dL/d rgb_map, dL/d mask and optionally dL/d weights
+ * [n,N] -> d sigma [n,N], d rgb [n,N,3] (written), d rd [n,3] and d t [n,N] (each optional). */
+int32_t nfi_composite_forward(const float* sigma, const float* rgb, const float* rd, const float* t, int64_t n,
+                              int32_t N, int32_t white_bg, float* rgb_map, float* depth, float* mask, float* weights,
+                              void* stream);
+int32_t nfi_composite_backward(const float* sigma, const float* rgb, const float* rd, const float* t, int64_t n,
+                               int32_t N, int32_t white_bg, const float* g_rgb, const float* g_mask,
+                               const float* g_weights, float* d_sigma, float* d_rgb, float* d_rd, float* d_t,
+                               void* stream);
+
+/* The sampler closure of Generator.forward (models/generator.py:587-681; TriplanarDecoder :301-331)
+ * at caller points x [B,P,3] (world coordinates; image b's points read image b's planes and
+ * palette): sigma [B*P], rgb [B*P,3] and, if y is not NULL, the decoder outputs y [B*P,11]
+ * (distance + 10 logits, or + 3 colour features zero-padded with NFI_HEAD_RGB_SIGMOID) from which a
+ * caller forms 'sdf_distance' / 'semantics'.  heads: 0, NFI_HEAD_RGB_SIGMOID, NFI_HEAD_NERF_DENSITY
+ * (the view-direction closure needs per-ray inputs: render() only).
+ * Backward: dL/d sigma, dL/d rgb, dL/d y (each optional) -> d planes (ACCUMULATED into, field.planes'
+ * layout; NULL skips it), per-chunk dL/d palette partials d_palette_part [nfi_sampler_chunks(B,P),30] (reduce per
+ * image with nfi_segment_sum, M = chunks / B; NULL with NFI_HEAD_RGB_SIGMOID) and d x [B*P,3]
+ * (optional; grid_sampler_2d's border / align_corners grid gradient). */
+int64_t nfi_sampler_chunks(int32_t B, int64_t P);
+int32_t nfi_sampler_forward(const nfi_field* f, const float* x, int32_t B, int64_t P, float* sigma, float* rgb,
+                            float* y, void* stream);
+int32_t nfi_sampler_backward(const nfi_field* f, const float* x, int32_t B, int64_t P, const float* g_sigma,
+                             const float* g_rgb, const float* g_y, float* d_planes, float* d_palette_part,
+                             float* d_x, void* stream);
 
 #ifdef __cplusplus
 }

@@ -67,6 +67,47 @@ __device__ __forceinline__ float fdecode(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
+// Slab test of one ray against [-sr, sr]^3 as nerf_utils.py:235-258 evaluates it (invdir = 1/d,
+// the bound picked by the sign of invdir, products of rounded differences); returns the hit flag.
+__device__ __forceinline__ bool slab_test(const float o[3], const float d[3], float sr, float& nr, float& fr) {
+  float tmin[3], tmax[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float inv = fdiv(1.f, d[i]);
+    const bool neg = inv < 0.f;
+    tmin[i] = fmul(fsub(neg ? sr : -sr, o[i]), inv);
+    tmax[i] = fmul(fsub(neg ? -sr : sr, o[i]), inv);
+  }
+  bool hit = !((tmin[0] > tmax[1]) || (tmin[1] > tmax[0]));
+  nr = fmaxf(tmin[0], tmin[1]);
+  fr = fminf(tmax[0], tmax[1]);
+  hit = hit && !((nr > tmax[2]) || (tmin[2] > fr));
+  nr = fmaxf(nr, tmin[2]);
+  fr = fminf(fr, tmax[2]);
+  return hit;
+}
+
+// min near / max far over the hits of a 256-ray block as order-preserving keys into part[2 block]
+// (combined by rays_fix_kernel: no contended atomics on one address), nerf_utils.py:260-261
+__device__ __forceinline__ void block_hit_range(bool hit, float nr, float fr, uint32_t* __restrict__ part) {
+  __shared__ uint32_t red[2][4];
+  uint32_t kmin = hit ? fkey(nr) : 0xFFFFFFFFu;
+  uint32_t kmax = hit ? fkey(fr) : 0u;
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = kmin;
+    red[1][threadIdx.x >> 6] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+    part[2 * blockIdx.x + 1] = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+  }
+}
+
 __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, float* __restrict__ ro,
                                                        float* __restrict__ rd, float* __restrict__ nearp,
                                                        float* __restrict__ farp, uint32_t* __restrict__ part,
@@ -112,42 +153,33 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
       rd[r * 3 + i] = d[i];
     }
     // slab test against [-sr, sr]^3 (nerf_utils.py:235-258)
-    float tmin[3], tmax[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float inv = fdiv(1.f, d[i]);
-      const bool neg = inv < 0.f;
-      tmin[i] = fmul(fsub(neg ? sr : -sr, o[i]), inv);
-      tmax[i] = fmul(fsub(neg ? -sr : sr, o[i]), inv);
-    }
-    hit = !((tmin[0] > tmax[1]) || (tmin[1] > tmax[0]));
-    nr = fmaxf(tmin[0], tmin[1]);
-    fr = fminf(tmax[0], tmax[1]);
-    hit = hit && !((nr > tmax[2]) || (tmin[2] > fr));
-    nr = fmaxf(nr, tmin[2]);
-    fr = fminf(fr, tmax[2]);
+    hit = slab_test(o, d, sr, nr, fr);
     nearp[r] = nr;
     farp[r] = fr;
     hitflag[r] = hit ? 1 : 0;
   }
-  // min near / max far over hits of the whole call (nerf_utils.py:260-261): this block's pair of
-  // keys to part[2 block], combined by rays_fix_kernel (no contended atomics on one address)
-  __shared__ uint32_t red[2][4];
-  uint32_t kmin = hit ? fkey(nr) : 0xFFFFFFFFu;
-  uint32_t kmax = hit ? fkey(fr) : 0u;
-  for (int o = 32; o > 0; o >>= 1) {
-    kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
-    kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+  // min near / max far over hits of the whole call (nerf_utils.py:260-261)
+  block_hit_range(hit, nr, fr, part);
+}
+
+// compute_near_far_planes (nerf_utils.py:227-275) on the caller's rays [n][3] (not normalised
+// here: the reference takes the directions as given), then rays_fix_kernel
+__global__ void __launch_bounds__(256) near_far_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                                       long long n, float sr, float* __restrict__ nearp,
+                                                       float* __restrict__ farp, uint32_t* __restrict__ part,
+                                                       uint8_t* __restrict__ hitflag) {
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  float nr = INFINITY, fr = -INFINITY;
+  bool hit = false;
+  if (r < n) {
+    const float o[3] = {ro[r * 3 + 0], ro[r * 3 + 1], ro[r * 3 + 2]};
+    const float d[3] = {rd[r * 3 + 0], rd[r * 3 + 1], rd[r * 3 + 2]};
+    hit = slab_test(o, d, sr, nr, fr);
+    nearp[r] = nr;
+    farp[r] = fr;
+    hitflag[r] = hit ? 1 : 0;
   }
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = kmin;
-    red[1][threadIdx.x >> 6] = kmax;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
-    part[2 * blockIdx.x + 1] = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
-  }
+  block_hit_range(hit, nr, fr, part);
 }
 
 __global__ void __launch_bounds__(256) rays_fix_kernel(long long n, float* __restrict__ nearp,
@@ -421,6 +453,25 @@ int32_t nfi_rays_forward(const nfi_camera* cam, float scene_range, float* ro, fl
   uint8_t* hit = reinterpret_cast<uint8_t*>(ws + 2 * (long long)blocks);
   rays_fwd_kernel<<<blocks, 256, 0, s>>>(*cam, scene_range, ro, rd, near_, far_, part, hit);
   NFI_CHECK_LAUNCH("rays_fwd_kernel");
+  rays_fix_kernel<<<blocks, 256, 0, s>>>(n, near_, far_, part, blocks, hit);
+  NFI_CHECK_LAUNCH("rays_fix_kernel");
+  return NFI_OK;
+}
+
+int64_t nfi_near_far_workspace_bytes(int64_t n) { return n <= 0 ? -1 : 8 * ((n + 255) / 256) + n; }
+
+int32_t nfi_near_far(const float* ro, const float* rd, int64_t n, float scene_range, float* near_, float* far_,
+                     void* ws, void* stream) {
+  NFI_REQUIRE(ro && rd && near_ && far_ && ws, "near_far: null pointer");
+  NFI_REQUIRE(n > 0, "near_far: no rays (n=%lld): the reference's min() of an empty tensor raises",
+              (long long)n);
+  NFI_REQUIRE(scene_range > 0.f && std::isfinite(scene_range), "near_far: bad scene_range");
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = (int)((n + 255) / 256);
+  uint32_t* part = reinterpret_cast<uint32_t*>(ws);
+  uint8_t* hit = reinterpret_cast<uint8_t*>(part + 2 * (long long)blocks);
+  near_far_kernel<<<blocks, 256, 0, s>>>(ro, rd, n, scene_range, near_, far_, part, hit);
+  NFI_CHECK_LAUNCH("near_far_kernel");
   rays_fix_kernel<<<blocks, 256, 0, s>>>(n, near_, far_, part, blocks, hit);
   NFI_CHECK_LAUNCH("rays_fix_kernel");
   return NFI_OK;

@@ -1131,6 +1131,41 @@ struct BwdArgs {
   float* d_xray;          // [rays][32] dL/d view-direction mapper output (NFI_HEAD_VIEWDIR), accumulated
 };
 
+// One 64-sample chunk of the compositing backward's reverse scan: lane k's map x -> A_k x + B_k
+// (A = a_k, B = e_k alpha_k); returns S_k = (f_{k+1} o ... o f_63)(cB), the suffix beyond lane k
+// evaluated at cB (the composition of the chunks after this one at 0), and advances cB past this
+// chunk.  Suffix composition on DPP: inside rows of 16 (row_shl 1, 2, 4, 8; the identity (1, 0)
+// past the row's end), then each row's result composed with the totals of the rows above it (read
+// from lanes 16, 32, 48 once, composed on uniform values).
+__device__ __forceinline__ float suffix_affine(float A, float B, float& cB) {
+  const int l = lane_id();
+  {
+    float A2 = dpp_fill<0x101>(A, 1.f), B2 = dpp_fill<0x101>(B, 0.f);
+    B = fmaf(A, B2, B), A = A * A2;
+    A2 = dpp_fill<0x102>(A, 1.f), B2 = dpp_fill<0x102>(B, 0.f);
+    B = fmaf(A, B2, B), A = A * A2;
+    A2 = dpp_fill<0x104>(A, 1.f), B2 = dpp_fill<0x104>(B, 0.f);
+    B = fmaf(A, B2, B), A = A * A2;
+    A2 = dpp_fill<0x108>(A, 1.f), B2 = dpp_fill<0x108>(B, 0.f);
+    B = fmaf(A, B2, B), A = A * A2;
+  }
+  {
+    const float a1 = readlane(A, 16), b1 = readlane(B, 16), a2 = readlane(A, 32), b2 = readlane(B, 32);
+    const float a3 = readlane(A, 48), b3 = readlane(B, 48);
+    const float c1a = a2 * a3, c1b = fmaf(a2, b3, b2);            // rows 2, 3
+    const float c0a = a1 * c1a, c0b = fmaf(a1, c1b, b1);          // rows 1, 2, 3
+    const int row = l >> 4;
+    const float ca = row == 0 ? c0a : (row == 1 ? c1a : (row == 2 ? a3 : 1.f));
+    const float cb = row == 0 ? c0b : (row == 1 ? c1b : (row == 2 ? b3 : 0.f));
+    B = fmaf(A, cb, B);
+    A = A * ca;
+  }
+  const float An = dpp_fill<0x130>(A, 1.f), Bn = dpp_fill<0x130>(B, 0.f);   // wave_shl:1
+  const float Sk = fmaf(An, cB, Bn);                       // lane 63: the identity -> cB
+  cB = fmaf(readlane(A, 0), cB, readlane(B, 0));
+  return Sk;
+}
+
 // Compositing backward (nerf_utils.py:125-163 under autograd), one wave per ray:
 // dL/d alpha_k = T_k (e_k - S_k), S_k = sum_{i>k} e_i alpha_i prod_{k<j<i} a_j (reverse affine
 // scan), e_i = g_rgb.c_i + g_mask(-white bg) -> dL/d sigma_i, weights w_i, and the ||rd|| term.
@@ -1188,31 +1223,7 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
     // suffix composition of the maps x -> A x + B on DPP: inside rows of 16 (row_shl 1, 2, 4, 8;
     // the identity (1, 0) past the row's end), then each row's result composed with the totals of
     // the rows above it (read from lanes 16, 32, 48 once, composed on uniform values)
-    float A = aa[e], B = ee[e] * al[e];
-    {
-      float A2 = dpp_fill<0x101>(A, 1.f), B2 = dpp_fill<0x101>(B, 0.f);
-      B = fmaf(A, B2, B), A = A * A2;
-      A2 = dpp_fill<0x102>(A, 1.f), B2 = dpp_fill<0x102>(B, 0.f);
-      B = fmaf(A, B2, B), A = A * A2;
-      A2 = dpp_fill<0x104>(A, 1.f), B2 = dpp_fill<0x104>(B, 0.f);
-      B = fmaf(A, B2, B), A = A * A2;
-      A2 = dpp_fill<0x108>(A, 1.f), B2 = dpp_fill<0x108>(B, 0.f);
-      B = fmaf(A, B2, B), A = A * A2;
-    }
-    {
-      const float a1 = readlane(A, 16), b1 = readlane(B, 16), a2 = readlane(A, 32), b2 = readlane(B, 32);
-      const float a3 = readlane(A, 48), b3 = readlane(B, 48);
-      const float c1a = a2 * a3, c1b = fmaf(a2, b3, b2);            // rows 2, 3
-      const float c0a = a1 * c1a, c0b = fmaf(a1, c1b, b1);          // rows 1, 2, 3
-      const int row = l >> 4;
-      const float ca = row == 0 ? c0a : (row == 1 ? c1a : (row == 2 ? a3 : 1.f));
-      const float cb = row == 0 ? c0b : (row == 1 ? c1b : (row == 2 ? b3 : 0.f));
-      B = fmaf(A, cb, B);
-      A = A * ca;
-    }
-    const float An = dpp_fill<0x130>(A, 1.f), Bn = dpp_fill<0x130>(B, 0.f);   // wave_shl:1
-    const float Sk = fmaf(An, cB, Bn);                       // lane 63: the identity -> cB
-    cB = fmaf(readlane(A, 0), cB, readlane(B, 0));
+    const float Sk = suffix_affine(aa[e], ee[e] * al[e], cB);
     const float dal = T[e] * (ee[e] - Sk);                   // dL/d alpha_k
     grdn += dal * sg[e] * ex[e] * raw[e];                    // dists = raw * ||rd||
     if (i < N) {
@@ -2230,6 +2241,427 @@ __global__ void __launch_bounds__(256) dcoord_reduce_kernel(nfi_render_args a, B
   }
 }
 
+// =======================================================================================
+// Per-stage seams: the nerf_utils functions and the sampler closure as launches
+// of their own, for callers that use one of them without the fused render.  They reuse the
+// fused kernels' device functions (tap gather, decoder on the matrix cores, heads, fp64 wave
+// scans, the compositing suffix scan) and the same rounding order.
+// =======================================================================================
+
+// ---- sample_pdf (nerf_utils.py:185-224): bins [n][NB], weights [n][NB-1] -> [n][S] ----------
+// One wave per ray: CDF in the wave's LDS slice (fp64 scan), one binary search per sample.
+constexpr int PDF_NBMAX = 1024;
+__global__ void __launch_bounds__(256) sample_pdf_kernel(const float* __restrict__ bins,
+                                                         const float* __restrict__ weights, long long n, int NB,
+                                                         int S, int deterministic, const float* __restrict__ u,
+                                                         unsigned long long seed, unsigned long long offset,
+                                                         float* __restrict__ out) {
+  __shared__ float lds[4 * 2 * PDF_NBMAX];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= n) return;
+  float* cdf = lds + wv * 2 * PDF_NBMAX;
+  float* bn = cdf + PDF_NBMAX;
+  const int NW = NB - 1;
+  const float* w = weights + r * NW;
+  // weights + 1e-5, normalised by their sum, cumsum (accumulated in fp64 as ATen's CPU kernels do)
+  double tot = 0.0;
+  for (int i = l; i < NW; i += 64) tot += (double)fadd(w[i], 1e-5f);
+  const float totf = (float)wave_sum_d(tot);
+  double carry = 0.0;
+  for (int c = 0; c < NW; c += 64) {
+    const int i = c + l;
+    const float pdf = (i < NW) ? fdiv(fadd(w[min(i, NW - 1)], 1e-5f), totf) : 0.f;
+    const double inc = wave_incl_sum_d((double)pdf) + carry;
+    if (i < NW) cdf[i + 1] = (float)inc;
+    carry = readlane(inc, 63);
+  }
+  for (int i = l; i < NB; i += 64) bn[i] = bins[r * NB + i];
+  if (l == 0) cdf[0] = 0.f;
+  wave_lds_sync();
+  for (int c = 0; c < S; c += 64) {
+    const int i = c + l;
+    if (i >= S) break;
+    const float uu = deterministic ? tlinspace01(i, S) : (u ? u[r * S + i] : rng_uniform(seed, offset, r, i, 1));
+    int lo = 0, hi = NB;          // searchsorted(cdf, u, right=True): entries <= u
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if (cdf[m] <= uu) lo = m + 1;
+      else hi = m;
+    }
+    const int below = max(0, lo - 1), above = min(NB - 1, lo);
+    const float c0 = cdf[below], c1 = cdf[above];
+    const float b0 = bn[below], b1 = bn[above];
+    float denom = fsub(c1, c0);
+    denom = (denom < 1e-5f) ? 1.f : denom;
+    const float tt = fdiv(fsub(uu, c0), denom);
+    out[r * S + i] = fadd(b0, fmul(tt, fsub(b1, b0)));
+  }
+}
+
+// ---- render_volume_density (nerf_utils.py:125-163) on caller samples ------------------------
+// sigma [n][N], rgb [n][N][3], rd [n][3] (its norm scales the distances), t [n][N] ->
+// rgb_map [n][3] (+ 1 - mask with a white background), depth [n], mask [n], weights [n][N]
+// (optional).  One wave per ray; chunks of 64 samples with the fp64 transmittance carried.
+constexpr int COMP_NMAX = 1024;
+__global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restrict__ sigma,
+                                                            const float* __restrict__ rgb,
+                                                            const float* __restrict__ rd,
+                                                            const float* __restrict__ tv, long long n, int N,
+                                                            int white, float* __restrict__ rgb_map,
+                                                            float* __restrict__ depth, float* __restrict__ mask,
+                                                            float* __restrict__ wts) {
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= n) return;
+  const float rdn = tnorm3(rd[r * 3 + 0], rd[r * 3 + 1], rd[r * 3 + 2]);
+  const float* t = tv + r * N;
+  double carry = 1.0;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, sm = 0.f, sd = 0.f;
+  for (int c = 0; c < N; c += 64) {
+    const int i = c + l;
+    const int ic = min(i, N - 1);
+    const float ti = t[ic], tn = t[min(i + 1, N - 1)], sg = sigma[r * N + ic];
+    const float c0 = rgb[(r * N + ic) * 3 + 0], c1 = rgb[(r * N + ic) * 3 + 1], c2 = rgb[(r * N + ic) * 3 + 2];
+    const float dist = (i < N - 1) ? fmul(fsub(tn, ti), rdn) : 0.f;
+    float al, aa, ex;
+    alpha_of(i < N ? sg : 0.f, dist, al, aa, ex);
+    al = i < N ? al : 0.f;
+    aa = i < N ? aa : 1.f;
+    const double inc = wave_incl_prod_d((double)aa);
+    const double exc = dpp_fill<0x138>(inc, 1.0);
+    const float T = (float)(carry * exc);
+    carry = carry * readlane(inc, 63);
+    const float w = fmul(al, T);
+    if (i < N) {
+      s0 = fmaf(w, c0, s0);
+      s1 = fmaf(w, c1, s1);
+      s2 = fmaf(w, c2, s2);
+      sm += w;
+      sd = fmaf(w, ti, sd);
+      if (wts) wts[r * N + i] = w;
+    }
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  sm = wave_sum(sm);
+  sd = wave_sum(sd);
+  if (l == 0) {
+    const float bg = white ? fsub(1.f, sm) : 0.f;
+    rgb_map[r * 3 + 0] = s0 + bg;
+    rgb_map[r * 3 + 1] = s1 + bg;
+    rgb_map[r * 3 + 2] = s2 + bg;
+    mask[r] = sm;
+    depth[r] = sd;
+  }
+}
+
+// Backward: dL/d rgb_map [n][3], dL/d mask [n] and optionally dL/d weights [n][N] (maps the
+// caller built on the weights output) -> d sigma [n][N], d rgb [n][N][3], and optionally
+// d rd [n][3] (through ||rd||) and d t [n][N] (through the distances; the reference's depth values
+// carry no gradient inside render(), but a caller's may).  The reverse affine scan of
+// composite_bwd_kernel (suffix_affine), the transmittance of the forward recomputed into LDS.
+__global__ void __launch_bounds__(256) composite_bwd_seam_kernel(
+    const float* __restrict__ sigma, const float* __restrict__ rgb, const float* __restrict__ rd,
+    const float* __restrict__ tv, long long n, int N, int white, const float* __restrict__ g_rgb,
+    const float* __restrict__ g_mask, const float* __restrict__ g_w, float* __restrict__ d_sigma,
+    float* __restrict__ d_rgb, float* __restrict__ d_rd, float* __restrict__ d_t) {
+  __shared__ float lds[4 * 2 * COMP_NMAX];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= n) return;
+  float* LT = lds + wv * 2 * COMP_NMAX;   // transmittance T_i
+  float* LG = LT + COMP_NMAX;             // dL/d dist_i (for d t)
+  const float d0 = rd[r * 3 + 0], d1 = rd[r * 3 + 1], d2 = rd[r * 3 + 2];
+  const float rdn = tnorm3(d0, d1, d2);
+  const float* t = tv + r * N;
+  double carry = 1.0;
+  for (int c = 0; c < N; c += 64) {
+    const int i = c + l;
+    const int ic = min(i, N - 1);
+    const float dist = (i < N - 1) ? fmul(fsub(t[min(i + 1, N - 1)], t[ic]), rdn) : 0.f;
+    float al, aa, ex;
+    alpha_of(i < N ? sigma[r * N + ic] : 0.f, dist, al, aa, ex);
+    aa = i < N ? aa : 1.f;
+    const double inc = wave_incl_prod_d((double)aa);
+    const double exc = dpp_fill<0x138>(inc, 1.0);
+    if (i < N) LT[i] = (float)(carry * exc);
+    carry = carry * readlane(inc, 63);
+  }
+  wave_lds_sync();
+  const float gr0 = g_rgb[r * 3 + 0], gr1 = g_rgb[r * 3 + 1], gr2 = g_rgb[r * 3 + 2];
+  const float gm = g_mask[r] - (white ? (gr0 + gr1 + gr2) : 0.f);
+  float grdn = 0.f, cB = 0.f;
+  const int nch = (N + 63) / 64;
+  for (int ch = nch - 1; ch >= 0; --ch) {
+    const int i = ch * 64 + l;
+    const bool v = i < N;
+    const int ic = min(i, N - 1);
+    const float raw = (i < N - 1) ? fsub(t[min(i + 1, N - 1)], t[ic]) : 0.f;
+    const float dist = fmul(raw, rdn);
+    const float sg = v ? sigma[r * N + ic] : 0.f;
+    float al, aa, ex;
+    alpha_of(sg, dist, al, aa, ex);
+    al = v ? al : 0.f;
+    aa = v ? aa : 1.f;
+    const float c0 = rgb[(r * N + ic) * 3 + 0], c1 = rgb[(r * N + ic) * 3 + 1], c2 = rgb[(r * N + ic) * 3 + 2];
+    const float gwx = (g_w && v) ? g_w[r * N + ic] : 0.f;
+    const float ee = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm + gwx : 0.f;
+    const float T = v ? LT[ic] : 0.f;
+    const float Sk = suffix_affine(aa, ee * al, cB);
+    const float dal = T * (ee - Sk);              // dL/d alpha_i
+    const float gdist = dal * sg * ex;            // dL/d dist_i (d alpha / d dist = sigma exp(-sigma dist))
+    grdn += gdist * raw;
+    if (v) {
+      d_sigma[r * N + i] = dal * dist * ex;
+      const float w = al * T;
+      d_rgb[(r * N + i) * 3 + 0] = w * gr0;
+      d_rgb[(r * N + i) * 3 + 1] = w * gr1;
+      d_rgb[(r * N + i) * 3 + 2] = w * gr2;
+      LG[i] = gdist;
+    }
+  }
+  if (d_rd) {
+    grdn = wave_sum(grdn);
+    if (l < 3) d_rd[r * 3 + l] = grdn * ((l == 0 ? d0 : (l == 1 ? d1 : d2)) / rdn);
+  }
+  if (d_t) {
+    wave_lds_sync();
+    // dist_i = (t_{i+1} - t_i) ||rd||: d t_i = ||rd|| (g_{i-1} - g_i), the last dist is constant 0
+    for (int i = l; i < N; i += 64) {
+      const float gi = (i < N - 1) ? LG[i] : 0.f;
+      const float gp = (i > 0) ? LG[i - 1] : 0.f;
+      d_t[r * N + i] = rdn * (gp - gi);
+    }
+  }
+}
+
+// ---- sampler closure (generator.py:587-681) at caller points -------------------------------
+// x [B][P][3] world coordinates -> sigma [B*P], rgb [B*P][3], decoder outputs y [B*P][11]
+// (distance + 10 logits / colour features; optional).  One wave per 64 points of one image.
+struct SamplerArgs {
+  nfi_field f;
+  const float* x;
+  int B;
+  long long P;
+  float* sigma;
+  float* rgb;
+  float* y;
+  // backward
+  const float* g_sigma;   // [B*P] or NULL
+  const float* g_rgb;     // [B*P][3] or NULL
+  const float* g_y;       // [B*P][11] or NULL (dL/d decoder outputs from the caller's own maps)
+  float* d_planes;        // field.planes' layout, accumulated (float atomics); NULL: not needed
+  float* d_palette_part;  // [B * chunks][30] per-chunk partial, or NULL
+  float* d_x;             // [B*P][3] or NULL
+};
+
+__device__ __forceinline__ void sampler_point(const SamplerArgs& A, long long gp, PointP& P) {
+  const float sr = A.f.scene_range;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) P.cx[k] = fdiv(A.x[gp * 3 + k], sr);   // x_in / scene_range (generator.py:604)
+  P.mask = (fabsf(P.cx[0]) > 1.f || fabsf(P.cx[1]) > 1.f || fabsf(P.cx[2]) > 1.f) ? 1.f : 0.f;
+  plane_params(P.cx[0], P.cx[1], A.f.R, P.pl[0]);
+  plane_params(P.cx[0], P.cx[2], A.f.R, P.pl[1]);
+  plane_params(P.cx[1], P.cx[2], A.f.R, P.pl[2]);
+}
+
+__global__ void __launch_bounds__(256) sampler_fwd_kernel(SamplerArgs A) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long cpi = (A.P + 63) / 64;
+  const long long job = (long long)blockIdx.x * 4 + wv;
+  if (job >= (long long)A.B * cpi) return;
+  const int b = (int)(job / cpi);
+  const long long p0 = (job % cpi) * 64;
+  const int npts = (int)min(64LL, A.P - p0);
+  const long long gp = (long long)b * A.P + p0 + min(l, npts - 1);
+  float* X = lds + wv * XTILE;
+  PointP P;
+  sampler_point(A, gp, P);
+  const PlaneView pv{A.f.planes + (long long)b * A.f.sb, (int)A.f.sq, (int)A.f.st, A.f.R};
+  gather_features(pv, P, npts, X);
+  wave_lds_sync();
+  float y[NO];
+  mlp_forward_tile<NO, true>(A.f.dec, X, y);
+  Head h;
+  head_forward(y, P.mask, A.f.inv_alpha, A.f.beta, A.f.palette ? A.f.palette + b * (NA * 3) : nullptr, A.f.heads, h);
+  if (l < npts) {
+    A.sigma[gp] = h.sigma;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) A.rgb[gp * 3 + c] = h.rgb[c];
+    if (A.y) {
+#pragma unroll
+      for (int k = 0; k < NO; ++k) A.y[gp * NO + k] = y[k];
+    }
+  }
+}
+
+// Backward: re-gather + decoder forward, head backward (+ the caller's dL/dy), decoder input
+// gradient on the matrix cores, then per point and plane the bilinear tap's adjoint: d planes by
+// float atomics (two 256-B wave instructions per plane: texels x0, x0+1 x 32 channels of rows y0,
+// y1) and the grid gradient (ATen grid_sampler_2d border / align_corners rule) -> d x.
+__global__ void __launch_bounds__(256) sampler_bwd_kernel(SamplerArgs A) {
+  using L = DecL<NO>;
+  __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long cpi = (A.P + 63) / 64;
+  const long long job = (long long)blockIdx.x * 4 + wv;
+  if (job >= (long long)A.B * cpi) return;
+  const int b = (int)(job / cpi);
+  const long long p0 = (job % cpi) * 64;
+  const int npts = (int)min(64LL, A.P - p0);
+  const bool v = l < npts;
+  const long long gp = (long long)b * A.P + p0 + min(l, npts - 1);
+  float* X = lds + wv * XTILE;
+  PointP P;
+  sampler_point(A, gp, P);
+  const PlaneView pv{A.f.planes + (long long)b * A.f.sb, (int)A.f.sq, (int)A.f.st, A.f.R};
+  gather_features(pv, P, npts, X);
+  wave_lds_sync();
+  // decoder inputs in the MFMA operand layout (lane (j, q): channels 8q.. of point 16sb + j)
+  f4v xa[4], xb[4];
+  {
+    const int j = l & 15, q = l >> 4;
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const bool vp = 16 * sb + j < npts;
+      const f4v z{0.f, 0.f, 0.f, 0.f};
+      const f4v a0 = ld4(X + (16 * sb + j) * XS + 8 * q), a1 = ld4(X + (16 * sb + j) * XS + 8 * q + 4);
+      xa[sb] = vp ? a0 : z;
+      xb[sb] = vp ? a1 : z;
+    }
+  }
+  float y[NO];
+  mlp_forward_tile<NO, true>(A.f.dec, X, y);
+  const float* pal = A.f.palette ? A.f.palette + b * (NA * 3) : nullptr;
+  Head h;
+  head_forward(y, P.mask, A.f.inv_alpha, A.f.beta, pal, A.f.heads, h);
+  float gy[NO];
+#pragma unroll
+  for (int k = 0; k < NO; ++k) gy[k] = (A.g_y && v) ? A.g_y[gp * NO + k] : 0.f;
+  const float gs = (A.g_sigma && v) ? A.g_sigma[gp] : 0.f;
+  if (A.f.heads & NFI_HEAD_NERF_DENSITY) {
+    const float z = fsub(y[0], 1.f);
+    const float gm = fmul(gs, fsub(1.f, P.mask));
+    const float ez = expf(z);
+    gy[0] += z > 20.f ? gm : gm * (ez / (ez + 1.f));
+  } else {
+    const float xn = -y[0];
+    const float sgn = tsign(xn);
+    const float ex2 = expf(-fabsf(xn) / A.f.beta);
+    const float gcdf = (gs * A.f.inv_alpha) * (1.f - P.mask);
+    gy[0] += -(((gcdf * 0.5f * sgn) * ex2 / A.f.beta) * sgn);
+  }
+  float gc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) gc[c] = (A.g_rgb && v) ? A.g_rgb[gp * 3 + c] : 0.f;
+  wave_lds_sync();
+  if (A.f.heads & NFI_HEAD_RGB_SIGMOID) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) gy[1 + c] += fmul(fmul(gc[c], 2.004f), fsub(1.f, h.p[c])) * h.p[c];
+  } else {
+    float gp_[NA], dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      gp_[k] = gc[0] * pal[k * 3 + 0] + gc[1] * pal[k * 3 + 1] + gc[2] * pal[k * 3 + 2];
+      dot = fmaf(gp_[k], h.p[k], dot);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) gy[1 + k] += (gp_[k] - dot) * h.p[k];
+    float* row = X + l * XS;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      row[k * 3 + 0] = h.p[k] * gc[0];
+      row[k * 3 + 1] = h.p[k] * gc[1];
+      row[k * 3 + 2] = h.p[k] * gc[2];
+    }
+    wave_lds_sync();
+    if (A.d_palette_part) {
+      const int col = l & 31, r0 = (l >> 5) * 32;
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (col < NA * 3) {
+#pragma unroll
+        for (int jj = 0; jj < 32; ++jj) s4[jj & 3] += X[(r0 + jj) * XS + col];
+      }
+      const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
+      if (l < NA * 3) A.d_palette_part[job * (NA * 3) + l] = sh;
+    }
+  }
+  // dY^T operands through the tile
+  wave_lds_sync();
+#pragma unroll
+  for (int o = 0; o < NO; ++o) X[l * XS + o] = v ? gy[o] : 0.f;
+#pragma unroll
+  for (int o = NO; o < 4 * L::KT; ++o) X[l * XS + o] = 0.f;
+  wave_lds_sync();
+  float gyb[4][L::KT];
+  {
+    const int j = l & 15, q = l >> 4;
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+      for (int t = 0; t < L::KT; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+  }
+  f4v gxo[2][4];
+  mlp_backward_mfma<NO>(A.f.dec, xa, xb, gyb, gxo);
+  // each plane's tap feature gradient dX/3 into the tile: row = point, 32 channels
+  wave_lds_sync();
+  {
+    const int j = l & 15, q = l >> 4;
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+        *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 16 * cb + 4 * q) = gxo[cb][sb] * (1.f / 3.f);
+  }
+  wave_lds_sync();
+  // adjoint of the three bilinear taps, point by point: lane (dx = l >> 5, c = l & 31)
+  const int dx = l >> 5, c = l & 31;
+  float* dpl = A.d_planes ? A.d_planes + (long long)b * A.f.sb : nullptr;
+  float gxs = 0.f, gys = 0.f, gzs = 0.f;   // this lane's point's d x (normalised coordinates)
+  for (int jp = 0; jp < npts; ++jp) {
+    const float g = X[jp * XS + c];
+    float du[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int pk = __shfl(P.pl[q].tex, jp);
+      const float w = __shfl(P.pl[q].w, jp), nn = __shfl(P.pl[q].n, jp);
+      const float e = 1.f - w, s = 1.f - nn;
+      const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
+      const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
+      const float wx = dx ? w : e;
+      if (dpl) {
+        atomicAdd(dpl + q * pv.sq + (long long)t0 * pv.st + c, g * (s * wx));
+        atomicAdd(dpl + q * pv.sq + (long long)t1 * pv.st + c, g * (nn * wx));
+      }
+      if (A.d_x) {
+        const float v0 = pv.base[q * pv.sq + (long long)t0 * pv.st + c];
+        const float v1 = pv.base[q * pv.sq + (long long)t1 * pv.st + c];
+        // d feat / d ix = s (V(x1,y0) - V(x0,y0)) + n (V(x1,y1) - V(x0,y1)); d / d iy = e (V(x0,y1) -
+        // V(x0,y0)) + w (V(x1,y1) - V(x1,y0))
+        const float gix = wave_sum(g * ((dx ? 1.f : -1.f) * (s * v0 + nn * v1)));
+        const float giy = wave_sum(g * (wx * (v1 - v0)));
+        const float gxm = __shfl(P.pl[q].gxm, jp), gym = __shfl(P.pl[q].gym, jp);
+        du[q == 2 ? 1 : 0] += gix * gxm;          // xy, xz: u = x0; yz: u = x1
+        du[q == 0 ? 1 : 2] += giy * gym;          // xy: v = x1; xz, yz: v = x2
+      }
+    }
+    if (l == jp) {
+      gxs = du[0];
+      gys = du[1];
+      gzs = du[2];
+    }
+  }
+  if (A.d_x && v) {
+    const float sr = A.f.scene_range;
+    A.d_x[gp * 3 + 0] = fdiv(gxs, sr);
+    A.d_x[gp * 3 + 1] = fdiv(gys, sr);
+    A.d_x[gp * 3 + 2] = fdiv(gzs, sr);
+  }
+}
+
 struct Workspace {
   float* gfeat;
   float* gsig;
@@ -2497,6 +2929,110 @@ int32_t nfi_render_backward_stage(const nfi_render_args* a, const nfi_render_gra
   NFI_REQUIRE(stage >= 0 && stage <= 2, "render_backward_stage: stage %d not in 0..2", stage);
   NFI_REQUIRE(!(a->field.heads & NFI_HEAD_VIEWDIR) || g->d_xray, "render_backward: NFI_HEAD_VIEWDIR needs d_xray");
   return nfi::launch_bwd(a, g, (hipStream_t)stream, stage);
+}
+
+// ---- per-stage seams ----
+
+int32_t nfi_sample_pdf(const float* bins, const float* weights, int64_t n, int32_t nbins, int32_t num_samples,
+                       int32_t deterministic, const float* u, uint64_t seed, uint64_t offset, float* out,
+                       void* stream) {
+  NFI_REQUIRE(bins && weights && out, "sample_pdf: null pointer");
+  NFI_REQUIRE(n > 0 && nbins >= 2 && nbins <= nfi::PDF_NBMAX && num_samples > 0,
+              "sample_pdf: bad shape n=%lld nbins=%d (2..%d) num_samples=%d", (long long)n, nbins, nfi::PDF_NBMAX,
+              num_samples);
+  nfi::sample_pdf_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      bins, weights, n, nbins, num_samples, deterministic, u, seed, offset, out);
+  NFI_CHECK_LAUNCH("sample_pdf_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_composite_forward(const float* sigma, const float* rgb, const float* rd, const float* t, int64_t n,
+                              int32_t N, int32_t white_bg, float* rgb_map, float* depth, float* mask, float* weights,
+                              void* stream) {
+  NFI_REQUIRE(sigma && rgb && rd && t && rgb_map && depth && mask, "composite_forward: null pointer");
+  NFI_REQUIRE(n > 0 && N >= 1 && N <= nfi::COMP_NMAX, "composite_forward: bad shape n=%lld N=%d (1..%d)",
+              (long long)n, N, nfi::COMP_NMAX);
+  nfi::composite_fwd_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      sigma, rgb, rd, t, n, N, white_bg, rgb_map, depth, mask, weights);
+  NFI_CHECK_LAUNCH("composite_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_composite_backward(const float* sigma, const float* rgb, const float* rd, const float* t, int64_t n,
+                               int32_t N, int32_t white_bg, const float* g_rgb, const float* g_mask,
+                               const float* g_weights, float* d_sigma, float* d_rgb, float* d_rd, float* d_t,
+                               void* stream) {
+  NFI_REQUIRE(sigma && rgb && rd && t && g_rgb && g_mask && d_sigma && d_rgb, "composite_backward: null pointer");
+  NFI_REQUIRE(n > 0 && N >= 1 && N <= nfi::COMP_NMAX, "composite_backward: bad shape n=%lld N=%d (1..%d)",
+              (long long)n, N, nfi::COMP_NMAX);
+  nfi::composite_bwd_seam_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      sigma, rgb, rd, t, n, N, white_bg, g_rgb, g_mask, g_weights, d_sigma, d_rgb, d_rd, d_t);
+  NFI_CHECK_LAUNCH("composite_bwd_seam_kernel");
+  return NFI_OK;
+}
+
+static int check_sampler_field(const nfi_field* f, int32_t B, int64_t P) {
+  NFI_REQUIRE(f && f->planes && f->dec, "sampler: null field pointer");
+  NFI_REQUIRE(B > 0 && P > 0, "sampler: bad shape B=%d P=%lld", B, (long long)P);
+  NFI_REQUIRE(f->R >= 2, "sampler: plane resolution R=%d < 2", f->R);
+  NFI_REQUIRE(!(f->heads & NFI_HEAD_VIEWDIR),
+              "sampler: the view-direction mapper closure needs per-ray inputs (render() only)");
+  NFI_REQUIRE((f->heads & ~(NFI_HEAD_RGB_SIGMOID | NFI_HEAD_NERF_DENSITY)) == 0, "sampler: unknown heads 0x%x",
+              f->heads);
+  NFI_REQUIRE(f->palette || (f->heads & NFI_HEAD_RGB_SIGMOID), "sampler: the attention head needs a palette");
+  NFI_REQUIRE(((uintptr_t)f->planes & 15) == 0 && f->st % 4 == 0 && f->sq % 4 == 0 && f->sb % 4 == 0,
+              "sampler: planes must be 16-byte aligned with strides divisible by 4");
+  NFI_REQUIRE(f->scene_range > 0.f, "sampler: bad scene_range");
+  return NFI_OK;
+}
+
+int64_t nfi_sampler_chunks(int32_t B, int64_t P) {
+  if (B <= 0 || P <= 0) return -1;
+  return (int64_t)B * ((P + 63) / 64);
+}
+
+int32_t nfi_sampler_forward(const nfi_field* f, const float* x, int32_t B, int64_t P, float* sigma, float* rgb,
+                            float* y, void* stream) {
+  int e = check_sampler_field(f, B, P);
+  if (e) return e;
+  NFI_REQUIRE(x && sigma && rgb, "sampler_forward: null pointer");
+  nfi::SamplerArgs A{};
+  A.f = *f;
+  A.x = x;
+  A.B = B;
+  A.P = P;
+  A.sigma = sigma;
+  A.rgb = rgb;
+  A.y = y;
+  const long long jobs = nfi_sampler_chunks(B, P);
+  nfi::sampler_fwd_kernel<<<(unsigned)((jobs + 3) / 4), 256, 0, (hipStream_t)stream>>>(A);
+  NFI_CHECK_LAUNCH("sampler_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_sampler_backward(const nfi_field* f, const float* x, int32_t B, int64_t P, const float* g_sigma,
+                             const float* g_rgb, const float* g_y, float* d_planes, float* d_palette_part,
+                             float* d_x, void* stream) {
+  int e = check_sampler_field(f, B, P);
+  if (e) return e;
+  NFI_REQUIRE(x, "sampler_backward: null pointer");
+  NFI_REQUIRE(d_palette_part || (f->heads & NFI_HEAD_RGB_SIGMOID),
+              "sampler_backward: the attention head needs d_palette_part");
+  nfi::SamplerArgs A{};
+  A.f = *f;
+  A.x = x;
+  A.B = B;
+  A.P = P;
+  A.g_sigma = g_sigma;
+  A.g_rgb = g_rgb;
+  A.g_y = g_y;
+  A.d_planes = d_planes;
+  A.d_palette_part = (f->heads & NFI_HEAD_RGB_SIGMOID) ? nullptr : d_palette_part;
+  A.d_x = d_x;
+  const long long jobs = nfi_sampler_chunks(B, P);
+  nfi::sampler_bwd_kernel<<<(unsigned)((jobs + 3) / 4), 256, 0, (hipStream_t)stream>>>(A);
+  NFI_CHECK_LAUNCH("sampler_bwd_kernel");
+  return NFI_OK;
 }
 
 }  // extern "C"

