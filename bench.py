@@ -187,16 +187,18 @@ def cpu_baseline(args):
 
 
 def cpu_inversion_step(inp, H, loss_kinds):
-    """One step of the inversion loop on the CPU, the reference's way: producer in PyTorch (the
-    'torch' backend, the reference's op sequence) + the oracle renderer, L1 loss, Adam; 1 image at
+    """One step of the inversion loop on the CPU, the reference's way: the producer's reference op
+    sequence in PyTorch (oracle/producer_oracle.py) + the oracle renderer, the loss, Adam; 1 image at
     HxH, 64+64 samples; s/image for 30 steps = 30 x the step (timed after one warm-up step)."""
     from nfi import inversion, lpips, producer
+    from oracle import producer_oracle as po
     from oracle import render_oracle as orc
     torch.manual_seed(4321)
-    gen = producer.InversionGenerator(scene_range=1.4, backend='torch')
+    gen = producer.InversionGenerator(scene_range=1.4)
     with torch.no_grad():
         gen.decoder.net[2].bias[0] -= 0.97
     gen.requires_grad_(False)
+    gen = po.ReferenceProducer(gen)
     w_avg = gen.mapping_network.get_average_w(n_samples=1000, generator=torch.Generator().manual_seed(7))
     target = torch.tanh(torch.randn((1, H, H, 3), generator=torch.Generator().manual_seed(99)))
 
@@ -212,13 +214,13 @@ def cpu_inversion_step(inp, H, loss_kinds):
     for loss in loss_kinds:
         progress(f'cpu inversion step ({loss})')
         cfg = inversion.InversionConfig(steps=1, resolution=H, samples=64, loss=loss, camera_flipped=True)
-        net = lpips.LPIPS(backend='torch') if loss in inversion.VGG_LOSSES else None
+        net = po.ReferenceLPIPS(lpips.LPIPS()) if loss in inversion.VGG_LOSSES else None
         inversion.invert(gen, target, inp['cam'], inp['focal'], w_avg, cfg, render_fn=render_fn, lpips_net=net)
         t0 = time.perf_counter()
         inversion.invert(gen, target, inp['cam'], inp['focal'], w_avg, cfg, render_fn=render_fn, lpips_net=net)
         step = time.perf_counter() - t0
         res[loss] = {'s_per_image': round(30 * step, 3), 'step_seconds': round(step, 3),
-                     'sample': f'1 image {H}x{H}, 64+64 samples, producer (torch backend) + oracle render '
+                     'sample': f'1 image {H}x{H}, 64+64 samples, producer (oracle: reference op sequence) + oracle render '
                                f'fwd+bwd, loss {loss}, Adam; one timed step after one warm-up, x30'}
     return res
 

@@ -664,6 +664,65 @@ __device__ __forceinline__ void excl_prod(const float (&a)[E], float (&T)[E]) {
   }
 }
 
+// ---- torch.sum of a float row on the CPU, in ATen's order ----------------------------------
+// ATen's CPU sum kernel (SumKernel.cpp cascade_sum) accumulates float in FLOAT: a row of n
+// contiguous values is read as n/8 vectors of 8 (the reduction kernels' Vectorized<float> width in
+// this torch build), each vector lane summed by row_sum — 4 interleaved partial sums, each a
+// multi_row_sum cascade of 4 levels of 16 — then the n%8 tail sequentially from 0, then the 8
+// lanes in order; rows shorter than 8 take row_sum directly.  Emulated exactly (checked against
+// torch 2.10 for n = 1..1023): sample_pdf's normalisation divides by this sum, and where the
+// CDF's last entry rounds to 1 + 1 ulp the reference interpolates the last fine sample inside the
+// last bin instead of at its end (u = 1 in deterministic mode).
+__device__ __forceinline__ float aten_multi_row_sum(const float* x, int start, int step, int size) {
+  // the column x[start + i*step], i < size, as multi_row_sum accumulates one of its nrows columns
+  int cl2 = 0;
+  while ((1 << cl2) < size) ++cl2;                           // CeilLog2
+  const int lp = max(4, cl2 / 4), lstep = 1 << lp, lmask = lstep - 1;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+  while (i + lstep <= size) {
+    for (int j = 0; j < lstep; ++j, ++i) acc[0] = fadd(acc[0], x[start + i * step]);
+    for (int j = 1; j < 4; ++j) {
+      acc[j] = fadd(acc[j], acc[j - 1]);
+      acc[j - 1] = 0.f;
+      if ((i & (lmask << (j * lp))) != 0) break;
+    }
+  }
+  for (; i < size; ++i) acc[0] = fadd(acc[0], x[start + i * step]);
+  for (int j = 1; j < 4; ++j) acc[0] = fadd(acc[0], acc[j]);
+  return acc[0];
+}
+// row_sum over the sequence x[start + i*step], i < size (ilp factor 4)
+__device__ __forceinline__ float aten_row_sum(const float* x, int start, int step, int size) {
+  const int si = size / 4;
+  float p[4];
+  for (int k = 0; k < 4; ++k) p[k] = si ? aten_multi_row_sum(x, start + k * step, 4 * step, si) : 0.f;
+  for (int i = si * 4; i < size; ++i) p[0] = fadd(p[0], x[start + i * step]);
+  for (int k = 1; k < 4; ++k) p[0] = fadd(p[0], p[k]);
+  return p[0];
+}
+// The sum of x[0..n) (wave-uniform n, x in LDS) in every lane: lanes 0..7 run the 8 vector
+// lanes' row_sums side by side, lane 8 the tail, then the 8 lane results are added in order.
+__device__ __forceinline__ float aten_sum_f32(const float* x, int n) {
+  constexpr int VEC = 8;
+  const int l = lane_id();
+  float v = 0.f;
+  if (n < VEC) {
+    if (l == 0) v = aten_row_sum(x, 0, 1, n);
+    return readlane(v, 0);
+  }
+  const int V = n / VEC;
+  if (l < VEC) {
+    v = aten_row_sum(x, l, VEC, V);
+  } else if (l == VEC) {
+    for (int k = V * VEC; k < n; ++k) v = fadd(v, x[k]);
+  }
+  float acc = readlane(v, VEC);
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) acc = fadd(acc, readlane(v, k));
+  return acc;
+}
+
 // Ascending bitonic sort of the 64*E values v[e] (element e*64 + lane) across the wave.
 template <int E>
 __device__ __forceinline__ void bitonic_sort(float (&v)[E]) {
@@ -896,18 +955,20 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NF
     wave_lds_sync();
     // ---- sample_pdf (nerf_utils.py:185-224): bins = midpoints [S-1], weights = sm[1..S-2]
     float pw[SPL], mid[SPL];
-    double tot = 0.0;
+    float* cdf = T2 + 0;        // [S-1]
+    float* bins = T2 + SMAX;    // [S-1] (first the padded weights, for their sum)
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
       const int i = e * 64 + l;
       pw[e] = (i < S - 2) ? fadd(Wl[i + 1], 1e-5f) : 0.f;
-      tot += (double)pw[e];
       mid[e] = (i < S - 1) ? fmul(.5f, fadd(T2[i + 1], T2[i])) : 0.f;
+      if (i < S - 2) bins[i] = pw[e];
     }
-    const float totf = (float)wave_sum_d(tot);
     wave_lds_sync();
-    float* cdf = T2 + 0;        // [S-1]
-    float* bins = T2 + SMAX;    // [S-1]
+    // weights.sum(-1) in float, in ATen's order (the CDF's last entry, hence the bin of u = 1,
+    // follows its rounding); the cumsum below accumulates in double as ATen's does
+    const float totf = aten_sum_f32(bins, S - 2);
+    wave_lds_sync();
     double carry = 0.0;
 #pragma unroll
     for (int e = 0; e < SPL; ++e) {
@@ -2264,18 +2325,20 @@ __global__ void __launch_bounds__(256) sample_pdf_kernel(const float* __restrict
   float* bn = cdf + PDF_NBMAX;
   const int NW = NB - 1;
   const float* w = weights + r * NW;
-  // weights + 1e-5, normalised by their sum, cumsum (accumulated in fp64 as ATen's CPU kernels do)
-  double tot = 0.0;
-  for (int i = l; i < NW; i += 64) tot += (double)fadd(w[i], 1e-5f);
-  const float totf = (float)wave_sum_d(tot);
+  // weights + 1e-5, normalised by their sum (float, ATen's order), cumsum (accumulated in fp64 as
+  // ATen's CPU cumsum does); the padded weights are staged in the bins' half of the slice
+  for (int i = l; i < NW; i += 64) bn[i] = fadd(w[i], 1e-5f);
+  wave_lds_sync();
+  const float totf = aten_sum_f32(bn, NW);
   double carry = 0.0;
   for (int c = 0; c < NW; c += 64) {
     const int i = c + l;
-    const float pdf = (i < NW) ? fdiv(fadd(w[min(i, NW - 1)], 1e-5f), totf) : 0.f;
+    const float pdf = (i < NW) ? fdiv(bn[min(i, NW - 1)], totf) : 0.f;
     const double inc = wave_incl_sum_d((double)pdf) + carry;
     if (i < NW) cdf[i + 1] = (float)inc;
     carry = readlane(inc, 63);
   }
+  wave_lds_sync();
   for (int i = l; i < NB; i += 64) bn[i] = bins[r * NB + i];
   if (l == 0) cdf[0] = 0.f;
   wave_lds_sync();

@@ -10,10 +10,12 @@ against, and random weights stand in unless `load_weights` is given the two stat
             lin_l a bias-free 1x1 conv to one channel (lpips/lpips.py NetLinLayer; dropout is
             inactive in eval)
 
-Backends: 'hip' (the VGG convolutions are bias-free MIOpen calls, each followed by one fused HIP
-epilogue — bias, ReLU and the 2x2 max pool where one follows; the distance head — normalisation,
-difference, lin, spatial mean — is one fused HIP kernel per layer, forward and backward,
-csrc/nfi_producer.hip) and 'torch' (the op sequence above in PyTorch).
+One implementation, on the device: the VGG 3x3 convolutions are Winograd F(4,3) blocks (nfi.conv)
+with bias, ReLU and the next 2x2 max pool in their output transform (bias-free MIOpen calls plus
+one fused HIP epilogue where Winograd does not apply; the 3-channel first layer one direct HIP
+pass); the distance head — normalisation, difference, lin, spatial mean — is one fused HIP kernel
+per layer, forward and backward (csrc/nfi_producer.hip).  The op sequence above in plain PyTorch
+over this module's parameters is test infrastructure: oracle/producer_oracle.py.
 """
 
 from __future__ import annotations
@@ -49,14 +51,8 @@ class VGG16Features(nn.Module):
                 c = v
         self.features = nn.Sequential(*layers)
 
-    def forward(self, x, fused: bool = False):
+    def forward(self, x):
         out = []
-        if not fused:
-            for i, layer in enumerate(self.features):
-                x = layer(x)
-                if i in TAPS:
-                    out.append(x)
-            return out
         # each conv block as MIOpen's bias-free convolution + one HIP epilogue pass (bias, ReLU and
         # the following MaxPool2d when there is one; producer_ops.vgg_epilogue)
         from . import conv as wconv, producer_ops
@@ -96,7 +92,7 @@ class LPIPS(nn.Module):
     """`LPIPSLoss` (metrics.py:104-146): forward(in0, in1) -> [N, 1] distances (reduction
     'none'), in0/in1 in [-1, 1] (normalize=False, as run.py:2231 calls it)."""
 
-    def __init__(self, backend: str = 'hip'):
+    def __init__(self):
         super().__init__()
         self.net = VGG16Features()
         self.lins = nn.ModuleList([nn.Conv2d(c, 1, 1, bias=False) for c in CHANNELS])
@@ -105,7 +101,6 @@ class LPIPS(nn.Module):
         with torch.no_grad():                  # lpips lin weights are non-negative
             for lin in self.lins:
                 lin.weight.abs_().mul_(0.1)
-        self.backend = backend
         self.eval()
         self.requires_grad_(False)
 
@@ -120,7 +115,7 @@ class LPIPS(nn.Module):
         return self
 
     def features(self, im):
-        return self.net((im - self.shift) / self.scale, fused=self.backend == 'hip')
+        return self.net((im - self.shift) / self.scale)
 
     def target_features(self, in1):
         """The second input's feature taps without gradient (forward(in0, f1=...) consumes them:
@@ -133,12 +128,9 @@ class LPIPS(nn.Module):
         if f1 is None:
             with torch.no_grad() if not in1.requires_grad else _null():
                 f1 = self.features(in1)
-        if self.backend == 'hip':
-            from . import producer_ops
-            return sum(producer_ops.lpips_head(a, b, lin.weight.view(-1))
-                       for a, b, lin in zip(f0, f1, self.lins))[:, None]
-        return sum(lin((normalize(a) - normalize(b)).square()).mean(dim=[2, 3])
-                   for a, b, lin in zip(f0, f1, self.lins))
+        from . import producer_ops
+        return sum(producer_ops.lpips_head(a, b, lin.weight.view(-1))
+                   for a, b, lin in zip(f0, f1, self.lins))[:, None]
 
 
 class _null:
@@ -148,7 +140,3 @@ class _null:
     def __exit__(self, *a):
         return False
 
-
-def normalize(x):
-    """lpips.normalize_tensor (eps 1e-10)."""
-    return x / (x.square().sum(dim=1, keepdim=True).sqrt() + EPS)

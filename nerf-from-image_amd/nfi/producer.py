@@ -5,19 +5,18 @@ generator.py:475-477), AttentionMapper -> palette [b,10,3] (generator.py:132-186
 455-462) — plus the mapping network used for the average latent (stylegan.py:228-290,
 generator.py:263-282) and the frozen SDF decoder weights.
 
-Two backends, chosen explicitly (never a silent fallback):
-  'hip'   (default) the convolutions' products are hipBLASLt GEMMs (3x3: Winograd F(4,3),
-          nfi/conv.py; stride-2 up-sampling: one GEMM over the 9 taps + HIP tap scatter fused with
-          the FIR and epilogue; 1x1 to-planes: one batched GEMM with the modulation folded into a
-          per-image weight) and everything between them runs in the fused HIP kernels of
-          csrc/nfi_producer.hip (producer_ops.py): modulation backward, demodulation + bias + gain
-          + leaky-ReLU epilogue, the skip-image upsample + add; the styles and demodulation
-          coefficients of all layers as two batched products (style_bank); device tensors only;
-  'torch' the reference's op sequence restated in plain PyTorch (any device) — the CPU-pinned
-          restatement the tests check against the reference's fixtures.
+One implementation, on the device: the convolutions' products are hipBLASLt GEMMs (3x3:
+Winograd F(4,3), nfi/conv.py; stride-2 up-sampling: one GEMM over the 9 taps + HIP tap scatter
+fused with the FIR and epilogue; 1x1 to-planes: one batched GEMM with the modulation folded into a
+per-image weight) and everything between them runs in the fused HIP kernels of
+csrc/nfi_producer.hip (producer_ops.py): modulation backward, demodulation + bias + gain +
+leaky-ReLU epilogue, the skip-image upsample + add; the styles and demodulation coefficients of
+all layers as two batched products (style_bank).  Device tensors only (CPU tensors raise).  The
+reference's op sequence in plain PyTorch over these modules' parameters is test infrastructure:
+oracle/producer_oracle.py (the tests' CPU loop and bench.py's cpu_baseline).
 Parameter and buffer names equal the reference Generator's state_dict keys, so a G_ema
 checkpoint loads with `load_state_dict(sd)`.  Pinned by tests/golden/producer.npz
-(tests/test_producer.py on CPU, tests/test_gpu_inversion.py for 'hip').  The HIP renderer
+(tests/test_gpu_inversion.py; the oracle restatement by tests/test_producer.py on CPU).  The HIP renderer
 consumes it through `nfi.render(generator, ...)` exactly as it consumes the reference Generator.
 """
 
@@ -30,9 +29,6 @@ import torch.nn.functional as F
 from torch import nn
 
 SQRT2 = math.sqrt(2.0)
-BACKENDS = ('hip', 'torch')
-
-
 def _hip():
     from . import producer_ops
     return producer_ops
@@ -48,21 +44,6 @@ def blur_kernel() -> torch.Tensor:
     k = torch.tensor([1.0, 3.0, 3.0, 1.0])
     k = k[:, None] * k[None, :]
     return k / k.sum()
-
-
-def _depthwise(x: torch.Tensor, k: torch.Tensor, stride: int, transpose: bool) -> torch.Tensor:
-    """Per-channel 4x4 FIR with padding 1 (`EfficientResample`): channels folded into the batch."""
-    b, c, h, w = x.shape
-    xf = x.reshape(b * c, 1, h, w)
-    kk = k[None, None].to(x.dtype)
-    y = (F.conv_transpose2d(xf, kk, padding=1, stride=stride) if transpose
-         else F.conv2d(xf, kk, padding=1, stride=stride))
-    return y.reshape(b, c, y.shape[-2], y.shape[-1])
-
-
-def upsample2x(x: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
-    """2x FIR upsampling of the skip image (`upsample2d`: transposed conv, gain 4)."""
-    return _depthwise(x, k * 4, stride=2, transpose=True)
 
 
 def frozen_value(mod: nn.Module, key: str, fn, *params):
@@ -123,25 +104,7 @@ class ModulatedConv(nn.Module):
         self.register_buffer('noise_const', torch.randn(resolution, resolution))
         self.register_buffer('resample_filter', blur_kernel())
 
-    backend = 'hip'
-
     def forward(self, x, w, pre=None):
-        if self.backend == 'hip':
-            return self._forward_hip(x, w, pre)
-        styles = self.affine(w)                                           # [b, in]
-        wmod = self.weight[None] * styles[:, None, :, None, None]         # [b, out, in, 3, 3]
-        dcoefs = (wmod.square().sum(dim=(2, 3, 4)) + 1e-8).rsqrt()        # [b, out]
-        x = x * styles[:, :, None, None]
-        if self.up:
-            x = F.conv_transpose2d(x, self.weight.transpose(0, 1), stride=2)
-            x = _depthwise(x, self.resample_filter * 4, stride=1, transpose=False)
-        else:
-            x = F.conv2d(x, self.weight, padding=1)
-        x = x * dcoefs[:, :, None, None]
-        x = (x + self.bias[None, :, None, None]) * SQRT2
-        return F.leaky_relu(x, 0.2)
-
-    def _forward_hip(self, x, w, pre=None):
         ops = _hip()
         if pre is None:
             styles = self.affine(w)
@@ -164,17 +127,13 @@ class ToPlanes(nn.Module):
         self.bias = nn.Parameter(torch.zeros(out_ch))
         self.weight_gain = 1.0 / math.sqrt(in_ch)
 
-    backend = 'hip'
-    out_layout = 'nhwc'     # 'hip' backend: the last resolution's layer is set to 'planes'
+    out_layout = 'nhwc'     # the last resolution's layer is set to 'planes'
 
     def forward(self, x, w, pre=None):
         styles = self.affine(w) * self.weight_gain if pre is None else pre
-        if self.backend == 'hip':
-            # channels-last (the skip-image chain's layout: its last image is the renderer's
-            # texel-major planes, no conversion pass); bias added in up_add
-            return _hip().modulated_conv1x1(x, styles, self.weight, layout=self.out_layout)
-        x = F.conv2d(x * styles[:, :, None, None], self.weight)
-        return x + self.bias[None, :, None, None]
+        # channels-last (the skip-image chain's layout: its last image is the renderer's
+        # texel-major planes, no conversion pass); bias added in up_add
+        return _hip().modulated_conv1x1(x, styles, self.weight, layout=self.out_layout)
 
 
 class SynthesisBlock(nn.Module):
@@ -192,8 +151,6 @@ class SynthesisBlock(nn.Module):
         self.register_buffer('resample_filter', blur_kernel())
         self.num_conv = 1 if in_ch == 0 else 2
 
-    backend = 'hip'
-
     def forward(self, x, img, ws, bank=None):
         """ws: this block's rows of the latent; bank: their precomputed (styles, dcoefs) per layer
         in the order conv0, conv1, torgb (SynthesisNetwork.style_bank), or None."""
@@ -206,10 +163,7 @@ class SynthesisBlock(nn.Module):
             k += 1
         x = self.conv1(x, ws[k], pre[k])
         y = self.torgb(x, ws[k + 1], pre[k + 1])
-        if self.backend == 'hip':
-            return x, _hip().up_add(img, y, self.torgb.bias)
-        img = y if img is None else upsample2x(img, self.resample_filter) + y
-        return x, img
+        return x, _hip().up_add(img, y, self.torgb.bias)
 
 
 class SynthesisNetwork(nn.Module):
@@ -228,7 +182,7 @@ class SynthesisNetwork(nn.Module):
             self.num_ws += blk.num_conv
         self.num_ws += 1   # the last block's toRGB
         # the last image is the tri-planes: written texel-major ([b, 3, 32, R, R] in the renderer's
-        # [b, 3, R, R, 32] storage, 'hip' backend), so render() reads it with no conversion pass
+        # [b, 3, R, R, 32] storage), so render() reads it with no conversion pass
         getattr(self, f'b{self.resolutions[-1]}').torgb.out_layout = 'planes'
 
     def forward(self, ws, noise_mode: str = 'const'):
@@ -236,7 +190,7 @@ class SynthesisNetwork(nn.Module):
         # (one unbind: its backward is one stack, not a zero-filled [b, num_ws, w_dim] gradient and
         # an accumulation per slice)
         bank = None
-        if torch.is_tensor(ws) and ws.is_cuda and self.b4.backend == 'hip':
+        if torch.is_tensor(ws) and ws.is_cuda:
             bank = iter(self.style_bank(ws))
         rows = ws.unbind(1) if torch.is_tensor(ws) else ws
         x = img = None
@@ -382,17 +336,14 @@ class MappingWrapper(nn.Module):
 
 
 class ConditionalLayerNorm(nn.Module):
-    """LayerNorm (no affine) with (1 + gamma(z)) scale and beta(z) shift (generator.py:42-60)."""
+    """LayerNorm (no affine) with (1 + gamma(z)) scale and beta(z) shift (generator.py:42-60): its
+    parameters; PaletteMapper applies all four norms from one batched projection (_conditions)."""
 
     def __init__(self, ch: int, emb_dim: int):
         super().__init__()
         self.ch = ch
         self.fc_gamma = EqualizedLinear(emb_dim, ch)
         self.fc_beta = EqualizedLinear(emb_dim, ch)
-
-    def forward(self, x, z):
-        x = F.layer_norm(x, (self.ch,))
-        return torch.addcmul(self.fc_beta(z), 1 + self.fc_gamma(z), x)
 
 
 def wide_sigmoid_rescaled(x):
@@ -413,21 +364,17 @@ class PaletteMapper(nn.Module):
         self.fc5 = EqualizedLinear(hidden, hidden)
         self.fc_values = EqualizedLinear(hidden, num_values * 3)
 
-    backend = 'hip'
-
     def forward(self, c):
         scale = SQRT2 / 2
         x = self.const.expand(c.shape[0], -1)
-        cond = self._conditions(c) if self.backend == 'hip' else None
+        cond = self._conditions(c)
         for pair in ((1, 2), (3, 4)):
             shortcut = x
             for i in pair:
                 h = getattr(self, f'fc{i}')(x)
-                if cond is None:
-                    x = F.leaky_relu(getattr(self, f'norm{i}')(h, c), 0.2)
-                else:        # (1 + gamma_i(c)) and beta_i(c) from the one batched projection
-                    g1, b = cond[2 * (i - 1)], cond[2 * (i - 1) + 1]
-                    x = F.leaky_relu(torch.addcmul(b, g1, F.layer_norm(h, (h.shape[-1],))), 0.2)
+                # (1 + gamma_i(c)) and beta_i(c) from the one batched projection
+                g1, b = cond[2 * (i - 1)], cond[2 * (i - 1) + 1]
+                x = F.leaky_relu(torch.addcmul(b, g1, F.layer_norm(h, (h.shape[-1],))), 0.2)
             x = (x + shortcut) * scale
         x = F.leaky_relu(self.fc5(x), 0.2)
         return wide_sigmoid_rescaled(self.fc_values(x).view(-1, self.num_values, 3))
@@ -468,7 +415,7 @@ class InversionGenerator(nn.Module):
     latent 512, attention_values=10, use_sdf, no viewdir / encoder / classes, StyleGAN noise
     disabled).  `nfi.render(gen, ...)` renders it; `planes_and_palette(ws)` exposes the producer."""
 
-    def __init__(self, scene_range: float, img_resolution: int = 256, backend: str = 'hip'):
+    def __init__(self, scene_range: float, img_resolution: int = 256):
         super().__init__()
         self.scene_range = scene_range
         self.attention_values = 10
@@ -482,19 +429,6 @@ class InversionGenerator(nn.Module):
         self.texture_mapper = PaletteMapper(512, 10)
         self.beta = nn.Parameter(torch.tensor([0.1]))
         self.alpha = nn.Parameter(torch.tensor([1.0]))
-        self.set_backend(backend)
-
-    def set_backend(self, backend: str):
-        """'hip' (fused HIP kernels between the convolutions, device tensors only) or 'torch'
-        (the reference's op sequence in plain PyTorch)."""
-        if backend not in BACKENDS:
-            raise ValueError(f'backend must be one of {BACKENDS}')
-        self.backend = backend
-        for m in self.synthesis_network.modules():
-            if isinstance(m, (ModulatedConv, ToPlanes, SynthesisBlock)):
-                m.backend = backend
-        self.texture_mapper.backend = backend
-        return self
 
     def planes_and_palette(self, ws):
         w_syn, w_tex = ws.split([14, ws.shape[1] - 14], dim=1)    # one split (its backward is one cat)

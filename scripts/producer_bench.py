@@ -16,8 +16,12 @@ def main():
     cl = '--channels-last' in sys.argv
     dev = torch.device('cuda:0')
     torch.manual_seed(0)
-    backend = 'torch' if '--torch' in sys.argv else 'hip'
-    gen = producer.InversionGenerator(1.4, backend=backend).to(dev).requires_grad_(False)
+    backend = 'torch' if '--torch' in sys.argv else 'hip'   # --torch: the oracle's reference op sequence
+    gen = producer.InversionGenerator(1.4).to(dev).requires_grad_(False)
+    if backend == 'torch':
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+        from oracle.producer_oracle import ReferenceProducer
+        gen = ReferenceProducer(gen)
     if cl:
         gen = gen.to(memory_format=torch.channels_last)
     ws = torch.randn(B, 15, 512, device=dev, requires_grad=True)

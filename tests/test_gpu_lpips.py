@@ -69,24 +69,24 @@ def _lpips_eval(net, a, b):
 
 
 def test_lpips_backends_agree():
-    """hip backend (Winograd F(4,3) trunk, fused epilogues and distance head) and hip with the
-    MIOpen trunk against an fp64 evaluation of the torch formulation; the torch backend in fp32
-    (MIOpen) is measured beside them.  The Winograd trunk's fp32 transform rounding (a few 1e-6
+    """nfi.lpips (Winograd F(4,3) trunk, fused epilogues and distance head) and the same with the
+    MIOpen trunk against an fp64 evaluation of the reference formulation (oracle/producer_oracle.py
+    over the same parameters); that formulation in fp32 (MIOpen) is measured beside them.  The Winograd trunk's fp32 transform rounding (a few 1e-6
     per layer, tests/test_gpu_conv.py) compounds over 13 layers and the ReLU masks to ~2e-4 in
     the image gradient: about 10x the MIOpen path's, still fp32-grade."""
     import copy
     torch.manual_seed(0)
-    net = lpips.LPIPS(backend='torch').to(DEV)
+    from oracle import producer_oracle as po
+    net = lpips.LPIPS().to(DEV)
     a = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV))
     b = torch.tanh(torch.randn(4, 3, 128, 128, device=DEV))
     net64 = copy.deepcopy(net).double().cpu()
-    ref, gref = _lpips_eval(net64, a.double().cpu(), b.double().cpu())
+    ref, gref = _lpips_eval(po.ReferenceLPIPS(net64), a.double().cpu(), b.double().cpu())
 
     def errs(r):
         return float((r[0] - ref).abs().max() / ref.abs().max()), float((r[1] - gref).norm() / gref.norm())
 
-    e_torch = errs(_lpips_eval(net, a, b))
-    net.backend = 'hip'
+    e_torch = errs(_lpips_eval(po.ReferenceLPIPS(net), a, b))
     e_wino = errs(_lpips_eval(net, a, b))
     try:
         lpips.VGG16Features.winograd = False

@@ -217,19 +217,20 @@ def test_up_add_channels_last(B, C, n, with_img):
 
 
 def test_backends_agree_on_gpu():
-    """Full producer: 'hip' (Winograd F(4,3) 3x3 convolutions, fused epilogues) and 'torch' (the
-    reference's op sequence, fp32) against the same op sequence in float64 on the device.  d ws
-    is ill-conditioned (sums over 2 x 96 x 256^2 plane gradients with cancellation): the torch
-    fp32 path itself is off by ~5e-4; 'hip' must stay within 4x of that (the GPU parity
-    convention of tests/test_gpu_parity.py)."""
+    """Full producer: nfi's (Winograd F(4,3) 3x3 convolutions, fused epilogues) and the reference's
+    op sequence (oracle/producer_oracle.py over the same modules, fp32) against that op sequence in
+    float64 on the device.  d ws is ill-conditioned (sums over 2 x 96 x 256^2 plane gradients with
+    cancellation): the reference's fp32 formulation itself is off by ~5e-4; nfi must stay within
+    4x of that (the GPU parity convention of tests/test_gpu_parity.py)."""
     import copy
+    from oracle.producer_oracle import ReferenceProducer
     torch.manual_seed(3)
     gen = producer.InversionGenerator(1.4).to(DEV).requires_grad_(False)
     ws = (0.6 * _rand(2, 15, 512, seed=16))
     g = _rand(2, 3, 32, 256, 256, seed=17)
 
     def ev(gn, dtype, be):
-        gn.set_backend(be)
+        gn = ReferenceProducer(gn) if be == 'torch' else gn
         w = ws.to(dtype).detach().clone().requires_grad_()
         planes, pal = gn.planes_and_palette(w)
         ((planes * g.to(dtype)).sum() + pal.sum()).backward()

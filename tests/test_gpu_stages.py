@@ -44,8 +44,9 @@ def test_near_far_matches_reference_fixture():
 
 def test_sample_pdf_matches_reference_fixture():
     """nerf_utils.py:185-224: deterministic (linspace u) and with the reference's torch.rand draws
-    injected; the first 16 rays have all-zero weights (a uniform pdf after + 1e-5).  The CDF is a
-    float cumulative sum: within 1e-5 of each ray's bin span (the fused kernel's bound)."""
+    injected; the first 16 rays have all-zero weights (a uniform pdf after + 1e-5).  The weight sum
+    is ATen's float sum in its order and the CDF its double-accumulated cumsum, so the bin choice is
+    the reference's (at u = 1 too); the interpolation within 1e-5 of each ray's bin span."""
     d, _ = load('stages')
     bins, w = d['pdf_bins'].to(DEV), d['pdf_w'].to(DEV)
     S = bins.shape[-1] + 1
@@ -76,7 +77,8 @@ def _comp_inputs(n=96, N=100, seed=0):
 
 
 def _comp_run(fn, inp, gr, dtype, dev, white, extras):
-    x = {k: v.to(dev, dtype).requires_grad_(k in ('t', 'sigma', 'rgb', 'rd', 'normals', 'sem')) for k, v in inp.items()}
+    x = {k: v.detach().to(dev, dtype, copy=True).requires_grad_(k in ('t', 'sigma', 'rgb', 'rd', 'normals', 'sem'))
+         for k, v in inp.items()}
     out = fn(x['sigma'], x['rgb'], x['ro'], x['rd'], x['t'], normals=x['normals'] if extras else None,
              semantics=x['sem'] if extras else None, white_background=white)
     rgb_map, depth, mask, nmap, smap = out
@@ -116,9 +118,9 @@ def _sampler_field(nattn=10, sdf=True, seed=3, B=2, R=32):
 
 
 def _sampler_run(inp, x, gs, gr, gd, dtype, dev, nattn, sdf, outputs):
-    planes = inp['planes'].to(dev, dtype).requires_grad_()
-    pal = inp['palette'].to(dev, dtype).requires_grad_() if nattn else None
-    xx = x.to(dev, dtype).requires_grad_()
+    planes = inp['planes'].detach().to(dev, dtype, copy=True).requires_grad_()
+    pal = inp['palette'].detach().to(dev, dtype, copy=True).requires_grad_() if nattn else None
+    xx = x.detach().to(dev, dtype, copy=True).requires_grad_()
     if dev == DEV:
         nfi.configure(scene_range=1.4)
         f = nfi.TriplaneField(planes=planes, palette=pal, w1=inp['w1'].to(dev), b1=inp['b1'].to(dev),

@@ -3,17 +3,19 @@ third-party `lpips` 0.1 package with pretrained VGG16 + lin weights (lib/metrics
 neither the package nor the weights exist offline, so no reference output can be produced.
 These CPU tests check the restated structure: state_dict layout of the two weight files it
 loads, the metric's identities (d(x, x) = 0, symmetry, non-negativity), and the distance head
-against a direct per-pixel evaluation.  The HIP head is checked against the torch backend in
-tests/test_gpu_lpips.py."""
+against a direct per-pixel evaluation — on the oracle's PyTorch formulation over the module's
+parameters (oracle/producer_oracle.py: nfi.lpips itself runs on the GPU only).  The HIP LPIPS is
+checked against it in tests/test_gpu_lpips.py."""
 
 import pytest
 import torch
 
 from nfi import lpips
+from oracle import producer_oracle as po
 
 
 def test_weight_layout_matches_torchvision_and_lpips_files():
-    net = lpips.LPIPS(backend='torch')
+    net = lpips.LPIPS()
     keys = set(net.net.state_dict())
     # torchvision vgg16().features conv indices
     convs = [0, 2, 5, 7, 10, 12, 14, 17, 19, 21, 24, 26, 28]
@@ -28,7 +30,7 @@ def test_weight_layout_matches_torchvision_and_lpips_files():
 
 def test_metric_identities():
     torch.manual_seed(0)
-    net = lpips.LPIPS(backend='torch')
+    net = po.ReferenceLPIPS(lpips.LPIPS())
     a = torch.tanh(torch.randn(3, 3, 64, 64))
     b = torch.tanh(torch.randn(3, 3, 64, 64))
     dab, dba, daa = net(a, b), net(b, a), net(a, a)
@@ -42,7 +44,7 @@ def test_distance_head_per_pixel():
     torch.manual_seed(1)
     f0, f1 = torch.randn(2, 5, 3, 4).relu(), torch.randn(2, 5, 3, 4).relu()
     w = torch.rand(5)
-    got = (lpips.normalize(f0) - lpips.normalize(f1)).square().mul(w[None, :, None, None]).sum(1).mean((1, 2))
+    got = (po.lpips_normalize(f0) - po.lpips_normalize(f1)).square().mul(w[None, :, None, None]).sum(1).mean((1, 2))
     want = torch.zeros(2)
     for n in range(2):
         for y in range(3):
@@ -60,7 +62,7 @@ def test_vgg_loss_matches_reference_augmentation_order(white):
     gradient to the prediction."""
     from nfi import inversion
     torch.manual_seed(3)
-    net = lpips.LPIPS(backend='torch')
+    net = po.ReferenceLPIPS(lpips.LPIPS())
     rgb = torch.tanh(torch.randn(2, 32, 32, 3)).requires_grad_()
     target = torch.tanh(torch.randn(2, 32, 32, 3))
     got = inversion.image_loss('vgg', rgb, target, net, white, torch.Generator().manual_seed(5))

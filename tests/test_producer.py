@@ -2,7 +2,9 @@
 outputs (tests/golden/producer.npz, pose.npz, inversion.npz; written by gen_golden.py from the
 reference Generator, pose_utils and render() with the seeded weights of golden_io.load_seeded).
 
-CPU: producer (mapping, synthesis, AttentionMapper) forward + latent gradient at full size;
+CPU: producer (mapping, synthesis, AttentionMapper) forward + latent gradient at full size — the
+oracle's restatement of the reference op sequence over nfi.producer's modules
+(oracle/producer_oracle.py; nfi's own producer runs on the GPU only: tests/test_gpu_inversion.py);
 pose_to_matrix / matrix_to_pose; the inversion loop with the oracle as its renderer (the loop,
 pose handling, Adam and producer are then the only things under test).
 The GPU trajectory (HIP renderer in the loop) is tests/test_gpu_inversion.py.
@@ -16,15 +18,16 @@ import torch
 
 from golden_io import load, load_seeded
 from nfi import inversion, producer
+from oracle.producer_oracle import ReferenceProducer
 
 
 @pytest.fixture(scope='module')
 def prod():
     d, meta = load('producer')
-    gen = producer.InversionGenerator(scene_range=1.4, backend='torch')
+    gen = producer.InversionGenerator(scene_range=1.4)
     load_seeded(gen, int(meta['seed']))
     gen.requires_grad_(False)
-    return gen, d
+    return ReferenceProducer(gen), d
 
 
 def test_state_dict_matches_reference(prod):
@@ -101,12 +104,13 @@ def oracle_render_fn(scene_range):
 
 def inversion_setup(device='cpu'):
     d, meta = load('inversion')
-    gen = producer.InversionGenerator(scene_range=float(meta['scene_range']),
-                                      backend='torch' if str(device) == 'cpu' else 'hip')
+    gen = producer.InversionGenerator(scene_range=float(meta['scene_range']))
     load_seeded(gen, int(meta['seed']))
     with torch.no_grad():
         gen.decoder.net[2].bias[0] += float(meta['sdf_shift'])
     gen.requires_grad_(False).to(device)
+    if str(device) == 'cpu':
+        gen = ReferenceProducer(gen)      # the CPU loop: the reference's producer op sequence
     cfg = inversion.InversionConfig(steps=int(meta['steps']), resolution=int(meta['H']),
                                     samples=int(meta['S']), loss='l1',
                                     camera_flipped=bool(meta['flipped']))
@@ -171,14 +175,13 @@ def test_inversion_default_renderer_is_hip_only():
                          uniforms=lambda it: (d['u_coarse'][it], d['u_fine'][it]))
 
 
-def test_hip_backend_refuses_cpu_tensors():
-    gen = producer.InversionGenerator(scene_range=1.4)          # default backend: hip
-    assert gen.backend == 'hip'
+def test_producer_refuses_cpu_tensors():
+    """nfi's producer has one implementation, the HIP one: CPU tensors raise (no fallback)."""
+    gen = producer.InversionGenerator(scene_range=1.4)
     gen.requires_grad_(False)
     with pytest.raises(RuntimeError, match='HIP devices only'):
         gen.planes_and_palette(torch.zeros(1, 15, 512))
-    with pytest.raises(ValueError):
-        gen.set_backend('cpu')
+    assert not hasattr(gen, 'set_backend')
 
 
 def test_style_bank_layer_rows():
