@@ -148,7 +148,8 @@ typedef struct nfi_render_grad_args {
   const int32_t* tile_counts; /* the forward's tile_counts, or NULL (the backward counts itself) */
   void* workspace;      /* device scratch of nfi_render_backward_workspace_bytes() bytes */
   int64_t workspace_bytes;
-  float* d_xray;        /* NFI_HEAD_VIEWDIR: [B*HW,32] dL/d xray, ACCUMULATED into (zero it); else NULL */
+  float* d_xray;        /* NFI_HEAD_VIEWDIR: [B*HW*ceil(N/64),32] per-(ray, 64-sample chunk) partial dL/d xray
+                           (written; the caller sums each ray's chunks); else NULL */
 } nfi_render_grad_args;
 
 int32_t nfi_abi_version(void);

@@ -1189,7 +1189,7 @@ struct BwdArgs {
   int* cursor;            // [K] tile fill cursors (NULL: bins filled by bin_fill_kernel)
   int4* list;             // [3*rays*N] tile entries
   TileGrid tg;            // tile grid of a plane
-  float* d_xray;          // [rays][32] dL/d view-direction mapper output (NFI_HEAD_VIEWDIR), accumulated
+  float* d_xray;          // [rays][npl][32] per-(ray, chunk) dL/d view-direction mapper output (NFI_HEAD_VIEWDIR)
 };
 
 // One 64-sample chunk of the compositing backward's reverse scan: lane k's map x -> A_k x + B_k
@@ -1487,7 +1487,9 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
 #pragma unroll
     for (int jj = 0; jj < 32; ++jj) s4[jj & 3] += X[(r0 + jj) * XS + 1 + col];
     const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
-    if (l < NVF) unsafeAtomicAdd(g.d_xray + r * NVF + l, sh);
+    // per-(ray, chunk) partial, summed over the chunks by the caller in a fixed order (no float
+    // atomics: the mapper's gradients are bitwise reproducible)
+    if (l < NVF) g.d_xray[(r * g.npl + e) * NVF + l] = sh;
   }
   NFI_STAMP(18)
   f4v gxo[2][4];

@@ -381,7 +381,8 @@ class _VolumeRender(torch.autograd.Function):
         npl = ((2 * opts.samples if opts.fine else opts.samples) + 63) // 64
         d_pal_ray = torch.empty((n * npl, 30), device=dev) if pal is not None else None
         need_coords = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
-        d_xray = torch.zeros((n, 32), device=dev) if xray is not None else None
+        # per-(ray, chunk) partials of dL/d xray, summed over a ray's chunks below (fixed order)
+        d_xray = torch.empty((n * npl, 32), device=dev) if xray is not None else None
         g_ro = torch.empty((n, 3), device=dev) if need_coords else None
         g_rd = torch.empty((n, 3), device=dev) if need_coords else None
         HW = H * W
@@ -412,7 +413,7 @@ class _VolumeRender(torch.autograd.Function):
                 d_palette_ray=_ptr(None if d_pal_ray is None else d_pal_ray[r0 * npl:r1 * npl]),
                 g_ro=_ptr(None if g_ro is None else g_ro[r0:r1]), g_rd=_ptr(None if g_rd is None else g_rd[r0:r1]),
                 tile_counts=_ptr(tc), workspace=_ptr(ws), workspace_bytes=nbytes,
-                d_xray=_ptr(None if d_xray is None else d_xray[r0:r1]))
+                d_xray=_ptr(None if d_xray is None else d_xray[r0 * npl:r1 * npl]))
             return a, g, ws
 
         def stage(p, k, name, strm):
@@ -459,7 +460,7 @@ class _VolumeRender(torch.autograd.Function):
         d_rd = g_rd.view(B, H, W, 3) if need_coords else None
         d_xr = None
         if xray is not None and ctx.needs_input_grad[12]:
-            d_xr = d_xray.view(xray.shape)
+            d_xr = d_xray.view(n, npl, 32).sum(dim=1).view(xray.shape)
         return (d_planes, d_pal, d_ro, d_rd, None, None, None, None, None, None, None, None, d_xr, None)
 
 
