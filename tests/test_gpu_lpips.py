@@ -6,6 +6,7 @@ tests/test_lpips.py)."""
 import pytest
 import torch
 
+from oracle import producer_oracle as po
 from nfi import inversion, lpips, producer_ops
 
 pytestmark = pytest.mark.gpu
@@ -23,7 +24,7 @@ def test_lpips_head_matches_torch(N, C, H):
     out = producer_ops.lpips_head(f0, f1, w)
     out.backward(gout)
     r0 = f0.detach().clone().requires_grad_()
-    ref = (lpips.normalize(r0) - lpips.normalize(f1)).square().mul(w[None, :, None, None]).sum(1).mean((1, 2))
+    ref = (po.lpips_normalize(r0) - po.lpips_normalize(f1)).square().mul(w[None, :, None, None]).sum(1).mean((1, 2))
     ref.backward(gout)
     torch.testing.assert_close(out.detach(), ref.detach(), rtol=1e-5, atol=1e-7)
     gref = torch.nan_to_num(r0.grad, nan=0.0)     # torch: 0/0 at the all-zero vector

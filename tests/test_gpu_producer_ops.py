@@ -8,6 +8,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from oracle import producer_oracle as po
 from nfi import producer, producer_ops
 
 pytestmark = pytest.mark.gpu
@@ -71,7 +72,7 @@ def test_fir_up_act(B, C, n):
     y = producer_ops.fir_up_act(t, d, bias, GAIN)
     y.backward(g)
     trf, drf = t.detach().clone().requires_grad_(), d.detach().clone().requires_grad_()
-    o = producer._depthwise(trf, producer.blur_kernel().to(DEV) * 4, stride=1, transpose=False)
+    o = po._depthwise(trf, producer.blur_kernel().to(DEV) * 4, stride=1, transpose=False)
     yr = _act_ref(o, drf, bias)
     yr.backward(g)
     _close(y.detach(), yr.detach())
@@ -162,7 +163,7 @@ def test_up_add(B, C, n, with_img):
     yr = crf + bias[None, :, None, None]
     if with_img:
         irf = img.detach().clone().requires_grad_()
-        yr = producer.upsample2x(irf, producer.blur_kernel().to(DEV)) + yr
+        yr = po._depthwise(irf, producer.blur_kernel().to(DEV) * 4, stride=2, transpose=True) + yr
     yr.backward(g)
     _close(out.detach(), yr.detach())
     _close(c.grad, crf.grad)
