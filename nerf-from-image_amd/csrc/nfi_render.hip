@@ -121,6 +121,105 @@ constexpr int GATHER_GB = NFI_GATHER_GB;
 #define NFI_GATHER_PIPE 0
 #endif
 
+// NFI_GATHER_V2 (default): the gather's addressing and interpolation trimmed for the VALU, which
+// the forward is bound by (r03 counters: VALU busy ~54 %, the gather ~half of it):
+//  * each lane turns its point's three cells into BYTE offsets once (flags in bits 30/31), and the
+//    texel rows load through a buffer resource on the image's planes (wave-uniform SGPRs: the plane
+//    offset goes in soffset) — no per-load 64-bit address arithmetic and no quarter-rate
+//    v_mul_lo_u32 per load;
+//  * the three planes' weighted texels are summed per lane before the one DPP row_ror:8 that adds
+//    the x0 / x0+1 lanes (the bilinear tap and the plane mean are both linear): one cross-lane add
+//    per group instead of three.
+#ifndef NFI_GATHER_V2
+#define NFI_GATHER_V2 1
+#endif
+
+#if NFI_GATHER_V2
+struct GatherCtx {
+  __amdgpu_buffer_rsrc_t rsrc;   // this image's planes
+  int sq4;                       // plane stride, bytes (wave-uniform: soffset)
+  int st4, rowb;                 // texel stride and texel-row stride, bytes
+  int off[3];                    // this lane's point: cell byte offsets | x0 < R-1 << 30 | y0 < R-1 << 31
+};
+
+__device__ __forceinline__ GatherCtx gather_ctx(const PlaneView& pv, const PointP& P) {
+  GatherCtx c;
+  const uint64_t b = reinterpret_cast<uint64_t>(pv.base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  c.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                             0x7FFFFFFF, 0x00020000);
+  c.sq4 = __builtin_amdgcn_readfirstlane(pv.sq * 4);
+  c.st4 = pv.st * 4;
+  c.rowb = pv.R * pv.st * 4;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int t = P.pl[q].tex;
+    c.off[q] = (int)(((uint32_t)(t & 0xFFFFF) * (uint32_t)c.st4) | (((uint32_t)t >> 20 & 1u) << 30) |
+                     (((uint32_t)t >> 21 & 1u) << 31));
+  }
+  return c;
+}
+
+__device__ __forceinline__ float4 buf_ld4(const GatherCtx& c, int voff, int q) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(c.rsrc, voff, q * c.sq4, 0);
+  return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
+}
+
+__device__ __forceinline__ void gather_issue(const GatherCtx& c, const PointP& P, int g, int sub, int dx, int q4,
+                                             float4 (&V0)[3], float4 (&V1)[3], float (&W0)[3], float (&W1)[3]) {
+  const int j = min(4 * g + sub, WAVE - 1);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int pk = __shfl(c.off[q], j);
+    const float w = __shfl(P.pl[q].w, j), n = __shfl(P.pl[q].n, j);
+    const float e = 1.f - w, s = 1.f - n;
+    const int t0 = (pk & 0x3FFFFFFF) + ((dx && (pk & 0x40000000)) ? c.st4 : 0) + 16 * q4;
+    const int t1 = t0 + (pk < 0 ? c.rowb : 0);
+    V0[q] = buf_ld4(c, t0, q);
+    V1[q] = buf_ld4(c, t1, q);
+    const float wx = dx ? w : e;
+    W0[q] = s * wx;
+    W1[q] = n * wx;
+  }
+}
+
+__device__ __forceinline__ void gather_consume(int g, int sub, int dx, int q4, int npts, const float4 (&V0)[3],
+                                               const float4 (&V1)[3], const float (&W0)[3],
+                                               const float (&W1)[3], float* __restrict__ X) {
+  const int j = 4 * g + sub;
+  float4 pr;
+  pr.x = (V0[0].x * W0[0] + V1[0].x * W1[0]) + (V0[1].x * W0[1] + V1[1].x * W1[1]) + (V0[2].x * W0[2] + V1[2].x * W1[2]);
+  pr.y = (V0[0].y * W0[0] + V1[0].y * W1[0]) + (V0[1].y * W0[1] + V1[1].y * W1[1]) + (V0[2].y * W0[2] + V1[2].y * W1[2]);
+  pr.z = (V0[0].z * W0[0] + V1[0].z * W1[0]) + (V0[1].z * W0[1] + V1[1].z * W1[1]) + (V0[2].z * W0[2] + V1[2].z * W1[2]);
+  pr.w = (V0[0].w * W0[0] + V1[0].w * W1[0]) + (V0[1].w * W0[1] + V1[1].w * W1[1]) + (V0[2].w * W0[2] + V1[2].w * W1[2]);
+  const float4 E = ror8_add(pr);
+  if (dx == 0 && j < npts) {
+    float4 f;
+    f.x = E.x * (1.f / 3.f);
+    f.y = E.y * (1.f / 3.f);
+    f.z = E.z * (1.f / 3.f);
+    f.w = E.w * (1.f / 3.f);
+    *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
+  }
+}
+
+__device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
+                                                float* __restrict__ X) {
+  const int l = lane_id();
+  const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
+  const int ngrp = (npts + 3) >> 2;
+  const GatherCtx c = gather_ctx(pv, P);
+#pragma unroll 1
+  for (int gb = 0; gb < ngrp; gb += GATHER_GB) {
+    float4 V0[GATHER_GB][3], V1[GATHER_GB][3];
+    float W0[GATHER_GB][3], W1[GATHER_GB][3];
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u) gather_issue(c, P, gb + u, sub, dx, q4, V0[u], V1[u], W0[u], W1[u]);
+#pragma unroll
+    for (int u = 0; u < GATHER_GB; ++u) gather_consume(gb + u, sub, dx, q4, npts, V0[u], V1[u], W0[u], W1[u], X);
+  }
+}
+#else
 // One group's loads: the parameters of point 4g + sub arrive by ds_bpermute (e = 1 - w and s = 1 - n
 // recomputed as plane_params rounds them: 3 ds_bpermute per plane instead of 5), then the two
 // texel rows of each plane.
@@ -200,6 +299,8 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
   }
 #endif
 }
+
+#endif
 
 // ---------------------------------------------------------------------------------------
 // d planes by plane tile: every (sample, plane) contribution is binned by the 7x4-cell tile of
@@ -701,6 +802,25 @@ __device__ __forceinline__ float aten_row_sum(const float* x, int start, int ste
   for (int k = 1; k < 4; ++k) p[0] = fadd(p[0], p[k]);
   return p[0];
 }
+// row_sum of at most 16 items with every load issued before the adds (no dependent LDS round
+// trips; the multi_row_sum cascade needs >= 16 rows of 4, so none here): the same order
+__device__ __forceinline__ float aten_row_sum16(const float* x, int start, int step, int size) {
+  float y[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) y[i] = x[start + min(i, max(size - 1, 0)) * step];
+  const int si = size / 4;
+  float p[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i < si) p[k] = fadd(p[k], y[4 * i + k]);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i >= si * 4 && i < size) p[0] = fadd(p[0], y[i]);
+  return fadd(fadd(fadd(p[0], p[1]), p[2]), p[3]);
+}
+
 // The sum of x[0..n) (wave-uniform n, x in LDS) in every lane: lanes 0..7 run the 8 vector
 // lanes' row_sums side by side, lane 8 the tail, then the 8 lane results are added in order.
 __device__ __forceinline__ float aten_sum_f32(const float* x, int n) {
@@ -708,14 +828,19 @@ __device__ __forceinline__ float aten_sum_f32(const float* x, int n) {
   const int l = lane_id();
   float v = 0.f;
   if (n < VEC) {
-    if (l == 0) v = aten_row_sum(x, 0, 1, n);
+    if (l == 0) v = aten_row_sum16(x, 0, 1, n);
     return readlane(v, 0);
   }
   const int V = n / VEC;
   if (l < VEC) {
-    v = aten_row_sum(x, l, VEC, V);
+    v = V <= 16 ? aten_row_sum16(x, l, VEC, V) : aten_row_sum(x, l, VEC, V);
   } else if (l == VEC) {
-    for (int k = V * VEC; k < n; ++k) v = fadd(v, x[k]);
+    float t[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) t[k] = x[min(V * VEC + k, n - 1)];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k)
+      if (V * VEC + k < n) v = fadd(v, t[k]);
   }
   float acc = readlane(v, VEC);
 #pragma unroll

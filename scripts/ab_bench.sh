@@ -9,12 +9,12 @@ show() {
 import json, sys
 line = [x for x in open(sys.argv[2]) if x.startswith('{')][-1]
 d = json.loads(line)
-print(f"{sys.argv[1]:5s} {d['value']:9.1f}", {k: v['ms'] for k, v in d['roofline']['stages'].items()}, flush=True)
+print(f"{sys.argv[1]:5s} {d['value']:9.1f}", {k: v['ms'] for k, v in d['stages'].items()}, flush=True)
 EOF
 }
 for i in $(seq "$rounds"); do
-  timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion "$@" > gpurun_out/ab_new.log 2>&1 || exit 1
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion --no-configs "$@" > gpurun_out/ab_new.log 2>&1 || exit 1
   show new gpurun_out/ab_new.log || exit 1
-  NFI_LIBRARY=$other timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion "$@" > gpurun_out/ab_old.log 2>&1 || exit 1
+  NFI_LIBRARY=$other timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion --no-configs "$@" > gpurun_out/ab_old.log 2>&1 || exit 1
   show other gpurun_out/ab_old.log || exit 1
 done
