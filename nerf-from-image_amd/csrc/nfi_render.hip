@@ -92,14 +92,27 @@ struct PlaneView {
   int sq, st, R;
 };
 
-// Gather + interpolate + mean-of-3 for points 0..npts-1 of the wave (point j's parameters live
-// in lane j); writes X[j][0..31] (j < npts) into the wave's LDS tile.
+// Gather + interpolate + mean-of-3 for points 0..npts-1 of the wave; writes X[j][0..31]
+// (j < npts) into the wave's LDS tile.
 //
 // Lane layout ("quad" gather): lane = (sub = l>>4, dx = (l>>3)&1, q4 = l&7).  One wave
 // instruction serves four points (sub), each a bilinear row pair of 2 texels x 32 channels
-// (dx selects x0 / x0+1, q4 a float4 of channels): 4 x 256 contiguous bytes per 1-KiB load.
-// Point parameters arrive by ds_bpermute from the owning lane; the two texels of a row are
-// combined with a DPP row_ror:8 (lanes l and l^8 of a 16-lane row).
+// (dx selects x0 / x0+1, q4 a float4 of channels): 4 x 256 contiguous bytes per 1-KiB load,
+// through a buffer resource on the image's planes (no per-load 64-bit address arithmetic).
+// The three planes' weighted texels are summed per lane before the one DPP row_ror:8 that adds
+// the x0 / x0+1 lanes (the bilinear tap and the plane mean are both linear).
+//
+// Load records: every lane first writes its own point's records into its row of the X tile —
+// per (plane, dx) the byte offsets of the two texel rows and their two weights with the mean's
+// 1/3 folded in, {t0, t1, W0/3, W1/3} — and a lane serving point j fetches its record with one
+// ds_read_b128 per plane.  The records of row j are read when group j/4 is issued; the row is
+// overwritten by that group's features only after (a wave's LDS operations complete in order).
+// Measured on MI355X (render_fwd, p3d B=8): 2.24 ms against 2.27-2.32 ms for the same gather
+// with the parameters ds_bpermuted from the owning lane and unpacked per serving lane and group
+// (~40 more VALU per group).  Variants that did not pay: a software pipeline over single groups
+// (2.58 vs 2.50 ms, r02), 3-4 groups per batch (spills at the occupancy-4 register budget),
+// dword prefetches of the next batch's lines (2.93 ms: the gather is bound by the texture
+// path's request rate, which the extra requests share, not by latency alone).
 __device__ __forceinline__ float4 ror8_add(float4 v) {
   v.x += dpp_mov<0x128>(v.x);
   v.y += dpp_mov<0x128>(v.y);
@@ -108,84 +121,48 @@ __device__ __forceinline__ float4 ror8_add(float4 v) {
   return v;
 }
 
-// Loads of GB groups (4*GB points) are issued before any is consumed: the gather is bound by
-// load latency (texels mostly come from MALL/HBM), so the wave keeps 6*GB KiB in flight.
+// Loads of GB groups (4*GB points) are issued before any is consumed (6*GB KiB in flight per wave).
 #ifndef NFI_GATHER_GB
 #define NFI_GATHER_GB 2
 #endif
 constexpr int GATHER_GB = NFI_GATHER_GB;
 
-// NFI_GATHER_PIPE 1: software pipeline over single groups (measured slower on MI355X: 2.58 vs
-// 2.50 ms forward — the batched form keeps more bytes in flight at the same register count)
-#ifndef NFI_GATHER_PIPE
-#define NFI_GATHER_PIPE 0
-#endif
-
-// NFI_GATHER_V2 (default): the gather's addressing and interpolation trimmed for the VALU, which
-// the forward is bound by (r03 counters: VALU busy ~54 %, the gather ~half of it):
-//  * each lane turns its point's three cells into BYTE offsets once (flags in bits 30/31), and the
-//    texel rows load through a buffer resource on the image's planes (wave-uniform SGPRs: the plane
-//    offset goes in soffset) — no per-load 64-bit address arithmetic and no quarter-rate
-//    v_mul_lo_u32 per load;
-//  * the three planes' weighted texels are summed per lane before the one DPP row_ror:8 that adds
-//    the x0 / x0+1 lanes (the bilinear tap and the plane mean are both linear): one cross-lane add
-//    per group instead of three.
-#ifndef NFI_GATHER_V2
-#define NFI_GATHER_V2 1
-#endif
-
-#if NFI_GATHER_V2
-struct GatherCtx {
-  __amdgpu_buffer_rsrc_t rsrc;   // this image's planes
-  int sq4;                       // plane stride, bytes (wave-uniform: soffset)
-  int st4, rowb;                 // texel stride and texel-row stride, bytes
-  int off[3];                    // this lane's point: cell byte offsets | x0 < R-1 << 30 | y0 < R-1 << 31
-};
-
-__device__ __forceinline__ GatherCtx gather_ctx(const PlaneView& pv, const PointP& P) {
-  GatherCtx c;
-  const uint64_t b = reinterpret_cast<uint64_t>(pv.base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  c.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
-                                             0x7FFFFFFF, 0x00020000);
-  c.sq4 = __builtin_amdgcn_readfirstlane(pv.sq * 4);
-  c.st4 = pv.st * 4;
-  c.rowb = pv.R * pv.st * 4;
+__device__ __forceinline__ void gather_records(const PlaneView& pv, const PointP& P, float* __restrict__ X) {
+  const int st4 = pv.st * 4, rowb = pv.R * pv.st * 4, sq4 = pv.sq * 4;
+  float* row = X + lane_id() * XS;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const int t = P.pl[q].tex;
-    c.off[q] = (int)(((uint32_t)(t & 0xFFFFF) * (uint32_t)c.st4) | (((uint32_t)t >> 20 & 1u) << 30) |
-                     (((uint32_t)t >> 21 & 1u) << 31));
+    const int o0 = (t & 0xFFFFF) * st4 + q * sq4;
+    const int o1 = o0 + (((t >> 20) & 1) ? st4 : 0);
+    const int dy = ((t >> 21) & 1) ? rowb : 0;
+    const float w = P.pl[q].w, n = P.pl[q].n, e = 1.f - w, s = 1.f - n;
+    *reinterpret_cast<float4*>(row + 8 * q) =
+        make_float4(__int_as_float(o0), __int_as_float(o0 + dy), (s * e) * (1.f / 3.f), (n * e) * (1.f / 3.f));
+    *reinterpret_cast<float4*>(row + 8 * q + 4) =
+        make_float4(__int_as_float(o1), __int_as_float(o1 + dy), (s * w) * (1.f / 3.f), (n * w) * (1.f / 3.f));
   }
-  return c;
 }
 
-__device__ __forceinline__ float4 buf_ld4(const GatherCtx& c, int voff, int q) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(c.rsrc, voff, q * c.sq4, 0);
-  return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
-}
-
-__device__ __forceinline__ void gather_issue(const GatherCtx& c, const PointP& P, int g, int sub, int dx, int q4,
-                                             float4 (&V0)[3], float4 (&V1)[3], float (&W0)[3], float (&W1)[3]) {
-  const int j = min(4 * g + sub, WAVE - 1);
+__device__ __forceinline__ void gather_issue(__amdgpu_buffer_rsrc_t rsrc, const float* __restrict__ X, int g,
+                                              int sub, int dx, int q4, float4 (&V0)[3], float4 (&V1)[3],
+                                              float (&W0)[3], float (&W1)[3]) {
+  const float* rec = X + (4 * g + sub) * XS + 4 * dx;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    const int pk = __shfl(c.off[q], j);
-    const float w = __shfl(P.pl[q].w, j), n = __shfl(P.pl[q].n, j);
-    const float e = 1.f - w, s = 1.f - n;
-    const int t0 = (pk & 0x3FFFFFFF) + ((dx && (pk & 0x40000000)) ? c.st4 : 0) + 16 * q4;
-    const int t1 = t0 + (pk < 0 ? c.rowb : 0);
-    V0[q] = buf_ld4(c, t0, q);
-    V1[q] = buf_ld4(c, t1, q);
-    const float wx = dx ? w : e;
-    W0[q] = s * wx;
-    W1[q] = n * wx;
+    const float4 R = *reinterpret_cast<const float4*>(rec + 8 * q);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __float_as_int(R.x) + 16 * q4, 0, 0);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __float_as_int(R.y) + 16 * q4, 0, 0);
+    V0[q] = make_float4(__int_as_float(v0[0]), __int_as_float(v0[1]), __int_as_float(v0[2]), __int_as_float(v0[3]));
+    V1[q] = make_float4(__int_as_float(v1[0]), __int_as_float(v1[1]), __int_as_float(v1[2]), __int_as_float(v1[3]));
+    W0[q] = R.z;
+    W1[q] = R.w;
   }
 }
 
 __device__ __forceinline__ void gather_consume(int g, int sub, int dx, int q4, int npts, const float4 (&V0)[3],
-                                               const float4 (&V1)[3], const float (&W0)[3],
-                                               const float (&W1)[3], float* __restrict__ X) {
+                                                const float4 (&V1)[3], const float (&W0)[3],
+                                                const float (&W1)[3], float* __restrict__ X) {
   const int j = 4 * g + sub;
   float4 pr;
   pr.x = (V0[0].x * W0[0] + V1[0].x * W1[0]) + (V0[1].x * W0[1] + V1[1].x * W1[1]) + (V0[2].x * W0[2] + V1[2].x * W1[2]);
@@ -193,14 +170,7 @@ __device__ __forceinline__ void gather_consume(int g, int sub, int dx, int q4, i
   pr.z = (V0[0].z * W0[0] + V1[0].z * W1[0]) + (V0[1].z * W0[1] + V1[1].z * W1[1]) + (V0[2].z * W0[2] + V1[2].z * W1[2]);
   pr.w = (V0[0].w * W0[0] + V1[0].w * W1[0]) + (V0[1].w * W0[1] + V1[1].w * W1[1]) + (V0[2].w * W0[2] + V1[2].w * W1[2]);
   const float4 E = ror8_add(pr);
-  if (dx == 0 && j < npts) {
-    float4 f;
-    f.x = E.x * (1.f / 3.f);
-    f.y = E.y * (1.f / 3.f);
-    f.z = E.z * (1.f / 3.f);
-    f.w = E.w * (1.f / 3.f);
-    *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
-  }
+  if (dx == 0 && j < npts) *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = E;
 }
 
 __device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
@@ -208,99 +178,22 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
   const int l = lane_id();
   const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
   const int ngrp = (npts + 3) >> 2;
-  const GatherCtx c = gather_ctx(pv, P);
+  gather_records(pv, P, X);
+  wave_lds_sync();
+  const uint64_t pb = reinterpret_cast<uint64_t>(pv.base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32));
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll 1
   for (int gb = 0; gb < ngrp; gb += GATHER_GB) {
     float4 V0[GATHER_GB][3], V1[GATHER_GB][3];
     float W0[GATHER_GB][3], W1[GATHER_GB][3];
 #pragma unroll
-    for (int u = 0; u < GATHER_GB; ++u) gather_issue(c, P, gb + u, sub, dx, q4, V0[u], V1[u], W0[u], W1[u]);
+    for (int u = 0; u < GATHER_GB; ++u) gather_issue(rsrc, X, gb + u, sub, dx, q4, V0[u], V1[u], W0[u], W1[u]);
 #pragma unroll
     for (int u = 0; u < GATHER_GB; ++u) gather_consume(gb + u, sub, dx, q4, npts, V0[u], V1[u], W0[u], W1[u], X);
   }
 }
-#else
-// One group's loads: the parameters of point 4g + sub arrive by ds_bpermute (e = 1 - w and s = 1 - n
-// recomputed as plane_params rounds them: 3 ds_bpermute per plane instead of 5), then the two
-// texel rows of each plane.
-__device__ __forceinline__ void gather_issue(const PlaneView& pv, const PointP& P, int g, int sub, int dx,
-                                             int q4, float4 (&V0)[3], float4 (&V1)[3], float (&W0)[3],
-                                             float (&W1)[3]) {
-  const int j = min(4 * g + sub, WAVE - 1);
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int pk = __shfl(P.pl[q].tex, j);
-    const float w = __shfl(P.pl[q].w, j), n = __shfl(P.pl[q].n, j);
-    const float e = 1.f - w, s = 1.f - n;
-    const int t0 = (pk & 0xFFFFF) + (dx ? ((pk >> 20) & 1) : 0);
-    const int t1 = t0 + (((pk >> 21) & 1) ? pv.R : 0);
-    const float* b = pv.base + q * pv.sq + 4 * q4;
-    V0[q] = *reinterpret_cast<const float4*>(b + t0 * pv.st);
-    V1[q] = *reinterpret_cast<const float4*>(b + t1 * pv.st);
-    const float wx = dx ? w : e;
-    W0[q] = s * wx;
-    W1[q] = n * wx;
-  }
-}
-
-// Interpolate one group and write its 4 feature vectors (mean of the 3 planes) to the X tile.
-__device__ __forceinline__ void gather_consume(int g, int sub, int dx, int q4, int npts, const float4 (&V0)[3],
-                                               const float4 (&V1)[3], const float (&W0)[3],
-                                               const float (&W1)[3], float* __restrict__ X) {
-  const int j = 4 * g + sub;
-  float4 E[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    float4 pr;
-    pr.x = V0[q].x * W0[q] + V1[q].x * W1[q];
-    pr.y = V0[q].y * W0[q] + V1[q].y * W1[q];
-    pr.z = V0[q].z * W0[q] + V1[q].z * W1[q];
-    pr.w = V0[q].w * W0[q] + V1[q].w * W1[q];
-    E[q] = ror8_add(pr);
-  }
-  if (dx == 0 && j < npts) {
-    float4 f;
-    f.x = ((E[0].x + E[1].x) + E[2].x) * (1.f / 3.f);
-    f.y = ((E[0].y + E[1].y) + E[2].y) * (1.f / 3.f);
-    f.z = ((E[0].z + E[1].z) + E[2].z) * (1.f / 3.f);
-    f.w = ((E[0].w + E[1].w) + E[2].w) * (1.f / 3.f);
-    *reinterpret_cast<float4*>(X + j * XS + 4 * q4) = f;
-  }
-}
-
-__device__ __forceinline__ void gather_features(const PlaneView& pv, const PointP& P, int npts,
-                                                float* __restrict__ X) {
-  const int l = lane_id();
-  const int sub = l >> 4, dx = (l >> 3) & 1, q4 = l & 7;
-  const int ngrp = (npts + 3) >> 2;
-#if NFI_GATHER_PIPE
-  // Software pipeline over groups, two register sets: group g + 1's loads are in flight while
-  // group g is interpolated (the batched form below issues GB groups, then waits for all of them).
-  float4 A0[3], A1[3], B0[3], B1[3];
-  float AW0[3], AW1[3], BW0[3], BW1[3];
-  gather_issue(pv, P, 0, sub, dx, q4, A0, A1, AW0, AW1);
-#pragma unroll 1
-  for (int g = 0; g < ngrp; g += 2) {
-    if (g + 1 < ngrp) gather_issue(pv, P, g + 1, sub, dx, q4, B0, B1, BW0, BW1);
-    gather_consume(g, sub, dx, q4, npts, A0, A1, AW0, AW1, X);
-    if (g + 1 >= ngrp) break;
-    if (g + 2 < ngrp) gather_issue(pv, P, g + 2, sub, dx, q4, A0, A1, AW0, AW1);
-    gather_consume(g + 1, sub, dx, q4, npts, B0, B1, BW0, BW1, X);
-  }
-#else
-#pragma unroll 1
-  for (int gb = 0; gb < ngrp; gb += GATHER_GB) {
-    float4 V0[GATHER_GB][3], V1[GATHER_GB][3];
-    float W0[GATHER_GB][3], W1[GATHER_GB][3];
-#pragma unroll
-    for (int u = 0; u < GATHER_GB; ++u) gather_issue(pv, P, gb + u, sub, dx, q4, V0[u], V1[u], W0[u], W1[u]);
-#pragma unroll
-    for (int u = 0; u < GATHER_GB; ++u) gather_consume(gb + u, sub, dx, q4, npts, V0[u], V1[u], W0[u], W1[u], X);
-  }
-#endif
-}
-
-#endif
 
 // ---------------------------------------------------------------------------------------
 // d planes by plane tile: every (sample, plane) contribution is binned by the 7x4-cell tile of
@@ -914,11 +807,11 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
     // decoder inputs for the backward: rows eval_base.. of this ray, one coalesced KiB per store
     const int N = a.fine ? 2 * a.S : a.S;
     float4* xs = reinterpret_cast<float4*>(a.x_saved + (R.r * N + eval_base) * NC);
+    const int l = lane_id();
+    const float* src = X + (l >> 3) * XS + 4 * (l & 7);   // row k*8 + l/8: a constant offset per k
 #pragma unroll
-    for (int k = 0; k < NC / 4; ++k) {
-      const int q = k * 64 + lane_id();
-      if (q < npts * (NC / 4)) nt_store4(xs + q, *reinterpret_cast<const float4*>(X + (q >> 3) * XS + 4 * (q & 7)));
-    }
+    for (int k = 0; k < NC / 4; ++k)
+      if (8 * k + (l >> 3) < npts) nt_store4(xs + k * 64 + l, *reinterpret_cast<const float4*>(src + k * 8 * XS));
   }
   NFI_STAMP(1)
   float y[NOUT];

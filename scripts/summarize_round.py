@@ -7,12 +7,17 @@ gfx950's FETCH_SIZE counts half the bytes of wide streaming reads, MI355X_MICROA
 Infinity-Cache hits are counted too), and from the SQ / TCC passes:
   MFMA FLOP rate   SQ_INSTS_VALU_MFMA_F32 x 2,048 FLOP (v_mfma_f32_16x16x4_f32 = 16x16x4 MACs)
                    / duration, against the 157.3 TF fp32 dense peak
-  MFMA busy        SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 256 CUs x 4)  (rocprof's gfx94x
-                   MfmaUtil formula; ROCm 7.2 ships no gfx950 derived metrics)
-  VALU / cycle     SQ_INSTS_VALU / (duration x 2.4 GHz x 1,024 SIMDs): VALU instructions issued per
-                   SIMD per cycle (1.0 = every SIMD issues one every cycle)
-  waves / SIMD     SQ_WAVE_CYCLES / (duration x 2.4 GHz x 1,024): mean resident waves per SIMD
-  wait share       SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
+  cycles           GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs): the kernel's active clocks
+                   per XCD (2.07 GHz effective for the long kernels); duration x 2.4 GHz without it
+  MFMA busy        SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs x cycles): share of SIMD-cycles the matrix
+                   pipe is occupied (a 16x16x4 f32 MFMA holds it 32 cycles)
+  VALU / cycle     SQ_INSTS_VALU / (1,024 SIMDs x cycles): VALU instructions issued per SIMD-cycle
+  VALU issue       SQ_ACTIVE_INST_VALU x 4 / (1,024 x cycles): share of SIMD-cycles issuing VALU
+                   (SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles,
+                   MI355X_MICROARCH.md PMC table)
+  waves / SIMD     SQ_WAVE_CYCLES x 4 / (1,024 x cycles): mean resident waves per SIMD
+  wait share       SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers);
+  issue stall      SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (ready but not issued: pipe busy, MFMA RAW)
   L2 hit           TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
 """
 import csv
@@ -27,6 +32,7 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLK = 2.4e9
 SIMDS = 1024
 CUS = 256
+XCDS = 8
 
 
 def short(n):
@@ -67,21 +73,27 @@ for r in stats:
     c = ctr.get(k, {})
     f, w = c.get('FETCH_SIZE'), c.get('WRITE_SIZE')
     hbm = None if f is None or w is None else 2 * f * 1024 + w * 1024
-    cyc = dur * CLK
+    cyc = c['GRBM_GUI_ACTIVE'] / XCDS if c.get('GRBM_GUI_ACTIVE') else dur * CLK
     d = {'avg_us': dur * 1e6, 'calls': int(r['Calls'])}
+    if c.get('GRBM_GUI_ACTIVE'):
+        d['clock_GHz'] = cyc / dur / 1e9
     if hbm is not None:
         d.update(fetch_kib=f, write_kib=w, hbm_bytes_corrected=hbm, hbm_GBps=hbm / dur / 1e9, hbm_frac=hbm / dur / 8e12)
     if 'SQ_INSTS_VALU_MFMA_F32' in c:
         fl = c['SQ_INSTS_VALU_MFMA_F32'] * 2048
         d.update(mfma_insts=c['SQ_INSTS_VALU_MFMA_F32'], mfma_TFLOPs=fl / dur / 1e12, mfma_flop_frac=fl / dur / 157.3e12)
-    if 'SQ_VALU_MFMA_BUSY_CYCLES' in c and c.get('GRBM_GUI_ACTIVE'):
-        d['mfma_busy_rocprof'] = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (c['GRBM_GUI_ACTIVE'] * CUS * 4)
+    if 'SQ_VALU_MFMA_BUSY_CYCLES' in c:
+        d['mfma_busy'] = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * SIMDS)
     if 'SQ_INSTS_VALU' in c:
         d['valu_per_simd_cycle'] = c['SQ_INSTS_VALU'] / (cyc * SIMDS)
+    if 'SQ_ACTIVE_INST_VALU' in c:
+        d['valu_issue_share'] = 4 * c['SQ_ACTIVE_INST_VALU'] / (cyc * SIMDS)
     if 'SQ_WAVE_CYCLES' in c:
-        d['waves_per_simd'] = c['SQ_WAVE_CYCLES'] / (cyc * SIMDS)
+        d['waves_per_simd'] = 4 * c['SQ_WAVE_CYCLES'] / (cyc * SIMDS)
         if 'SQ_WAIT_ANY' in c:
             d['wait_share'] = c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']
+        if 'SQ_WAIT_INST_ANY' in c:
+            d['issue_stall_share'] = c['SQ_WAIT_INST_ANY'] / c['SQ_WAVE_CYCLES']
     if 'TCC_HIT_sum' in c:
         tot = c['TCC_HIT_sum'] + c['TCC_MISS_sum']
         d['l2_hit'] = c['TCC_HIT_sum'] / tot if tot else None
@@ -100,15 +112,16 @@ lines = [f'# rocprofv3 summary — {tag}', '',
          f'`--pmc` passes (FETCH_SIZE; WRITE_SIZE; 8 SQ; 7 SQ + GRBM; TCC hit/miss + GRBM) of '
          f'`python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-inversion --no-configs` '
          f'(config {config}, B={batch}).  Derived metrics: see scripts/summarize_round.py.', '',
-         '| kernel | calls | avg us | HBM GB/launch | HBM TB/s | HBM frac | MFMA TF | MFMA frac | MFMA busy (rocprof) | '
-         'VALU/SIMD/cyc | waves/SIMD | wait share | L2 hit |',
-         '|---|---|---|---|---|---|---|---|---|---|---|---|---|']
+         '| kernel | calls | avg us | HBM GB/launch | HBM TB/s | HBM frac | MFMA TF | MFMA frac | MFMA busy | '
+         'VALU issue | VALU/SIMD/cyc | waves/SIMD | wait share | issue stall | L2 hit | clock GHz |',
+         '|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|']
 for k, d in sorted(kern.items(), key=lambda kv: -kv[1]['avg_us'] * kv[1]['calls']):
     lines.append(f"| `{k}` | {d['calls']} | {d['avg_us']:.1f} | {fmt(d.get('hbm_bytes_corrected') and d['hbm_bytes_corrected'] / 1e9)} | "
                  f"{fmt(d.get('hbm_GBps') and d['hbm_GBps'] / 1e3)} | {fmt(d.get('hbm_frac'))} | "
-                 f"{fmt(d.get('mfma_TFLOPs'))} | {fmt(d.get('mfma_flop_frac'))} | {fmt(d.get('mfma_busy_rocprof'))} | "
-                 f"{fmt(d.get('valu_per_simd_cycle'))} | {fmt(d.get('waves_per_simd'))} | {fmt(d.get('wait_share'))} | "
-                 f"{fmt(d.get('l2_hit'))} |")
+                 f"{fmt(d.get('mfma_TFLOPs'))} | {fmt(d.get('mfma_flop_frac'))} | {fmt(d.get('mfma_busy'))} | "
+                 f"{fmt(d.get('valu_issue_share'))} | {fmt(d.get('valu_per_simd_cycle'))} | {fmt(d.get('waves_per_simd'))} | "
+                 f"{fmt(d.get('wait_share'))} | {fmt(d.get('issue_stall_share'))} | {fmt(d.get('l2_hit'))} | "
+                 f"{fmt(d.get('clock_GHz'))} |")
 lines += ['', '## Raw counters (per launch)', '']
 for k, d in kern.items():
     if d['raw']:
