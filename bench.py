@@ -507,7 +507,7 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
     st = stages[dom]
     sec = st['ms'] * 1e-3 / st['launches_per_step']
     per_launch = samples_per_step / st['launches_per_step']
-    traffic, traffic_src = None, 'none'
+    traffic, traffic_src, counters = None, 'none', None
     try:
         from nfi.build import source_digest
         with open(os.path.join(ROOT, 'profiles', 'latest_counters.json')) as fh:
@@ -519,6 +519,13 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
             traffic = round(ctr['hbm_bytes_corrected'] / 1e9, 3)
             traffic_src = (f"profiles/latest_counters.json ({cj.get('tag')}, source digest {cj['source_digest']}): "
                            f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes")
+            # the same profile's SQ / TCC passes for this kernel (scripts/summarize_round.py):
+            # matrix-pipe busy share and EXECUTED MFMA rate (incl. the backward's layer-1
+            # recompute and the padded output block), VALU issue share, L2 hit rate
+            counters = {k: round(ctr[k], 4) for k in ('mfma_busy', 'mfma_TFLOPs', 'mfma_flop_frac',
+                                                      'valu_issue_share', 'waves_per_simd',
+                                                      'issue_stall_share', 'l2_hit', 'avg_us')
+                        if ctr.get(k) is not None}
     except (OSError, ValueError, KeyError):
         pass
     model_bytes = per_launch * hbm_model(dom, pose, bwd, H, S)
@@ -542,6 +549,8 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
         'gather_ceiling_frac': round(st['tap_rate_GBps'] / GATHER_CEILING_GBS, 4),
         'fp32_TFLOPs': st['fp32_TFLOPs'], 'mfma_TFLOPs': st['mfma_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
         'mfma_frac': round(st['mfma_TFLOPs'] / 157.3, 4),
+        'mfma_basis': 'the reference MLP\'s fp32 FLOPs per sample (DESIGN.md §3) / HIP-event launch time',
+        'counters': counters,
     }
     return res
 
