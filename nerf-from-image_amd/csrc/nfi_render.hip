@@ -182,8 +182,11 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
   wave_lds_sync();
   const uint64_t pb = reinterpret_cast<uint64_t>(pv.base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32));
+  // the resource spans exactly this image's three planes (last texel's last channel + 1): a load
+  // at any offset past them returns zeros instead of touching memory
+  const int extent = __builtin_amdgcn_readfirstlane(((pv.R * pv.R - 1) * pv.st + 2 * pv.sq + NC) * 4);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, 0x7FFFFFFF, 0x00020000);
+      reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, extent, 0x00020000);
 #pragma unroll 1
   for (int gb = 0; gb < ngrp; gb += GATHER_GB) {
     float4 V0[GATHER_GB][3], V1[GATHER_GB][3];
