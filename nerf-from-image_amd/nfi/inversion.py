@@ -363,7 +363,11 @@ class _State:
                 p.requires_grad_()
             params += pose
         self.params = params
-        self.opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas, capturable=capturable)
+        # on the GPU the fused Adam: one kernel for the latent and the pose tensors instead of the
+        # foreach form's per-op launches (same update formula, run.py:2007)
+        fused = bool(params[0].is_cuda)
+        self.opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas, capturable=capturable,
+                                    **({'fused': True} if fused else {}))
         self.target = target_img[..., :3]
         if capturable:
             # a private static buffer: later batches are copied into it (load), which must never
