@@ -324,6 +324,9 @@ class _VolumeRender(torch.autograd.Function):
             debug['t_sorted'] = t_saved
             debug['sigma_sorted'] = s_saved
             debug['rgb_sorted'] = c_saved
+            # the launch's argument block and the tensors it points at (scripts/gather_probe.py)
+            debug['args'] = args
+            debug['args_tensors'] = (planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec)
         ctx.save_for_backward(planes_tm, pal_c, ro_c, rd_c, near_c, far_c, dec, t_saved, s_saved, c_saved,
                               y_saved, perm, x_saved, tile_counts, xray_c, vhead)
         ctx.opts = opts
