@@ -410,9 +410,10 @@ def main():
 FLOPS = {'render_fwd': (6450, 5504), 'bwd_bins': (0, 0), 'bwd_field': (5700, 5504)}
 KERNEL_OF = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
              'bwd_tiles': 'tile_kernel', 'bwd_bins': 'scan_blocks_kernel'}
-# gather ceiling (MI355X_MICROARCH.md, 'Indexed rows: gather into LDS'): rows shared by every
-# workgroup, served by the XCD's L2, 16.8-18.8 TB/s chip-wide (the table's upper figure)
-GATHER_CEILING_GBS = 18800.0
+# gather ceiling of the forward's own tap stream, measured: the product gather alone over the
+# forward's merged samples at its occupancy (scripts/gather_probe.py, profiles/r03_gather_probe.json:
+# 0.865 ms for 25.8 GB of taps; L1 hits on top of MI355X_MICROARCH.md's 16.8-18.8 TB/s from L2)
+GATHER_CEILING_GBS = 29790.0
 
 
 def hbm_model(name, pose, bwd, H, S):
