@@ -1723,15 +1723,6 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 // per-lane b128 row stores / reads and the per-entry row reads conflict-free, with
 // immediate-offset addressing).  60 rows, not 64, so that the stages, the tile texels and 4
 // workgroups fit one CU's LDS; the stage (2,160 floats) still holds a wave's 2,048-float image.
-#ifndef NFI_TILE_DBUF
-#define NFI_TILE_DBUF 0   // 1: two batches of rows in registers at occupancy 3 (measured 2.64 vs 2.28 ms)
-#endif
-#ifndef NFI_TILE_REC2
-#define NFI_TILE_REC2 1   // records loaded two batches ahead (coalesced form)
-#endif
-#ifndef NFI_TILE_COALESCED
-#define NFI_TILE_COALESCED 1   // 0: each lane loads its own entry's whole row (8 b128 loads, 56 rows each)
-#endif
 #ifndef NFI_TILE_BATCH
 #define NFI_TILE_BATCH 56
 #endif
@@ -1858,15 +1849,6 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       int cur = 0;
       float a0 = 0.f, a1 = 0.f;
       const cint4_p L = (cint4_p)A.list;
-#if NFI_TILE_DBUF || !NFI_TILE_COALESCED
-      float4 r0, r1, r2, r3, r4, r5, r6, r7;   // named (an array here is not promoted to registers)
-#endif
-#define NFI_LOAD_ROW(P, REC)                                                                     \
-  {                                                                                              \
-    const float4* src_ = reinterpret_cast<const float4*>(A.gfeat + (long long)(REC).x * NC);     \
-    P##0 = src_[0]; P##1 = src_[1]; P##2 = src_[2]; P##3 = src_[3];                              \
-    P##4 = src_[4]; P##5 = src_[5]; P##6 = src_[6]; P##7 = src_[7];                              \
-  }
       // 8 entries per step.  Scalar (record) and LDS (row) loads share lgkmcnt and scalar loads
       // return out of order, so a step that waits for its LDS rows also waits for every scalar load
       // in flight: the next step's records are issued only after this step's rows have been
@@ -1886,48 +1868,6 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];                \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
   }
-      // One batch of <= BATCH entries: rows P (zeroed past the chunk end: the last step's surplus
-      // entries then add 0) -> the wave's LDS stage; the pose gradient of each lane's own entry
-      // against the staged texels; the rows of batch BASE + AHEAD issued into P (they load while
-      // this batch is summed); then the entry loop.
-#define NFI_BATCH(BASE, P, VREC, AHEAD)                                                              \
-  {                                                                                                  \
-    const int base_ = (BASE);                                                                        \
-    const int n = min(BATCH, b1 - base_);                                                            \
-    if (l >= n) P##0 = P##1 = P##2 = P##3 = P##4 = P##5 = P##6 = P##7 = make_float4(0.f, 0.f, 0.f, 0.f); \
-    if (l < BATCH) {                                                                                 \
-      float4* dst = reinterpret_cast<float4*>(G + l * XS);                                           \
-      dst[0] = P##0; dst[1] = P##1; dst[2] = P##2; dst[3] = P##3;                                    \
-      dst[4] = P##4; dst[5] = P##5; dst[6] = P##6; dst[7] = P##7;                                    \
-    }                                                                                                \
-    wave_lds_sync();                                                                                 \
-    if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
-    VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];                                                 \
-    NFI_LOAD_ROW(P, VREC)                                                                            \
-    NFI_STAMP(24)                                                                                    \
-    iv4 ra[8], rb[8];                                                                                \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];                             \
-    for (int u = 0; u < n; u += 16) {                                                                \
-      NFI_STEP(u, ra, rb)                                                                            \
-      if (u + 8 >= n) break;                                                                         \
-      NFI_STEP(u + 8, rb, ra)                                                                        \
-    }                                                                                                \
-    wave_lds_sync();                                                                                 \
-    NFI_STAMP(25)                                                                                    \
-  }
-#if NFI_TILE_DBUF
-      // two batches of rows in registers (occupancy 3): a batch's rows were issued two batches
-      // before they are staged
-      float4 s0, s1, s2, s3, s4, s5, s6, s7;
-      int4 vrec = A.list[min(b0 + l, b1 - 1)], vrecb = A.list[min(b0 + BATCH + l, b1 - 1)];
-      NFI_LOAD_ROW(r, vrec)
-      NFI_LOAD_ROW(s, vrecb)
-      for (int bb = b0; bb < b1; bb += 2 * BATCH) {
-        NFI_BATCH(bb, r, vrec, 2 * BATCH)
-        if (bb + BATCH >= b1) break;
-        NFI_BATCH(bb + BATCH, s, vrecb, 2 * BATCH)
-      }
-#elif NFI_TILE_COALESCED
       // Rows loaded coalesced: lane l holds float4 (l & 7) of entry 8j + (l >> 3), j = 0..6 (the
       // entry's row index comes from its lane's record by ds_bpermute): each b128 load reads 8
       // whole 128-B rows instead of one 16-B piece of 56 different rows.
@@ -1946,13 +1886,9 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int e_ = 8 * (J) + (l >> 3);                                                               \
     *reinterpret_cast<float4*>(G + e_ * XS + 4 * (l & 7)) = e_ < n ? V : make_float4(0.f, 0.f, 0.f, 0.f); \
   }
-#if NFI_TILE_REC2
 #define NFI_NEXT_REC(VREC, AHEAD)                                                                    \
     VREC = vnext;                                                                                    \
     vnext = A.list[min(base_ + 2 * (AHEAD) + l, b1 - 1)];
-#else
-#define NFI_NEXT_REC(VREC, AHEAD) VREC = A.list[min(base_ + (AHEAD) + l, b1 - 1)];
-#endif
 #define NFI_BATCHC(BASE, VREC, AHEAD)                                                                \
   {                                                                                                  \
     const int base_ = (BASE);                                                                        \
@@ -1976,11 +1912,9 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       static_assert(BATCH % 8 == 0, "coalesced row loads of 8 entries each");
       float4 rc[BATCH / 8];
       int4 vrec = A.list[min(b0 + l, b1 - 1)];
-#if NFI_TILE_REC2
       // the next batch's records are already in registers when its rows are issued (the row
       // loads do not wait a record round trip)
       int4 vnext = A.list[min(b0 + BATCH + l, b1 - 1)];
-#endif
       NFI_LOAD_ROWC(vrec)
       for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
 #undef NFI_BATCHC
@@ -1988,15 +1922,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #undef NFI_ST1
 #undef NFI_LOAD_ROWC
 #undef NFI_LD1
-#else
-      int4 vrec = A.list[min(b0 + l, b1 - 1)];
-      NFI_LOAD_ROW(r, vrec)
-      for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCH(bb, r, vrec, BATCH)
-#endif
-#undef NFI_BATCH
 #undef NFI_STEP
 #undef NFI_ENTRY
-#undef NFI_LOAD_ROW
       img_add(img, cur, a0, a1);
     }
     NFI_STAMP(26)
@@ -2237,7 +2164,7 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
 // d planes and the per-(sample, plane) grid gradients of the pose path, one workgroup per tile
 // chunk (the grid is sized for a bound on the chunk count; blocks past meta[0] exit at once).
 #ifndef NFI_TILE_OCC
-#define NFI_TILE_OCC (NFI_TILE_DBUF ? 3 : 4)
+#define NFI_TILE_OCC 4
 #endif
 // XCD-grouped chunk order (NFI_TILE_XCD = G > 0): workgroups are dealt to the 8 XCDs
 // round-robin (block b runs on XCD b % 8); with G > 0 each XCD takes runs of G consecutive
