@@ -29,7 +29,8 @@ def main():
     with torch.no_grad():
         nfi.render(f, H, H, batch['cam'], batch['focal'], None, None, None, S, randomize=True, debug=dbg)
     torch.cuda.synchronize()
-    args, keep = dbg['args'], dbg['args_tensors']
+    args = dbg['args']
+    tensors = dbg['args_tensors']   # (the tensors args points at stay referenced while it is used)
     N = 2 * S
     n = B * H * H
     out = torch.empty((n * N,), device=dev)
@@ -62,6 +63,7 @@ def main():
     res['tap_bytes'] = samples * 1536
     res['gather_only_tap_TBps'] = round(samples * 1536 / (res['gather_only'] * 1e-3) / 1e12, 2)
     res['checksum_finite'] = bool(torch.isfinite(out).all())
+    del tensors
     print(json.dumps(res), flush=True)
 
 
