@@ -33,9 +33,9 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 12
-#define NFI_DEC_SIZE 7184   /* floats in the packed decoder buffer (11 outputs) */
-#define NFI_DEC_SIZE_VIEWDIR 11312 /* ... with the view-direction mapper (33 outputs) */
+#define NFI_ABI_VERSION 13
+#define NFI_DEC_SIZE 10256  /* floats in the packed decoder buffer (11 outputs) */
+#define NFI_DEC_SIZE_VIEWDIR 14384 /* ... with the view-direction mapper (33 outputs) */
 
 enum {
   NFI_OK = 0,

@@ -23,6 +23,7 @@ constexpr int NA = 10;     // attention values (palette rows)
 //   DT3 [hb][l][t]     W2s[4t + (l>>4)][16hb + (l&15)]          d hidden = W2s^T gy, A (t = 0..2)
 //   DT4 [cb][hb][l][r] W1s[16hb + 4(l>>4) + r][16cb + (l&15)]   d x = W1s^T d z, A
 //   DB2 [16]           b2s (zero padded)
+//   DT1S, DB1S         DT1 and DB1 times log2(e) (the field backward's layer-1 recompute)
 // The same layout for a decoder of NOUT outputs (NOB row blocks of 16; the d hidden product
 // W2s^T dY^T runs over KT k-steps of 4 output rows, stored padded to KTP):
 //   DT2 [ob][hb][l][r] W2s[16ob + (l&15)][16hb + 4(l>>4) + r]
@@ -42,7 +43,11 @@ struct DecL {
   static constexpr int DT3 = DT2 + NOB * 4 * 64 * 4;
   static constexpr int DT4 = DT3 + 4 * 64 * KTP;
   static constexpr int DB2 = DT4 + 2 * 4 * 64 * 4;
-  static constexpr int SIZE = DB2 + 16 * NOB;
+  // the field backward's layer-1 recompute: DT1 and DB1 times log2(e), so that sigmoid(z) =
+  // 1 / (1 + 2^-z') needs no scaling multiply (nfi_render.hip mlp_backward_mfma)
+  static constexpr int DT1S = DB2 + 16 * NOB;
+  static constexpr int DB1S = DT1S + 4 * 64 * 8;
+  static constexpr int SIZE = DB1S + 4 * 64 * 4;
 };
 constexpr int NOV = 33;    // decoder outputs with the view-direction mapper
 constexpr int NVF = 32;    // view-direction mapper features (generator.py:376-377, 398-399)
@@ -52,8 +57,8 @@ constexpr int DT2 = DecL<NO>::DT2;
 constexpr int DT3 = DecL<NO>::DT3;
 constexpr int DT4 = DecL<NO>::DT4;
 constexpr int DB2 = DecL<NO>::DB2;
-constexpr int DEC_SIZE = DecL<NO>::SIZE;       // 7184 floats
-static_assert(DEC_SIZE == 7184 && DT4 == 5120, "inversion decoder layout");
+constexpr int DEC_SIZE = DecL<NO>::SIZE;       // 10,256 floats
+static_assert(DEC_SIZE == 10256 && DT4 == 5120, "inversion decoder layout");
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

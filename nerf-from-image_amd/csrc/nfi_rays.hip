@@ -376,9 +376,15 @@ __global__ void decoder_pack_kernel(const float* __restrict__ w1, const float* _
   } else if (t < L::DB2) {
     const int u = t - L::DT4, cb = u / 1024, hb = (u / 256) % 4, l = (u / 4) % 64, r = u % 4;
     v = W1(16 * hb + 4 * (l >> 4) + r, 16 * cb + (l & 15));
-  } else {
+  } else if (t < L::DT1S) {
     const int k = t - L::DB2;
     v = (k < NOUT) ? b2[k] * gb : 0.f;
+  } else if (t < L::DB1S) {
+    const int u = t - L::DT1S, hb = u / 512, l = (u / 8) % 64, k = u % 8;
+    v = W1(16 * hb + (l & 15), 8 * (l >> 4) + k) * 1.44269504f;
+  } else {
+    const int u = t - L::DB1S, hb = u / 256, l = (u / 4) % 64, r = u % 4;
+    v = (b1[16 * hb + 4 * (l >> 4) + r] * gb) * 1.44269504f;
   }
   dec[t] = v;
 }

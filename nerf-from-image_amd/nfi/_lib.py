@@ -12,9 +12,9 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 12
-DEC_SIZE = 7184
-DEC_SIZE_VIEWDIR = 11312
+ABI_VERSION = 13
+DEC_SIZE = 10256
+DEC_SIZE_VIEWDIR = 14384
 
 c_float_p = ctypes.POINTER(ctypes.c_float)
 c_void_p = ctypes.c_void_p
