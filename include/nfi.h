@@ -33,8 +33,8 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 13
-#define NFI_DEC_SIZE 10256  /* floats in the packed decoder buffer (11 outputs) */
+#define NFI_ABI_VERSION 14
+#define NFI_DEC_SIZE 7200   /* floats in the packed decoder buffer (11 outputs: split-f16 tables) */
 #define NFI_DEC_SIZE_VIEWDIR 14384 /* ... with the view-direction mapper (33 outputs) */
 
 enum {

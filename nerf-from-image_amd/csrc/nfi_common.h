@@ -12,11 +12,9 @@ constexpr int NH = 64;     // decoder hidden width (generator.py:293)
 constexpr int NO = 11;     // decoder outputs: 1 distance + 10 attention logits (generator.py:380-385)
 constexpr int NA = 10;     // attention values (palette rows)
 
-// Packed decoder: per hidden unit o a 48-float record {W1s[o][0..31], W2s^T[o][0..10], b1[o], pad}
-// so that one unit is three s_load_dwordx16 from a wave-uniform address; b2 follows.
-// Packed decoder = per-lane MFMA operand tables for v_mfma_f32_16x16x4_f32 (lane l: A[l&15][l>>4],
-// B[l>>4][l&15]; C/D: row 4(l>>4)+reg, col l&15), built by nfi_decoder_pack from the
-// gain-scaled EqualizedLinear weights W1s [64,32], b1s [64], W2s [11,64], b2s [11]:
+// Exact-f32 decoder = per-lane MFMA operand tables for v_mfma_f32_16x16x4_f32 (lane l: A[l&15][l>>4],
+// B[l>>4][l&15]; C/D: row 4(l>>4)+reg, col l&15), built by nfi_decoder_pack_n from the
+// gain-scaled EqualizedLinear weights W1s [64,32], b1s [64], W2s [NOUT,64], b2s [NOUT]:
 //   DT1 [hb][l][t]     W1s[16hb + (l&15)][8(l>>4) + t]          layer 1 A (t = 0..7)
 //   DB1 [hb][l][r]     b1s[16hb + 4(l>>4) + r]                  layer 1 C init
 //   DT2 [hb][l][r]     W2s[l&15][16hb + 4(l>>4) + r]            layer 2 A (rows >= 11 zero)
@@ -29,9 +27,9 @@ constexpr int NA = 10;     // attention values (palette rows)
 //   DT2 [ob][hb][l][r] W2s[16ob + (l&15)][16hb + 4(l>>4) + r]
 //   DT3 [hb][l][t]     W2s[4t + (l>>4)][16hb + (l&15)]          (t < KTP; rows >= NOUT zero)
 //   DB2 [16 NOB]       b2s
-// NOUT = 11: 1 distance + 10 attention logits (or 3 colour features, zero padded) — the
-// inversion field; NOUT = 33: 1 distance + 32 features for the view-direction mapper
-// (--use_viewdir, generator.py:376-377).
+// NOUT = 33: 1 distance + 32 features for the view-direction mapper (--use_viewdir,
+// generator.py:376-377) uses these exact-f32 tables; the inversion decoder (NOUT = 11: 1 distance +
+// 10 attention logits, or 3 colour features zero padded) is packed as DecH below.
 template <int NOUT>
 struct DecL {
   static constexpr int NOB = (NOUT + 15) / 16;
@@ -49,16 +47,44 @@ struct DecL {
   static constexpr int DB1S = DT1S + 4 * 64 * 8;
   static constexpr int SIZE = DB1S + 4 * 64 * 4;
 };
+// Split-f16 decoder tables (the inversion decoder, NOUT = 11): A operands of
+// v_mfma_f32_16x16x32_f16 (lane l: A[l&15][8(l>>4) + j], j < 8; B[8(l>>4) + j][l&15]; C/D row
+// 4(l>>4) + r, col l&15) holding each gain-scaled fp32 weight times a power of two 2^e as an fp16
+// pair hi + lo (hi = f16(w 2^e), lo = f16(w 2^e - hi), both round-to-nearest): per lane 4 dwords of
+// hi halves, then 4 dwords of lo halves.  Three products hi.hi + hi.lo + lo.hi per contraction give
+// the fp32 result to the error of an fp32 dot product (DESIGN.md §3 "Decoder on the matrix cores").
+// The hidden unit of K-step kb (32 units: blocks 2kb, 2kb + 1) at k = 8q + j is
+//   hk(kb, q, j) = 16 (2kb + (j >> 2)) + 4q + (j & 3)
+// — the order in which lane (., q) holds a layer-1 accumulator block, so the activations and their
+// gradients feed the next product from registers.
+//   H1  [hb 4][l][8]       W1s[16hb + (l&15)][8(l>>4) + j] 2^e1                layer 1 A
+//   B1S [hb][l][r 4]       b1s[16hb + 4(l>>4) + r] log2(e)                       layer 1 bias (base 2)
+//   H2  [kb 2][l][8]       W2s[l&15][hk(kb, l>>4, j)] 2^e2 (rows >= 11 zero)     layer 2 A
+//   H3  [hb][l][4]         k = 8(l>>4) + j: hi of W2s[k][16hb + (l&15)] 2^e3 for k < 16, the lo of
+//                          W2s[k - 16][..] for k >= 16 (outputs >= 11 zero)      d hidden A: one
+//                          MFMA gives hi.hi + lo.hi against [dY hi; dY hi], one hi.lo + lo.lo
+//                          against [dY lo; dY lo]
+//   H4  [cb 2][kb 2][l][8] W1s[hk(kb, l>>4, j)][16cb + (l&15)] 2^e4             d x A
+//   B2  [16]               b2s
+//   SC  [16]               2^-e1 log2(e), 2^-e2, C3 = max_h sum_o |W2s[o][h]| 2^e3, 2^-(e3 + e4)
+// e1, e2, e4 put the matrix's largest |weight| in [2^14, 2^15); e3 its largest in [2^6, 2^7), so the
+// d hidden product (<= C3 max|dY 2^ey| with dY scaled to C3 max|dY 2^ey| in [2^13, 2^14)) stays in
+// fp16 range.
+struct DecH {
+  static constexpr int H1 = 0;
+  static constexpr int B1S = H1 + 4 * 64 * 8;
+  static constexpr int H2 = B1S + 4 * 64 * 4;
+  static constexpr int H3 = H2 + 2 * 64 * 8;
+  static constexpr int H4 = H3 + 4 * 64 * 4;
+  static constexpr int B2 = H4 + 2 * 2 * 64 * 8;
+  static constexpr int SC = B2 + 16;
+  static constexpr int SIZE = SC + 16;
+};
+static_assert(DecH::SIZE == 7200, "split decoder layout");
+
 constexpr int NOV = 33;    // decoder outputs with the view-direction mapper
 constexpr int NVF = 32;    // view-direction mapper features (generator.py:376-377, 398-399)
-constexpr int DT1 = DecL<NO>::DT1;
-constexpr int DB1 = DecL<NO>::DB1;
-constexpr int DT2 = DecL<NO>::DT2;
-constexpr int DT3 = DecL<NO>::DT3;
-constexpr int DT4 = DecL<NO>::DT4;
-constexpr int DB2 = DecL<NO>::DB2;
-constexpr int DEC_SIZE = DecL<NO>::SIZE;       // 10,256 floats
-static_assert(DEC_SIZE == 10256 && DT4 == 5120, "inversion decoder layout");
+constexpr int DEC_SIZE = DecH::SIZE;           // 7,200 floats (the inversion decoder: split-f16 tables)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

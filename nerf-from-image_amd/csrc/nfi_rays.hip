@@ -389,6 +389,89 @@ __global__ void decoder_pack_kernel(const float* __restrict__ w1, const float* _
   dec[t] = v;
 }
 
+// The inversion decoder's split-f16 tables (DecH, nfi_common.h): one workgroup finds each
+// matrix's power-of-two scale, then writes the hi / lo halves of every scaled weight.
+__device__ __forceinline__ unsigned short f16_bits(float v) { return __builtin_bit_cast(unsigned short, (_Float16)v); }
+// hi (part 0) or lo (part 1) half of v: hi = f16(v), lo = f16(v - hi), round-to-nearest each
+__device__ __forceinline__ unsigned short f16_part(float v, int part) {
+  const _Float16 h = (_Float16)v;
+  return part ? f16_bits(v - (float)h) : __builtin_bit_cast(unsigned short, h);
+}
+// exponent e with m 2^e in [2^(top-1), 2^top) (0 for m = 0), kept within +-100
+__device__ __forceinline__ int pow2_exp(float m, int top) {
+  if (!(m > 0.f) || !isfinite(m)) return 0;
+  int E;
+  frexpf(m, &E);
+  return min(max(top - E, -100), 100);
+}
+
+__global__ void __launch_bounds__(256) decoder_pack_h_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                                             const float* __restrict__ w2, const float* __restrict__ b2,
+                                                             float g1, float g2, float gb, float* __restrict__ dec) {
+  using H = DecH;
+  __shared__ float red[3][256];
+  const int t = threadIdx.x;
+  auto W1 = [&](int h, int c) { return w1[h * NC + c] * g1; };
+  auto W2 = [&](int o, int h) { return (o < NO) ? w2[o * NH + h] * g2 : 0.f; };
+  float m1 = 0.f, m2 = 0.f, c3 = 0.f;
+  for (int i = t; i < NH * NC; i += 256) m1 = fmaxf(m1, fabsf(W1(i / NC, i % NC)));
+  for (int i = t; i < NO * NH; i += 256) m2 = fmaxf(m2, fabsf(W2(i / NH, i % NH)));
+  if (t < NH)
+    for (int o = 0; o < NO; ++o) c3 += fabsf(W2(o, t));
+  red[0][t] = m1;
+  red[1][t] = m2;
+  red[2][t] = c3;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w)
+      for (int k = 0; k < 3; ++k) red[k][t] = fmaxf(red[k][t], red[k][t + w]);
+    __syncthreads();
+  }
+  m1 = red[0][0];
+  m2 = red[1][0];
+  c3 = red[2][0];
+  const int e1 = pow2_exp(m1, 15), e2 = pow2_exp(m2, 15), e3 = pow2_exp(m2, 7), e4 = e1;
+  // hidden unit of K-step kb at k = 8q + j
+  auto hk = [](int kb, int q, int j) { return 16 * (2 * kb + (j >> 2)) + 4 * q + (j & 3); };
+  // one table dword: the hi (part 0) or lo (part 1) halves of two consecutive operand elements
+  auto pair = [](float v0, float v1, int part) {
+    return __builtin_bit_cast(float, (unsigned)f16_part(v0, part) | ((unsigned)f16_part(v1, part) << 16));
+  };
+  for (int i = t; i < H::SIZE; i += 256) {
+    float v = 0.f;
+    if (i < H::B1S) {
+      const int hb = i / 512, l = (i / 8) % 64, w = i % 8, part = w >> 2, j = 2 * (w & 3);
+      const int row = 16 * hb + (l & 15), c = 8 * (l >> 4) + j;
+      v = pair(ldexpf(W1(row, c), e1), ldexpf(W1(row, c + 1), e1), part);
+    } else if (i < H::H2) {
+      const int u = i - H::B1S, hb = u / 256, l = (u / 4) % 64, r = u % 4;
+      v = (b1[16 * hb + 4 * (l >> 4) + r] * gb) * 1.44269504f;
+    } else if (i < H::H3) {
+      const int u = i - H::H2, kb = u / 512, l = (u / 8) % 64, w = u % 8, part = w >> 2, j = 2 * (w & 3);
+      const int o = l & 15, q = l >> 4;
+      v = pair(ldexpf(W2(o, hk(kb, q, j)), e2), ldexpf(W2(o, hk(kb, q, j + 1)), e2), part);
+    } else if (i < H::H4) {
+      const int u = i - H::H3, hb = u / 256, l = (u / 4) % 64, w = u % 4;
+      const int h = 16 * hb + (l & 15), k = 8 * (l >> 4) + 2 * w, part = k >= 16, o = k & 15;
+      v = pair(ldexpf(W2(o, h), e3), ldexpf(W2(o + 1, h), e3), part);
+    } else if (i < H::B2) {
+      const int u = i - H::H4, cb = u / 1024, kb = (u / 512) % 2, l = (u / 8) % 64, w = u % 8;
+      const int part = w >> 2, j = 2 * (w & 3), c = 16 * cb + (l & 15), q = l >> 4;
+      v = pair(ldexpf(W1(hk(kb, q, j), c), e4), ldexpf(W1(hk(kb, q, j + 1), c), e4), part);
+    } else if (i < H::SC) {
+      const int k = i - H::B2;
+      v = (k < NO) ? b2[k] * gb : 0.f;
+    } else {
+      const int k = i - H::SC;
+      v = (k == 0) ? ldexpf(1.44269504f, -e1)
+        : (k == 1) ? ldexpf(1.f, -e2)
+        : (k == 2) ? ldexpf(c3, e3)
+        : (k == 3) ? ldexpf(1.f, -(e3 + e4)) : 0.f;
+    }
+    dec[i] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Plane layout: [B,3,32,R,R] <-> [B,3,R,R,32]  (LDS-tiled transpose, 32 ch x 64 texels)
 // ---------------------------------------------------------------------------------------
@@ -434,7 +517,7 @@ using namespace nfi;
 
 extern "C" {
 
-static_assert(DecL<NO>::SIZE == NFI_DEC_SIZE && DecL<NOV>::SIZE == NFI_DEC_SIZE_VIEWDIR, "nfi.h decoder sizes");
+static_assert(DecH::SIZE == NFI_DEC_SIZE && DecL<NOV>::SIZE == NFI_DEC_SIZE_VIEWDIR, "nfi.h decoder sizes");
 int32_t nfi_abi_version(void) { return NFI_ABI_VERSION; }
 const char* nfi_last_error(void) { return nfi::g_err.c_str(); }
 
@@ -512,7 +595,7 @@ int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, cons
 }
 
 int64_t nfi_decoder_size(int32_t nout) {
-  if (nout == NO) return DecL<NO>::SIZE;
+  if (nout == NO) return DecH::SIZE;
   if (nout == NOV) return DecL<NOV>::SIZE;
   return -1;
 }
@@ -522,8 +605,7 @@ int32_t nfi_decoder_pack_n(const float* w1, const float* b1, const float* w2, co
   NFI_REQUIRE(w1 && b1 && w2 && b2 && dec, "decoder_pack: null pointer");
   NFI_REQUIRE(nout == NO || nout == NOV, "decoder_pack: nout must be %d or %d (got %d)", NO, NOV, nout);
   if (nout == NO)
-    decoder_pack_kernel<NO><<<(DecL<NO>::SIZE + 255) / 256, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1,
-                                                                                            g2, gb, dec);
+    decoder_pack_h_kernel<<<1, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1, g2, gb, dec);
   else
     decoder_pack_kernel<NOV><<<(DecL<NOV>::SIZE + 255) / 256, 256, 0, (hipStream_t)stream>>>(w1, b1, w2, b2, g1,
                                                                                               g2, gb, dec);

@@ -34,6 +34,22 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// N floats to LDS with 32-bit stores whose data registers stay live until the stores completed
+// (an s_waitcnt lgkmcnt(0), then an empty use of every value).  Measured on MI355X: a
+// ds_write_b64/b128 whose data registers the next VALU instruction rewrote (hipcc builds the
+// register tuple with moves and reuses it right after the store) left the NEW value in LDS in a
+// few lanes when the CU's LDS pipe was busy — run-to-run different palette partials in the field
+// backward once its decoder read operands from LDS; hipcc inserts no wait for it.
+template <int N>
+__device__ __forceinline__ void lds_store_keep(float* __restrict__ dst, const float (&v)[N]) {
+  volatile float* d = dst;
+#pragma unroll
+  for (int k = 0; k < N; ++k) d[k] = v[k];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" ::"v"(v[k]));
+}
+
 // v + v(lane ^ 32), in every lane (gfx950 v_permlane32_swap).
 __device__ __forceinline__ float sum_halves(float v) {
   auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
@@ -534,6 +550,337 @@ __device__ __forceinline__ void mlp_backward_mfma(const float* __restrict__ dec,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The inversion decoder (11 outputs) on the f16 matrix cores at fp32 accuracy.
+// v_mfma_f32_16x16x32_f16 runs a 16x16x32 product in 16 cycles, v_mfma_f32_16x16x4_f32 a 16x16x4
+// in 32: per unit of K the f16 form is 16x the f32 one.  Every fp32 operand v (scaled by a power
+// of two, exact) is carried as hi = f16(v), lo = f16(v - hi) (round-to-nearest: v = hi + lo to
+// 2^-22 |v| at worst, 2^-24 typically), and a contraction is lo.hi + hi.lo + hi.hi on one fp32
+// accumulator — the dropped lo.lo term is below an fp32 rounding of the product.  Products of f16
+// pairs are exact in fp32, so the result has the error of an fp32 dot product (measured against
+// fp64: tests/test_gpu_stages.py::test_decoder_split_precision).  Scales keep every scaled value
+// in fp16's normal range: the weights' per-matrix 2^e in the tables (DecH), the decoder inputs and
+// the output gradients a power of two per wave from their largest magnitude; the hidden
+// activations softplus(z) >= 0 are split unscaled (an O(1) activation below 2^-14 keeps an
+// absolute error under 2^-25).  Per 64 points: forward 72 f16 MFMAs (1,152 cycles) instead of
+// 192 f32 ones (6,144); backward 128 (2,048) instead of 304 (9,728).
+// ---------------------------------------------------------------------------------------
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u4v ldu4(const float* p) { return *reinterpret_cast<const u4v*>(p); }
+__device__ __forceinline__ f4v mfma_h(u4v a, u4v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+}
+// (ah + al)(bh + bl) without al.bl, the small terms first
+__device__ __forceinline__ f4v mfma3(u4v ah, u4v al, u4v bh, u4v bl, f4v c) {
+  c = mfma_h(al, bh, c);
+  c = mfma_h(ah, bl, c);
+  return mfma_h(ah, bh, c);
+}
+// two fp32 values -> their f16 hi halves and lo halves (packed pairs): hi = f16(v), lo = f16(v - hi),
+// both round-to-nearest (v_cvt_pk_f16_f32; v - hi is exact in fp32).  Written in plain operations so
+// hipcc's hazard recognizer sees every VGPR write ahead of the MFMAs that read it: an inline-asm
+// v_fma_mix form (one instruction per lo half) let an MFMA read a register the asm had rewritten
+// too early — wrong and run-to-run different results, no fault (the recognizer does not look
+// inside asm strings).
+__device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  const h2v h = h2v{(_Float16)a, (_Float16)b};
+  hi = __builtin_bit_cast(unsigned, h);
+  lo = __builtin_bit_cast(unsigned, h2v{(_Float16)(a - (float)h[0]), (_Float16)(b - (float)h[1])});
+}
+__device__ __forceinline__ void split8(const float (&v)[8], u4v& hi, u4v& lo) {
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    unsigned h, o;
+    split2(v[2 * w], v[2 * w + 1], h, o);
+    hi[w] = h;
+    lo[w] = o;
+  }
+}
+// max over the 64 lanes (DPP inside rows, then across rows)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  v = fmaxf(v, __shfl_xor(v, 16));
+  auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(s[0]), __int_as_float(s[1]));
+}
+// s = 2^e, inv = 2^-e with m s in [2^(top-1), 2^top) (e = 0 for m = 0 or not finite; |e| <= 100)
+__device__ __forceinline__ void pow2_scale(float m, int top, float& s, float& inv) {
+  int e = top - __builtin_amdgcn_frexp_expf(m);
+  e = (m > 0.f && m < __builtin_inff()) ? min(max(e, -100), 100) : 0;
+  s = __builtin_ldexpf(1.f, e);
+  inv = __builtin_ldexpf(1.f, -e);
+}
+// softplus(z) (threshold 20) from zs = z log2(e)
+__device__ __forceinline__ float softplus_b2(float zs) {
+  const float h = __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(zs));
+  return ((zs > 28.8539009f) ? zs : h) * 0.69314718f;
+}
+// the wave's 64 decoder inputs (xa/xb: channels 8q..8q+3, 8q+4..8q+7 of point 16sb + j) times a
+// power of two for the wave, split; returns the inverse scale
+__device__ __forceinline__ float split_inputs(const f4v xa[4], const f4v xb[4], u4v Xh[4], u4v Xl[4]) {
+  float m = 0.f;
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m = fmaxf(m, fmaxf(fabsf(xa[sb][r]), fabsf(xb[sb][r])));
+  float sx, isx;
+  pow2_scale(wave_max_dpp(m), 15, sx, isx);
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) {
+    const float v[8] = {xa[sb][0] * sx, xa[sb][1] * sx, xa[sb][2] * sx, xa[sb][3] * sx,
+                        xb[sb][0] * sx, xb[sb][1] * sx, xb[sb][2] * sx, xb[sb][3] * sx};
+    split8(v, Xh[sb], Xl[sb]);
+  }
+  return isx;
+}
+
+// the decoder inputs of points 16sb + j (lane (j, q): channels 8q..8q+7) from the X tile, times s
+__device__ __forceinline__ void split_tile_inputs(const float* __restrict__ X, int sb, float s, u4v& xh, u4v& xl) {
+  const int l = lane_id(), j = l & 15, q = l >> 4;
+  const f4v a = ld4(X + (16 * sb + j) * XS + 8 * q), b = ld4(X + (16 * sb + j) * XS + 8 * q + 4);
+  const float v[8] = {a[0] * s, a[1] * s, a[2] * s, a[3] * s, b[0] * s, b[1] * s, b[2] * s, b[3] * s};
+  split8(v, xh, xl);
+}
+
+// Decoder forward for the npts points of the wave's X tile (LDS rows of XS floats; the stale rows
+// past npts are zeroed first, so they neither enter the per-wave input scale nor produce inf / NaN
+// that a caller's masked sums would pick up): point l's 11 outputs.  Z^T = W1s X^T by hidden blocks hb; each K-step kb of Y^T = W2s softplus(Z)^T takes its
+// B operand (hidden blocks 2kb, 2kb+1 of a point) straight from two layer-1 accumulators.  The
+// inputs are re-read from the tile and split per K-step (registers: the operand tables of one
+// K-step, 32, and the output accumulators, 16, stay live — the forward runs at occupancy 4).
+__device__ __forceinline__ void mlp_forward_h(const float* __restrict__ dec, float* __restrict__ X, int npts,
+                                              float y[NO]) {
+  using H = DecH;
+  const int l = lane_id(), j = l & 15, q = l >> 4;
+  if (npts < 64) {   // (wave-uniform) zero the stale rows: no inf / NaN from them in the products
+    if (l >= npts) {
+#pragma unroll
+      for (int k = 0; k < NC / 4; ++k) *reinterpret_cast<f4v*>(X + l * XS + 4 * k) = f4v{0.f, 0.f, 0.f, 0.f};
+    }
+    wave_lds_sync();
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) {
+    const f4v a = ld4(X + (16 * sb + j) * XS + 8 * q), b = ld4(X + (16 * sb + j) * XS + 8 * q + 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m = fmaxf(m, fmaxf(fabsf(a[r]), fabsf(b[r])));
+  }
+  float sx, isx;
+  pow2_scale(wave_max_dpp(m), 15, sx, isx);
+  const float cz = dec[H::SC] * isx;   // 2^-(e1 + ex) log2(e)
+  f4v Y[4];
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) Y[sb] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int kb = 0; kb < 2; ++kb) {
+    const float* t1 = dec + H::H1 + (2 * kb * 64 + l) * 8;
+    const u4v a0h = ldu4(t1), a0l = ldu4(t1 + 4), a1h = ldu4(t1 + 512), a1l = ldu4(t1 + 516);
+    const f4v bz0 = ld4(dec + H::B1S + (2 * kb * 64 + l) * 4), bz1 = ld4(dec + H::B1S + ((2 * kb + 1) * 64 + l) * 4);
+    const u4v a2h = ldu4(dec + H::H2 + (kb * 64 + l) * 8), a2l = ldu4(dec + H::H2 + (kb * 64 + l) * 8 + 4);
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      u4v xh, xl;
+      split_tile_inputs(X, sb, sx, xh, xl);
+      const f4v z0 = mfma3(a0h, a0l, xh, xl, f4v{0.f, 0.f, 0.f, 0.f});
+      const f4v z1 = mfma3(a1h, a1l, xh, xl, f4v{0.f, 0.f, 0.f, 0.f});
+      float hv[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hv[r] = softplus_b2(fmaf(z0[r], cz, bz0[r]));
+        hv[4 + r] = softplus_b2(fmaf(z1[r], cz, bz1[r]));
+      }
+      u4v hh, hl;
+      split8(hv, hh, hl);
+      Y[sb] = mfma3(a2h, a2l, hh, hl, Y[sb]);
+    }
+  }
+  // lane (j, q) holds outputs 4q..4q+3 of point 16sb + j: transpose through the tile
+  wave_lds_sync();
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) {
+    const float yv[4] = {Y[sb][0], Y[sb][1], Y[sb][2], Y[sb][3]};
+    lds_store_keep(X + (16 * sb + j) * XS + 4 * q, yv);
+  }
+  wave_lds_sync();
+  const float s2 = dec[H::SC + 1];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) y[o] = fmaf(X[l * XS + o], s2, dec[H::B2 + o]);
+}
+
+// Decoder input gradient for 64 points: xa/xb the decoder inputs (lane (j, q): channels 8q..8q+7
+// of point 16sb + j), dY the X tile's rows (point l's 11 output gradients in columns 0..10, zeros
+// in 11..15).  Calls emit(cb, sb, v) with v = dX^T (lane (j, q): channels 16cb + 4q + r of point
+// 16sb + j) times post.  Two passes of two point blocks each keep the live
+// registers to one K-step's tables (48), two blocks' inputs (16) and accumulators (16): the field
+// backward runs at occupancy 4.
+// A/B knobs of the split backward (measured, p3d_fwdbwd B=8 field backward): scheduling barriers
+// between K-steps (1) / point blocks (2) 2.37-2.47 ms vs none 2.20 ms at occupancy 4 (spills) and
+// 2.06 ms at occupancy 3; point blocks per pass 4 (tables loaded once) 1.89-1.90 ms vs 2 (tables
+// loaded per pass) 2.06-2.07; dY operands split once and held 1.93 vs re-split per K-step 1.89-1.90.
+#ifndef NFI_BWD_SB
+#define NFI_BWD_SB 0
+#endif
+#ifndef NFI_BWD_DYHOLD
+#define NFI_BWD_DYHOLD 0
+#endif
+#ifndef NFI_BWD_NSB
+#define NFI_BWD_NSB 4   // point blocks per pass
+#endif
+template <class Emit>
+__device__ __forceinline__ void mlp_backward_h(const float* __restrict__ dec, const f4v xa[4], const f4v xb[4],
+                                               const float* __restrict__ X, float post, Emit emit) {
+  using H = DecH;
+  constexpr int NSB = NFI_BWD_NSB;
+  const int l = lane_id(), j = l & 15, q = l >> 4;
+  float m = 0.f;
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m = fmaxf(m, fmaxf(fabsf(xa[sb][r]), fabsf(xb[sb][r])));
+  float sx, isx;
+  pow2_scale(wave_max_dpp(m), 15, sx, isx);
+  const float cz = dec[H::SC] * isx;
+  // dY scale: C3 max|dY| sy in [2^13, 2^14), so |d hidden| <= C3 max|dY sy| stays in fp16 range
+  float my = 0.f;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) my = fmaxf(my, fabsf(X[l * XS + o]));
+  float sy, isy;
+  pow2_scale(wave_max_dpp(my) * dec[H::SC + 2], 14, sy, isy);
+  const float fac = post * (dec[H::SC + 3] * isy);   // 2^-(e3 + e4 + ey)
+#if NFI_BWD_DYHOLD
+  // B operands of d hidden, per point block: [dY hi; dY hi] and [dY lo; dY lo] (lane (j, q): outputs
+  // 8(q&1)..+7).  Against H3 = [W2 hi | W2 lo] the second adds hi.lo + lo.lo.
+  u4v DH[4], DL[4];
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) {
+    const float* dr = X + (16 * sb + j) * XS + 8 * (q & 1);
+    const f4v d0 = ld4(dr), d1 = ld4(dr + 4);
+    const float v[8] = {d0[0] * sy, d0[1] * sy, d0[2] * sy, d0[3] * sy, d1[0] * sy, d1[1] * sy, d1[2] * sy, d1[3] * sy};
+    split8(v, DH[sb], DL[sb]);
+  }
+#endif
+#pragma unroll
+  for (int sp = 0; sp < 4 / NSB; ++sp) {
+    // the second pass reloads the tables (L1 hits) instead of keeping the first pass's live: an
+    // opaque zero offset keeps the compiler from merging the two passes' loads (an opaque pointer
+    // would lose its global address space: flat loads)
+    int zo = 0;
+    asm volatile("" : "+s"(zo));
+    const float* dk = dec + zo;
+    u4v Xh[NSB], Xl[NSB];
+#pragma unroll
+    for (int s = 0; s < NSB; ++s) {
+      const int sb = NSB * sp + s;
+      f4v a = xa[sb], b = xb[sb];
+      asm volatile("" : "+v"(a), "+v"(b));   // (split here, not hoisted into the first pass)
+      const float v[8] = {a[0] * sx, a[1] * sx, a[2] * sx, a[3] * sx, b[0] * sx, b[1] * sx, b[2] * sx, b[3] * sx};
+      split8(v, Xh[s], Xl[s]);
+    }
+    f4v gx[2][NSB];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      // (no load of the next K-step's tables is hoisted above this point: they would be live
+      //  beside this one's)
+#if NFI_BWD_SB & 1
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      const float* t1 = dk + H::H1 + (2 * kb * 64 + l) * 8;
+      const u4v a0h = ldu4(t1), a0l = ldu4(t1 + 4), a1h = ldu4(t1 + 512), a1l = ldu4(t1 + 516);
+      const f4v bz0 = ld4(dk + H::B1S + (2 * kb * 64 + l) * 4), bz1 = ld4(dk + H::B1S + ((2 * kb + 1) * 64 + l) * 4);
+      const u4v a30 = ldu4(dk + H::H3 + (2 * kb * 64 + l) * 4), a31 = ldu4(dk + H::H3 + ((2 * kb + 1) * 64 + l) * 4);
+      const float* t4 = dk + H::H4 + (kb * 64 + l) * 8;
+      const u4v a40h = ldu4(t4), a40l = ldu4(t4 + 4), a41h = ldu4(t4 + 1024), a41l = ldu4(t4 + 1028);
+#pragma unroll
+      for (int s = 0; s < NSB; ++s) {
+#if NFI_BWD_SB & 2
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        const int sb = NSB * sp + s;
+#if NFI_BWD_DYHOLD
+        const u4v dh = DH[sb], dl = DL[sb];
+#else
+        // B operands of d hidden: [dY hi; dY hi] and [dY lo; dY lo] (lane (j, q): outputs
+        // 8(q&1)..+7); against H3 = [W2 hi | W2 lo] the second product adds hi.lo + lo.lo
+        u4v dh, dl;
+        {
+          const float* dr = X + (16 * sb + j) * XS + 8 * (q & 1);
+          const f4v d0 = ld4(dr), d1 = ld4(dr + 4);
+          const float v[8] = {d0[0] * sy, d0[1] * sy, d0[2] * sy, d0[3] * sy,
+                              d1[0] * sy, d1[1] * sy, d1[2] * sy, d1[3] * sy};
+          split8(v, dh, dl);
+        }
+#endif
+        const f4v z0 = mfma3(a0h, a0l, Xh[s], Xl[s], f4v{0.f, 0.f, 0.f, 0.f});
+        const f4v z1 = mfma3(a1h, a1l, Xh[s], Xl[s], f4v{0.f, 0.f, 0.f, 0.f});
+        const f4v g0 = mfma_h(a30, dh, mfma_h(a30, dl, f4v{0.f, 0.f, 0.f, 0.f}));
+        const f4v g1 = mfma_h(a31, dh, mfma_h(a31, dl, f4v{0.f, 0.f, 0.f, 0.f}));
+        float gv[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gv[r] = g0[r] * softplus_grad2(fmaf(z0[r], cz, bz0[r]));
+          gv[4 + r] = g1[r] * softplus_grad2(fmaf(z1[r], cz, bz1[r]));
+        }
+        u4v gh, gl;
+        split8(gv, gh, gl);
+        const f4v c0 = kb ? gx[0][s] : f4v{0.f, 0.f, 0.f, 0.f}, c1 = kb ? gx[1][s] : f4v{0.f, 0.f, 0.f, 0.f};
+        gx[0][s] = mfma3(a40h, a40l, gh, gl, c0);
+        gx[1][s] = mfma3(a41h, a41l, gh, gl, c1);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < NSB; ++s) {
+      emit(0, NSB * sp + s, gx[0][s] * fac);
+      emit(1, NSB * sp + s, gx[1][s] * fac);
+    }
+  }
+}
+
+// Dispatch: the inversion decoder on the split-f16 path, the 33-output (view-direction) decoder on
+// the exact-f32 tables.  dY rows for mlp_backward: the tile's columns 0..NOUT-1, zeros up to DYC.
+template <int NOUT>
+constexpr int DYC = (NOUT == NO) ? 16 : 4 * DecL<NOUT>::KT;
+static_assert(DYC<NOV> <= XS && DYC<NO> <= XS, "dY rows fit an X tile row");
+
+template <int NOUT, bool PREFETCH>
+__device__ __forceinline__ void mlp_forward(const float* __restrict__ dec, float* __restrict__ X, int npts,
+                                            float y[NOUT]) {
+  if constexpr (NOUT == NO)
+    mlp_forward_h(dec, X, npts, y);
+  else
+    mlp_forward_tile<NOUT, PREFETCH>(dec, X, y);
+}
+// emit(cb, sb, v): v = dX^T block (cb, sb) (lane (j, q): channels 16cb + 4q + r of point 16sb + j)
+// times post
+template <int NOUT, class Emit>
+__device__ __forceinline__ void mlp_backward(const float* __restrict__ dec, const f4v xa[4], const f4v xb[4],
+                                             const float* __restrict__ X, float post, Emit emit) {
+  if constexpr (NOUT == NO) {
+    mlp_backward_h(dec, xa, xb, X, post, emit);
+  } else {
+    using L = DecL<NOUT>;
+    const int l = lane_id(), j = l & 15, q = l >> 4;
+    float gyb[4][L::KT];
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb)
+#pragma unroll
+      for (int t = 0; t < L::KT; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+    f4v gxo[2][4];
+    mlp_backward_mfma<NOUT>(dec, xa, xb, gyb, gxo);
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      emit(0, sb, gxo[0][sb] * post);
+      emit(1, sb, gxo[1][sb] * post);
+    }
+  }
+}
+
 // Head: sigma = (1/alpha) * laplace_cdf(-d, beta) * (1 - mask)  (generator.py:629-636, 30-33)
 //       rgb   = softmax(features) @ palette                    (generator.py:668-679)
 // and the reference's other heads (nfi_field.heads, wave-uniform):
@@ -835,7 +1182,7 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
   }
   NFI_STAMP(1)
   float y[NOUT];
-  mlp_forward_tile<NOUT, MLP_PREFETCH>(a.field.dec, X, y);
+  mlp_forward<NOUT, MLP_PREFETCH>(a.field.dec, X, npts, y);
   NFI_STAMP(2)
   if (a.y_saved && lane_id() < npts) {     // (no saved state in forward-only calls)
     const int N = a.fine ? 2 * a.S : a.S;
@@ -891,11 +1238,12 @@ __device__ __forceinline__ void alpha_of(float sigma, float dist, float& al, flo
 // ---------------------------------------------------------------------------------------
 // Forward kernel.  SPL = coarse samples per lane (S <= 64*SPL), NPL = merged per lane.
 // ---------------------------------------------------------------------------------------
-// The inversion-sized kernels (<= 128 merged samples, 11 outputs) run at occupancy 4: 128 VGPRs
-// with the decoder tables loaded at their use (4 VGPRs spill, outside the loops); with the
-// tables prefetched a hidden block ahead they need 147 (occupancy 3): forward 2.39 vs 2.51 ms.
+// The inversion-sized kernels (<= 128 merged samples, 11 outputs) run at occupancy 3 with the
+// split-f16 decoder (168 VGPRs, 6 spilled outside the loops): 2.04 ms vs 2.57 ms at occupancy 4
+// (128 VGPRs, 54 spilled).  (The exact-f32 decoder measured the other way: 2.39 at occupancy 4 vs
+// 2.51 ms at 3.)
 #ifndef NFI_FWD_OCC
-#define NFI_FWD_OCC 4
+#define NFI_FWD_OCC 3
 #endif
 #ifndef NFI_FWD_OCC4
 #define NFI_FWD_OCC4 3   // the 256-merged-sample kernel (imagenet_256)
@@ -1343,15 +1691,16 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 // and decoder, sigma/colour head backward, decoder input-gradient, per-sample feature
 // gradient -> gfeat (d planes is summed per tile afterwards), palette partial, and the
 // grid_sampler_2d d-grid -> d ray origins/directions (re-gather, generator.py:312-326).
+// (occupancy 3: the split decoder backward holds its 48 table registers, the four point blocks'
+//  inputs and accumulators at 162 VGPRs without spills: 1.89 ms vs 2.20 ms at occupancy 4 with spills)
 #ifndef NFI_FIELD_OCC
-#define NFI_FIELD_OCC 4
+#define NFI_FIELD_OCC 3
 #endif
 // VARIANT = false: the inversion field (heads == 0 at compile time, the register budget of the
 // hot path is not shared with the other heads); true: nfi_field.heads read at run time.
 // NOUT = 33: the view-direction mapper field (NFI_HEAD_VIEWDIR, always with VARIANT).
 template <bool VARIANT, int NOUT>
 __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd_kernel(nfi_render_args a, BwdArgs g) {
-  using L = DecL<NOUT>;
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -1475,12 +1824,14 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
       // per-point palette contributions p_k * gc, column-summed through the LDS tile
       wave_lds_sync();
       float* row = X + l * XS;
+      float pv[NA * 3];
 #pragma unroll
       for (int k = 0; k < NA; ++k) {
-        row[k * 3 + 0] = h.p[k] * gc0;
-        row[k * 3 + 1] = h.p[k] * gc1;
-        row[k * 3 + 2] = h.p[k] * gc2;
+        pv[k * 3 + 0] = h.p[k] * gc0;
+        pv[k * 3 + 1] = h.p[k] * gc1;
+        pv[k * 3 + 2] = h.p[k] * gc2;
       }
+      lds_store_keep(row, pv);
     }
   }
   wave_lds_sync();
@@ -1505,19 +1856,13 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     for (int k = 0; k < NO; ++k) gyo[k] = gy[k];
   }
   wave_lds_sync();
-#pragma unroll
-  for (int o = 0; o < NOUT; ++o) X[l * XS + o] = gyo[o];
-#pragma unroll
-  for (int o = NOUT; o < 4 * L::KT; ++o) X[l * XS + o] = 0.f;
-  wave_lds_sync();
-  float gyb[4][L::KT];
   {
-    const int j = l & 15, q = l >> 4;
+    float dyr[DYC<NOUT>];
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-      for (int t = 0; t < L::KT; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+    for (int o = 0; o < DYC<NOUT>; ++o) dyr[o] = (o < NOUT) ? gyo[o] : 0.f;
+    lds_store_keep(X + l * XS, dyr);
   }
+  wave_lds_sync();
   if constexpr (NOUT == NOV) {
     // dL/d xray of this ray chunk: column sums of the feature gradients (tile columns 1..32)
     const int col = l & 31, r0 = (l >> 5) * 32;
@@ -1530,23 +1875,16 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     if (l < NVF) g.d_xray[(r * g.npl + e) * NVF + l] = sh;
   }
   NFI_STAMP(18)
-  f4v gxo[2][4];
-  mlp_backward_mfma<NOUT>(a.field.dec, xa, xb, gyb, gxo);
-  NFI_STAMP(19)
   // x = (e1+e2+e3)/3: each plane's tap feature gradient is dX/3.  Lane (j, q) holds channels
   // 16cb + 4q.. of point 16sb + j
   {
     const int j = l & 15, q = l >> 4;
-#pragma unroll
-    for (int sb = 0; sb < 4; ++sb) {
-      const int ip = e * 64 + 16 * sb + j;
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const f4v gv = gxo[cb][sb] * (1.f / 3.f);
-        if (ip < N) *reinterpret_cast<f4v*>(g.gfeat + (r * N + ip) * NC + 16 * cb + 4 * q) = gv;
-      }
-    }
+    float* gf = g.gfeat + (r * N + e * 64 + j) * NC + 4 * q;
+    mlp_backward<NOUT>(a.field.dec, xa, xb, X, 1.f / 3.f, [&](int cb, int sb, f4v gv) {
+      if (e * 64 + 16 * sb + j < N) *reinterpret_cast<f4v*>(gf + 16 * sb * NC + 16 * cb) = gv;
+    });
   }
+  NFI_STAMP(19)
   NFI_STAMP(20)
   if (g.cursor) {
     // append this sample's three (plane, tile) entries to the d-planes bins
@@ -1980,7 +2318,6 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 // ---------------------------------------------------------------------------------------
 template <int NPL, int NOUT>
 __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
-  using L = DecL<NOUT>;
   __shared__ __attribute__((aligned(16))) float lds[4 * (XTILE + 256)];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long nrays = (long long)a.B * a.HW;
@@ -2091,7 +2428,6 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
       const int npts = min(64, N - e * 64);
       // d sdf / d x for the chunk's points: decoder backward with dY = e_0 on the matrix cores
       f4v xa[4], xb[4];
-      float gyb[4][L::KT];
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb) {
         const int ip = e * 64 + 16 * sb + j16;
@@ -2102,17 +2438,24 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
           xa[sb] = ld4(xr);
           xb[sb] = ld4(xr + 4);
         }
-#pragma unroll
-        for (int tt = 0; tt < L::KT; ++tt) gyb[sb][tt] = (tt == 0 && q == 0) ? 1.f : 0.f;
       }
+      // dY rows: the unit vector of the distance output
+      wave_lds_sync();
+      {
+        float dyr[DYC<NOUT>];
+#pragma unroll
+        for (int o = 0; o < DYC<NOUT>; ++o) dyr[o] = (o == 0) ? 1.f : 0.f;
+        lds_store_keep(X + l * XS, dyr);
+      }
+      wave_lds_sync();
       f4v gxo[2][4];
-      mlp_backward_mfma<NOUT>(a.field.dec, xa, xb, gyb, gxo);
+      mlp_backward<NOUT>(a.field.dec, xa, xb, X, 1.f / 3.f, [&](int cb, int sb, f4v gv) { gxo[cb][sb] = gv; });
       wave_lds_sync();
 #pragma unroll
       for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          *reinterpret_cast<f4v*>(X + (16 * sb + j16) * XS + 16 * cb + 4 * q) = gxo[cb][sb] * (1.f / 3.f);
+          *reinterpret_cast<f4v*>(X + (16 * sb + j16) * XS + 16 * cb + 4 * q) = gxo[cb][sb];
       wave_lds_sync();
       // tap derivative per point (quad layout), reduced over the point's 16 lanes
       PointP P;
@@ -2514,7 +2857,7 @@ __global__ void __launch_bounds__(256) sampler_fwd_kernel(SamplerArgs A) {
   gather_features(pv, P, npts, X);
   wave_lds_sync();
   float y[NO];
-  mlp_forward_tile<NO, true>(A.f.dec, X, y);
+  mlp_forward<NO, true>(A.f.dec, X, npts, y);
   Head h;
   head_forward(y, P.mask, A.f.inv_alpha, A.f.beta, A.f.palette ? A.f.palette + b * (NA * 3) : nullptr, A.f.heads, h);
   if (l < npts) {
@@ -2533,7 +2876,6 @@ __global__ void __launch_bounds__(256) sampler_fwd_kernel(SamplerArgs A) {
 // float atomics (two 256-B wave instructions per plane: texels x0, x0+1 x 32 channels of rows y0,
 // y1) and the grid gradient (ATen grid_sampler_2d border / align_corners rule) -> d x.
 __global__ void __launch_bounds__(256) sampler_bwd_kernel(SamplerArgs A) {
-  using L = DecL<NO>;
   __shared__ __attribute__((aligned(16))) float lds[4 * XTILE];
   const int wv = threadIdx.x >> 6, l = lane_id();
   const long long cpi = (A.P + 63) / 64;
@@ -2564,7 +2906,7 @@ __global__ void __launch_bounds__(256) sampler_bwd_kernel(SamplerArgs A) {
     }
   }
   float y[NO];
-  mlp_forward_tile<NO, true>(A.f.dec, X, y);
+  mlp_forward<NO, true>(A.f.dec, X, npts, y);
   const float* pal = A.f.palette ? A.f.palette + b * (NA * 3) : nullptr;
   Head h;
   head_forward(y, P.mask, A.f.inv_alpha, A.f.beta, pal, A.f.heads, h);
@@ -2600,13 +2942,14 @@ __global__ void __launch_bounds__(256) sampler_bwd_kernel(SamplerArgs A) {
     }
 #pragma unroll
     for (int k = 0; k < NA; ++k) gy[1 + k] += (gp_[k] - dot) * h.p[k];
-    float* row = X + l * XS;
+    float pv[NA * 3];
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
-      row[k * 3 + 0] = h.p[k] * gc[0];
-      row[k * 3 + 1] = h.p[k] * gc[1];
-      row[k * 3 + 2] = h.p[k] * gc[2];
+      pv[k * 3 + 0] = h.p[k] * gc[0];
+      pv[k * 3 + 1] = h.p[k] * gc[1];
+      pv[k * 3 + 2] = h.p[k] * gc[2];
     }
+    lds_store_keep(X + l * XS, pv);
     wave_lds_sync();
     if (A.d_palette_part) {
       const int col = l & 31, r0 = (l >> 5) * 32;
@@ -2621,21 +2964,15 @@ __global__ void __launch_bounds__(256) sampler_bwd_kernel(SamplerArgs A) {
   }
   // dY^T operands through the tile
   wave_lds_sync();
-#pragma unroll
-  for (int o = 0; o < NO; ++o) X[l * XS + o] = v ? gy[o] : 0.f;
-#pragma unroll
-  for (int o = NO; o < 4 * L::KT; ++o) X[l * XS + o] = 0.f;
-  wave_lds_sync();
-  float gyb[4][L::KT];
   {
-    const int j = l & 15, q = l >> 4;
+    float dyr[DYC<NO>];
 #pragma unroll
-    for (int sb = 0; sb < 4; ++sb)
-#pragma unroll
-      for (int t = 0; t < L::KT; ++t) gyb[sb][t] = X[(16 * sb + j) * XS + 4 * t + q];
+    for (int o = 0; o < DYC<NO>; ++o) dyr[o] = (o < NO && v) ? gy[o] : 0.f;
+    lds_store_keep(X + l * XS, dyr);
   }
+  wave_lds_sync();
   f4v gxo[2][4];
-  mlp_backward_mfma<NO>(A.f.dec, xa, xb, gyb, gxo);
+  mlp_backward<NO>(A.f.dec, xa, xb, X, 1.f / 3.f, [&](int cb, int sb, f4v gv) { gxo[cb][sb] = gv; });
   // each plane's tap feature gradient dX/3 into the tile: row = point, 32 channels
   wave_lds_sync();
   {
@@ -2644,7 +2981,7 @@ __global__ void __launch_bounds__(256) sampler_bwd_kernel(SamplerArgs A) {
     for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
-        *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 16 * cb + 4 * q) = gxo[cb][sb] * (1.f / 3.f);
+        *reinterpret_cast<f4v*>(X + (16 * sb + j) * XS + 16 * cb + 4 * q) = gxo[cb][sb];
   }
   wave_lds_sync();
   // adjoint of the three bilinear taps, point by point: lane (dx = l >> 5, c = l & 31)

@@ -12,8 +12,8 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 13
-DEC_SIZE = 10256
+ABI_VERSION = 14
+DEC_SIZE = 7200
 DEC_SIZE_VIEWDIR = 14384
 
 c_float_p = ctypes.POINTER(ctypes.c_float)

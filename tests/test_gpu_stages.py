@@ -180,3 +180,66 @@ def test_sampler_extras():
     assert float((out['normals'].cpu().double() - extras['normals']).abs().max()) < 1e-4
     assert torch.equal(out['coords'].cpu(), x)
     assert float((out['sigma'].cpu().double() - sigma).abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize('plane_scale,w_scale,g_scale', [(1.0, 1.0, 1.0), (1e-3, 1.0, 1e-6), (1e3, 1.0, 1e4),
+                                                         (1.0, 1e-2, 1.0), (1.0, 30.0, 1e-3)])
+def test_decoder_split_precision(plane_scale, w_scale, g_scale):
+    """The inversion decoder runs on the f16 matrix cores as hi/lo splits of power-of-two-scaled
+    fp32 operands (nfi_render.hip): its outputs and gradients must carry the error
+    of an fp32 evaluation at any operand magnitude.  The raw decoder output (sdf distance) and the
+    gradients through the decoder backward, with features, weights and loss gradients scaled by
+    powers of ten, against the fp64 oracle: err(hip) <= 4 err(fp32 reference) + 1e-6 of the
+    value range (no absolute floor)."""
+    inp = _sampler_field(10, True, seed=31)
+    inp['planes'] = inp['planes'] * plane_scale
+    inp['w1'], inp['w2'] = inp['w1'] * w_scale, inp['w2'] * w_scale
+    g = torch.Generator().manual_seed(13)
+    B, P = 2, 256
+    x = (torch.rand(B, P, 3, generator=g) * 2 - 1) * 1.3
+    gs, gr, gd = (torch.randn(B, P, generator=g) * g_scale, torch.randn(B, P, 3, generator=g) * g_scale,
+                  torch.randn(B, P, generator=g) * g_scale)
+    hip = _sampler_run(inp, x, gs, gr, gd, torch.float32, DEV, 10, True, ('sigma', 'rgb', 'sdf_distance'))
+    r32 = _sampler_run(inp, x, gs, gr, gd, torch.float32, 'cpu', 10, True, None)
+    r64 = _sampler_run(inp, x, gs, gr, gd, torch.float64, 'cpu', 10, True, None)
+    d64 = r64['dist'].double()
+    e_hip = float((hip['dist'].double() - d64).abs().max())
+    e_ref = float((r32['dist'].double() - d64).abs().max())
+    print(f'  dist  hip {e_hip:.3g}  ref32 {e_ref:.3g}  (|dist| max {float(d64.abs().max()):.3g})')
+    assert e_hip <= 4 * e_ref + 1e-6 * float(d64.abs().max())
+    for k in ('d_planes', 'd_x'):
+        e_hip, e_ref = rel_l2(hip[k], r64[k]), rel_l2(r32[k], r64[k])
+        print(f'  {k:8s} hip {e_hip:.3g}  ref32 {e_ref:.3g}')
+        assert e_hip <= 4 * e_ref + 1e-6, k
+
+
+@pytest.mark.parametrize('case', ['render_p3d', 'render_shapenet'])
+def test_forward_decoder_outputs(case):
+    """The decoder inside the fused forward, sample by sample: the decoder outputs the forward saves
+    for the backward against an fp64 evaluation of the decoder on the inputs it saved (the golden
+    cases' S = 16: 16 of 64 lanes per evaluation, the rest of the wave's tile rows stale — they
+    must not enter the per-wave input scale of the split-f16 products)."""
+    import torch.nn.functional as F
+    from golden_io import load
+    d, meta = load(case)
+    nfi.configure(scene_range=meta['scene_range'], white_background=bool(meta['white_bg']))
+    planes = d['planes'].to(DEV).requires_grad_()
+    f = nfi.TriplaneField(planes=planes, palette=d['palette'].to(DEV), w1=d['w1'].to(DEV), b1=d['b1'].to(DEV),
+                          w2=d['w2'].to(DEV), b2=d['b2'].to(DEV), alpha=float(d['alpha']), beta=float(d['beta']))
+    kw = (dict(randomize=True, u_coarse=d['u_coarse'].to(DEV), u_fine=d['u_fine'].to(DEV)) if meta['randomize']
+          else dict(randomize=False))
+    rgb = nfi.render(f, meta['H'], meta['W'], d['cam'].to(DEV), d['focal'].to(DEV), None, None, None, meta['S'], **kw)[0]
+    fn = rgb.grad_fn
+    while fn is not None and len(getattr(fn, 'saved_tensors', ())) < 13:
+        fn = fn.next_functions[0][0] if fn.next_functions else None
+    st = fn.saved_tensors
+    y_saved, x_saved = st[10].cpu().double(), st[12].cpu().double()
+    n, nout, N = y_saved.shape
+    w1, b1, w2, b2 = (d[k].double() for k in ('w1', 'b1', 'w2', 'b2'))
+    y64 = (F.softplus(x_saved @ (w1 / w1.shape[1] ** 0.5).T + b1) @ (w2 / w2.shape[1] ** 0.5).T + b2)
+    y64 = y64.view(n, N, nout).transpose(1, 2)
+    den = (F.softplus(x_saved @ (w1 / w1.shape[1] ** 0.5).T + b1).abs() @ (w2 / w2.shape[1] ** 0.5).abs().T
+           + b2.abs()).view(n, N, nout).transpose(1, 2)
+    rel = float(((y_saved - y64).abs() / den).max())
+    print(f'  max |y - y64| / sum|terms| = {rel:.3g}')
+    assert rel < 2e-6
