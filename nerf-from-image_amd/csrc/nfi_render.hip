@@ -579,16 +579,31 @@ __device__ __forceinline__ f4v mfma3(u4v ah, u4v al, u4v bh, u4v bl, f4v c) {
   return mfma_h(ah, bh, c);
 }
 // two fp32 values -> their f16 hi halves and lo halves (packed pairs): hi = f16(v), lo = f16(v - hi),
-// both round-to-nearest (v_cvt_pk_f16_f32; v - hi is exact in fp32).  Written in plain operations so
-// hipcc's hazard recognizer sees every VGPR write ahead of the MFMAs that read it: an inline-asm
-// v_fma_mix form (one instruction per lo half) let an MFMA read a register the asm had rewritten
-// too early — wrong and run-to-run different results, no fault (the recognizer does not look
-// inside asm strings).
+// both round-to-nearest (v_cvt_pk_f16_f32; v - hi is exact in fp32).  hipcc's hazard recognizer
+// does not look inside an asm string: an asm result read by an MFMA needs its wait states inside the
+// string, and an asm output register must not be one a matrix-core instruction may still be reading.
+// (NFI_SPLIT_ASM 1: lo halves by v_fma_mix, 4 VALU per pair instead of 5: forward 2.07 -> 2.01 ms,
+//  field backward 2.02 -> 1.99 ms; 0: plain operations)
+#ifndef NFI_SPLIT_ASM
+#define NFI_SPLIT_ASM 1
+#endif
 __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
   typedef _Float16 h2v __attribute__((ext_vector_type(2)));
   const h2v h = h2v{(_Float16)a, (_Float16)b};
   hi = __builtin_bit_cast(unsigned, h);
+#if NFI_SPLIT_ASM
+  // lo by the mixed-precision FMA f16(hi * -1 + v), one instruction per value, in a register the
+  // compiler has just written itself (the copy of hi: its own wait states cover any matrix-core
+  // read still pending on that register); the string ends with the 2 wait states before an MFMA
+  // reads the result
+  lo = hi;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "+v"(lo) : "v"(hi), "v"(a), "v"(b));
+#else
   lo = __builtin_bit_cast(unsigned, h2v{(_Float16)(a - (float)h[0]), (_Float16)(b - (float)h[1])});
+#endif
 }
 __device__ __forceinline__ void split8(const float (&v)[8], u4v& hi, u4v& lo) {
 #pragma unroll
@@ -648,6 +663,11 @@ __device__ __forceinline__ void split_tile_inputs(const float* __restrict__ X, i
   split8(v, xh, xl);
 }
 
+// (NFI_FWD_XHOLD 1: the inputs split once and held across the two K-steps instead of re-read from the
+//  tile and re-split per K-step: measured 2.06 vs 2.01-2.07 ms, not used)
+#ifndef NFI_FWD_XHOLD
+#define NFI_FWD_XHOLD 0
+#endif
 // Decoder forward for the npts points of the wave's X tile (LDS rows of XS floats; the stale rows
 // past npts are zeroed first, so they neither enter the per-wave input scale nor produce inf / NaN
 // that a caller's masked sums would pick up): point l's 11 outputs.  Z^T = W1s X^T by hidden blocks hb; each K-step kb of Y^T = W2s softplus(Z)^T takes its
@@ -675,6 +695,11 @@ __device__ __forceinline__ void mlp_forward_h(const float* __restrict__ dec, flo
   float sx, isx;
   pow2_scale(wave_max_dpp(m), 15, sx, isx);
   const float cz = dec[H::SC] * isx;   // 2^-(e1 + ex) log2(e)
+#if NFI_FWD_XHOLD
+  u4v XH[4], XL[4];
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) split_tile_inputs(X, sb, sx, XH[sb], XL[sb]);
+#endif
   f4v Y[4];
 #pragma unroll
   for (int sb = 0; sb < 4; ++sb) Y[sb] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -686,8 +711,12 @@ __device__ __forceinline__ void mlp_forward_h(const float* __restrict__ dec, flo
     const u4v a2h = ldu4(dec + H::H2 + (kb * 64 + l) * 8), a2l = ldu4(dec + H::H2 + (kb * 64 + l) * 8 + 4);
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
+#if NFI_FWD_XHOLD
+      const u4v xh = XH[sb], xl = XL[sb];
+#else
       u4v xh, xl;
       split_tile_inputs(X, sb, sx, xh, xl);
+#endif
       const f4v z0 = mfma3(a0h, a0l, xh, xl, f4v{0.f, 0.f, 0.f, 0.f});
       const f4v z1 = mfma3(a1h, a1l, xh, xl, f4v{0.f, 0.f, 0.f, 0.f});
       float hv[8];
