@@ -5,8 +5,11 @@ sources' digest so bench.py uses them only for the kernels they describe).
 Per kernel: average duration (kernel trace), HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE;
 gfx950's FETCH_SIZE counts half the bytes of wide streaming reads, MI355X_MICROARCH.md §HBM;
 Infinity-Cache hits are counted too), and from the SQ / TCC passes:
-  MFMA FLOP rate   SQ_INSTS_VALU_MFMA_F32 x 2,048 FLOP (v_mfma_f32_16x16x4_f32 = 16x16x4 MACs)
-                   / duration, against the 157.3 TF fp32 dense peak
+  MFMA FLOP rate   executed matrix-core FLOP: SQ_INSTS_VALU_MFMA_F32 x 2,048 (v_mfma_f32_16x16x4_f32)
+                   + SQ_INSTS_VALU_MFMA_F16 x 16,384 (v_mfma_f32_16x16x32_f16) / duration; the fp32
+                   work they carry (the split-f16 decoder runs three f16 products per fp32 product:
+                   F16 x 16,384 / 3) against the 157.3 TF fp32 dense peak, the executed f16 rate
+                   against the 2.5 PF f16 dense peak
   cycles           GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs): the kernel's active clocks
                    per XCD (2.07 GHz effective for the long kernels); duration x 2.4 GHz without it
   MFMA busy        SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs x cycles): share of SIMD-cycles the matrix
@@ -80,8 +83,12 @@ for r in stats:
     if hbm is not None:
         d.update(fetch_kib=f, write_kib=w, hbm_bytes_corrected=hbm, hbm_GBps=hbm / dur / 1e9, hbm_frac=hbm / dur / 8e12)
     if 'SQ_INSTS_VALU_MFMA_F32' in c:
-        fl = c['SQ_INSTS_VALU_MFMA_F32'] * 2048
-        d.update(mfma_insts=c['SQ_INSTS_VALU_MFMA_F32'], mfma_TFLOPs=fl / dur / 1e12, mfma_flop_frac=fl / dur / 157.3e12)
+        f16 = c.get('SQ_INSTS_VALU_MFMA_F16', 0.0)
+        fl = c['SQ_INSTS_VALU_MFMA_F32'] * 2048 + f16 * 16384 / 3   # fp32 work carried
+        d.update(mfma_insts=c['SQ_INSTS_VALU_MFMA_F32'] + f16, mfma_TFLOPs=fl / dur / 1e12,
+                 mfma_flop_frac=fl / dur / 157.3e12)
+        if f16:
+            d.update(mfma_f16_exec_TFLOPs=f16 * 16384 / dur / 1e12, mfma_f16_exec_frac=f16 * 16384 / dur / 2500e12)
     if 'SQ_VALU_MFMA_BUSY_CYCLES' in c:
         d['mfma_busy'] = c['SQ_VALU_MFMA_BUSY_CYCLES'] / (cyc * SIMDS)
     if 'SQ_INSTS_VALU' in c:
@@ -109,16 +116,16 @@ def fmt(v, f='{:.3g}'):
 
 lines = [f'# rocprofv3 summary — {tag}', '',
          f'`scripts/profile_round.sh` on one MI355X: `rocprofv3 --kernel-trace --stats`, then separate '
-         f'`--pmc` passes (FETCH_SIZE; WRITE_SIZE; 8 SQ; 7 SQ + GRBM; TCC hit/miss + GRBM) of '
+         f'`--pmc` passes (FETCH_SIZE; WRITE_SIZE; 8 SQ; 8 SQ + GRBM; TCC hit/miss + GRBM) of '
          f'`python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-inversion --no-configs` '
          f'(config {config}, B={batch}).  Derived metrics: see scripts/summarize_round.py.', '',
-         '| kernel | calls | avg us | HBM GB/launch | HBM TB/s | HBM frac | MFMA TF | MFMA frac | MFMA busy | '
+         '| kernel | calls | avg us | HBM GB/launch | HBM TB/s | HBM frac | MFMA fp32-work TF | of fp32 peak | f16 MFMA exec TF | MFMA busy | '
          'VALU issue | VALU/SIMD/cyc | waves/SIMD | wait share | issue stall | L2 hit | clock GHz |',
-         '|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|']
+         '|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|']
 for k, d in sorted(kern.items(), key=lambda kv: -kv[1]['avg_us'] * kv[1]['calls']):
     lines.append(f"| `{k}` | {d['calls']} | {d['avg_us']:.1f} | {fmt(d.get('hbm_bytes_corrected') and d['hbm_bytes_corrected'] / 1e9)} | "
                  f"{fmt(d.get('hbm_GBps') and d['hbm_GBps'] / 1e3)} | {fmt(d.get('hbm_frac'))} | "
-                 f"{fmt(d.get('mfma_TFLOPs'))} | {fmt(d.get('mfma_flop_frac'))} | {fmt(d.get('mfma_busy'))} | "
+                 f"{fmt(d.get('mfma_TFLOPs'))} | {fmt(d.get('mfma_flop_frac'))} | {fmt(d.get('mfma_f16_exec_TFLOPs'))} | {fmt(d.get('mfma_busy'))} | "
                  f"{fmt(d.get('valu_issue_share'))} | {fmt(d.get('valu_per_simd_cycle'))} | {fmt(d.get('waves_per_simd'))} | "
                  f"{fmt(d.get('wait_share'))} | {fmt(d.get('issue_stall_share'))} | {fmt(d.get('l2_hit'))} | "
                  f"{fmt(d.get('clock_GHz'))} |")
