@@ -59,7 +59,8 @@ struct DecL {
 // gradients feed the next product from registers.
 //   H1  [hb 4][l][8]       W1s[16hb + (l&15)][8(l>>4) + j] 2^e1                layer 1 A
 //   B1S [hb][l][r 4]       b1s[16hb + 4(l>>4) + r] log2(e)                       layer 1 bias (base 2)
-//   H2  [kb 2][l][8]       W2s[l&15][hk(kb, l>>4, j)] 2^e2 (rows >= 11 zero)     layer 2 A
+//   H2  [kb 2][l][8]       W2s[l&15][hk(kb, l>>4, j)] ln2 2^e2 (rows >= 11 zero) layer 2 A (the
+//                          hidden activations arrive as softplus / ln 2)
 //   H3  [hb][l][4]         k = 8(l>>4) + j: hi of W2s[k][16hb + (l&15)] 2^e3 for k < 16, the lo of
 //                          W2s[k - 16][..] for k >= 16 (outputs >= 11 zero)      d hidden A: one
 //                          MFMA gives hi.hi + lo.hi against [dY hi; dY hi], one hi.lo + lo.lo

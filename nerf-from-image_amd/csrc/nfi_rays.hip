@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(256) decoder_pack_h_kernel(const float* __rest
   m1 = red[0][0];
   m2 = red[1][0];
   c3 = red[2][0];
-  const int e1 = pow2_exp(m1, 15), e2 = pow2_exp(m2, 15), e3 = pow2_exp(m2, 7), e4 = e1;
+  const int e1 = pow2_exp(m1, 15), e2 = pow2_exp(m2 * 0.69314718f, 15), e3 = pow2_exp(m2, 7), e4 = e1;
   // hidden unit of K-step kb at k = 8q + j
   auto hk = [](int kb, int q, int j) { return 16 * (2 * kb + (j >> 2)) + 4 * q + (j & 3); };
   // one table dword: the hi (part 0) or lo (part 1) halves of two consecutive operand elements
@@ -449,7 +449,9 @@ __global__ void __launch_bounds__(256) decoder_pack_h_kernel(const float* __rest
     } else if (i < H::H3) {
       const int u = i - H::H2, kb = u / 512, l = (u / 8) % 64, w = u % 8, part = w >> 2, j = 2 * (w & 3);
       const int o = l & 15, q = l >> 4;
-      v = pair(ldexpf(W2(o, hk(kb, q, j)), e2), ldexpf(W2(o, hk(kb, q, j + 1)), e2), part);
+      // (times ln 2: the forward's hidden activations arrive as softplus / ln 2, nfi_render.hip)
+      v = pair(ldexpf(W2(o, hk(kb, q, j)) * 0.69314718f, e2), ldexpf(W2(o, hk(kb, q, j + 1)) * 0.69314718f, e2),
+               part);
     } else if (i < H::H4) {
       const int u = i - H::H3, hb = u / 256, l = (u / 4) % 64, w = u % 4;
       const int h = 16 * hb + (l & 15), k = 8 * (l >> 4) + 2 * w, part = k >= 16, o = k & 15;

@@ -631,10 +631,11 @@ __device__ __forceinline__ void pow2_scale(float m, int top, float& s, float& in
   s = __builtin_ldexpf(1.f, e);
   inv = __builtin_ldexpf(1.f, -e);
 }
-// softplus(z) (threshold 20) from zs = z log2(e)
+// softplus(z) / ln 2 (threshold z > 20) from zs = z log2(e): the ln 2 is folded into the layer-2
+// table (DecH H2), one multiply fewer per hidden unit
 __device__ __forceinline__ float softplus_b2(float zs) {
   const float h = __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(zs));
-  return ((zs > 28.8539009f) ? zs : h) * 0.69314718f;
+  return (zs > 28.8539009f) ? zs : h;
 }
 // the wave's 64 decoder inputs (xa/xb: channels 8q..8q+3, 8q+4..8q+7 of point 16sb + j) times a
 // power of two for the wave, split; returns the inverse scale
