@@ -157,7 +157,9 @@ const char* nfi_last_error(void);
 
 /* EqualizedLinear parameters (stylegan.py:173-176) -> packed, gain-scaled decoder:
  * W1s = w1*g1 [64,32], b1s = b1*gb, W2s = w2*g2 [11,64], b2s = b2*gb (a [4,64] decoder of
- * NFI_HEAD_RGB_SIGMOID is passed zero-padded to 11 rows). */
+ * NFI_HEAD_RGB_SIGMOID is passed zero-padded to 11 rows).  The 11-output decoder is packed for
+ * the f16 matrix cores: every weight times a per-matrix power of two as an fp16 pair hi + lo
+ * (fp32-accurate three-product contractions; NFI_DEC_SIZE floats, one workgroup launch). */
 int32_t nfi_decoder_pack(const float* w1, const float* b1, const float* w2, const float* b2,
                          float g1, float g2, float gb, float* dec, void* stream);
 /* The same for a decoder of nout outputs: 11 (= nfi_decoder_pack) or 33 (NFI_HEAD_VIEWDIR:
