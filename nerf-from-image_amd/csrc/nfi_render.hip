@@ -669,6 +669,9 @@ __device__ __forceinline__ void split_tile_inputs(const float* __restrict__ X, i
 #ifndef NFI_FWD_XHOLD
 #define NFI_FWD_XHOLD 0
 #endif
+#ifndef NFI_FWD_PERMT
+#define NFI_FWD_PERMT 1   // outputs transposed by lane swaps (1) or through the LDS tile (0)
+#endif
 // Decoder forward for the npts points of the wave's X tile (LDS rows of XS floats; the stale rows
 // past npts are zeroed first, so they neither enter the per-wave input scale nor produce inf / NaN
 // that a caller's masked sums would pick up): point l's 11 outputs.  Z^T = W1s X^T by hidden blocks hb; each K-step kb of Y^T = W2s softplus(Z)^T takes its
@@ -731,6 +734,35 @@ __device__ __forceinline__ void mlp_forward_h(const float* __restrict__ dec, flo
       Y[sb] = mfma3(a2h, a2l, hh, hl, Y[sb]);
     }
   }
+  const float s2 = dec[H::SC + 1];
+#if NFI_FWD_PERMT
+  // lane (j, q) holds outputs 4q..4q+3 of point 16sb + j in Y[sb]: a 4x4 transpose of (lane row q,
+  // block sb) in registers — v_permlane32_swap exchanges lanes 32-63 of its first operand with
+  // lanes 0-31 of its second, v_permlane16_swap the odd 16-lane rows of the first with the even
+  // rows of the second — leaves lane (j, R) with outputs 4q'..4q'+3 of point 16R + j in Y[q']
+  auto swap32 = [](f4v& a, f4v& b) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[c]), __float_as_uint(b[c]), false, false);
+      a[c] = __uint_as_float(r[0]);
+      b[c] = __uint_as_float(r[1]);
+    }
+  };
+  auto swap16 = [](f4v& a, f4v& b) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[c]), __float_as_uint(b[c]), false, false);
+      a[c] = __uint_as_float(r[0]);
+      b[c] = __uint_as_float(r[1]);
+    }
+  };
+  swap32(Y[0], Y[2]);
+  swap32(Y[1], Y[3]);
+  swap16(Y[0], Y[1]);
+  swap16(Y[2], Y[3]);
+#pragma unroll
+  for (int o = 0; o < NO; ++o) y[o] = fmaf(Y[o >> 2][o & 3], s2, dec[H::B2 + o]);
+#else
   // lane (j, q) holds outputs 4q..4q+3 of point 16sb + j: transpose through the tile
   wave_lds_sync();
 #pragma unroll
@@ -739,9 +771,9 @@ __device__ __forceinline__ void mlp_forward_h(const float* __restrict__ dec, flo
     lds_store_keep(X + (16 * sb + j) * XS + 4 * q, yv);
   }
   wave_lds_sync();
-  const float s2 = dec[H::SC + 1];
 #pragma unroll
   for (int o = 0; o < NO; ++o) y[o] = fmaf(X[l * XS + o], s2, dec[H::B2 + o]);
+#endif
 }
 
 // Decoder input gradient for 64 points: xa/xb the decoder inputs (lane (j, q): channels 8q..8q+7
