@@ -529,6 +529,28 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
                         if ctr.get(k) is not None}
     except (OSError, ValueError, KeyError):
         pass
+    # the decoder's matrix-core utilisation (north star: "MFMA utilisation for the MLP against gfx950
+    # peak"): per decoder launch, live HIP-event fp32-work rate of the reference MLP's FLOPs, and the
+    # same profile's counters (executed f16 MFMA rate; the split-f16 decoder does three f16 products
+    # per fp32 product)
+    decoder = {}
+    for stg in ('render_fwd', 'bwd_field'):
+        if stg not in stages:
+            continue
+        ent = {'fp32_work_TFLOPs': stages[stg]['mfma_TFLOPs'],
+               'fp32_work_frac': round(stages[stg]['mfma_TFLOPs'] / 157.3, 4), 'fp32_peak_TFLOPs': 157.3}
+        try:
+            if cj.get('source_digest') == source_digest():
+                c2 = cj['kernels'].get(KERNEL_OF[stg], {})
+                for key in ('mfma_f16_exec_TFLOPs', 'mfma_f16_exec_frac', 'mfma_busy', 'valu_issue_share'):
+                    if c2.get(key) is not None:
+                        ent['counters_' + key] = round(c2[key], 4)
+                ent['counters_f16_peak_TFLOPs'] = 2500.0
+        except (NameError, KeyError, AttributeError, TypeError):
+            pass
+        decoder[KERNEL_OF[stg]] = ent
+    res['decoder_mfma'] = dict(decoder, dtype='fp32 operands as hi/lo fp16 pairs on v_mfma_f32_16x16x32_f16 '
+                                     '(three products per fp32 product; fp32-accurate, DESIGN.md §3)')
     model_bytes = per_launch * hbm_model(dom, pose, bwd, H, S)
     if traffic is not None:
         achieved, basis = traffic * 1e9 / sec / 1e9, 'measured HBM bytes per launch (traffic) / HIP-event launch time'
