@@ -1883,31 +1883,18 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
       }
 #pragma unroll
       for (int k = 0; k < NA; ++k) gy[1 + k] = (gp[k] - dot) * h.p[k];
-      // per-point palette contributions p_k * gc, column-summed through the LDS tile
-      wave_lds_sync();
-      float* row = X + l * XS;
-      float pv[NA * 3];
+      // the chunk's palette partial sum_i p_k(i) gc_c(i) = g_rgb_c(ray) sum_i w_i p_k(i) (the
+      // upstream rgb gradient is one per ray): ten wave sums on DPP (fixed order), no LDS
+      float pw[NA];
 #pragma unroll
-      for (int k = 0; k < NA; ++k) {
-        pv[k * 3 + 0] = h.p[k] * gc0;
-        pv[k * 3 + 1] = h.p[k] * gc1;
-        pv[k * 3 + 2] = h.p[k] * gc2;
-      }
-      lds_store_keep(row, pv);
-    }
-  }
-  wave_lds_sync();
-  if (!VARIANT || !(a.field.heads & NFI_HEAD_RGB_SIGMOID)) {
-    // column sums over the 64 rows (rows of lanes >= npts are zero): lanes (half, column) sum 32
-    // rows each with all reads in flight, then the halves are added
-    const int col = l & 31, r0 = (l >> 5) * 32;
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (col < NA * 3) {
+      for (int k = 0; k < NA; ++k) pw[k] = wave_sum(h.p[k] * w);
+      const int lk = l / 3, lc = l - 3 * lk;
+      float sel = pw[0];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) s4[j & 3] += X[(r0 + j) * XS + col];
+      for (int k = 1; k < NA; ++k) sel = (lk == k) ? pw[k] : sel;
+      const float grc = (lc == 0) ? gr0 : ((lc == 1) ? gr1 : gr2);
+      if (l < NA * 3) g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = sel * grc;
     }
-    const float sh = sum_halves((s4[0] + s4[1]) + (s4[2] + s4[3]));
-    if (l < NA * 3) g.d_palette_part[(r * g.npl + e) * (NA * 3) + l] = sh;
   }
   // dY^T operands through the tile: row = point, 4 KT columns (NOUT outputs + zeros)
   float gyo[NOUT];
