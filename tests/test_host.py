@@ -142,3 +142,43 @@ def test_stage_seams_refuse_cpu_tensors():
         stages.render_volume_density(torch.zeros(4, 8), torch.zeros(4, 8, 3), ro, rd, torch.zeros(4, 8))
     with pytest.raises(RuntimeError, match='HIP devices only'):
         stages.make_sampler(_field())(torch.zeros(1, 5, 3))
+
+
+def test_split_f16_products_carry_fp32_error():
+    """The arithmetic of the split-f16 decoder (nfi_render.hip), emulated in numpy:
+    operands scaled by a power of two (largest |v| in [2^14, 2^15)), split as hi = f16(v),
+    lo = f16(v - hi); a contraction is lo.hi + hi.lo + hi.hi with exact products accumulated in
+    fp32.  Its error against fp64, relative to sum |a b|, matches an fp32 dot product's at operand
+    magnitudes 1e-5 .. 1e3 (the per-wave / per-matrix scaling keeps every value in fp16's normal
+    range); without the scaling, small operands lose that accuracy."""
+    import numpy as np
+
+    def scale(a, axis=None):
+        m = np.max(np.abs(a), axis=axis, keepdims=True)
+        e = 15 - np.frexp(np.where(m > 0, m, 1.0))[1]
+        return np.ldexp(np.float32(1), e).astype(np.float32)
+
+    def split(a):
+        h = a.astype(np.float16)
+        return h, (a - h.astype(np.float32)).astype(np.float16)
+
+    def split_mm(W, X, sw, sx):
+        wh, wl = split(W * sw)
+        xh, xl = split(X * sx)
+        f = lambda p, q: p.astype(np.float32) @ q.astype(np.float32)   # f16 x f16 products: exact in fp32
+        return (f(wl, xh) + f(wh, xl) + f(wh, xh)) / (sw * sx)
+
+    rng = np.random.default_rng(0)
+    W = (rng.standard_normal((64, 32)) / np.sqrt(32)).astype(np.float32)
+    for mag in (1e-5, 1e-2, 1.0, 1e3):
+        X = (rng.standard_normal((32, 512)) * mag).astype(np.float32)
+        ref = W.astype(np.float64) @ X.astype(np.float64)
+        den = np.abs(W).astype(np.float64) @ np.abs(X).astype(np.float64)
+        e32 = np.max(np.abs((W @ X).astype(np.float64) - ref) / den)
+        es = np.max(np.abs(split_mm(W, X, scale(W), scale(X, axis=0)) - ref) / den)
+        assert es <= 4 * e32 + 1e-7, (mag, es, e32)
+    # unscaled small operands fall into fp16 subnormals: far from fp32 accuracy
+    X = (rng.standard_normal((32, 512)) * 1e-5).astype(np.float32)
+    ref = W.astype(np.float64) @ X.astype(np.float64)
+    den = np.abs(W).astype(np.float64) @ np.abs(X).astype(np.float64)
+    assert np.max(np.abs(split_mm(W, X, np.float32(1), np.float32(1)) - ref) / den) > 1e-4
