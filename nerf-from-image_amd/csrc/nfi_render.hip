@@ -1758,6 +1758,9 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
 #ifndef NFI_FIELD_OCC
 #define NFI_FIELD_OCC 3
 #endif
+#ifndef NFI_BIN_BATCH
+#define NFI_BIN_BATCH 1
+#endif
 // VARIANT = false: the inversion field (heads == 0 at compile time, the register budget of the
 // hot path is not shared with the other heads); true: nfi_field.heads read at run time.
 // NOUT = 33: the view-direction mapper field (NFI_HEAD_VIEWDIR, always with VARIANT).
@@ -1940,6 +1943,28 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     PointP P;
     point_params(R.o, R.d, te, sr, pv.R, P);
     const bool vb = v && P.mask == 0.f;
+#if NFI_BIN_BATCH
+    // the three cursor atomics issued together (one return latency instead of three in a row),
+    // then the three record stores
+    int4 rec[3];
+    int key[3], old[3];
+    LaneRuns lr[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      key[q] = plane_tile_key(P, q, R.b, pv.R, g.tg, r * N + i, rec[q]);
+      lr[q] = lane_runs(key[q], vb);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      old[q] = 0;
+      if (lr[q].start && vb) old[q] = atomicAdd(g.cursor + key[q], lr[q].len);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int pos = __shfl(old[q], lr[q].leader) + (lane_id() - lr[q].leader);
+      if (vb) g.list[pos] = rec[q];
+    }
+#else
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       int4 rec;
@@ -1947,6 +1972,7 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
       const int pos = run_increment(g.cursor, key, vb);
       if (vb) g.list[pos] = rec;
     }
+#endif
   }
   NFI_STAMP(21)
 }
