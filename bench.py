@@ -410,26 +410,37 @@ def main():
 FLOPS = {'render_fwd': (6450, 5504), 'bwd_bins': (0, 0), 'bwd_field': (5700, 5504)}
 KERNEL_OF = {'render_fwd': 'render_fwd_kernel', 'bwd_field': 'field_bwd_kernel',
              'bwd_tiles': 'tile_kernel', 'bwd_bins': 'scan_blocks_kernel'}
-# gather ceiling of the forward's own tap stream, measured: the product gather alone over the
+# gather ceiling of the FORWARD's own tap stream, measured: the product gather alone over the
 # forward's merged samples at its occupancy (scripts/gather_probe.py, profiles/r03_gather_probe.json:
-# 0.865 ms for 25.8 GB of taps; L1 hits on top of MI355X_MICROARCH.md's 16.8-18.8 TB/s from L2)
+# 0.865 ms for 25.8 GB of taps; L1 hits on top of MI355X_MICROARCH.md's 16.8-18.8 TB/s from L2).
+# Reported only for render_fwd: no other kernel's access pattern was measured against it.
 GATHER_CEILING_GBS = 29790.0
 
 
-def hbm_model(name, pose, bwd, H, S):
-    """Algorithmic HBM bytes per sample of each launch: the bytes this design must
-    stream through HBM — planes once per image and tap pass (25.17 MB = 12 B per sample at
-    128^2 x 128), the per-sample state the forward saves for the backward, the backward's
-    streamed rows and records; per-ray I/O is < 0.5 B per sample."""
+def compulsory_bytes(name, pose, H, S):
+    """SURVEY §8(d) compulsory HBM bytes per sample of each launch: the planes read once per image and
+    tap pass (25.17 MB = 12 B per sample at 128^2 x 128), d planes written once; nothing else a launch
+    handles is compulsory (the per-sample intermediates are this design's, per-ray I/O < 0.5 B)."""
     plane = 3 * 32 * 256 * 256 * 4 / (H * H * 2 * S)
+    return {'render_fwd': plane, 'bwd_bins': 0.0, 'bwd_field': 0.0,
+            # d planes written once + (pose gradients) the planes read once for the grid gradients
+            'bwd_tiles': plane * (2 if pose else 1)}[name]
+
+
+def hbm_model(name, pose, bwd, H, S):
+    """This DESIGN's streamed HBM bytes per sample of each launch: the compulsory
+    bytes plus the per-sample state the design moves between launches."""
+    plane = compulsory_bytes('render_fwd', pose, H, S)
     return {
         # planes + saved state written (t, sigma 8 B, rgb 12, decoder outputs 44, inputs 128, perm 2)
         'render_fwd': plane + (194 if bwd else 0),
         'bwd_bins': 12.0,
         # saved state read (194) + feature-gradient row written (128) + 3 entry records (48) + 8
         'bwd_field': 194 + 128 + 48 + 8,
-        # d planes written once + (pose) the tile texels read once + each sample's gradient row and records
-        'bwd_tiles': plane * (2 if pose else 1) + 128 + 48 + (24 if pose else 0),
+        # compulsory (d planes, planes for the grid gradients) + the sample's 128-B gradient row read
+        # once per plane (3x: the three planes' tiles of a sample are different tiles) + its three 16-B
+        # records + (pose) the 24-B grid-gradient row written
+        'bwd_tiles': compulsory_bytes('bwd_tiles', pose, H, S) + 3 * 128 + 48 + (24 if pose else 0),
     }[name]
 
 
@@ -479,8 +490,10 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
         sec = v * 1e-3 / launches[k]
         per_launch = samples_per_step / launches[k]
         stages[k] = {'ms': round(v, 4), 'launches_per_step': launches[k],
-                     'hbm_model_bytes_per_sample': round(hbm_model(k, pose, bwd, H, S), 1),
-                     'hbm_model_GBps': round(per_launch * hbm_model(k, pose, bwd, H, S) / sec / 1e9, 1),
+                     'compulsory_bytes_per_sample': round(compulsory_bytes(k, pose, H, S), 2),
+                     'compulsory_GBps': round(per_launch * compulsory_bytes(k, pose, H, S) / sec / 1e9, 1),
+                     'design_stream_bytes_per_sample': round(hbm_model(k, pose, bwd, H, S), 1),
+                     'design_stream_GBps': round(per_launch * hbm_model(k, pose, bwd, H, S) / sec / 1e9, 1),
                      'tap_rate_GBps': round(per_launch * tap[k] / sec / 1e9, 1),
                      'fp32_TFLOPs': round(per_launch * flops[k][0] / sec / 1e12, 2),
                      'mfma_TFLOPs': round(per_launch * flops[k][1] / sec / 1e12, 2)}
@@ -488,7 +501,8 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
                       else f'Msamples/sec fwd ({H}^2, {S}+{S} samples/ray)'),
            'value': round(value, 3), 'unit': 'Msamples/s', 'n_gpus': world, 'steps': steps,
            'warmup': args.warmup if headline else 2, 'ms_per_step': round(ms_per_step, 4),
-           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+           'dtype': 'f32 (decoder: 3-term split-f16 MFMA)',
            'data': 'synthetic',
            'config': {'workload': name, 'global_batch': B * world, 'resolution': H,
                       'samples_per_ray': f'{S}+{S}', 'plane_res': 256, 'pose_grad': pose,
@@ -537,8 +551,12 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
     for stg in ('render_fwd', 'bwd_field'):
         if stg not in stages:
             continue
+        # fp32_work: the reference MLP's 5,504 FLOP per sample / launch time, against the
+        # fp32 peak; f16_pipe: the same work as the three f16 products per fp32 product the split needs,
+        # against the f16 matrix peak (counters_*: EXECUTED f16 MFMAs incl. recompute and padding)
         ent = {'fp32_work_TFLOPs': stages[stg]['mfma_TFLOPs'],
-               'fp32_work_frac': round(stages[stg]['mfma_TFLOPs'] / 157.3, 4), 'fp32_peak_TFLOPs': 157.3}
+               'fp32_work_frac': round(stages[stg]['mfma_TFLOPs'] / 157.3, 4), 'fp32_peak_TFLOPs': 157.3,
+               'f16_pipe_frac': round(3 * stages[stg]['mfma_TFLOPs'] / 2500.0, 4), 'f16_peak_TFLOPs': 2500.0}
         try:
             if cj.get('source_digest') == source_digest():
                 c2 = cj['kernels'].get(KERNEL_OF[stg], {})
@@ -551,30 +569,46 @@ def measure(name, args, nfi, ops, dev, world, rank, headline):
         decoder[KERNEL_OF[stg]] = ent
     res['decoder_mfma'] = dict(decoder, dtype='fp32 operands as hi/lo fp16 pairs on v_mfma_f32_16x16x32_f16 '
                                      '(three products per fp32 product; fp32-accurate, DESIGN.md §3)')
+    # roofline of the dominant launch (DESIGN.md §5 gives each formula):
+    #   achieved = SURVEY §8(d) compulsory bytes per sample x samples per launch / HIP-event launch time
+    #   tap_rate = §8(d) tap bytes per sample (1,536 per tap pass) x samples / time: an effective rate
+    #              that exceeds the HBM peak where L2 / the Infinity Cache serve the taps
+    #   traffic  = rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch (profiles/latest_counters.json; the
+    #              counters include Infinity-Cache hits), and its ratio to the compulsory bytes
+    #   design_stream = this design's streamed bytes (hbm_model) / time
+    comp_b = compulsory_bytes(dom, pose, H, S)
+    comp_bytes = per_launch * comp_b
+    achieved = comp_bytes / sec / 1e9
     model_bytes = per_launch * hbm_model(dom, pose, bwd, H, S)
-    if traffic is not None:
-        achieved, basis = traffic * 1e9 / sec / 1e9, 'measured HBM bytes per launch (traffic) / HIP-event launch time'
-    else:
-        achieved, basis = model_bytes / sec / 1e9, ('algorithmic HBM stream bytes per launch '
-                                                    '(DESIGN.md §3 model) / HIP-event launch time')
-    res['roofline'] = {
+    tap_b = tap[dom]
+    roof = {
         'bound': 'hbm', 'kernel': KERNEL_OF[dom], 'stage': dom,
         'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-        'frac': round(achieved / HBM_PEAK_GBS, 4), 'frac_basis': basis,
+        'frac': round(achieved / HBM_PEAK_GBS, 4),
+        'frac_basis': (f'SURVEY §8(d) compulsory bytes {comp_b:.1f} B/sample (planes read once per image and tap '
+                       f'pass, d planes written once) x {per_launch:.0f} samples / HIP-event launch time'),
         'traffic': traffic, 'traffic_unit': 'GB per launch', 'traffic_source': traffic_src,
+        'traffic_over_compulsory': (round(traffic * 1e9 / comp_bytes, 1) if traffic is not None and comp_bytes > 0
+                                    else None),
+        'traffic_GBps': round(traffic / sec, 1) if traffic is not None else None,
+        'traffic_frac': round(traffic / sec / HBM_PEAK_GBS, 4) if traffic is not None else None,
         'launch_ms': round(sec * 1e3, 4),
-        'hbm_model_bytes_per_sample': round(hbm_model(dom, pose, bwd, H, S), 1),
-        'hbm_model_frac': round(model_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
-        # SURVEY §8(d)'s tap bytes (1,536 B per sample and tap pass), served mostly by L2 / the
-        # Infinity Cache: a rate against the guide's L2 gather ceiling, not against HBM
+        'compulsory_bytes_per_sample': round(comp_b, 2),
+        'tap_bytes_per_sample': tap_b,
         'tap_rate_GBps': st['tap_rate_GBps'],
-        'gather_ceiling_GBps': GATHER_CEILING_GBS,
-        'gather_ceiling_frac': round(st['tap_rate_GBps'] / GATHER_CEILING_GBS, 4),
-        'fp32_TFLOPs': st['fp32_TFLOPs'], 'mfma_TFLOPs': st['mfma_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
-        'mfma_frac': round(st['mfma_TFLOPs'] / 157.3, 4),
-        'mfma_basis': 'the reference MLP\'s fp32 FLOPs per sample (DESIGN.md §3) / HIP-event launch time',
+        'tap_rate_over_hbm_peak': round(st['tap_rate_GBps'] / HBM_PEAK_GBS, 4),
+        'design_stream_bytes_per_sample': round(hbm_model(dom, pose, bwd, H, S), 1),
+        'design_stream_GBps': round(model_bytes / sec / 1e9, 1),
+        'design_stream_frac': round(model_bytes / sec / 1e9 / HBM_PEAK_GBS, 4),
+        'fp32_TFLOPs': st['fp32_TFLOPs'], 'fp32_peak_TFLOPs': 157.3,
+        'fp32_frac': round(st['fp32_TFLOPs'] / 157.3, 4),
+        'fp32_basis': 'SURVEY §8(d) algorithmic fp32 FLOPs per sample / HIP-event launch time',
         'counters': counters,
     }
+    if dom == 'render_fwd':
+        roof['gather_ceiling_GBps'] = GATHER_CEILING_GBS
+        roof['gather_ceiling_frac'] = round(st['tap_rate_GBps'] / GATHER_CEILING_GBS, 4)
+    res['roofline'] = roof
     return res
 
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 14
+#define NFI_ABI_VERSION 15
 #define NFI_DEC_SIZE 7200   /* floats in the packed decoder buffer (11 outputs: split-f16 tables) */
 #define NFI_DEC_SIZE_VIEWDIR 14384 /* ... with the view-direction mapper (33 outputs) */
 
@@ -198,7 +198,8 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
  * summed per tile chunk in registers and flushed once per chunk, each entry's grid gradient
  * computed there against the tile's texels; d ray origins / directions are reduced per ray. */
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
-int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * 3 * ((R-2)/7+1) * ((R-2)/4+1) */
+int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * beams * 3 * ((R-2)/7+1) * ((R-2)/4+1),
+                                                            beams = 1 unless built with NFI_BEAM_SAMPLES */
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 /* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
  * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,
@@ -227,6 +228,40 @@ int32_t nfi_near_far(const float* ro, const float* rd, int64_t n, float scene_ra
 int32_t nfi_sample_pdf(const float* bins, const float* weights, int64_t n, int32_t nbins, int32_t num_samples,
                        int32_t deterministic, const float* u, uint64_t seed, uint64_t offset, float* out,
                        void* stream);
+
+/* get_ray_bundle (lib/nerf_utils.py:28-93) alone: ro, rd [B*H*W,3], rd NOT normalised (render() runs
+ * F.normalize after it, run.py:196; nfi_rays_forward fuses both).  Backward: g_ro, g_rd of these raw
+ * directions -> per-pixel partials contrib [B*H*W,16] in nfi_rays_backward's layout (d cam 12, d cam[3][3],
+ * d focal); no gradient to center / bbox (dataset inputs in the reference). */
+int32_t nfi_ray_bundle(const nfi_camera* cam, float* ro, float* rd, void* stream);
+int32_t nfi_ray_bundle_backward(const nfi_camera* cam, const float* g_ro, const float* g_rd, float* contrib,
+                                void* stream);
+
+/* compute_query_points_from_rays (lib/nerf_utils.py:96-122) on n rays ro, rd [n,3], near, far [n]:
+ * depth [n,S] = lerp(near, far, i/S) (+ u (far - near)/S if randomize: u [n,S] given, or the Philox
+ * stream of (seed, offset) the fused render draws its coarse jitter from), points [n,S,3] = ro + rd t.
+ * Backward (to the rays; the depth values carry none, near/far being detached, run.py:197-200):
+ * g_points [n,S,3] -> d_ro, d_rd [n,3] (either may be NULL). */
+int32_t nfi_query_points(const float* ro, const float* rd, const float* near_, const float* far_, int64_t n,
+                         int32_t S, int32_t randomize, const float* u, uint64_t seed, uint64_t offset, float* points,
+                         float* depth, void* stream);
+int32_t nfi_query_points_backward(const float* depth, const float* g_points, int64_t n, int32_t S, float* d_ro,
+                                  float* d_rd, void* stream);
+
+/* cumprod_exclusive (lib/nerf_utils.py:20-25) along the last axis of x [n,N]: out[:,0] = 1,
+ * out[:,k] = prod_{j<k} x[:,j] (product carried in fp64, as ATen's CPU cumprod of float).
+ * Backward: g_out [n,N] -> d_x [n,N] (no division: exact zeros handled; d_x[:,N-1] = 0; N <= 1024). */
+int32_t nfi_cumprod_exclusive(const float* x, int64_t n, int32_t N, float* out, void* stream);
+int32_t nfi_cumprod_exclusive_backward(const float* x, const float* g_out, int64_t n, int32_t N, float* d_x,
+                                       void* stream);
+
+/* render_volume_density_weights_only (lib/nerf_utils.py:166-182): sigma [n,N], rd [n,3], t [n,N] ->
+ * weights [n,N] (1 <= N <= 1024).  Backward: dL/d weights -> d sigma [n,N] (written), d rd [n,3] and
+ * d t [n,N] (optional). */
+int32_t nfi_volume_weights_forward(const float* sigma, const float* rd, const float* t, int64_t n, int32_t N,
+                                   float* weights, void* stream);
+int32_t nfi_volume_weights_backward(const float* sigma, const float* rd, const float* t, int64_t n, int32_t N,
+                                    const float* g_weights, float* d_sigma, float* d_rd, float* d_t, void* stream);
 
 /* render_volume_density (lib/nerf_utils.py:125-163, with cumprod_exclusive :20-25) on n rays of
  * N samples (1 <= N <= 1024): sigma [n,N], rgb [n,N,3], rd [n,3] (distances are scaled by ||rd||),

@@ -89,6 +89,36 @@ constexpr int DEC_SIZE = DecH::SIZE;           // 7,200 floats (the inversion de
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// A wide (64- / 128-bit) LDS store whose data VGPRs no instruction rewrites for 2 wait states.
+// Measured on MI355X ("Wide LDS stores"): ds_write_b128 / b64 whose data tuple the
+// next 1-2 VALU instructions rewrote stored the NEW value in some lanes when the LDS pipe was
+// backed up.  LLVM's hazard recognizer pads this hazard only for VMEM / FLAT stores wider than 8
+// bytes (GCNHazardRecognizer::createsVALUHazard), not for DS stores.  The two scheduling barriers
+// keep the compiler from moving any instruction between the store and the s_nop, so whatever
+// reuses the data registers comes after the 2 wait states; the store itself stays a compiler
+// instruction (counted in lgkmcnt).  scripts/isa_lint.py checks every wide DS store of the build.
+// (The address escapes into an empty statement ahead of the store: with only the "memory" clobber, a
+// store through a __restrict__ pointer the s_nop statement cannot see was moved past it and merged with
+// the next store; with the address as an operand of the s_nop statement itself, the register that
+// materialises it was written between the store and the nop.)
+#ifndef NFI_LDS_GAP
+#define NFI_LDS_GAP 1   // 0: plain stores (and round 3's 32-bit kept-alive rows): A/B builds only
+#endif
+template <class T>
+__device__ __forceinline__ void lds_st(T* p, const T& v) {
+#if !NFI_LDS_GAP
+  *p = v;
+  return;
+#endif
+  typedef __attribute__((address_space(3))) T* lds_ptr;
+  const lds_ptr lp = (lds_ptr)p;
+  asm volatile("" ::"v"(lp));
+  *p = v;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));

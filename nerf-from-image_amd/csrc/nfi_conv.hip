@@ -20,6 +20,7 @@
 // F.conv2d(x, w, padding=1) as the LPIPS VGG16 trunk (lpips 0.1 via lib/metrics.py:107) and the
 // synthesis layers (models/stylegan.py:130-145) call it; the reference runs fp32 with TF32 off
 // (run.py:59-60), which this keeps (fp32 transforms, fp32 GEMM).
+#include "nfi_common.h"
 #include "nfi_host.h"
 #include "../../include/nfi_producer.h"
 
@@ -353,7 +354,7 @@ __device__ __forceinline__ void stage_patch(float (&d)[6][6], float* __restrict_
     float o[6];
     bt_col(d[r], o);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) dst[(r * 6 + j) * (FK * FP)] = o[j];
+    for (int j = 0; j < 6; ++j) lds_st(dst + (r * 6 + j) * (FK * FP), o[j]);
   }
 }
 

@@ -108,6 +108,50 @@ __device__ __forceinline__ void block_hit_range(bool hit, float nr, float fr, ui
   }
 }
 
+// get_ray_bundle (nerf_utils.py:28-93) at ray r = (image b, pixel y, x): origin o, raw direction d
+__device__ __forceinline__ void bundle_ray(const nfi_camera& c, long long r, float o[3], float d[3]) {
+  const int HW = c.H * c.W;
+  const int b = (int)(r / HW);
+  const int p = (int)(r % HW);
+  const int y = p / c.W, x = p % c.W;
+  const float* M = c.cam + b * 16;
+  float ii, jj;
+  pixel_coords(c, b, x, y, ii, jj);
+  if (c.focal) {
+    const float f = c.focal[b];
+    ii = fdiv(ii, f);
+    jj = fdiv(jj, f);
+    const float dc[3] = {ii, -jj, -1.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      d[i] = rowdot3(dc, M + i * 4);
+      o[i] = M[i * 4 + 3];
+    }
+  } else {
+    const float oc[3] = {ii, -jj, 0.f};
+    const float dc[3] = {0.f, 0.f, -1.f};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      o[i] = fadd(rowdot3(oc, M + i * 4), M[i * 4 + 3]);
+      d[i] = fdiv(rowdot3(dc, M + i * 4), M[15]);
+    }
+  }
+}
+
+// the ray bundle alone (the get_ray_bundle seam): ro, raw rd [B*H*W][3]
+__global__ void __launch_bounds__(256) ray_bundle_kernel(nfi_camera c, float* __restrict__ ro, float* __restrict__ rd) {
+  const long long n = (long long)c.B * c.H * c.W;
+  const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  float o[3], d[3];
+  bundle_ray(c, r, o, d);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    ro[r * 3 + i] = o[i];
+    rd[r * 3 + i] = d[i];
+  }
+}
+
 __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, float* __restrict__ ro,
                                                        float* __restrict__ rd, float* __restrict__ nearp,
                                                        float* __restrict__ farp, uint32_t* __restrict__ part,
@@ -118,32 +162,8 @@ __global__ void __launch_bounds__(256) rays_fwd_kernel(nfi_camera c, float sr, f
   float nr = INFINITY, fr = -INFINITY;
   bool hit = false;
   if (r < n) {
-    const int b = (int)(r / HW);
-    const int p = (int)(r % HW);
-    const int y = p / c.W, x = p % c.W;
-    const float* M = c.cam + b * 16;
-    float ii, jj;
-    pixel_coords(c, b, x, y, ii, jj);
     float o[3], d[3];
-    if (c.focal) {
-      const float f = c.focal[b];
-      ii = fdiv(ii, f);
-      jj = fdiv(jj, f);
-      const float dc[3] = {ii, -jj, -1.f};
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        d[i] = rowdot3(dc, M + i * 4);
-        o[i] = M[i * 4 + 3];
-      }
-    } else {
-      const float oc[3] = {ii, -jj, 0.f};
-      const float dc[3] = {0.f, 0.f, -1.f};
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        o[i] = fadd(rowdot3(oc, M + i * 4), M[i * 4 + 3]);
-        d[i] = fdiv(rowdot3(dc, M + i * 4), M[15]);
-      }
-    }
+    bundle_ray(c, r, o, d);
     // F.normalize: x / clamp_min(||x||, 1e-12)
     const float nrm = fmaxf(tnorm3(d[0], d[1], d[2]), 1e-12f);
 #pragma unroll
@@ -201,8 +221,8 @@ __global__ void __launch_bounds__(256) rays_fix_kernel(long long n, float* __res
       kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
     }
     if ((threadIdx.x & 63) == 0) {
-      red[0][threadIdx.x >> 6] = kmin;
-      red[1][threadIdx.x >> 6] = kmax;
+      lds_st(&red[0][threadIdx.x >> 6], kmin);
+      lds_st(&red[1][threadIdx.x >> 6], kmax);
     }
     __syncthreads();
     kmin = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
@@ -221,7 +241,9 @@ __global__ void __launch_bounds__(256) rays_fix_kernel(long long n, float* __res
   farp[r] = fr;
 }
 
-// Backward of get_ray_bundle + F.normalize; per-pixel partials of d cam / d focal.
+// Backward of get_ray_bundle + F.normalize (NORM) or of get_ray_bundle alone (the seam: g_rd is the
+// gradient of the raw directions); per-pixel partials of d cam / d focal.
+template <bool NORM>
 __global__ void __launch_bounds__(256) rays_bwd_kernel(nfi_camera c, const float* __restrict__ g_ro,
                                                        const float* __restrict__ g_rd,
                                                        float* __restrict__ contrib) {
@@ -268,7 +290,7 @@ __global__ void __launch_bounds__(256) rays_bwd_kernel(nfi_camera c, const float
   const float yg = yv[0] * g[0] + yv[1] * g[1] + yv[2] * g[2];
   float graw[3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) graw[i] = (nn > 1e-12f) ? (g[i] - yv[i] * yg) / nrm : g[i] / nrm;
+  for (int i = 0; i < 3; ++i) graw[i] = !NORM ? g[i] : ((nn > 1e-12f) ? (g[i] - yv[i] * yg) / nrm : g[i] / nrm);
   const float gro[3] = {g_ro[r * 3 + 0], g_ro[r * 3 + 1], g_ro[r * 3 + 2]};
   if (c.focal) {
     // d = sum_k dc[k] M[i][k]
@@ -418,13 +440,13 @@ __global__ void __launch_bounds__(256) decoder_pack_h_kernel(const float* __rest
   for (int i = t; i < NO * NH; i += 256) m2 = fmaxf(m2, fabsf(W2(i / NH, i % NH)));
   if (t < NH)
     for (int o = 0; o < NO; ++o) c3 += fabsf(W2(o, t));
-  red[0][t] = m1;
-  red[1][t] = m2;
-  red[2][t] = c3;
+  lds_st(&red[0][t], m1);
+  lds_st(&red[1][t], m2);
+  lds_st(&red[2][t], c3);
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (t < w)
-      for (int k = 0; k < 3; ++k) red[k][t] = fmaxf(red[k][t], red[k][t + w]);
+      for (int k = 0; k < 3; ++k) lds_st(&red[k][t], fmaxf(red[k][t], red[k][t + w]));
     __syncthreads();
   }
   m1 = red[0][0];
@@ -574,7 +596,28 @@ int32_t nfi_rays_backward(const nfi_camera* cam, const float* g_ro, const float*
   if (e) return e;
   NFI_REQUIRE(g_ro && g_rd && contrib, "rays_backward: null pointer");
   const long long n = (long long)cam->B * cam->H * cam->W;
-  rays_bwd_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(*cam, g_ro, g_rd, contrib);
+  rays_bwd_kernel<true><<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(*cam, g_ro, g_rd, contrib);
+  NFI_CHECK_LAUNCH("rays_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_ray_bundle(const nfi_camera* cam, float* ro, float* rd, void* stream) {
+  int e = check_cam(cam);
+  if (e) return e;
+  NFI_REQUIRE(ro && rd, "ray_bundle: null output");
+  const long long n = (long long)cam->B * cam->H * cam->W;
+  ray_bundle_kernel<<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(*cam, ro, rd);
+  NFI_CHECK_LAUNCH("ray_bundle_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_ray_bundle_backward(const nfi_camera* cam, const float* g_ro, const float* g_rd, float* contrib,
+                                void* stream) {
+  int e = check_cam(cam);
+  if (e) return e;
+  NFI_REQUIRE(g_ro && g_rd && contrib, "ray_bundle_backward: null pointer");
+  const long long n = (long long)cam->B * cam->H * cam->W;
+  rays_bwd_kernel<false><<<(int)((n + 255) / 256), 256, 0, (hipStream_t)stream>>>(*cam, g_ro, g_rd, contrib);
   NFI_CHECK_LAUNCH("rays_bwd_kernel");
   return NFI_OK;
 }

@@ -34,20 +34,25 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// N floats to LDS with 32-bit stores whose data registers stay live until the stores completed
-// (an s_waitcnt lgkmcnt(0), then an empty use of every value).  Measured on MI355X: a
-// ds_write_b64/b128 whose data registers the next VALU instruction rewrote (hipcc builds the
-// register tuple with moves and reuses it right after the store) left the NEW value in LDS in a
-// few lanes when the CU's LDS pipe was busy — run-to-run different palette partials in the field
-// backward once its decoder read operands from LDS; hipcc inserts no wait for it.
+// N floats (dst 16-byte aligned) to LDS as b128 stores (the tail b64 / b32), each followed by the 2 wait
+// states of lds_st (nfi_common.h).  (Round 3 used 32-bit stores + s_waitcnt lgkmcnt(0) here, for
+// the same hazard: DESIGN.md §3.)
 template <int N>
 __device__ __forceinline__ void lds_store_keep(float* __restrict__ dst, const float (&v)[N]) {
-  volatile float* d = dst;
+#if !NFI_LDS_GAP
+  volatile float* d = dst;   // round 3: 32-bit stores, then lgkmcnt(0) and an empty use of every value
 #pragma unroll
   for (int k = 0; k < N; ++k) d[k] = v[k];
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int k = 0; k < N; ++k) asm volatile("" ::"v"(v[k]));
+  return;
+#endif
+#pragma unroll
+  for (int k = 0; k + 4 <= N; k += 4)
+    lds_st(reinterpret_cast<float4*>(dst + k), make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]));
+  if constexpr (N % 4 >= 2) lds_st(reinterpret_cast<float2*>(dst + N / 4 * 4), make_float2(v[N / 4 * 4], v[N / 4 * 4 + 1]));
+  if constexpr (N % 2 == 1) dst[N - 1] = v[N - 1];
 }
 
 // v + v(lane ^ 32), in every lane (gfx950 v_permlane32_swap).
@@ -153,10 +158,10 @@ __device__ __forceinline__ void gather_records(const PlaneView& pv, const PointP
     const int o1 = o0 + (((t >> 20) & 1) ? st4 : 0);
     const int dy = ((t >> 21) & 1) ? rowb : 0;
     const float w = P.pl[q].w, n = P.pl[q].n, e = 1.f - w, s = 1.f - n;
-    *reinterpret_cast<float4*>(row + 8 * q) =
-        make_float4(__int_as_float(o0), __int_as_float(o0 + dy), (s * e) * (1.f / 3.f), (n * e) * (1.f / 3.f));
-    *reinterpret_cast<float4*>(row + 8 * q + 4) =
-        make_float4(__int_as_float(o1), __int_as_float(o1 + dy), (s * w) * (1.f / 3.f), (n * w) * (1.f / 3.f));
+    lds_st(reinterpret_cast<float4*>(row + 8 * q),
+           make_float4(__int_as_float(o0), __int_as_float(o0 + dy), (s * e) * (1.f / 3.f), (n * e) * (1.f / 3.f)));
+    lds_st(reinterpret_cast<float4*>(row + 8 * q + 4),
+           make_float4(__int_as_float(o1), __int_as_float(o1 + dy), (s * w) * (1.f / 3.f), (n * w) * (1.f / 3.f)));
   }
 }
 
@@ -234,22 +239,54 @@ constexpr int TTX = TSX + 1, TTY = TSY + 1;   // texels per tile (8 x 5)
 #endif
 constexpr int CHUNK = NFI_TILE_CHUNK;         // (sample, plane) entries per accumulation workgroup
 
+// Ray blocks ("beams"): every image's pixels are split into sx x sy rectangles and the bins are
+// keyed per (beam, plane, tile), so the tile pass works through the batch beam by beam.  A beam's
+// samples have their three (plane, tile) entries in three different tiles; keyed per image, the
+// three reads of one sample's 128-B gradient row were a third of an image's entries apart (HBM
+// each time: B=8 reads 6.4 GB of rows per launch); keyed per beam of ~NFI_BEAM_SAMPLES samples
+// (rows + records ~90 MB at 2^19) the second and third reads fall inside one beam's window and hit
+// the 256 MB Infinity Cache.  0 = one beam per image (the per-image keys).
+#ifndef NFI_BEAM_SAMPLES
+#define NFI_BEAM_SAMPLES 0
+#endif
 struct TileGrid {
-  int nx, ny;
+  int nx, ny;   // plane tiles
+  int sx, sy;   // beams per image: sx columns x sy rows of pixels
+  int W, H;     // image (H = 0: one beam per image)
 };
-__host__ __device__ __forceinline__ TileGrid tile_grid(int R) { return {(R - 2) / TSX + 1, (R - 2) / TSY + 1}; }
-
-// Tile keys order the accumulation chunks.  Planes xy and xz share their x tile column, so per
-// image the key runs over x-slabs tx with the xy tiles (tx, y) and the xz tiles (tx, z) of a slab
-// next to each other — the same samples' gradient rows are read twice within a short window
-// (L2 / Infinity Cache) — followed by the yz tiles.
-__host__ __device__ __forceinline__ int tile_key(int b, int q, int tx, int ty, TileGrid G) {
-  const int T = G.nx * G.ny;
-  return b * 3 * T + (q == 2 ? 2 * T + ty * G.nx + tx : (tx * 2 + q) * G.ny + ty);
+__host__ __device__ __forceinline__ TileGrid tile_grid(int R, int HW = 0, int W = 0, int N = 0) {
+  TileGrid g{(R - 2) / TSX + 1, (R - 2) / TSY + 1, 1, 1, W, 0};
+  if (NFI_BEAM_SAMPLES > 0 && W > 0 && HW % W == 0 && N > 0) {
+    g.H = HW / W;
+    // halve the longer side of the beam while a beam holds more than NFI_BEAM_SAMPLES samples
+    while ((long long)HW * N / (g.sx * g.sy) > NFI_BEAM_SAMPLES && g.sx * g.sy < 64) {
+      if (W / g.sx >= g.H / g.sy && W / g.sx >= 32) g.sx *= 2;
+      else if (g.H / g.sy >= 32) g.sy *= 2;
+      else break;
+    }
+  }
+  return g;
 }
+__host__ __device__ __forceinline__ int beams_per_image(TileGrid G) { return G.sx * G.sy; }
+// beam index of ray r (of B*HW, images HW = H*W pixels apart, row-major pixels)
+__device__ __forceinline__ int beam_of(long long r, int HW, TileGrid G) {
+  const int b = (int)(r / HW);
+  if (G.sx * G.sy == 1) return b;
+  const int p = (int)(r - (long long)b * HW), row = p / G.W, col = p - row * G.W;
+  return b * (G.sx * G.sy) + (row * G.sy / G.H) * G.sx + col * G.sx / G.W;
+}
+
+// Tile keys order the accumulation chunks: beam-major (above), then per beam the x-slabs tx with
+// the xy tiles (tx, y) and the xz tiles (tx, z) of a slab next to each other, followed by the yz
+// tiles.
+__host__ __device__ __forceinline__ int tile_key(int beam, int q, int tx, int ty, TileGrid G) {
+  const int T = G.nx * G.ny;
+  return beam * 3 * T + (q == 2 ? 2 * T + ty * G.nx + tx : (tx * 2 + q) * G.ny + ty);
+}
+// b = the IMAGE of the key's beam
 __device__ __forceinline__ void tile_decode(int key, TileGrid G, int& b, int& q, int& tx, int& ty) {
   const int T = G.nx * G.ny;
-  b = key / (3 * T);
+  b = key / (3 * T) / beams_per_image(G);
   const int r = key % (3 * T);
   if (r >= 2 * T) {
     q = 2;
@@ -262,7 +299,7 @@ __device__ __forceinline__ void tile_decode(int key, TileGrid G, int& b, int& q,
   }
 }
 
-// Tile key of plane q for point P of image b, and the entry record {s, slot | flags, w, n}:
+// Tile key of plane q for point P of beam `beam` (beam_of), and the entry record {s, slot | flags, w, n}:
 // slot = ly*8 + lx inside the tile, flags bit 8/9 = grid-gradient multiplier gxm/gym nonzero.
 __device__ __forceinline__ int plane_tile_key(const PointP& P, int q, int b, int R, TileGrid G, long long s,
                                               int4& rec) {
@@ -685,7 +722,7 @@ __device__ __forceinline__ void mlp_forward_h(const float* __restrict__ dec, flo
   if (npts < 64) {   // (wave-uniform) zero the stale rows: no inf / NaN from them in the products
     if (l >= npts) {
 #pragma unroll
-      for (int k = 0; k < NC / 4; ++k) *reinterpret_cast<f4v*>(X + l * XS + 4 * k) = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < NC / 4; ++k) lds_st(reinterpret_cast<f4v*>(X + l * XS + 4 * k), f4v{0.f, 0.f, 0.f, 0.f});
     }
     wave_lds_sync();
   }
@@ -1575,7 +1612,8 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NF
   NFI_STAMP(6)
   if (a.tile_counts) {
     // per-tile sample counts for the backward's d-planes binning (same keys as bin_fill)
-    const TileGrid Tg = tile_grid(pv.R);
+    const TileGrid Tg = tile_grid(pv.R, a.HW, a.W, N);
+    const int beam = beam_of(r, a.HW, Tg);
 #pragma unroll
     for (int e = 0; e < NPL; ++e) {
       const int i = e * 64 + l;
@@ -1585,7 +1623,7 @@ __global__ void __launch_bounds__(256, (NPL <= 2 && SPL <= 2 && NOUT == NO) ? NF
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         int4 rec;
-        const int key = plane_tile_key(P, q, R.b, pv.R, Tg, r * N + i, rec);
+        const int key = plane_tile_key(P, q, beam, pv.R, Tg, r * N + i, rec);
         run_count(a.tile_counts, key, v);
       }
     }
@@ -1744,7 +1782,9 @@ __global__ void __launch_bounds__(256) composite_bwd_kernel(nfi_render_args a, B
     grdn = wave_sum(grdn);
     if (l < 3) {
       g.g_ro[r * 3 + l] = 0.f;
-      g.g_rd[r * 3 + l] = grdn * (R.d[l] / R.rdn);           // d rd += d||rd|| * rd / ||rd||
+      // (R.d by a select, not R.d[l]: a lane-indexed RayCtx is a memory object the compiler puts in LDS)
+      const float dl = l == 0 ? R.d[0] : (l == 1 ? R.d[1] : R.d[2]);
+      g.g_rd[r * 3 + l] = grdn * (dl / R.rdn);               // d rd += d||rd|| * rd / ||rd||
     }
   }
 }
@@ -1943,6 +1983,7 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     PointP P;
     point_params(R.o, R.d, te, sr, pv.R, P);
     const bool vb = v && P.mask == 0.f;
+    const int beam = beam_of(r, a.HW, g.tg);
 #if NFI_BIN_BATCH
     // the three cursor atomics issued together (one return latency instead of three in a row),
     // then the three record stores
@@ -1951,7 +1992,7 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
     LaneRuns lr[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      key[q] = plane_tile_key(P, q, R.b, pv.R, g.tg, r * N + i, rec[q]);
+      key[q] = plane_tile_key(P, q, beam, pv.R, g.tg, r * N + i, rec[q]);
       lr[q] = lane_runs(key[q], vb);
     }
 #pragma unroll
@@ -1968,7 +2009,7 @@ __global__ void __launch_bounds__(256, NOUT == NO ? NFI_FIELD_OCC : 2) field_bwd
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       int4 rec;
-      const int key = plane_tile_key(P, q, R.b, pv.R, g.tg, r * N + i, rec);
+      const int key = plane_tile_key(P, q, beam, pv.R, g.tg, r * N + i, rec);
       const int pos = run_increment(g.cursor, key, vb);
       if (vb) g.list[pos] = rec;
     }
@@ -1995,7 +2036,7 @@ struct BinArgs {
 // the box (their gradient is exactly zero: sigma * (1 - mask) and weight 0).
 __device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int key[3], int4 rec[3]) {
   const long long ray = s / A.N;
-  const int b = (int)(ray / A.HW);
+  const int beam = beam_of(ray, A.HW, A.tg);
   float o[3], d[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -2005,7 +2046,7 @@ __device__ __forceinline__ bool sample_keys(const BinArgs& A, long long s, int k
   PointP P;
   point_params(o, d, A.t[s], A.sr, A.R, P);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) key[q] = plane_tile_key(P, q, b, A.R, A.tg, s, rec[q]);
+  for (int q = 0; q < 3; ++q) key[q] = plane_tile_key(P, q, beam, A.R, A.tg, s, rec[q]);
   return P.mask == 0.f;
 }
 
@@ -2053,8 +2094,8 @@ __device__ __forceinline__ void block_scan2(int& a, int& b, int& ta, int& tb) {
   a = wave_incl_scan_i(a);
   b = wave_incl_scan_i(b);
   if (l == 63) {
-    sa[wv] = a;
-    sbx[wv] = b;
+    lds_st(sa + wv, a);
+    lds_st(sbx + wv, b);
   }
   __syncthreads();
   int pa = 0, pb = 0;
@@ -2136,7 +2177,7 @@ struct TileArgs {
   const int* offsets;
   const int* chunk_start; // [K+1]
   const int* chunk_tile;  // [total chunks]
-  const int* meta;        // meta[0] = total chunks
+  int* meta;              // meta[0] = total chunks, meta[1] = the tile pass's chunk queue
   const int4* list;
   float* dplanes;
   long long sb;
@@ -2194,6 +2235,27 @@ __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1
 }
 
 // One entry: run-merge into (a0, a1) while the cell repeats, else flush to the image.
+#ifndef NFI_TILE_AB
+#define NFI_TILE_AB 1
+#endif
+#if NFI_TILE_AB
+// A run of one cell is kept as (A, B) = (sum gw, sum gw w): the texel x0 gets A - B, x0 + 1 gets B
+// when the run ends.  Per entry 4 VALU (the row weight, gw, A, B with w read from its SGPR) instead of
+// building the (1 - w, w) register pair for a packed fma each time (6).
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
+                                           float nn, float g, float wsgn, float woff) {
+  const float gw = g * fmaf(nn, wsgn, woff);
+  if (slot != cur) {
+    img_add(img, cur, a0 - a1, a1);
+    a0 = 0.f;
+    a1 = 0.f;
+    cur = slot;
+  }
+  a0 += gw;
+  a1 = fmaf(gw, w, a1);
+}
+#define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0 - a1, a1)
+#else
 __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
                                            float nn, float g, float wsgn, float woff) {
   const float gw = g * fmaf(nn, wsgn, woff);
@@ -2206,6 +2268,8 @@ __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, floa
   a0 = fmaf(gw, 1.f - w, a0);
   a1 = fmaf(gw, w, a1);
 }
+#define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0, a1)
+#endif
 
 // Grid gradient of one (sample, plane) entry from its gradient row g (stage row l of G) and the
 // tile texels: grid_sampler_2d_backward (generator.py:312-326 through ATen, border padding,
@@ -2314,7 +2378,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #define NFI_ST1(J, V)                                                                                \
   {                                                                                                  \
     const int e_ = 8 * (J) + (l >> 3);                                                               \
-    *reinterpret_cast<float4*>(G + e_ * XS + 4 * (l & 7)) = e_ < n ? V : make_float4(0.f, 0.f, 0.f, 0.f); \
+    lds_st(reinterpret_cast<float4*>(G + e_ * XS + 4 * (l & 7)), e_ < n ? V : make_float4(0.f, 0.f, 0.f, 0.f)); \
   }
 #define NFI_NEXT_REC(VREC, AHEAD)                                                                    \
     VREC = vnext;                                                                                    \
@@ -2354,7 +2418,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #undef NFI_LD1
 #undef NFI_STEP
 #undef NFI_ENTRY
-      img_add(img, cur, a0, a1);
+      NFI_TILE_FLUSH(img, cur, a0, a1);
     }
     NFI_STAMP(26)
     __syncthreads();   // every wave is done with its row stage
@@ -2530,7 +2594,7 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
       for (int sb = 0; sb < 4; ++sb)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          *reinterpret_cast<f4v*>(X + (16 * sb + j16) * XS + 16 * cb + 4 * q) = gxo[cb][sb];
+          lds_st(reinterpret_cast<f4v*>(X + (16 * sb + j16) * XS + 16 * cb + 4 * q), gxo[cb][sb]);
       wave_lds_sync();
       // tap derivative per point (quad layout), reduced over the point's 16 lanes
       PointP P;
@@ -2596,35 +2660,31 @@ __global__ void __launch_bounds__(256) extras_kernel(nfi_render_args a) {
   }
 }
 
-// d planes and the per-(sample, plane) grid gradients of the pose path, one workgroup per tile
-// chunk (the grid is sized for a bound on the chunk count; blocks past meta[0] exit at once).
+// d planes and the per-(sample, plane) grid gradients of the pose path: a grid of at most
+// TILE_WGS workgroups takes the chunks IN KEY ORDER from a queue (one atomic per chunk on
+// meta[1], zeroed before the launch), so the chunks in flight at any time are those of one or
+// two beams (tile_grid) whatever the hardware's dispatch order, and a chunk-count bound of
+// 10^5..10^6 mostly empty tiles costs no empty workgroups.  Every workgroup leaves when the
+// queue passes meta[0].  (Replaces an XCD-grouped static chunk order, measured no faster.)
 #ifndef NFI_TILE_OCC
 #define NFI_TILE_OCC 4
 #endif
-// XCD-grouped chunk order (NFI_TILE_XCD = G > 0): workgroups are dealt to the 8 XCDs
-// round-robin (block b runs on XCD b % 8); with G > 0 each XCD takes runs of G consecutive
-// chunks instead of every 8th chunk, so the chunks of an x-slab's xy and xz tiles (the same
-// samples' gradient rows, tile_key) tend to run on one XCD, where the second read of a row can
-// hit that XCD's L2.  The grid is a multiple of 8G blocks.  Measured on MI355X, tile pass ms
-// (off / G): G = 16: 2.22 / 2.26, G = 64: 2.22 / 2.21, G = whole eighths of the list: 2.18 /
-// 2.34 — the row reads are latency-bound, not short of L2 reuse; off by default.
-#ifndef NFI_TILE_XCD
-#define NFI_TILE_XCD 0
+constexpr int TILE_WGS = 2048;   // >= 256 CUs x NFI_TILE_OCC workgroups resident
+#ifndef NFI_TILE_REV
+#define NFI_TILE_REV 0   // 1: last key first (the beams the field backward wrote last)
 #endif
-constexpr int TILE_GRID_MULT = NFI_TILE_XCD > 0 ? 8 * NFI_TILE_XCD : 1;
 __global__ void __launch_bounds__(256, NFI_TILE_OCC) tile_kernel(TileArgs A) {
   __shared__ __attribute__((aligned(16))) float lds[TILE_LDS];
+  __shared__ int next;
   const int M = A.meta[0];
-#if NFI_TILE_XCD
-  constexpr unsigned G = NFI_TILE_XCD;
-  const unsigned k = blockIdx.x >> 3;
-  const int c = (int)((k / G) * (8 * G) + (blockIdx.x & 7) * G + k % G);
-  if (c >= M) return;
-#else
-  const int c = (int)blockIdx.x;
-  if (c >= M) return;
-#endif
-  tile_chunk(A, lds, c);
+  for (;;) {
+    if (threadIdx.x == 0) next = atomicAdd(A.meta + 1, 1);
+    __syncthreads();
+    const int k = next;
+    __syncthreads();   // (every lane has read it before lane 0 takes the next one)
+    if (k >= M) return;
+    tile_chunk(A, lds, NFI_TILE_REV ? M - 1 - k : k);
+  }
 }
 
 // Ray-coordinate gradients from the tile pass's grid gradients, one wave per 64 merged samples:
@@ -2770,7 +2830,9 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restr
     const int i = c + l;
     const int ic = min(i, N - 1);
     const float ti = t[ic], tn = t[min(i + 1, N - 1)], sg = sigma[r * N + ic];
-    const float c0 = rgb[(r * N + ic) * 3 + 0], c1 = rgb[(r * N + ic) * 3 + 1], c2 = rgb[(r * N + ic) * 3 + 2];
+    // (rgb NULL: the weights only, render_volume_density_weights_only)
+    const float c0 = rgb ? rgb[(r * N + ic) * 3 + 0] : 0.f, c1 = rgb ? rgb[(r * N + ic) * 3 + 1] : 0.f;
+    const float c2 = rgb ? rgb[(r * N + ic) * 3 + 2] : 0.f;
     const float dist = (i < N - 1) ? fmul(fsub(tn, ti), rdn) : 0.f;
     float al, aa, ex;
     alpha_of(i < N ? sg : 0.f, dist, al, aa, ex);
@@ -2795,7 +2857,7 @@ __global__ void __launch_bounds__(256) composite_fwd_kernel(const float* __restr
   s2 = wave_sum(s2);
   sm = wave_sum(sm);
   sd = wave_sum(sd);
-  if (l == 0) {
+  if (l == 0 && rgb_map) {
     const float bg = white ? fsub(1.f, sm) : 0.f;
     rgb_map[r * 3 + 0] = s0 + bg;
     rgb_map[r * 3 + 1] = s1 + bg;
@@ -2838,8 +2900,10 @@ __global__ void __launch_bounds__(256) composite_bwd_seam_kernel(
     carry = carry * readlane(inc, 63);
   }
   wave_lds_sync();
-  const float gr0 = g_rgb[r * 3 + 0], gr1 = g_rgb[r * 3 + 1], gr2 = g_rgb[r * 3 + 2];
-  const float gm = g_mask[r] - (white ? (gr0 + gr1 + gr2) : 0.f);
+  // (g_rgb / g_mask NULL: zero — the weights-only seam)
+  const float gr0 = g_rgb ? g_rgb[r * 3 + 0] : 0.f, gr1 = g_rgb ? g_rgb[r * 3 + 1] : 0.f;
+  const float gr2 = g_rgb ? g_rgb[r * 3 + 2] : 0.f;
+  const float gm = (g_mask ? g_mask[r] : 0.f) - (white ? (gr0 + gr1 + gr2) : 0.f);
   float grdn = 0.f, cB = 0.f;
   const int nch = (N + 63) / 64;
   for (int ch = nch - 1; ch >= 0; --ch) {
@@ -2853,7 +2917,8 @@ __global__ void __launch_bounds__(256) composite_bwd_seam_kernel(
     alpha_of(sg, dist, al, aa, ex);
     al = v ? al : 0.f;
     aa = v ? aa : 1.f;
-    const float c0 = rgb[(r * N + ic) * 3 + 0], c1 = rgb[(r * N + ic) * 3 + 1], c2 = rgb[(r * N + ic) * 3 + 2];
+    const float c0 = rgb ? rgb[(r * N + ic) * 3 + 0] : 0.f, c1 = rgb ? rgb[(r * N + ic) * 3 + 1] : 0.f;
+    const float c2 = rgb ? rgb[(r * N + ic) * 3 + 2] : 0.f;
     const float gwx = (g_w && v) ? g_w[r * N + ic] : 0.f;
     const float ee = v ? (gr0 * c0 + gr1 * c1 + gr2 * c2) + gm + gwx : 0.f;
     const float T = v ? LT[ic] : 0.f;
@@ -2864,9 +2929,11 @@ __global__ void __launch_bounds__(256) composite_bwd_seam_kernel(
     if (v) {
       d_sigma[r * N + i] = dal * dist * ex;
       const float w = al * T;
-      d_rgb[(r * N + i) * 3 + 0] = w * gr0;
-      d_rgb[(r * N + i) * 3 + 1] = w * gr1;
-      d_rgb[(r * N + i) * 3 + 2] = w * gr2;
+      if (d_rgb) {
+        d_rgb[(r * N + i) * 3 + 0] = w * gr0;
+        d_rgb[(r * N + i) * 3 + 1] = w * gr1;
+        d_rgb[(r * N + i) * 3 + 2] = w * gr2;
+      }
       LG[i] = gdist;
     }
   }
@@ -2882,6 +2949,108 @@ __global__ void __launch_bounds__(256) composite_bwd_seam_kernel(
       const float gp = (i > 0) ? LG[i - 1] : 0.f;
       d_t[r * N + i] = rdn * (gp - gi);
     }
+  }
+}
+
+// ---- cumprod_exclusive (nerf_utils.py:20-25) on n rows of N: out_0 = 1, out_k = prod_{j<k} x_j ------
+// One wave per row, chunks of 64, the product carried in fp64 (ATen's CPU cumprod of float accumulates
+// in double; the last input is not used, :23).  Backward: d x_i = out_i S_i with
+// S_i = sum_{k>i} g_k prod_{i<j<k} x_j (the reverse affine scan suffix_affine, lane map s -> x s + g;
+// no division, so exact zeros in x need no special case), d x_{N-1} = 0.
+__global__ void __launch_bounds__(256) cumprod_excl_kernel(const float* __restrict__ x, long long n, int N,
+                                                           float* __restrict__ out) {
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= n) return;
+  double carry = 1.0;
+  for (int c = 0; c < N; c += 64) {
+    const int i = c + l;
+    const float xi = x[r * N + min(i, N - 1)];
+    const double inc = wave_incl_prod_d(i < N - 1 ? (double)xi : 1.0);
+    const double exc = dpp_fill<0x138>(inc, 1.0);   // wave_shr:1, lane 0 takes 1
+    if (i < N) out[r * N + i] = (float)(carry * exc);
+    carry = carry * readlane(inc, 63);
+  }
+}
+
+__global__ void __launch_bounds__(256) cumprod_excl_bwd_kernel(const float* __restrict__ x,
+                                                               const float* __restrict__ g, long long n, int N,
+                                                               float* __restrict__ dx) {
+  __shared__ float lds[4 * COMP_NMAX];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= n) return;
+  float* LO = lds + wv * COMP_NMAX;   // the forward's outputs
+  double carry = 1.0;
+  for (int c = 0; c < N; c += 64) {
+    const int i = c + l;
+    const float xi = x[r * N + min(i, N - 1)];
+    const double inc = wave_incl_prod_d(i < N - 1 ? (double)xi : 1.0);
+    const double exc = dpp_fill<0x138>(inc, 1.0);
+    if (i < N) LO[i] = (float)(carry * exc);
+    carry = carry * readlane(inc, 63);
+  }
+  wave_lds_sync();
+  float cB = 0.f;
+  for (int ch = (N + 63) / 64 - 1; ch >= 0; --ch) {
+    const int i = ch * 64 + l;
+    const bool v = i < N;
+    const int ic = min(i, N - 1);
+    const float xi = x[r * N + ic], gi = g[r * N + ic];
+    const float Sk = suffix_affine(v ? xi : 1.f, v ? gi : 0.f, cB);
+    if (v) dx[r * N + i] = (i < N - 1) ? LO[ic] * Sk : 0.f;
+  }
+}
+
+// ---- compute_query_points_from_rays (nerf_utils.py:96-122) --------------------------------------
+// rays ro, rd [n][3], near, far [n] -> depth [n][S] = lerp(near, far, i/S) (+ u (far - near)/S when
+// randomized: u [n][S] given, or the Philox stream of the fused render's coarse draws), points
+// [n][S][3] = ro + rd t, in ATen's rounding order.  Backward to the rays (depth values carry no
+// gradient: near / far come from compute_near_far_planes under no_grad, run.py:197-200):
+// d ro = sum_i g_i, d rd = sum_i g_i t_i, one wave per ray (fixed-order sums).
+__global__ void __launch_bounds__(256) query_points_kernel(const float* __restrict__ ro, const float* __restrict__ rd,
+                                                           const float* __restrict__ nearp,
+                                                           const float* __restrict__ farp, long long n, int S,
+                                                           int randomize, const float* __restrict__ u,
+                                                           unsigned long long seed, unsigned long long offset,
+                                                           float* __restrict__ pts, float* __restrict__ depth) {
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n * S) return;
+  const long long r = k / S;
+  const int i = (int)(k - r * S);
+  const float nr = nearp[r], fr = farp[r];
+  float t = tlerp(nr, fr, fdiv((float)i, (float)S));
+  if (randomize) {
+    const float uu = u ? u[k] : rng_uniform(seed, offset, r, i, 0);
+    t = fadd(t, fmul(uu, fdiv(fsub(fr, nr), (float)S)));
+  }
+  depth[k] = t;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) pts[k * 3 + c] = fadd(ro[r * 3 + c], fmul(rd[r * 3 + c], t));
+}
+
+__global__ void __launch_bounds__(256) query_points_bwd_kernel(const float* __restrict__ depth,
+                                                               const float* __restrict__ g_pts, long long n, int S,
+                                                               float* __restrict__ d_ro, float* __restrict__ d_rd) {
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const long long r = (long long)blockIdx.x * 4 + wv;
+  if (r >= n) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+  for (int i = l; i < S; i += 64) {
+    const float t = depth[r * S + i];
+    const float* g = g_pts + (r * S + i) * 3;
+    a0 += g[0];
+    a1 += g[1];
+    a2 += g[2];
+    b0 = fmaf(g[0], t, b0);
+    b1 = fmaf(g[1], t, b1);
+    b2 = fmaf(g[2], t, b2);
+  }
+  a0 = wave_sum(a0), a1 = wave_sum(a1), a2 = wave_sum(a2);
+  b0 = wave_sum(b0), b1 = wave_sum(b1), b2 = wave_sum(b2);
+  if (l < 3) {
+    if (d_ro) d_ro[r * 3 + l] = l == 0 ? a0 : (l == 1 ? a1 : a2);
+    if (d_rd) d_rd[r * 3 + l] = l == 0 ? b0 : (l == 1 ? b1 : b2);
   }
 }
 
@@ -3124,8 +3293,8 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   const long long nrays = (long long)a->B * a->HW;
   const int N = a->fine ? 2 * a->S : a->S;
   const long long nsamp = nrays * N;
-  const TileGrid tg = tile_grid(a->field.R);
-  const long long K = (long long)a->B * 3 * tg.nx * tg.ny;
+  const TileGrid tg = tile_grid(a->field.R, a->HW, a->W, N);
+  const long long K = (long long)a->B * beams_per_image(tg) * 3 * tg.nx * tg.ny;
   char* p = static_cast<char*>(base);
   Workspace w;
   auto take = [&](long long bytes) {
@@ -3154,8 +3323,8 @@ template <int SPL, int NPL, bool FINE, int NOUT>
 static int launch_fwd(const nfi_render_args* a, hipStream_t s) {
   const long long nrays = (long long)a->B * a->HW;
   if (a->tile_counts) {
-    const TileGrid tg = tile_grid(a->field.R);
-    NFI_REQUIRE(hipMemsetAsync(a->tile_counts, 0, (size_t)a->B * 3 * tg.nx * tg.ny * 4, s) == hipSuccess,
+    const TileGrid tg = tile_grid(a->field.R, a->HW, a->W, FINE ? 2 * a->S : a->S);
+    NFI_REQUIRE(hipMemsetAsync(a->tile_counts, 0, (size_t)a->B * beams_per_image(tg) * 3 * tg.nx * tg.ny * 4, s) == hipSuccess,
                 "render_forward: memset failed");
   }
   render_fwd_kernel<SPL, NPL, FINE, NOUT><<<(unsigned)((nrays + 3) / 4), 256, 0, s>>>(*a);
@@ -3176,8 +3345,8 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
   const long long nrays = (long long)a->B * a->HW;
   const int N = a->fine ? 2 * a->S : a->S;
   const long long nsamp = nrays * N;
-  const TileGrid tg = tile_grid(a->field.R);
-  const int K = a->B * 3 * tg.nx * tg.ny;
+  const TileGrid tg = tile_grid(a->field.R, a->HW, a->W, N);
+  const int K = a->B * beams_per_image(tg) * 3 * tg.nx * tg.ny;
   Workspace w = carve(a, g->workspace);
   NFI_REQUIRE(w.bytes <= g->workspace_bytes, "render_backward: workspace too small (%lld < %lld)",
               (long long)g->workspace_bytes, w.bytes);
@@ -3238,10 +3407,10 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
               a->field.R, tg};
   if (do_tiles) {
     // 3) per-tile register accumulation of d planes (+ per-entry grid gradients for the pose)
-    // (a bound on the chunk count meta[0], rounded up to whole groups of the XCD order)
-    const long long TB = (3 * nsamp / CHUNK + K + TILE_GRID_MULT) / TILE_GRID_MULT * TILE_GRID_MULT;
-    NFI_REQUIRE(TB < (1LL << 31), "render_backward: grid too large");
-    tile_kernel<<<(unsigned)TB, 256, 0, s>>>(TA);
+    // (a bound on the chunk count meta[0]; the chunk queue meta[1] starts at 0)
+    const long long TB = 3 * nsamp / CHUNK + K + 1;
+    NFI_REQUIRE(hipMemsetAsync(w.meta + 1, 0, 4, s) == hipSuccess, "render_backward: memset failed");
+    tile_kernel<<<(unsigned)std::min<long long>(TB, TILE_WGS), 256, 0, s>>>(TA);
     NFI_CHECK_LAUNCH("tile_kernel");
     // 4) ray-coordinate gradients
 #if defined(NFI_ABLATE) && (NFI_ABLATE == 5 || NFI_ABLATE == 6)
@@ -3336,8 +3505,8 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream) {
 
 int64_t nfi_tile_count_size(const nfi_render_args* a) {
   if (nfi::validate(a)) return -1;
-  const nfi::TileGrid tg = nfi::tile_grid(a->field.R);
-  return (int64_t)a->B * 3 * tg.nx * tg.ny;
+  const nfi::TileGrid tg = nfi::tile_grid(a->field.R, a->HW, a->W, a->fine ? 2 * a->S : a->S);
+  return (int64_t)a->B * nfi::beams_per_image(tg) * 3 * tg.nx * tg.ny;
 }
 
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {
@@ -3410,6 +3579,69 @@ int32_t nfi_composite_backward(const float* sigma, const float* rgb, const float
   nfi::composite_bwd_seam_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(
       sigma, rgb, rd, t, n, N, white_bg, g_rgb, g_mask, g_weights, d_sigma, d_rgb, d_rd, d_t);
   NFI_CHECK_LAUNCH("composite_bwd_seam_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_volume_weights_forward(const float* sigma, const float* rd, const float* t, int64_t n, int32_t N,
+                                   float* weights, void* stream) {
+  NFI_REQUIRE(sigma && rd && t && weights, "volume_weights_forward: null pointer");
+  NFI_REQUIRE(n > 0 && N >= 1 && N <= nfi::COMP_NMAX, "volume_weights_forward: bad shape n=%lld N=%d (1..%d)",
+              (long long)n, N, nfi::COMP_NMAX);
+  nfi::composite_fwd_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      sigma, nullptr, rd, t, n, N, 0, nullptr, nullptr, nullptr, weights);
+  NFI_CHECK_LAUNCH("composite_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_volume_weights_backward(const float* sigma, const float* rd, const float* t, int64_t n, int32_t N,
+                                    const float* g_weights, float* d_sigma, float* d_rd, float* d_t, void* stream) {
+  NFI_REQUIRE(sigma && rd && t && g_weights && d_sigma, "volume_weights_backward: null pointer");
+  NFI_REQUIRE(n > 0 && N >= 1 && N <= nfi::COMP_NMAX, "volume_weights_backward: bad shape n=%lld N=%d (1..%d)",
+              (long long)n, N, nfi::COMP_NMAX);
+  nfi::composite_bwd_seam_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(
+      sigma, nullptr, rd, t, n, N, 0, nullptr, nullptr, g_weights, d_sigma, nullptr, d_rd, d_t);
+  NFI_CHECK_LAUNCH("composite_bwd_seam_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_cumprod_exclusive(const float* x, int64_t n, int32_t N, float* out, void* stream) {
+  NFI_REQUIRE(x && out, "cumprod_exclusive: null pointer");
+  NFI_REQUIRE(n > 0 && N >= 1, "cumprod_exclusive: bad shape n=%lld N=%d", (long long)n, N);
+  nfi::cumprod_excl_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(x, n, N, out);
+  NFI_CHECK_LAUNCH("cumprod_excl_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_cumprod_exclusive_backward(const float* x, const float* g_out, int64_t n, int32_t N, float* d_x,
+                                       void* stream) {
+  NFI_REQUIRE(x && g_out && d_x, "cumprod_exclusive_backward: null pointer");
+  NFI_REQUIRE(n > 0 && N >= 1 && N <= nfi::COMP_NMAX, "cumprod_exclusive_backward: bad shape n=%lld N=%d (1..%d)",
+              (long long)n, N, nfi::COMP_NMAX);
+  nfi::cumprod_excl_bwd_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(x, g_out, n, N, d_x);
+  NFI_CHECK_LAUNCH("cumprod_excl_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_query_points(const float* ro, const float* rd, const float* near_, const float* far_, int64_t n,
+                         int32_t S, int32_t randomize, const float* u, uint64_t seed, uint64_t offset, float* points,
+                         float* depth, void* stream) {
+  NFI_REQUIRE(ro && rd && near_ && far_ && points && depth, "query_points: null pointer");
+  NFI_REQUIRE(n > 0 && S >= 1 && n * (long long)S < (1LL << 40), "query_points: bad shape n=%lld S=%d",
+              (long long)n, S);
+  const long long k = n * S;
+  nfi::query_points_kernel<<<(unsigned)((k + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      ro, rd, near_, far_, n, S, randomize, u, seed, offset, points, depth);
+  NFI_CHECK_LAUNCH("query_points_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_query_points_backward(const float* depth, const float* g_points, int64_t n, int32_t S, float* d_ro,
+                                  float* d_rd, void* stream) {
+  NFI_REQUIRE(depth && g_points && (d_ro || d_rd), "query_points_backward: null pointer");
+  NFI_REQUIRE(n > 0 && S >= 1, "query_points_backward: bad shape n=%lld S=%d", (long long)n, S);
+  nfi::query_points_bwd_kernel<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(depth, g_points, n, S, d_ro,
+                                                                                        d_rd);
+  NFI_CHECK_LAUNCH("query_points_bwd_kernel");
   return NFI_OK;
 }
 

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 14
+ABI_VERSION = 15
 DEC_SIZE = 7200
 DEC_SIZE_VIEWDIR = 14384
 
@@ -100,6 +100,22 @@ SIGNATURES = {
                                              c_void_p, c_void_p, c_void_p, c_void_p]),
     'nfi_sampler_backward': (ctypes.c_int32, [ctypes.POINTER(NfiField), c_void_p, ctypes.c_int32, ctypes.c_int64]
                              + [c_void_p] * 7),
+    # the remaining nerf_utils seams (ABI 15)
+    'nfi_ray_bundle': (ctypes.c_int32, [ctypes.POINTER(NfiCamera), c_void_p, c_void_p, c_void_p]),
+    'nfi_ray_bundle_backward': (ctypes.c_int32, [ctypes.POINTER(NfiCamera), c_void_p, c_void_p, c_void_p,
+                                                 c_void_p]),
+    'nfi_query_points': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, c_void_p,
+                                                          ctypes.c_uint64, ctypes.c_uint64, c_void_p, c_void_p,
+                                                          c_void_p]),
+    'nfi_query_points_backward': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int32, c_void_p,
+                                                   c_void_p, c_void_p]),
+    'nfi_cumprod_exclusive': (ctypes.c_int32, [c_void_p, ctypes.c_int64, ctypes.c_int32, c_void_p, c_void_p]),
+    'nfi_cumprod_exclusive_backward': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                                        c_void_p, c_void_p]),
+    'nfi_volume_weights_forward': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int32, c_void_p,
+                                                                     c_void_p]),
+    'nfi_volume_weights_backward': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int32]
+                                    + [c_void_p] * 5),
     # include/nfi_producer.h
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),

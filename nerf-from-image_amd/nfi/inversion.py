@@ -169,6 +169,10 @@ class InversionConfig:
     overlap_target: bool = True          # 'vgg' losses: target features on a side stream (GPU)
     graph: bool = False                  # GPU: replay the step as a captured HIP graph (see invert;
                                          # measured slower than eager launches on ROCm 7.2)
+    adam: str = 'fused'                  # GPU Adam kernel: 'fused' (one kernel for all parameters) or
+                                         # 'foreach' (torch's default on CUDA, the reference's run.py:2007):
+                                         # the same update formula, rounded differently at ulp level
+                                         # (tests/test_gpu_inversion.py bounds the trajectories' distance)
 
 
 @dataclass
@@ -363,9 +367,12 @@ class _State:
                 p.requires_grad_()
             params += pose
         self.params = params
-        # on the GPU the fused Adam: one kernel for the latent and the pose tensors instead of the
-        # foreach form's per-op launches (same update formula, run.py:2007)
-        fused = bool(params[0].is_cuda)
+        # on the GPU the fused Adam by default: one kernel for the latent and the pose tensors instead of
+        # the foreach form's per-op launches (same update formula as run.py:2007's default Adam, rounded
+        # differently: cfg.adam = 'foreach' selects the reference's form for parity runs)
+        if cfg.adam not in ('fused', 'foreach'):
+            raise ValueError(f"InversionConfig.adam must be 'fused' or 'foreach', not {cfg.adam!r}")
+        fused = bool(params[0].is_cuda) and cfg.adam == 'fused'
         self.opt = torch.optim.Adam(params, lr=cfg.lr, betas=cfg.betas, capturable=capturable,
                                     **({'fused': True} if fused else {}))
         self.target = target_img[..., :3]

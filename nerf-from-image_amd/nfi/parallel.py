@@ -160,9 +160,10 @@ def invert_sharded(generator, target_img: torch.Tensor, cam2world: torch.Tensor,
         losses = torch.tensor(res.losses, dtype=torch.float64, device=dev)
         parts = res
     else:
-        # an empty chunk (b < world): nothing to invert; still joins every collective
+        # an empty chunk (b < world): nothing to invert; still joins every collective, in the order
+        # invert() fires them on the other ranks: each step in [0, cfg.steps] once, ascending
         if on_checkpoint is not None:
-            for it in checkpoints:
+            for it in sorted({int(c) for c in checkpoints if 0 <= int(c) <= cfg.steps}):
                 on_checkpoint(it, None, chunk=(a, e))
         losses = torch.zeros(cfg.steps, dtype=torch.float64, device=dev)
         parts = None

@@ -113,8 +113,8 @@ def field_from_generator(gen, c, extra_model_outputs: Sequence[str] = (),
         raise NotImplementedError('encoder-/class-conditioned generators are outside the inversion path')
     nattn = int(getattr(gen, 'attention_values', 0))
     use_sdf = bool(getattr(gen, 'use_sdf', False))
-    if nattn not in (0, 10):
-        raise NotImplementedError('nfi renders fields with 10 or 0 attention values')
+    if not 0 <= nattn <= MAX_ATTENTION:
+        raise NotImplementedError(f'nfi renders fields with 0..{MAX_ATTENTION} attention values (got {nattn})')
     if c.dim() == 3:
         ws = c.expand(-1, gen.mapping_network.backbone.num_ws, -1).contiguous() if c.shape[1] == 1 else c
     else:
@@ -157,6 +157,27 @@ def _resolve_field(target_model, model_input, extra_model_outputs, extra_model_i
         return field_from_generator(target_model, model_input, extra_model_outputs, extra_model_inputs)
     raise TypeError('target_model must be a TriplaneField, provide nfi_field(), or be a '
                     'reference-style Generator (synthesis_network + decoder)')
+
+
+MAX_ATTENTION = 10   # the kernels' attention head: 10 logits (nfi_common.h NA); fewer are padded
+
+
+def attention_padded(f: TriplaneField):
+    """(w2, b2, palette) of a field with N = 1..9 attention values (generator.py:363-402, 665-679 allow
+    any N) padded to the kernels' 10: zero decoder rows and palette rows, and a bias of -1e30 on the
+    padded logits, whose softmax terms exp(-1e30 - max) are then exactly 0 — the softmax over the N
+    real logits, the colour, and every gradient (0 to the padded rows; the palette's own rows through
+    the concatenation) are those of the N-value head.  N = 0 or 10: the field's own tensors."""
+    n = int(f.attention_values)
+    if n in (0, MAX_ATTENTION):
+        return f.w2, f.b2, f.palette
+    if not 0 < n < MAX_ATTENTION:
+        raise NotImplementedError(f'nfi renders fields with 0..{MAX_ATTENTION} attention values (got {n})')
+    pad = MAX_ATTENTION - n
+    w2 = torch.cat([f.w2.detach(), f.w2.new_zeros((pad, f.w2.shape[1]))]) if f.viewdir_mapper is None else f.w2
+    b2 = torch.cat([f.b2.detach(), f.b2.new_full((pad,), -1e30)]) if f.viewdir_mapper is None else f.b2
+    pal = torch.cat([f.palette, f.palette.new_zeros((f.palette.shape[0], pad, 3))], dim=1)
+    return w2, b2, pal
 
 
 def _check_frozen(f: TriplaneField):
@@ -223,17 +244,26 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
         # run.py:216-219: viewdirs = the (unit, possibly detached) ray directions; the mapper's
         # per-ray trunk (generator.py:223-238) here, its per-sample closure in the kernels
         xray = viewdir_trunk(f.viewdir_mapper, rd.unsqueeze(-2)).squeeze(-2)
-        vhead = ops.pack_viewdir_head(f.viewdir_mapper.output.weight, f.viewdir_mapper.output.bias)
+        vw, vb = f.viewdir_mapper.output.weight, f.viewdir_mapper.output.bias
+        if 0 < f.attention_values < MAX_ATTENTION:
+            # the mapper's output layer gives the N logits here: padded like the decoder rows below
+            pad = MAX_ATTENTION - int(f.attention_values)
+            vw = torch.cat([vw.detach(), vw.new_zeros((pad, vw.shape[1]))])
+            vb = torch.cat([vb.detach(), vb.new_full((pad,), -1e30)])
+        vhead = ops.pack_viewdir_head(vw, vb)
     planes_tm = ops.planes_texel_major(f.planes)
-    dec = ops.pack_decoder(f.w1, f.b1, f.w2, f.b2)
+    w2, b2, palette = attention_padded(f)
+    dec = ops.pack_decoder(f.w1, f.b1, w2, b2)
     opts = ops.RenderOptions(samples=int(depth_samples_per_ray), fine=bool(cfg.fine_sampling),
                              white_background=bool(cfg.white_background), randomize=bool(randomize),
                              scene_range=float(cfg.scene_range), inv_alpha=1.0 / float(f.alpha),
                              beta=float(f.beta), extras=extras, heads=heads)
-    out = ops.volume_render(planes_tm, f.palette, ro, rd, near, far, dec, opts,
+    out = ops.volume_render(planes_tm, palette, ro, rd, near, far, dec, opts,
                             u_coarse=u_coarse, u_fine=u_fine, seed=seed, debug=debug, xray=xray, vhead=vhead)
     if extras:
         rgb, depth, mask, normals, semantics = out
+        if semantics is not None and extras & 2 and 0 < f.attention_values < MAX_ATTENTION:
+            semantics = semantics[..., :int(f.attention_values)]
     else:
         (rgb, depth, mask), normals, semantics = out, None, None
     if depth_mode == 'zbuffer':

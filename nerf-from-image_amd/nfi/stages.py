@@ -3,6 +3,14 @@ uses one nerf_utils function, or the Generator's `sampler` closure, without the 
 drops these in.  Same names, arguments, shapes and return values as the reference functions;
 device tensors only (CPU tensors raise, as everywhere in nfi).
 
+  cumprod_exclusive(tensor)                                            nerf_utils.py:20-25
+  get_ray_bundle(height, width, focal_length, tform_cam2world, bbox,
+                 center=None)                                          nerf_utils.py:28-93
+  compute_query_points_from_rays(ray_origins, ray_directions,
+                                 near_thresh, far_thresh, num_samples,
+                                 randomize=True)                       nerf_utils.py:96-122
+  render_volume_density_weights_only(sigma_a, ray_origins,
+                                     ray_directions, depth_values)     nerf_utils.py:166-182
   compute_near_far_planes(ray_origins, ray_directions, scene_range)   nerf_utils.py:227-275
   sample_pdf(bins, weights, num_samples, deterministic=False)          nerf_utils.py:185-224
   render_volume_density(sigma_a, rgb, ray_origins, ray_directions,
@@ -10,9 +18,11 @@ device tensors only (CPU tensors raise, as everywhere in nfi).
                         white_background=True)                         nerf_utils.py:125-163
   make_sampler(field) / sampler(generator, ws)                         generator.py:587-681
 
-Gradients: render_volume_density to sigma_a, rgb, ray_directions (through ||rd||) and
-depth_values; the sampler to the planes, the palette and the points x_in.  near/far and
-sample_pdf carry none (the reference runs them under no_grad / on detached inputs).
+Gradients: render_volume_density / render_volume_density_weights_only to sigma_a, (rgb,)
+ray_directions (through ||rd||) and depth_values; cumprod_exclusive to its input; get_ray_bundle to
+the camera and the focal length; compute_query_points_from_rays to the rays; the sampler to the
+planes, the palette and the points x_in.  near/far and sample_pdf carry none (the reference runs
+them under no_grad / on detached inputs).
 """
 
 from __future__ import annotations
@@ -23,7 +33,201 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib
-from .ops import HEAD_NERF_DENSITY, HEAD_RGB_SIGMOID, _ptr, _require_device, _stream, pack_decoder, planes_texel_major
+from .ops import (HEAD_NERF_DENSITY, HEAD_RGB_SIGMOID, _camera_struct, _ptr, _require_device, _stream, pack_decoder,
+                  planes_texel_major)
+
+
+class _CumprodExclusive(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        lib = _lib.load()
+        N = x.shape[-1]
+        n = x.numel() // N
+        xc = x.contiguous()
+        out = torch.empty_like(xc)
+        _lib.check(lib.nfi_cumprod_exclusive(_ptr(xc), n, N, _ptr(out), _stream(x.device)), 'nfi_cumprod_exclusive')
+        ctx.save_for_backward(xc)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        x, = ctx.saved_tensors
+        N = x.shape[-1]
+        n = x.numel() // N
+        dx = torch.empty_like(x)
+        _lib.check(lib.nfi_cumprod_exclusive_backward(_ptr(x), _ptr(g.contiguous()), n, N, _ptr(dx),
+                                                      _stream(x.device)), 'nfi_cumprod_exclusive_backward')
+        return dx
+
+
+def cumprod_exclusive(tensor: torch.Tensor) -> torch.Tensor:
+    """nerf_utils.py:20-25: the exclusive cumulative product along the last axis (out[..., 0] = 1)."""
+    _require_device(tensor)
+    if tensor.dtype != torch.float32:
+        raise TypeError('nfi: fp32 tensors only')
+    if tensor.shape[-1] > 1024 and tensor.requires_grad:
+        raise ValueError('cumprod_exclusive backward: at most 1024 entries per row')
+    return _CumprodExclusive.apply(tensor)
+
+
+class _RayBundle(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cam, focal, center, bbox, H: int, W: int):
+        lib = _lib.load()
+        B = cam.shape[0]
+        dev = cam.device
+        cam_c = cam.contiguous()
+        foc_c = None if focal is None else focal.contiguous()
+        cen_c = None if center is None else center.contiguous()
+        bb_c = None if bbox is None else bbox.contiguous()
+        ro = torch.empty((B, H, W, 3), device=dev)
+        rd = torch.empty((B, H, W, 3), device=dev)
+        cs = _camera_struct(cam_c, foc_c, cen_c, bb_c, H, W)
+        _lib.check(lib.nfi_ray_bundle(ctypes.byref(cs), _ptr(ro), _ptr(rd), _stream(dev)), 'nfi_ray_bundle')
+        ctx.save_for_backward(cam_c, foc_c, cen_c, bb_c)
+        ctx.HW = (H, W)
+        return ro, rd
+
+    @staticmethod
+    def backward(ctx, g_ro, g_rd):
+        lib = _lib.load()
+        cam, focal, center, bbox = ctx.saved_tensors
+        H, W = ctx.HW
+        B = cam.shape[0]
+        dev = cam.device
+        n = B * H * W
+        g_ro = torch.zeros((n, 3), device=dev) if g_ro is None else g_ro.contiguous()
+        g_rd = torch.zeros((n, 3), device=dev) if g_rd is None else g_rd.contiguous()
+        contrib = torch.empty((n, 16), device=dev)
+        cs = _camera_struct(cam, focal, center, bbox, H, W)
+        st = _stream(dev)
+        _lib.check(lib.nfi_ray_bundle_backward(ctypes.byref(cs), _ptr(g_ro), _ptr(g_rd), _ptr(contrib), st),
+                   'nfi_ray_bundle_backward')
+        red = torch.empty((B, 16), device=dev)
+        ws = torch.empty((B * 64 * 16,), device=dev)
+        _lib.check(lib.nfi_segment_sum(_ptr(contrib), B, H * W, 16, _ptr(red), _ptr(ws), st), 'nfi_segment_sum')
+        d_cam = torch.zeros((B, 4, 4), device=dev)
+        d_cam[:, :3, :] = red[:, :12].view(B, 3, 4)
+        d_cam[:, 3, 3] = red[:, 12]
+        d_focal = red[:, 13].clone() if focal is not None else None
+        return d_cam, d_focal, None, None, None, None
+
+
+def get_ray_bundle(height: int, width: int, focal_length: Optional[torch.Tensor], tform_cam2world: torch.Tensor,
+                   bbox: Optional[torch.Tensor], center: Optional[torch.Tensor] = None):
+    """nerf_utils.py:28-93 -> (ray_origins, ray_directions) [B, H, W, 3], the directions NOT
+    normalised (perspective when focal_length [B] is given, else orthographic; optional center [B, 2]
+    and bbox [B, 2, 2]).  Gradients to tform_cam2world and focal_length (center / bbox: none)."""
+    _require_device(tform_cam2world, focal_length, bbox, center)
+    if (center is not None and center.requires_grad) or (bbox is not None and bbox.requires_grad):
+        raise NotImplementedError('nfi.stages.get_ray_bundle: no gradient to center / bbox')
+    return _RayBundle.apply(tform_cam2world, focal_length, center, bbox, int(height), int(width))
+
+
+class _QueryPoints(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ro, rd, near, far, S: int, randomize: bool, u, seed: int):
+        lib = _lib.load()
+        lead = ro.shape[:-1]
+        n = ro.numel() // 3
+        dev = ro.device
+        ro_c, rd_c = ro.contiguous(), rd.contiguous()
+        nr, fr = near.contiguous(), far.contiguous()
+        uu = None if u is None else u.contiguous()
+        pts = torch.empty((*lead, S, 3), device=dev)
+        depth = torch.empty((*lead, S), device=dev)
+        _lib.check(lib.nfi_query_points(_ptr(ro_c), _ptr(rd_c), _ptr(nr), _ptr(fr), n, S, int(randomize), _ptr(uu),
+                                        seed & ((1 << 64) - 1), 0, _ptr(pts), _ptr(depth), _stream(dev)),
+                   'nfi_query_points')
+        ctx.save_for_backward(depth)
+        ctx.mark_non_differentiable(depth)
+        return pts, depth
+
+    @staticmethod
+    def backward(ctx, g_pts, g_depth):
+        lib = _lib.load()
+        depth, = ctx.saved_tensors
+        S = depth.shape[-1]
+        n = depth.numel() // S
+        dev = depth.device
+        lead = depth.shape[:-1]
+        d_ro = torch.empty((*lead, 3), device=dev) if ctx.needs_input_grad[0] else None
+        d_rd = torch.empty((*lead, 3), device=dev) if ctx.needs_input_grad[1] else None
+        if d_ro is None and d_rd is None:
+            return None, None, None, None, None, None, None, None
+        _lib.check(lib.nfi_query_points_backward(_ptr(depth), _ptr(g_pts.contiguous()), n, S, _ptr(d_ro), _ptr(d_rd),
+                                                 _stream(dev)), 'nfi_query_points_backward')
+        return d_ro, d_rd, None, None, None, None, None, None
+
+
+def compute_query_points_from_rays(ray_origins: torch.Tensor, ray_directions: torch.Tensor,
+                                   near_thresh: torch.Tensor, far_thresh: torch.Tensor, num_samples: int,
+                                   randomize: bool = True, *, u: Optional[torch.Tensor] = None,
+                                   seed: Optional[int] = None):
+    """nerf_utils.py:96-122 -> (query_points [..., S, 3], depth_values [..., S]) for rays [..., 3] and
+    per-ray near / far [...].  randomize: stratified jitter u (far - near) / S with u [..., S] given
+    (the reference's torch.rand_like draws) or from a Philox stream (`seed`; with the fused render's
+    seed this is the stream its coarse samples draw).  Gradients to the rays (near / far: none)."""
+    _require_device(ray_origins, ray_directions, near_thresh, far_thresh, u)
+    lead = ray_origins.shape[:-1]
+    if (ray_directions.shape != ray_origins.shape or near_thresh.shape != lead or far_thresh.shape != lead
+            or ray_origins.shape[-1] != 3):
+        raise ValueError('ray_origins / ray_directions [..., 3] and near_thresh / far_thresh [...] expected')
+    if near_thresh.requires_grad or far_thresh.requires_grad:
+        raise NotImplementedError('nfi.stages.compute_query_points_from_rays: no gradient to near / far '
+                                  '(the reference passes detached planes, run.py:197-200)')
+    S = int(num_samples)
+    if u is not None and u.shape != (*lead, S):
+        raise ValueError(f'u must be {(*lead, S)}')
+    if seed is None:
+        seed = 0 if (not randomize or u is not None) else int(torch.randint(0, 2 ** 62, (1,)).item())
+    return _QueryPoints.apply(ray_origins, ray_directions, near_thresh.detach(), far_thresh.detach(), S,
+                              bool(randomize), None if u is None else u.detach(), int(seed))
+
+
+class _VolumeWeights(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, sigma, rd, t):
+        lib = _lib.load()
+        N = sigma.shape[-1]
+        n = sigma.numel() // N
+        dev = sigma.device
+        sig_c, rd_c, t_c = sigma.contiguous(), rd.contiguous(), t.contiguous()
+        w = torch.empty_like(sig_c)
+        _lib.check(lib.nfi_volume_weights_forward(_ptr(sig_c), _ptr(rd_c), _ptr(t_c), n, N, _ptr(w), _stream(dev)),
+                   'nfi_volume_weights_forward')
+        ctx.save_for_backward(sig_c, rd_c, t_c)
+        return w
+
+    @staticmethod
+    def backward(ctx, g_w):
+        lib = _lib.load()
+        sigma, rd, t = ctx.saved_tensors
+        N = sigma.shape[-1]
+        n = sigma.numel() // N
+        dev = sigma.device
+        d_sigma = torch.empty_like(sigma)
+        d_rd = torch.empty_like(rd) if ctx.needs_input_grad[1] else None
+        d_t = torch.empty_like(t) if ctx.needs_input_grad[2] else None
+        _lib.check(lib.nfi_volume_weights_backward(_ptr(sigma), _ptr(rd), _ptr(t), n, N, _ptr(g_w.contiguous()),
+                                                   _ptr(d_sigma), _ptr(d_rd), _ptr(d_t), _stream(dev)),
+                   'nfi_volume_weights_backward')
+        return d_sigma, d_rd, d_t
+
+
+def render_volume_density_weights_only(sigma_a: torch.Tensor, ray_origins: torch.Tensor,
+                                       ray_directions: torch.Tensor, depth_values: torch.Tensor) -> torch.Tensor:
+    """nerf_utils.py:166-182 -> weights [..., N] = alpha * cumprod_exclusive(1 - alpha + 1e-10) of
+    sigma_a [..., N] at depth_values [..., N] (distances scaled by ||ray_directions||; ray_origins is not
+    used, as in the reference).  One HIP launch each way (fp64 transmittance scan)."""
+    _require_device(sigma_a, ray_directions, depth_values)
+    lead = sigma_a.shape[:-1]
+    if depth_values.shape != sigma_a.shape or ray_directions.shape != (*lead, 3):
+        raise ValueError('sigma_a [..., N], ray_directions [..., 3], depth_values [..., N] expected')
+    if sigma_a.shape[-1] > 1024:
+        raise ValueError('render_volume_density_weights_only: at most 1024 samples per ray')
+    return _VolumeWeights.apply(sigma_a, ray_directions, depth_values)
 
 
 def compute_near_far_planes(ray_origins: torch.Tensor, ray_directions: torch.Tensor, scene_range: float):
@@ -204,15 +408,17 @@ def make_sampler(field, scene_range: Optional[float] = None):
     [B, N, 1], 'semantics' [B, N, 10] (softmax of the logits), 'normals' [B, ..., 3] (normalised
     d distance / d x_in, computed through the HIP backward; needs grad mode, :599-622) and
     'coords' (x_in).  scene_range defaults to nfi.configure()'s."""
-    from .render import get_config
+    from .render import MAX_ATTENTION, _check_frozen, attention_padded, get_config
     if field.viewdir_mapper is not None:
         raise NotImplementedError('the view-direction closure needs per-ray inputs: use render()')
     sr = float(scene_range if scene_range is not None else get_config().scene_range)
     heads = ((HEAD_RGB_SIGMOID if field.attention_values == 0 else 0)
              | (0 if field.use_sdf else HEAD_NERF_DENSITY))
     planes_tm = planes_texel_major(field.planes)
-    dec = pack_decoder(field.w1, field.b1, field.w2, field.b2)
-    palette = field.palette if field.attention_values else None
+    w2, b2, pal_padded = attention_padded(field)     # 1..9 attention values: padded to the kernels' 10
+    nattn = int(field.attention_values)
+    dec = pack_decoder(field.w1, field.b1, w2, b2)
+    palette = pal_padded if nattn else None
     inv_alpha = 1.0 / float(field.alpha) if field.use_sdf else 1.0
     beta = float(field.beta) if field.use_sdf else 0.1
 
@@ -220,6 +426,8 @@ def make_sampler(field, scene_range: Optional[float] = None):
         for o in request_sampler_outputs:
             assert o in SAMPLER_OUTPUTS, o
         _require_device(x_in)
+        # the packed decoder carries no gradient: a trainable decoder raises, as in render()
+        _check_frozen(field)
         out = {}
         bs = x_in.shape[0]
         normals = 'normals' in request_sampler_outputs
@@ -243,7 +451,7 @@ def make_sampler(field, scene_range: Optional[float] = None):
             out['coords'] = x_in
         if 'semantics' in request_sampler_outputs:
             assert field.attention_values > 0
-            out['semantics'] = torch.softmax(y[..., 1:11], dim=-1)
+            out['semantics'] = torch.softmax(y[..., 1:1 + nattn], dim=-1)
         if 'rgb' in request_sampler_outputs:
             out['rgb'] = rgb
         return out

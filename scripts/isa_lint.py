@@ -1,0 +1,209 @@
+"""ISA lint over the gfx950 code of nfi's HIP sources (CPU only; hipcc cross-compiles).
+
+Rule ("LDS rows written with kept-alive 32-bit stores"): a wide LDS store
+(ds_write_b64 / b96 / b128, ds_write2_b32 / b64 and their st64 forms) reads its data VGPRs after
+issue; an instruction that WRITES one of those VGPRs within WINDOW wait states after the store (one per
+instruction, N + 1 for an s_nop N) can race with that read.  hipcc's hazard recognizer pads this for VMEM / FLAT stores wider than 8 bytes
+but models no DS data hazard, and it does not look inside inline asm at all.  The lint lists every
+wide DS store whose data registers are rewritten within WINDOW instructions (straight-line order;
+labels do not stop the scan, an unconditional branch or s_endpgm does), says whether the writer sits
+inside an inline-asm block (;;#ASMSTART .. ;;#ASMEND), and exits 1 if any is found.
+Rule 2 (lint_gpr_idx): the M0-indexed register-image regions of the tile pass.
+
+Usage: python scripts/isa_lint.py [--window N] [--keep DIR] [source.hip ...]
+(default: every nfi_*.hip in nerf-from-image_amd/csrc, compiled exactly as nfi/build.py compiles them,
+with --cuda-device-only -S: the assembler text of the code object the product library carries).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, 'nerf-from-image_amd', 'csrc')
+sys.path.insert(0, os.path.join(ROOT, 'nerf-from-image_amd'))
+
+WIDE_DS = re.compile(r'^\s*(ds_write(?:_b64|_b96|_b128|2_b32|2_b64|2st64_b32|2st64_b64))\s+(.*)$')
+INSN = re.compile(r'^\s*([a-z_][a-z0-9_]*)(?:\s+(.*))?$')
+VREG = re.compile(r'\bv(\d+)\b|\bv\[(\d+):(\d+)\]')
+# instructions whose first operand is NOT a VGPR destination
+NO_VDST = re.compile(r'^(ds_write|ds_store|global_store|buffer_store|flat_store|scratch_store|s_|v_cmp_|v_cmpx_|'
+                     r'v_readlane|v_readfirstlane|ds_add_|ds_min_|ds_max_|ds_and_|ds_or_|ds_xor_|ds_inc_|'
+                     r'ds_dec_|ds_cmpst|ds_nop|exp\b|buffer_wbl2|buffer_inv|global_atomic|buffer_atomic)')
+STOP = re.compile(r'^\s*(s_branch|s_endpgm|s_setpc_b64)\b')
+
+
+def regs(text: str) -> set[int]:
+    out = set()
+    for m in VREG.finditer(text):
+        if m.group(1) is not None:
+            out.add(int(m.group(1)))
+        else:
+            out.update(range(int(m.group(2)), int(m.group(3)) + 1))
+    return out
+
+
+def split_ops(s: str) -> list[str]:
+    ops, depth, cur = [], 0, ''
+    for ch in s:
+        if ch == '[':
+            depth += 1
+        elif ch == ']':
+            depth -= 1
+        if ch == ',' and depth == 0:
+            ops.append(cur.strip())
+            cur = ''
+        else:
+            cur += ch
+    if cur.strip():
+        ops.append(cur.strip())
+    return ops
+
+
+def vdst(mnem: str, rest: str) -> set[int]:
+    """VGPRs an instruction writes (its first operand, for the opcodes that have a VGPR destination)."""
+    if NO_VDST.match(mnem) or not rest:
+        return set()
+    if mnem.startswith('ds_') and ('_rtn' not in mnem and not mnem.startswith(('ds_read', 'ds_load', 'ds_bpermute',
+                                                                              'ds_permute', 'ds_swizzle'))):
+        return set()
+    first = split_ops(rest)[0]
+    return regs(first) if first.startswith('v') else set()
+
+
+def lint_asm(path: str, window: int):
+    findings = []
+    kernel = None
+    lines = open(path).read().splitlines()
+    in_asm = [False] * len(lines)
+    state = False
+    for i, ln in enumerate(lines):
+        if ';;#ASMSTART' in ln:
+            state = True
+        elif ';;#ASMEND' in ln:
+            state = False
+        in_asm[i] = state
+    loc = None
+    files = {}
+    for i, ln in enumerate(lines):
+        if re.match(r'^_Z\S+:', ln):
+            kernel = ln.split(':')[0]
+        fm = re.match(r'^\s*\.file\s+(\d+)\s+"([^"]*)"(?:\s+"([^"]*)")?', ln)
+        if fm:
+            files[fm.group(1)] = os.path.basename(fm.group(3) or fm.group(2))
+        lm = re.match(r'^\s*\.loc\s+(\d+)\s+(\d+)', ln)
+        if lm:
+            loc = f"{files.get(lm.group(1), lm.group(1))}:{lm.group(2)}"
+        m = WIDE_DS.match(ln)
+        if not m:
+            continue
+        ops = split_ops(m.group(2))
+        data = set()
+        for op in ops[1:]:
+            if op.startswith('v'):
+                data |= regs(op)
+        if m.group(1) in ('ds_write_b64',) and not data:
+            continue
+        n = 0
+        j = i + 1
+        while j < len(lines) and n < window:
+            t = lines[j].split(';')[0].rstrip()
+            j += 1
+            if not t.strip() or t.strip().endswith(':') or t.strip().startswith('.'):
+                continue
+            im = INSN.match(t)
+            if not im:
+                continue
+            w = vdst(im.group(1), im.group(2) or '') & data
+            n += 1
+            if im.group(1) == 's_nop':   # s_nop N = N + 1 wait states
+                n += int((im.group(2) or '0').strip(), 0)
+            if w:
+                findings.append({'kernel': kernel, 'line': i + 1, 'src': loc, 'store': ln.strip(), 'writer_line': j,
+                                 'writer': t.strip(), 'distance': n, 'writer_in_inline_asm': in_asm[j - 1],
+                                 'store_in_inline_asm': in_asm[i]})
+                break
+            if STOP.match(t):
+                break
+    return findings
+
+
+def lint_gpr_idx(path: str):
+    """Rule 2 (the tile pass's register image, nfi_render.hip img_add): every M0-indexed region
+    (s_set_gpr_idx_on .. s_set_gpr_idx_off) holds only 32-bit v_add_f32 on the pinned image base
+    v40 / v41 (no packed or 64-bit operand: an odd index would address an unaligned VGPR pair), and
+    its index SGPR was clamped to <= 30 by an s_min just before (v40 + 31 + 1 = v72 is outside the
+    image), so no index reaches past v71."""
+    bad = []
+    lines = open(path).read().splitlines()
+    kernel = None
+    for i, ln in enumerate(lines):
+        if re.match(r'^_Z\S+:', ln):
+            kernel = ln.split(':')[0]
+        m = re.match(r'^\s*s_set_gpr_idx_on\s+(s\d+)', ln)
+        if not m:
+            continue
+        idx = m.group(1)
+        prev = [x.split(';')[0].strip() for x in lines[max(0, i - 12):i]]
+        prev = [x for x in prev if x and not x.startswith('.') and not x.endswith(':')]
+        if not any(re.match(rf's_min_[iu]32\s+{idx},\s*{idx},\s*30$', x) or
+                   re.match(rf's_min_[iu]32\s+{idx},\s*s\d+,\s*30$', x) for x in prev):
+            bad.append((kernel, i + 1, f'index {idx} not clamped to 30 before the region'))
+        j = i + 1
+        while j < len(lines) and 's_set_gpr_idx_off' not in lines[j]:
+            t = lines[j].split(';')[0].strip()
+            j += 1
+            if not t or t.startswith('.'):
+                continue
+            if not re.match(r'v_add_f32(_e32)?\s+v4[01],\s*v4[01],\s*v\d+$', t):
+                bad.append((kernel, j, f'unexpected instruction in an indexed region: {t}'))
+    return bad
+
+
+def compile_asm(src: str, out: str, extra=()):
+    from nfi.build import FLAGS
+    flags = [f for f in FLAGS if f not in ('-shared', '-fPIC')]
+    cmd = [os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')] + flags + ['-w', '-gline-tables-only', '--cuda-device-only', '-S', '-o', out,
+                                                                     src] + list(extra)
+    subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--window', type=int, default=2)
+    ap.add_argument('--keep', default=None, help='directory to keep the .s files in')
+    ap.add_argument('-D', action='append', default=[], help='extra -D defines (a variant build)')
+    ap.add_argument('sources', nargs='*')
+    a = ap.parse_args()
+    srcs = a.sources or [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith('.hip')]
+    tmp = a.keep or tempfile.mkdtemp(prefix='nfi_isa_')
+    os.makedirs(tmp, exist_ok=True)
+    total = []
+    for s in srcs:
+        out = os.path.join(tmp, os.path.basename(s).replace('.hip', '.s'))
+        compile_asm(s, out, ['-D' + d for d in a.D])
+        f = lint_asm(out, a.window)
+        nstores = sum(1 for ln in open(out) if WIDE_DS.match(ln))
+        print(f'{os.path.basename(s)}: {nstores} wide DS stores, {len(f)} with a data VGPR rewritten within '
+              f'{a.window} instructions')
+        for x in f:
+            print(f"  {x['kernel'][:70]}  line {x['line']} ({x['src']}): {x['store']}\n"
+                  f"      -> +{x['distance']} {x['writer']}"
+                  f"{'  [writer inside inline asm]' if x['writer_in_inline_asm'] else ''}")
+        total += f
+        g = lint_gpr_idx(out)
+        nreg = sum(1 for ln in open(out) if 's_set_gpr_idx_on' in ln)
+        print(f'{os.path.basename(s)}: {nreg} M0-indexed regions, {len(g)} violations')
+        for k, ln, msg in g:
+            print(f'  {k[:70]}  line {ln}: {msg}')
+        total += g
+    print('isa lint:', 'FAIL' if total else 'ok')
+    return 1 if total else 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

@@ -9,7 +9,9 @@ and expected outputs/gradients of
                 TriplanarDecoder (F.grid_sample), Laplace density, softmax colour head,
                 nerf_utils ray bundle / near-far / stratified sampling / sample_pdf /
                 compositing are all the reference's code;
-  * per-stage nerf_utils functions (compute_near_far_planes, sample_pdf, get_ray_bundle).
+  * per-stage nerf_utils functions (compute_near_far_planes, sample_pdf; seams.npz:
+    cumprod_exclusive, get_ray_bundle, compute_query_points_from_rays,
+    render_volume_density_weights_only in fp32 and fp64 with input gradients).
   * the producer: the reference Generator (mapping network, StyleGAN2
     synthesis network, AttentionMapper) at full size with seeded weights (golden_io.load_seeded,
     so no weights are stored), sampled planes + checksums, palette, and the latent gradient;
@@ -108,7 +110,7 @@ def render_case(name, seed, b, H, W, S, R, scene_range, white_bg, flipped, rando
                         else 0.2 * r if k.endswith('bias') else r)
     planes = (1.87 * torch.randn(b, 3, 32, R, R)).requires_grad_()
     gen.synthesis_network = PlanesLeaf(planes)
-    palette = generator.wide_sigmoid_rescaled(torch.randn(b, 10, 3)).detach().requires_grad_()
+    palette = generator.wide_sigmoid_rescaled(torch.randn(b, attention_values or 10, 3)).detach().requires_grad_()
     cam, focal = make_cameras(b, scene_range, flipped, seed, ortho=ortho)
     if inside:
         # nerf_utils.py:264-270: image 0's camera sits INSIDE the scene box (0.6 scene_range from
@@ -269,6 +271,111 @@ def stage_cases():
                         pdf_bins=bins.numpy(), pdf_w=w.numpy(), pdf_det=det.numpy(),
                         pdf_u=u.numpy(), pdf_rnd=rnd.numpy())
     print('stages written')
+
+
+def seam_cases():
+    """The remaining nerf_utils seams as functions of their own (cumprod_exclusive :20-25,
+    get_ray_bundle :28-93, compute_query_points_from_rays :96-122,
+    render_volume_density_weights_only :166-182): outputs and input gradients in fp32 AND fp64 (the
+    reference functions evaluated on double tensors), so the GPU tests can apply the 4x rule."""
+    g = torch.Generator().manual_seed(321)
+    out = {}
+
+    def both(fn, inputs, grads):
+        """outputs + VJPs of fn at fp32 and fp64 inputs (requires_grad where grads says)."""
+        res = {}
+        for dt, tag in ((torch.float32, '32'), (torch.float64, '64')):
+            xs = [x.to(dt).clone().requires_grad_(rg) if x is not None else None for x, rg in inputs]
+            ys = fn(*xs)
+            ys = ys if isinstance(ys, tuple) else (ys,)
+            loss = sum((y * gg.to(dt)).sum() for y, gg in zip(ys, grads) if gg is not None)
+            loss.backward()
+            res[tag] = ([y.detach().numpy() for y in ys],
+                        [x.grad.numpy() if (x is not None and x.requires_grad) else None for x in xs])
+        return res
+
+    # cumprod_exclusive on rows with exact zeros / ones and long rows (several 64-lanes chunks)
+    x = torch.rand(48, 150, generator=g) * 0.5 + 0.5
+    x[:4, 10] = 0.0
+    x[4:8, 70:] = 1.0
+    x[8:12, -1] = 0.0                                      # the unused last input
+    gx = torch.randn(48, 150, generator=g)
+    r = both(nerf_utils.cumprod_exclusive, [(x, True)], [gx])
+    out.update(cp_x=x.numpy(), cp_g=gx.numpy(), cp_out32=r['32'][0][0], cp_out64=r['64'][0][0],
+               cp_dx32=r['32'][1][0], cp_dx64=r['64'][1][0])
+    # get_ray_bundle: perspective, perspective + center + bbox, ortho + bbox
+    B, H, W = 2, 6, 8
+    for tag, persp, ctr, bb in (('p', True, False, False), ('pcb', True, True, True), ('ob', False, False, True)):
+        cam = torch.eye(4).repeat(B, 1, 1)
+        cam[:, :3, :3] = torch.linalg.qr(torch.randn(B, 3, 3, generator=g))[0]
+        cam[:, :3, 3] = torch.randn(B, 3, generator=g) * 3
+        if not persp:
+            cam[:, 3, 3] = 0.5 + torch.rand(B, generator=g)
+        focal = (1.5 + torch.rand(B, generator=g)) if persp else None
+        center = torch.rand(B, 2, generator=g) if ctr else None
+        bbox = (torch.rand(B, 2, 2, generator=g) - 0.5) if bb else None
+        gro, grd = torch.randn(B, H, W, 3, generator=g), torch.randn(B, H, W, 3, generator=g)
+
+        def fn(c, f, ce, bx):
+            return nerf_utils.get_ray_bundle(H, W, f, c, bx, ce)
+        r = both(fn, [(cam, True), (focal, persp), (center, False), (bbox, False)], [gro, grd])
+        out.update({f'rb{tag}_cam': cam.numpy(), f'rb{tag}_gro': gro.numpy(), f'rb{tag}_grd': grd.numpy(),
+                    f'rb{tag}_ro32': r['32'][0][0], f'rb{tag}_rd32': r['32'][0][1],
+                    f'rb{tag}_ro64': r['64'][0][0], f'rb{tag}_rd64': r['64'][0][1],
+                    f'rb{tag}_dcam32': r['32'][1][0], f'rb{tag}_dcam64': r['64'][1][0]})
+        if persp:
+            out.update({f'rb{tag}_focal': focal.numpy(), f'rb{tag}_dfocal32': r['32'][1][1],
+                        f'rb{tag}_dfocal64': r['64'][1][1]})
+        if ctr:
+            out[f'rb{tag}_center'] = center.numpy()
+        if bb:
+            out[f'rb{tag}_bbox'] = bbox.numpy()
+    # compute_query_points_from_rays: deterministic, and randomized with the draws recovered
+    ro = torch.randn(2, 4, 5, 3, generator=g)
+    rd = F.normalize(torch.randn(2, 4, 5, 3, generator=g), dim=-1)
+    near = 0.5 + torch.rand(2, 4, 5, generator=g)
+    far = near + 0.2 + 2 * torch.rand(2, 4, 5, generator=g)
+    S = 20
+    gp = torch.randn(2, 4, 5, S, 3, generator=g)
+    for tag, rnd in (('d', False), ('r', True)):
+        res = {}
+        o, d = ro.clone().requires_grad_(), rd.clone().requires_grad_()
+        torch.manual_seed(77)
+        pts, depth = nerf_utils.compute_query_points_from_rays(o, d, near, far, S, randomize=rnd)
+        (pts * gp).sum().backward()
+        res['32'] = (pts.detach().numpy(), depth.detach().numpy(), o.grad.numpy(), d.grad.numpy())
+        # fp64 truth (the reference's lerp rejects double inputs with its float arange weight): the same
+        # depths in double, points and gradients of p = ro + rd t evaluated in fp64
+        o64, d64 = ro.double().requires_grad_(), rd.double().requires_grad_()
+        t64 = depth.detach().double()
+        p64 = o64[..., None, :] + d64[..., None, :] * t64[..., :, None]
+        (p64 * gp.double()).sum().backward()
+        res['64'] = (p64.detach().numpy(), t64.numpy(), o64.grad.numpy(), d64.grad.numpy())
+        torch.manual_seed(77)
+        u = torch.rand(2, 4, 5, S)                       # rand_like(depth_values): the same draws
+        out.update({f'qp{tag}_pts32': res['32'][0], f'qp{tag}_depth32': res['32'][1],
+                    f'qp{tag}_dro32': res['32'][2], f'qp{tag}_drd32': res['32'][3],
+                    f'qp{tag}_pts64': res['64'][0], f'qp{tag}_depth64': res['64'][1],
+                    f'qp{tag}_dro64': res['64'][2], f'qp{tag}_drd64': res['64'][3], f'qp{tag}_u': u.numpy()})
+    out.update(qp_ro=ro.numpy(), qp_rd=rd.numpy(), qp_near=near.numpy(), qp_far=far.numpy(), qp_g=gp.numpy())
+    # render_volume_density_weights_only: densities with empty and opaque stretches
+    N = 90
+    t = torch.sort(torch.rand(2, 4, 5, N, generator=g) * 3 + 1, dim=-1)[0]
+    sig = torch.relu(torch.randn(2, 4, 5, N, generator=g) * 3)
+    sig[0, 0, :2] = 0.0                                  # empty rays
+    sig[1, 1, :, 40:] = 50.0                             # opaque tails
+    rdw = torch.randn(2, 4, 5, 3, generator=g)
+    gw = torch.randn(2, 4, 5, N, generator=g)
+
+    def wfn(sg, d, tt):
+        return nerf_utils.render_volume_density_weights_only(sg, torch.zeros_like(d), d, tt)
+    r = both(wfn, [(sig, True), (rdw, True), (t, True)], [gw])
+    out.update(vw_sigma=sig.numpy(), vw_rd=rdw.numpy(), vw_t=t.numpy(), vw_g=gw.numpy(),
+               vw_w32=r['32'][0][0], vw_w64=r['64'][0][0],
+               vw_dsigma32=r['32'][1][0], vw_drd32=r['32'][1][1], vw_dt32=r['32'][1][2],
+               vw_dsigma64=r['64'][1][0], vw_drd64=r['64'][1][1], vw_dt64=r['64'][1][2])
+    np.savez_compressed(os.path.join(OUT, 'seams.npz'), **{k: v for k, v in out.items() if v is not None})
+    print('seams written')
 
 
 def extract_function(name, ns):
@@ -451,6 +558,9 @@ def field_variant_cases():
     softplus(d - 1) (use_sdf False), and both."""
     render_case('rgbhead', 7, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=False,
                 flipped=True, randomize=True, attention_values=0)
+    # --attention_values N < 10 (generator.py:363-402, 665-679 allow any N; nfi pads to its 10)
+    render_case('attn5', 12, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=False,
+                flipped=True, randomize=True, attention_values=5)
     render_case('nerfdensity', 8, b=2, H=12, W=12, S=16, R=16, scene_range=1.4, white_bg=True,
                 flipped=True, randomize=True, use_sdf=False)
     render_case('nerf_rgbhead', 9, b=1, H=8, W=8, S=8, R=12, scene_range=0.55, white_bg=False,
@@ -488,6 +598,7 @@ if __name__ == '__main__':
     augment_cases()
     metrics_cases()
     stage_cases()
+    seam_cases()
     # p3d_car-like: perspective, flipped, black bg, pose grads, random sampling
     render_case('p3d', 0, b=2, H=16, W=16, S=16, R=16, scene_range=1.4, white_bg=False,
                 flipped=True, randomize=True)

@@ -7,7 +7,7 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 RENDER_CASES = ['p3d', 'shapenet', 'cub', 'persp_center_bbox', 'inside']
-VARIANT_CASES = ['rgbhead', 'nerfdensity', 'nerf_rgbhead']   # attention_values 0 / use_sdf False
+VARIANT_CASES = ['rgbhead', 'nerfdensity', 'nerf_rgbhead', 'attn5']   # attention_values 0 / 5, use_sdf False
 VIEWDIR_CASES = ['viewdir', 'viewdir_rgbhead']               # --use_viewdir
 ZBUFFER_CASES = ['zbuffer']        # eval_nusc_persp.py's render copy (z-buffer depth)
 EXTRAS_CASES = ['extras_ns', 'extras_nw', 'extras_coords']   # eval outputs, no gradients

@@ -60,9 +60,13 @@ def test_backward_linear_in_upstream_gradient(full):
     inp, meta = full
     a = _render(inp, meta, seed=5)
     b = _render(inp, meta, seed=5, g_scale=2.0)
-    assert torch.equal(b['d_palette'], 2 * a['d_palette'])    # deterministic reduction, exact in fp32
-    for k in ('d_planes', 'd_cam', 'd_focal'):                # float atomics: order varies
-        assert rel_l2(b[k], 2 * a[k]) < 1e-5, k
+    # fixed-order reductions, exact in fp32 (x2 is exact through every product and sum): d palette,
+    # and the pose gradients (per-entry grid gradients, per-ray sums, per-image segment sums)
+    for k in ('d_palette', 'd_cam', 'd_focal'):
+        assert torch.equal(b[k], 2 * a[k]), k
+    # d planes: the tile bins are filled by cursor atomics, so the order of a tile's entries (and the
+    # fp32 rounding of its register sums) varies run to run (determinism)
+    assert rel_l2(b['d_planes'], 2 * a['d_planes']) < 1e-5
 
 
 def test_loss_linear_in_palette(full):
@@ -88,9 +92,9 @@ def test_backward_image_halves_match(full):
         b = _render(inp, meta, seed=3)
     finally:
         ops.BACKWARD_PIPELINE = old
-    assert torch.equal(a['d_palette'], b['d_palette'])
-    for k in ('d_planes', 'd_cam', 'd_focal'):
-        assert rel_l2(b[k], a[k]) < 1e-5, k
+    for k in ('d_palette', 'd_cam', 'd_focal'):
+        assert torch.equal(a[k], b[k]), k
+    assert rel_l2(b['d_planes'], a['d_planes']) < 1e-5
 
 
 def _render_shapenet(inp, meta, sl, g_rgb, g_mask):

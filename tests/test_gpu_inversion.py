@@ -34,6 +34,27 @@ def test_inversion_trajectory_hip():
     print(f'latent distance / reference displacement: {rel:.2e}')
 
 
+def test_inversion_adam_forms_agree():
+    """The fused Adam kernel (default) against the foreach form of the reference's default Adam
+    (run.py:2007; InversionConfig.adam = 'foreach'): the same update formula rounded differently.  Both
+    trajectories follow the reference's golden one within the HIP loop's bound, and each other to a
+    small fraction of the latent displacement."""
+    dev = torch.device('cuda:0')
+    res = {}
+    for form in ('fused', 'foreach'):
+        gen, d, meta, cfg = inversion_setup(dev)
+        nfi.configure(scene_range=float(meta['scene_range']), white_background=False,
+                      fine_sampling=True, use_sdf=True, attention_values=10, use_viewdir=False)
+        cfg.adam = form
+        res[form] = inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg,
+                                     uniforms=lambda it: (d['u_coarse'][it], d['u_fine'][it]))
+        check_trajectory(res[form], d, loss_rtol=1e-4, w_rel=3e-2)
+    disp = float((res['foreach'].ws - d['w_init'].to(dev)).norm())
+    dist = float((res['fused'].ws - res['foreach'].ws).norm())
+    print(f'fused vs foreach latent distance / displacement: {dist / disp:.2e}')
+    assert dist <= 1e-2 * disp
+
+
 def test_inversion_decreases_loss_hip():
     """30 steps at 64² (Philox draws): the L1 loss goes down and the pose stays valid."""
     dev = torch.device('cuda:0')

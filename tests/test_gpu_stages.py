@@ -213,6 +213,50 @@ def test_decoder_split_precision(plane_scale, w_scale, g_scale):
         assert e_hip <= 4 * e_ref + 1e-6, k
 
 
+@pytest.mark.parametrize('spread', ['features', 'grads', 'both'])
+def test_decoder_split_wave_spread(spread):
+    """Worst case of the per-wave power-of-two scaling of the split-f16 decoder (nfi_render.hip
+    split_inputs / the dY scale): inside every 64-point wave ONE point has operands of
+    magnitude 1 and the other 63 of magnitude 2^-20 (tap features: the planes are 2^-20 except in the
+    region only the outlier samples; and/or loss gradients).  The wave's scale is set by the outlier, so
+    a small point's hi/lo pair is exact to 2^-25 of the scaled max, i.e. 2^-(39-k) of its own value at
+    2^-k below the max.  Bound: the fp64-relative 4x rule of test_decoder_split_precision over all points
+    AND over the small points alone."""
+    inp = _sampler_field(10, True, seed=41)
+    R = inp['planes'].shape[-1]
+    tiny = 2.0 ** -20
+    if spread in ('features', 'both'):
+        col = torch.arange(R).view(1, 1, 1, 1, R)
+        inp['planes'] = torch.where(col >= R // 2 + 2, inp['planes'], inp['planes'] * tiny)
+    g = torch.Generator().manual_seed(17)
+    B, P = 2, 256
+    x = torch.empty(B, P, 3)
+    small = torch.ones(B, P, dtype=torch.bool)
+    small[:, ::64] = False                                   # the outlier: lane 0 of every wave
+    u = torch.rand(B, P, 3, generator=g)
+    x[..., :2] = torch.where(small[..., None], -(0.3 + 0.6 * u[..., :2]), 0.3 + 0.6 * u[..., :2]) * 1.4
+    x[..., 2] = (u[..., 2] * 2 - 1) * 1.3
+    gs, gr, gd = torch.randn(B, P, generator=g), torch.randn(B, P, 3, generator=g), torch.randn(B, P, generator=g)
+    if spread in ('grads', 'both'):
+        sc = torch.where(small, torch.tensor(tiny), torch.tensor(1.0))
+        gs, gr, gd = gs * sc, gr * sc[..., None], gd * sc
+    hip = _sampler_run(inp, x, gs, gr, gd, torch.float32, DEV, 10, True, ('sigma', 'rgb', 'sdf_distance'))
+    r32 = _sampler_run(inp, x, gs, gr, gd, torch.float32, 'cpu', 10, True, None)
+    r64 = _sampler_run(inp, x, gs, gr, gd, torch.float64, 'cpu', 10, True, None)
+    for sel, tag in ((torch.ones_like(small), 'all'), (small, 'small')):
+        d64 = r64['dist'][sel].double()
+        e_hip = float((hip['dist'][sel].double() - d64).abs().max())
+        e_ref = float((r32['dist'][sel].double() - d64).abs().max())
+        print(f'  {spread:8s} {tag:5s} dist hip {e_hip:.3g} ref32 {e_ref:.3g} (|dist| max {float(d64.abs().max()):.3g})')
+        assert e_hip <= 4 * e_ref + 1e-6 * float(d64.abs().max()), (tag, 'dist')
+        e_hip, e_ref = rel_l2(hip['d_x'][sel], r64['d_x'][sel]), rel_l2(r32['d_x'][sel], r64['d_x'][sel])
+        print(f'  {spread:8s} {tag:5s} d_x  hip {e_hip:.3g} ref32 {e_ref:.3g}')
+        assert e_hip <= 4 * e_ref + 1e-6, (tag, 'd_x')
+    e_hip, e_ref = rel_l2(hip['d_planes'], r64['d_planes']), rel_l2(r32['d_planes'], r64['d_planes'])
+    print(f'  {spread:8s} all   d_planes hip {e_hip:.3g} ref32 {e_ref:.3g}')
+    assert e_hip <= 4 * e_ref + 1e-6
+
+
 @pytest.mark.parametrize('case', ['render_p3d', 'render_shapenet'])
 def test_forward_decoder_outputs(case):
     """The decoder inside the fused forward, sample by sample: the decoder outputs the forward saves
@@ -243,3 +287,106 @@ def test_forward_decoder_outputs(case):
     rel = float(((y_saved - y64).abs() / den).max())
     print(f'  max |y - y64| / sum|terms| = {rel:.3g}')
     assert rel < 2e-6
+
+
+# ---- the remaining nerf_utils seams (ABI 15), against the reference's own fixture (seams.npz:
+# fp32 = the reference functions, fp64 = the same functions on double inputs) -------------------
+
+def _g64(d, key):
+    return d[key].double()
+
+
+def test_seam_cumprod_exclusive():
+    """nerf_utils.py:20-25 on rows of 150 (three 64-lane chunks) with exact zeros, a run of ones and a
+    zero in the unused last input: forward equal to the reference's fp32 cumprod to one ulp (the fp64
+    product is carried in a different association), d x by the 4x rule against fp64."""
+    d, _ = load('seams')
+    x = d['cp_x'].to(DEV).requires_grad_()
+    out = stages.cumprod_exclusive(x)
+    (out * d['cp_g'].to(DEV)).sum().backward()
+    ref = d['cp_out32']
+    ulp = (ref.abs().clamp_min(1e-30) * 2.0 ** -23)
+    assert float(((out.detach().cpu() - ref).abs() / ulp).max()) <= 1.0
+    assert bool((out[:, 0] == 1).all())
+    _bound('cp_out', out.detach().cpu(), ref, _g64(d, 'cp_out64'), 1e-7, elementwise=True)
+    _bound('cp_dx', x.grad.cpu(), d['cp_dx32'], _g64(d, 'cp_dx64'), 1e-6)
+    assert bool((x.grad[:, -1] == 0).all())
+
+
+@pytest.mark.parametrize('tag', ['p', 'pcb', 'ob'])
+def test_seam_get_ray_bundle(tag):
+    """nerf_utils.py:28-93 alone (directions NOT normalised): perspective, perspective + center + bbox,
+    ortho + bbox.  Rays bit for bit (ATen's rounding order); d cam / d focal by the 4x rule."""
+    d, _ = load('seams')
+    B, H, W = 2, 6, 8
+    cam = d[f'rb{tag}_cam'].to(DEV).requires_grad_()
+    focal = d[f'rb{tag}_focal'].to(DEV).requires_grad_() if f'rb{tag}_focal' in d else None
+    center = d[f'rb{tag}_center'].to(DEV) if f'rb{tag}_center' in d else None
+    bbox = d[f'rb{tag}_bbox'].to(DEV) if f'rb{tag}_bbox' in d else None
+    ro, rd = stages.get_ray_bundle(H, W, focal, cam, bbox, center)
+    assert ro.shape == (B, H, W, 3) and rd.shape == (B, H, W, 3)
+    assert torch.equal(ro.detach().cpu(), d[f'rb{tag}_ro32'])
+    assert torch.equal(rd.detach().cpu(), d[f'rb{tag}_rd32'])
+    ((ro * d[f'rb{tag}_gro'].to(DEV)).sum() + (rd * d[f'rb{tag}_grd'].to(DEV)).sum()).backward()
+    _bound('d_cam', cam.grad.cpu(), d[f'rb{tag}_dcam32'], _g64(d, f'rb{tag}_dcam64'), 1e-5)
+    if focal is not None:
+        _bound('d_focal', focal.grad.cpu(), d[f'rb{tag}_dfocal32'], _g64(d, f'rb{tag}_dfocal64'), 1e-5)
+
+
+@pytest.mark.parametrize('tag', ['d', 'r'])
+def test_seam_query_points(tag):
+    """nerf_utils.py:96-122: stratified depths and points bit for bit against the reference
+    (deterministic, and randomized with its torch.rand_like draws injected); d ro / d rd (the depth
+    values carry no gradient) by the 4x rule; a Philox-drawn call reproduces the fused render's coarse
+    depths for the same seed."""
+    d, _ = load('seams')
+    ro, rd = d['qp_ro'].to(DEV).requires_grad_(), d['qp_rd'].to(DEV).requires_grad_()
+    near, far = d['qp_near'].to(DEV), d['qp_far'].to(DEV)
+    S = d[f'qp{tag}_u'].shape[-1]
+    u = d[f'qp{tag}_u'].to(DEV) if tag == 'r' else None
+    pts, depth = stages.compute_query_points_from_rays(ro, rd, near, far, S, randomize=(tag == 'r'), u=u)
+    assert torch.equal(depth.cpu(), d[f'qp{tag}_depth32'])
+    assert torch.equal(pts.detach().cpu(), d[f'qp{tag}_pts32'])
+    (pts * d['qp_g'].to(DEV)).sum().backward()
+    _bound('d_ro', ro.grad.cpu(), d[f'qp{tag}_dro32'], _g64(d, f'qp{tag}_dro64'), 1e-6)
+    _bound('d_rd', rd.grad.cpu(), d[f'qp{tag}_drd32'], _g64(d, f'qp{tag}_drd64'), 1e-6)
+    if tag == 'r':
+        # Philox: repeatable per seed, inside each stratum
+        a = stages.compute_query_points_from_rays(ro.detach(), rd.detach(), near, far, S, seed=11)[1]
+        b = stages.compute_query_points_from_rays(ro.detach(), rd.detach(), near, far, S, seed=11)[1]
+        assert torch.equal(a, b)
+        lo = stages.compute_query_points_from_rays(ro.detach(), rd.detach(), near, far, S, randomize=False)[1]
+        step = ((far - near) / S)[..., None]
+        assert bool(((a >= lo - 1e-6) & (a <= lo + step * (1 + 1e-5) + 1e-6)).all())
+
+
+def test_seam_query_points_match_fused_render_draws():
+    """The seam's Philox stream is the fused render's coarse stream: same seed, same depths."""
+    from gpu_helpers import synthetic_inputs
+    inp, meta = synthetic_inputs(B=1, H=8, W=8, S=16, R=16, scene_range=1.4, seed=3)
+    nfi.configure(scene_range=1.4)
+    f = nfi.TriplaneField(planes=inp['planes'].to(DEV), palette=inp['palette'].to(DEV), w1=inp['w1'].to(DEV),
+                          b1=inp['b1'].to(DEV), w2=inp['w2'].to(DEV), b2=inp['b2'].to(DEV), alpha=1.0, beta=0.1)
+    dbg = {}
+    cam, focal = inp['cam'].to(DEV), inp['focal'].to(DEV)
+    with torch.no_grad():
+        nfi.render(f, 8, 8, cam, focal, None, None, None, 16, randomize=True, seed=1234, debug=dbg)
+        from nfi import ops
+        ro, rd, near, far = ops.rays(cam, focal, None, None, 8, 8, 1.4)   # the render's own rays
+        depth = stages.compute_query_points_from_rays(ro, rd, near, far, 16, seed=1234)[1]
+    assert torch.equal(depth.reshape(-1, 16), dbg['z_coarse'].reshape(-1, 16))
+
+
+def test_seam_volume_weights():
+    """nerf_utils.py:166-182 on rays of 90 samples (empty rays, opaque tails, non-unit directions):
+    weights, and the gradients to sigma, the directions (through ||rd||) and the depths, by the
+    4x rule against the reference in fp64."""
+    d, _ = load('seams')
+    sig = d['vw_sigma'].to(DEV).requires_grad_()
+    rdw = d['vw_rd'].to(DEV).requires_grad_()
+    t = d['vw_t'].to(DEV).requires_grad_()
+    w = stages.render_volume_density_weights_only(sig, torch.zeros_like(rdw), rdw, t)
+    _bound('weights', w.detach().cpu(), d['vw_w32'], _g64(d, 'vw_w64'), 2e-6, elementwise=True)
+    (w * d['vw_g'].to(DEV)).sum().backward()
+    for k, x in (('dsigma', sig), ('drd', rdw), ('dt', t)):
+        _bound(k, x.grad.cpu(), d[f'vw_{k}32'], _g64(d, f'vw_{k}64'), 1e-5)

@@ -87,3 +87,45 @@ def test_oracle_eval_outputs_match_reference(case):
         torch.testing.assert_close(smap.detach(), d['semantics'], **tol)
     else:
         assert smap is None
+
+
+def test_oracle_seams():
+    """The oracle's restatements of the nerf_utils seams (cumprod_exclusive, get_ray_bundle,
+    compute_query_points_from_rays, render_volume_density_weights_only) against the reference's
+    own outputs and input gradients (tests/golden/seams.npz, fp32): the same op graphs, so equal
+    to fp32 rounding (in practice bit for bit)."""
+    d, _ = load('seams')
+
+    def close(a, b, tol=1e-6):
+        torch.testing.assert_close(a.detach(), b, rtol=tol, atol=tol)
+
+    x = d['cp_x'].clone().requires_grad_()
+    out = orc.cumprod_exclusive(x)
+    (out * d['cp_g']).sum().backward()
+    close(out, d['cp_out32'])
+    close(x.grad, d['cp_dx32'], 1e-5)
+    for tag in ('p', 'pcb', 'ob'):
+        cam = d[f'rb{tag}_cam'].clone().requires_grad_()
+        focal = d[f'rb{tag}_focal'].clone().requires_grad_() if f'rb{tag}_focal' in d else None
+        ro, rd = orc.get_ray_bundle(6, 8, focal, cam, d.get(f'rb{tag}_bbox'), d.get(f'rb{tag}_center'))
+        assert torch.equal(ro.detach(), d[f'rb{tag}_ro32']) and torch.equal(rd.detach(), d[f'rb{tag}_rd32'])
+        ((ro * d[f'rb{tag}_gro']).sum() + (rd * d[f'rb{tag}_grd']).sum()).backward()
+        close(cam.grad, d[f'rb{tag}_dcam32'], 1e-5)
+        if focal is not None:
+            close(focal.grad, d[f'rb{tag}_dfocal32'], 1e-5)
+    for tag in ('d', 'r'):
+        ro, rd = d['qp_ro'].clone().requires_grad_(), d['qp_rd'].clone().requires_grad_()
+        S = d[f'qp{tag}_u'].shape[-1]
+        pts, depth = orc.compute_query_points_from_rays(ro, rd, d['qp_near'], d['qp_far'], S, randomize=tag == 'r',
+                                                        u=d[f'qp{tag}_u'])
+        assert torch.equal(depth, d[f'qp{tag}_depth32']) and torch.equal(pts.detach(), d[f'qp{tag}_pts32'])
+        (pts * d['qp_g']).sum().backward()
+        close(ro.grad, d[f'qp{tag}_dro32'], 1e-5)
+        close(rd.grad, d[f'qp{tag}_drd32'], 1e-5)
+    sig, rdw, t = (d[k].clone().requires_grad_() for k in ('vw_sigma', 'vw_rd', 'vw_t'))
+    w = orc.render_volume_density_weights_only(sig, torch.zeros_like(rdw), rdw, t)
+    close(w, d['vw_w32'])
+    (w * d['vw_g']).sum().backward()
+    close(sig.grad, d['vw_dsigma32'], 1e-5)
+    close(rdw.grad, d['vw_drd32'], 1e-5)
+    close(t.grad, d['vw_dt32'], 1e-5)
