@@ -207,6 +207,28 @@ int32_t nfi_aug_sample_forward(const float* img, const float* grid, float* out, 
 int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gimg, int32_t B, int32_t K, int32_t H,
                                 int32_t W, int32_t Ho, int32_t Wo, void* stream);
 
+/* ---- Split-f16 batched GEMM (csrc/nfi_gemm.hip): C[b] = A[b] . B[b] in fp32 on the f16 matrix cores
+ * (v_mfma_f32_16x16x32_f16), each fp32 operand a power-of-two-scaled hi + lo fp16 pair and each
+ * product lo.hi + hi.lo + hi.hi on an fp32 accumulator (fp32-level error).  Replaces the
+ * torch.bmm (hipBLASLt fp32) of the Winograd products of the 3x3 convolutions (stylegan.py:130-145,
+ * lpips VGG16 via metrics.py:107).
+ * nfi_split16_pack: A [batch][per] -> hi, lo [batch][per] (fp16 bits) and a_inv [batch] = 2^-e, with
+ *   the largest |A[b]| 2^e in [2^14, 2^15) (one workgroup per batch entry; frozen operands: once).
+ * nfi_wino_input_transform_max: nfi_wino_input_transform_scaled (scale may be NULL) or, with relu_y,
+ *   the ReLU-masked gradient transform, also leaving the running maximum of |V| in vmax[64] (float
+ *   bits; zeroed by the call).
+ * nfi_absmax_slots: the same running maximum of any x [n] (zeroes slots[64] first).
+ * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max[64] from one of the above,
+ *   C [batch][M][N] fp32 (written); K a multiple of 32. */
+int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* Ah, uint16_t* Al, float* a_inv,
+                         void* stream);
+int32_t nfi_wino_input_transform_max(const float* x, const float* scale, const float* relu_y, float* V,
+                                     uint32_t* vmax, int32_t N, int32_t C, int32_t H, int32_t W, void* stream);
+int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* stream);
+int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                         const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

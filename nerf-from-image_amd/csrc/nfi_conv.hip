@@ -139,12 +139,17 @@ __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ w
 // grid (ceil(P / 256), C).  scale (optional, [N][C]): the transform of x * scale[n][c] (the
 // modulation of the synthesis layers, stylegan.py:130, applied to the input of the convolution;
 // the transform is linear, so the per-(image, channel) factor multiplies the 36 outputs)
+// vmax (optional, 64 slots of float bits): the running maximum of |V| for the split-f16 product
+// (nfi_gemm.hip), one atomic per workgroup into slot (x + y) % 64
 __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x, const float* __restrict__ scale,
                                                     const float* __restrict__ mask, float* __restrict__ V, int C,
-                                                    int H, int W, int TW, int T, int64_t P) {
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                    int H, int W, int TW, int T, int64_t P,
+                                                    unsigned* __restrict__ vmax) {
+  const int64_t p0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c = blockIdx.y;
-  if (p >= P) return;
+  const bool live = p0 < P;
+  if (!live && vmax == nullptr) return;
+  const int64_t p = live ? p0 : P - 1;   // (lanes past P run a clamped tile and store nothing)
   const int n = (int)(p / T);
   const int t = (int)(p - (int64_t)n * T);
   const int ty = t / TW, tx = t - ty * TW;
@@ -179,12 +184,25 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
   }
   const int64_t plane = (int64_t)C * P;
   float* out = V + (int64_t)c * P + p;
+  float m = 0.f;
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     float o[6];
     bt_col(s[r], o);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) st_stream(o[j], out + (r * 6 + j) * plane);
+    for (int j = 0; j < 6; ++j) {
+      if (live) st_stream(o[j], out + (r * 6 + j) * plane);
+      m = fmaxf(m, fabsf(o[j]));
+    }
+  }
+  if (vmax != nullptr) {
+    __shared__ float red[4];
+    m = wave_max(live ? m : 0.f);
+    if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicMax(vmax + (blockIdx.x + blockIdx.y) % 64,
+                __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
   }
 }
 
@@ -567,7 +585,7 @@ int32_t nfi_wino_input_transform_scaled(const float* x, const float* scale, floa
   const int TW = W / 4, T = (H / 4) * TW;
   const int64_t P = (int64_t)N * T;
   hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
-                     (hipStream_t)stream, x, scale, nullptr, V, C, H, W, TW, T, P);
+                     (hipStream_t)stream, x, scale, nullptr, V, C, H, W, TW, T, P, nullptr);
   NFI_CHECK_LAUNCH("wino input_kernel");
   return NFI_OK;
 }
@@ -581,7 +599,23 @@ int32_t nfi_wino_input_transform_relu_grad(const float* g, const float* y, float
   const int TW = W / 4, T = (H / 4) * TW;
   const int64_t P = (int64_t)N * T;
   hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
-                     (hipStream_t)stream, g, nullptr, y, V, C, H, W, TW, T, P);
+                     (hipStream_t)stream, g, nullptr, y, V, C, H, W, TW, T, P, nullptr);
+  NFI_CHECK_LAUNCH("wino input_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_wino_input_transform_max(const float* x, const float* scale, const float* relu_y, float* V,
+                                     uint32_t* vmax, int32_t N, int32_t C, int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(x && V && vmax, "wino_input_transform_max: null pointer");
+  NFI_REQUIRE(N > 0 && C > 0 && C <= 65535 && H >= 4 && W >= 4 && H % 4 == 0 && W % 4 == 0,
+              "wino_input_transform_max: bad shape (H, W multiples of 4)");
+  NFI_REQUIRE(((uintptr_t)x & 15) == 0 && (relu_y == nullptr || ((uintptr_t)relu_y & 15) == 0),
+              "wino_input_transform_max: misaligned");
+  NFI_REQUIRE(hipMemsetAsync(vmax, 0, 64 * 4, (hipStream_t)stream) == hipSuccess, "wino_input_transform_max: memset");
+  const int TW = W / 4, T = (H / 4) * TW;
+  const int64_t P = (int64_t)N * T;
+  hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
+                     (hipStream_t)stream, x, scale, relu_y, V, C, H, W, TW, T, P, (unsigned*)vmax);
   NFI_CHECK_LAUNCH("wino input_kernel");
   return NFI_OK;
 }

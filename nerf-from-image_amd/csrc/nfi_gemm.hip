@@ -1,0 +1,269 @@
+// Batched fp32 GEMM on the f16 matrix cores at fp32 accuracy (the split of DESIGN.md §3's decoder,
+// applied to the Winograd products of the inversion step's caller side):
+//
+//   C[b] (M x N) = A[b] (M x K) . B[b] (K x N),     fp32 in, fp32 out, b < batch
+//
+// Every fp32 operand v, times a power of two (exact), is carried as hi = f16(v), lo = f16(v - hi);
+// one fp32 product is three f16 products lo.hi + hi.lo + hi.hi on an fp32 accumulator
+// (v_mfma_f32_16x16x32_f16, 16x the fp32 MFMA rate per product): the error of an fp32 dot product
+// (3 2^-22 |a||b| per product at worst, below the K 2^-24 accumulation bound for K >= 12; K here is
+// the channel count, 64..512).  Scales: A (frozen Winograd weights U) per batch entry, computed once
+// when A is split (nfi_split16_pack: largest |A[b]| to [2^14, 2^15)); B (the input transform V) one
+// scale for the whole call, from the running maximum the input transform leaves in 64 slots
+// (nfi_wino_input_transform_max; slots combined in the prologue).  An operand 2^-k below its scale's
+// maximum is exact to 2^-(39-k) of itself — fp32-level to k ~ 15 and, beyond, below the Winograd
+// transform's own rounding (a few 1e-6 of the largest output, tests/test_gpu_conv.py).
+//
+// Tiling: a 256-thread workgroup computes a 128 x 128 tile of C, each wave 64 x 64 (4 x 4 blocks of
+// 16 x 16, 16 accumulators of 4 floats); K in steps of 32 (one f16 MFMA deep).  Per step the
+// workgroup stages A's hi / lo rows (pre-split in HBM: 16 KB) and B's 32 x 128 fp32 slab, split in
+// registers on its way to LDS as B^T hi / lo rows (each thread: one column, 16 consecutive k —
+// coalesced 256-B row reads across the wave), 40 KB of LDS; the next step's global loads are in
+// flight during the step's 48 MFMAs per wave.  Rows padded by 8 halves (80 B) so the b128 operand
+// reads of 16 lanes spread over the banks.
+#include "nfi_common.h"
+#include "nfi_host.h"
+#include "../../include/nfi_producer.h"
+
+namespace nfi {
+namespace gemm {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int LDK = BK + 8;                    // halves per LDS row (80 B)
+constexpr int TILE_H = BM * LDK;               // halves per operand image (A and B^T: BM == BN)
+constexpr int SLOTS = 64;                      // running-maximum slots of B
+
+__device__ __forceinline__ f4v mfma_h(u4v a, u4v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+}
+
+// s = 2^e, inv = 2^-e with m s in [2^14, 2^15) (e = 0 for m = 0 or not finite)
+__device__ __forceinline__ void pow2_scale15(float m, float& s, float& inv) {
+  int e = 15 - __builtin_amdgcn_frexp_expf(m);
+  e = (m > 0.f && m < __builtin_inff()) ? min(max(e, -120), 120) : 0;
+  s = __builtin_ldexpf(1.f, e);
+  inv = __builtin_ldexpf(1.f, -e);
+}
+
+__device__ __forceinline__ unsigned short h_bits(float v) { return __builtin_bit_cast(unsigned short, (_Float16)v); }
+__device__ __forceinline__ float h_val(unsigned short b) { return (float)__builtin_bit_cast(_Float16, b); }
+
+// ---- A: split once (frozen weights) --------------------------------------------------------------
+// one workgroup per batch entry: the largest |A[b]|, then hi / lo halves of A[b] * 2^e and 2^-e
+__global__ void __launch_bounds__(256) split_pack_kernel(const float* __restrict__ A, long long per,
+                                                         unsigned short* __restrict__ Ah,
+                                                         unsigned short* __restrict__ Al, float* __restrict__ inv) {
+  __shared__ float red[4];
+  const long long b = blockIdx.x;
+  const float* a = A + b * per;
+  float m = 0.f;
+  for (long long i = threadIdx.x; i < per; i += 256) m = fmaxf(m, fabsf(a[i]));
+  m = wave_max(m);
+  if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float s, is;
+  pow2_scale15(m, s, is);
+  for (long long i = threadIdx.x; i < per; i += 256) {
+    const float v = a[i] * s;
+    const unsigned short h = h_bits(v);
+    Ah[b * per + i] = h;
+    Al[b * per + i] = h_bits(v - h_val(h));
+  }
+  if (threadIdx.x == 0) inv[b] = is;
+}
+
+// ---- the product ---------------------------------------------------------------------------------
+struct Args {
+  const unsigned short* Ah;   // [batch][M][K] f16 bits
+  const unsigned short* Al;
+  const float* a_inv;         // [batch]
+  const float* B;             // [batch][K][N]
+  const unsigned* b_max;      // [SLOTS] running maxima of |B| (float bits)
+  float* C;                   // [batch][M][N]
+  int M, N, K;
+};
+
+__global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[4 * TILE_H];   // A hi, A lo, Bt hi, Bt lo
+  unsigned short* Ahs = lds;
+  unsigned short* Als = lds + TILE_H;
+  unsigned short* Bhs = lds + 2 * TILE_H;
+  unsigned short* Bls = lds + 3 * TILE_H;
+  const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int M = g.M, N = g.N, K = g.K;
+  // B's scale: the maximum over the input transform's slots
+  float bm = __uint_as_float(g.b_max[l]);
+  bm = wave_max(bm);
+  float sb, isb;
+  pow2_scale15(bm, sb, isb);
+  const float out_scale = g.a_inv[b] * isb;
+
+  const unsigned short* Ahg = g.Ah + (long long)b * M * K;
+  const unsigned short* Alg = g.Al + (long long)b * M * K;
+  const float* Bg = g.B + (long long)b * K * N;
+
+  // global -> register staging: A rows (row ar = tid >> 1, halves 16 (tid & 1) .. +15 of the K-step:
+  // two b128 loads each of hi and lo), B column (bn = tid & 127, k = 16 (tid >> 7) .. +15)
+  const int ar = tid >> 1, ak = 16 * (tid & 1);
+  const int arow = min(m0 + ar, M - 1);
+  const bool a_ok = m0 + ar < M;
+  const int bn = tid & 127, bk = 16 * (tid >> 7);
+  const int bcol = min(n0 + bn, N - 1);
+  const bool b_ok = n0 + bn < N;
+  u4v ra[4];
+  float rb[16];
+  auto load = [&](int k0) {
+    const u4v* ph = reinterpret_cast<const u4v*>(Ahg + (long long)arow * K + k0 + ak);
+    const u4v* pl = reinterpret_cast<const u4v*>(Alg + (long long)arow * K + k0 + ak);
+    ra[0] = ph[0];
+    ra[1] = ph[1];
+    ra[2] = pl[0];
+    ra[3] = pl[1];
+    const float* pb = Bg + (long long)(k0 + bk) * N + bcol;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) rb[i] = pb[(long long)i * N];
+  };
+  auto store = [&]() {
+    const u4v z = {0u, 0u, 0u, 0u};
+    u4v* dh = reinterpret_cast<u4v*>(Ahs + ar * LDK + ak);
+    u4v* dl = reinterpret_cast<u4v*>(Als + ar * LDK + ak);
+    lds_st(dh, a_ok ? ra[0] : z);
+    lds_st(dh + 1, a_ok ? ra[1] : z);
+    lds_st(dl, a_ok ? ra[2] : z);
+    lds_st(dl + 1, a_ok ? ra[3] : z);
+    u4v hv[2], lv[2];
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      const float v0 = b_ok ? rb[i] * sb : 0.f, v1 = b_ok ? rb[i + 1] * sb : 0.f;
+      const unsigned short h0 = h_bits(v0), h1 = h_bits(v1);
+      const unsigned short l0 = h_bits(v0 - h_val(h0)), l1 = h_bits(v1 - h_val(h1));
+      hv[i >> 3][(i >> 1) & 3] = (unsigned)h0 | ((unsigned)h1 << 16);
+      lv[i >> 3][(i >> 1) & 3] = (unsigned)l0 | ((unsigned)l1 << 16);
+    }
+    u4v* eh = reinterpret_cast<u4v*>(Bhs + bn * LDK + bk);
+    u4v* el = reinterpret_cast<u4v*>(Bls + bn * LDK + bk);
+    lds_st(eh, hv[0]);
+    lds_st(eh + 1, hv[1]);
+    lds_st(el, lv[0]);
+    lds_st(el + 1, lv[1]);
+  };
+
+  // wave (wm, wn) computes rows 64 wm.., columns 64 wn.. of the tile
+  const int wm = wv >> 1, wn = wv & 1;
+  const int i16 = l & 15, kg = l >> 4;
+  f4v acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    store();
+    __syncthreads();
+    if (k0 + BK < K) load(k0 + BK);   // in flight during this step's products
+    u4v ah[4], al[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int r = (64 * wm + 16 * x + i16) * LDK + 8 * kg;
+      ah[x] = *reinterpret_cast<const u4v*>(Ahs + r);
+      al[x] = *reinterpret_cast<const u4v*>(Als + r);
+    }
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int r = (64 * wn + 16 * y + i16) * LDK + 8 * kg;
+      const u4v bh = *reinterpret_cast<const u4v*>(Bhs + r);
+      const u4v bl = *reinterpret_cast<const u4v*>(Bls + r);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        acc[x][y] = mfma_h(al[x], bh, acc[x][y]);   // small terms first
+        acc[x][y] = mfma_h(ah[x], bl, acc[x][y]);
+        acc[x][y] = mfma_h(ah[x], bh, acc[x][y]);
+      }
+    }
+    __syncthreads();
+  }
+  // C rows m0 + 64 wm + 16 x + 4 kg + r, column n0 + 64 wn + 16 y + i16
+  float* Cg = g.C + (long long)b * M * N;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 64 * wm + 16 * x + 4 * kg + r;
+      if (m >= M) continue;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int n = n0 + 64 * wn + 16 * y + i16;
+        if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * out_scale;
+      }
+    }
+}
+
+// running maximum of |x| over n floats into the 64 slots (generic callers; the Winograd input
+// transform keeps its own, nfi_conv.hip)
+__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ x, long long n,
+                                                     unsigned* __restrict__ slots) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(x[i]));
+  m = wave_max(m);
+  if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(slots + blockIdx.x % SLOTS, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
+}  // namespace gemm
+}  // namespace nfi
+
+using namespace nfi;
+
+extern "C" {
+
+int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* Ah, uint16_t* Al, float* a_inv,
+                         void* stream) {
+  NFI_REQUIRE(A && Ah && Al && a_inv, "split16_pack: null pointer");
+  NFI_REQUIRE(batch > 0 && per > 0, "split16_pack: bad shape batch=%d per=%lld", batch, (long long)per);
+  hipLaunchKernelGGL(gemm::split_pack_kernel, dim3(batch), dim3(256), 0, (hipStream_t)stream, A, (long long)per, Ah,
+                     Al, a_inv);
+  NFI_CHECK_LAUNCH("split_pack_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* stream) {
+  NFI_REQUIRE(x && slots && n > 0, "absmax_slots: bad arguments");
+  NFI_REQUIRE(hipMemsetAsync(slots, 0, gemm::SLOTS * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(gemm::absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long long)n,
+                     slots);
+  NFI_CHECK_LAUNCH("absmax_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                         const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                         void* stream) {
+  NFI_REQUIRE(Ah && Al && a_inv && B && b_max && C, "gemm_split16: null pointer");
+  NFI_REQUIRE(batch > 0 && batch <= 65535 && M > 0 && N > 0 && K > 0 && K % gemm::BK == 0,
+              "gemm_split16: bad shape batch=%d M=%d N=%d K=%d (K a multiple of %d)", batch, M, N, K, gemm::BK);
+  NFI_REQUIRE((long long)M * K < (1ll << 31) && (long long)K * N < (1ll << 31) && (long long)M * N < (1ll << 31),
+              "gemm_split16: matrix too large");
+  NFI_REQUIRE(((uintptr_t)Ah & 15) == 0 && ((uintptr_t)Al & 15) == 0, "gemm_split16: A halves must be 16-B aligned");
+  gemm::Args g{reinterpret_cast<const unsigned short*>(Ah), reinterpret_cast<const unsigned short*>(Al), a_inv, B,
+               b_max, C, M, N, K};
+  const dim3 grid((unsigned)((N + gemm::BN - 1) / gemm::BN), (unsigned)((M + gemm::BM - 1) / gemm::BM), (unsigned)batch);
+  NFI_REQUIRE(grid.y <= 65535, "gemm_split16: M too large");
+  hipLaunchKernelGGL(gemm::split16_gemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+  NFI_CHECK_LAUNCH("split16_gemm_kernel");
+  return NFI_OK;
+}
+
+}  // extern "C"

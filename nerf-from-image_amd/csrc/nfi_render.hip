@@ -846,13 +846,21 @@ __device__ __forceinline__ void mlp_backward_h(const float* __restrict__ dec, co
   float sx, isx;
   pow2_scale(wave_max_dpp(m), 15, sx, isx);
   const float cz = dec[H::SC] * isx;
-  // dY scale: C3 max|dY| sy in [2^13, 2^14), so |d hidden| <= C3 max|dY sy| stays in fp16 range
+  // dY scale, per point (a column of every product below, so it commutes through them and comes off
+  // at emit): point p's C3 max|dY_p| sy_p in [2^13, 2^14), so |d hidden| <= C3 max|dY_p sy_p| stays in
+  // fp16 range.  (A per-wave scale left a point whose gradients sit 2^-20 below the wave's largest
+  // with a hi / lo pair exact to 2^-2 of itself: tests/test_gpu_stages.py::test_decoder_split_wave_spread.)
   float my = 0.f;
 #pragma unroll
   for (int o = 0; o < NO; ++o) my = fmaxf(my, fabsf(X[l * XS + o]));
-  float sy, isy;
-  pow2_scale(wave_max_dpp(my) * dec[H::SC + 2], 14, sy, isy);
-  const float fac = post * (dec[H::SC + 3] * isy);   // 2^-(e3 + e4 + ey)
+  float syl, isyl;
+  pow2_scale(my * dec[H::SC + 2], 14, syl, isyl);
+  float sys[4];   // lane (j, q): the scale of point 16sb + j
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) sys[sb] = __shfl(syl, 16 * sb + j);
+  const float fac = post * dec[H::SC + 3];   // 2^-(e3 + e4), times 2^-ey of the point at emit
+  // 2^-e of sy = 2^e (exact)
+  auto inv_pow2 = [](float v) { return __builtin_ldexpf(1.f, 1 - __builtin_amdgcn_frexp_expf(v)); };
 #if NFI_BWD_DYHOLD
   // B operands of d hidden, per point block: [dY hi; dY hi] and [dY lo; dY lo] (lane (j, q): outputs
   // 8(q&1)..+7).  Against H3 = [W2 hi | W2 lo] the second adds hi.lo + lo.lo.
@@ -861,6 +869,7 @@ __device__ __forceinline__ void mlp_backward_h(const float* __restrict__ dec, co
   for (int sb = 0; sb < 4; ++sb) {
     const float* dr = X + (16 * sb + j) * XS + 8 * (q & 1);
     const f4v d0 = ld4(dr), d1 = ld4(dr + 4);
+    const float sy = sys[sb];
     const float v[8] = {d0[0] * sy, d0[1] * sy, d0[2] * sy, d0[3] * sy, d1[0] * sy, d1[1] * sy, d1[2] * sy, d1[3] * sy};
     split8(v, DH[sb], DL[sb]);
   }
@@ -911,6 +920,7 @@ __device__ __forceinline__ void mlp_backward_h(const float* __restrict__ dec, co
         {
           const float* dr = X + (16 * sb + j) * XS + 8 * (q & 1);
           const f4v d0 = ld4(dr), d1 = ld4(dr + 4);
+          const float sy = sys[sb];
           const float v[8] = {d0[0] * sy, d0[1] * sy, d0[2] * sy, d0[3] * sy,
                               d1[0] * sy, d1[1] * sy, d1[2] * sy, d1[3] * sy};
           split8(v, dh, dl);
@@ -935,8 +945,9 @@ __device__ __forceinline__ void mlp_backward_h(const float* __restrict__ dec, co
     }
 #pragma unroll
     for (int s = 0; s < NSB; ++s) {
-      emit(0, NSB * sp + s, gx[0][s] * fac);
-      emit(1, NSB * sp + s, gx[1][s] * fac);
+      const float f = fac * inv_pow2(sys[NSB * sp + s]);
+      emit(0, NSB * sp + s, gx[0][s] * f);
+      emit(1, NSB * sp + s, gx[1][s] * f);
     }
   }
 }

@@ -117,6 +117,11 @@ SIGNATURES = {
     'nfi_volume_weights_backward': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int32]
                                     + [c_void_p] * 5),
     # include/nfi_producer.h
+    'nfi_split16_pack': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int64, c_void_p, c_void_p, c_void_p,
+                                          c_void_p]),
+    'nfi_wino_input_transform_max': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
+    'nfi_absmax_slots': (ctypes.c_int32, [c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
+    'nfi_gemm_split16': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),
     'nfi_syn_act_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -195,12 +200,22 @@ def load(path: str = LIB_PATH):
             raise NfiError(f'nfi HIP library not found at {path}; build it with '
                            f'`python __graft_entry__.py` (build()) — there is no CPU fallback')
         lib = ctypes.CDLL(path)
+        # NFI_AB_OLDER=1 (A/B timing of an older build through scripts/ab_multi.sh only): entry points
+        # the older library lacks stay unbound and an older ABI version is accepted (the render
+        # structs are unchanged since ABI 14); never set for product runs
+        ab_older = (os.environ.get('NFI_AB_OLDER') == '1'
+                    and os.path.abspath(path) != os.path.join(_HERE, 'libnfi_hip.so'))
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                if ab_older:
+                    continue
+                raise
             fn.restype = res
             fn.argtypes = args
         v = lib.nfi_abi_version()
-        if v != ABI_VERSION:
+        if v != ABI_VERSION and not (ab_older and v >= 14):
             raise NfiError(f'nfi ABI mismatch: library {v}, binding {ABI_VERSION}')
         _lib = lib
         return lib

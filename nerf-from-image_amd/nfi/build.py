@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), 'csrc')
 OUT = os.path.join(HERE, 'libnfi_hip.so')
-SOURCES = ['nfi_rays.hip', 'nfi_render.hip', 'nfi_producer.hip', 'nfi_conv.hip']
+SOURCES = ['nfi_rays.hip', 'nfi_render.hip', 'nfi_producer.hip', 'nfi_conv.hip', 'nfi_gemm.hip']
 HEADERS = ['nfi_common.h', 'nfi_host.h']
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-munsafe-fp-atomics',
          '-Wall', '-Wno-unused-result']
@@ -42,6 +42,33 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+TORCH_OPS_SRC = os.path.join(CSRC, 'nfi_torch.cpp')
+TORCH_OPS_OUT = os.path.join(HERE, 'libnfi_torch.so')
+
+
+def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
+    """nfi/libnfi_torch.so: the TORCH_LIBRARY(nfi, ...) operators (csrc/nfi_torch.cpp) over the C-ABI,
+    host C++ only (g++ against torch's headers and libraries), linked to nfi/libnfi_hip.so by rpath
+    $ORIGIN; loaded with torch.ops.load_library (nfi.torch_ops)."""
+    deps = [TORCH_OPS_SRC, OUT, os.path.join(os.path.dirname(os.path.dirname(HERE)), 'include', 'nfi.h')]
+    if (not force and os.path.exists(TORCH_OPS_OUT)
+            and all(os.path.getmtime(d) <= os.path.getmtime(TORCH_OPS_OUT) for d in deps if os.path.exists(d))):
+        return TORCH_OPS_OUT
+    import torch
+    ti = os.path.dirname(torch.__file__)
+    abi = int(torch.compiled_with_cxx11_abi())
+    cmd = [os.environ.get('CXX', 'g++'), '-O2', '-std=c++17', '-fPIC', '-shared', TORCH_OPS_SRC, '-o',
+           TORCH_OPS_OUT + '.tmp', f'-I{ti}/include', f'-I{ti}/include/torch/csrc/api/include', '-I/opt/rocm/include',
+           '-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1', f'-D_GLIBCXX_USE_CXX11_ABI={abi}', f'-L{ti}/lib', '-lc10',
+           '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_hip', f'-L{HERE}', '-lnfi_hip', "-Wl,-rpath,$ORIGIN",
+           f'-Wl,-rpath,{ti}/lib']
+    if verbose:
+        print(' '.join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(TORCH_OPS_OUT + '.tmp', TORCH_OPS_OUT)
+    return TORCH_OPS_OUT
+
+
 def build(force: bool = False, verbose: bool = True, variant: str = '') -> str:
     """variant 'stamps': profiling library libnfi_hip_stamps.so with per-phase cycle counters
     (-DNFI_STAMPS, loaded via NFI_LIBRARY by scripts/stamps.py); never the product build."""
@@ -68,3 +95,5 @@ if __name__ == '__main__':
         if a.startswith('--variant='):
             var = a.split('=', 1)[1]
     build(force='--force' in sys.argv, variant=var)
+    if not var:
+        build_torch_ops(force='--force' in sys.argv)

@@ -44,6 +44,21 @@ FUSED_MAX_CI = int(os.environ.get('NFI_FUSED_MAX_CI', '64'))
 # the VGG blocks' ReLU threshold_backward inside the data gradient's input transform (no pool
 # gradient; three-pass layers)
 RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
+# the three-pass layers' 36 products on the f16 matrix cores at fp32 accuracy (csrc/nfi_gemm.hip:
+# hi / lo splits, three products each; the weights split once, V's scale from the input
+# transform's running maximum); 0: torch.bmm (hipBLASLt fp32)
+SPLIT16 = os.environ.get('NFI_SPLIT16', '0') != '0'
+SPLIT16_BK = 32       # the split GEMM's K step: channel counts must be multiples of it
+
+
+class WeightSet:
+    """One orientation of a frozen 3x3 weight, transformed: U [36, M, K] fp32 (the hipBLASLt
+    product), `packed` (the fused kernel's MFMA operands, or None) and `split` = (hi, lo, inverse
+    scales) f16 halves for the split-f16 product (or None)."""
+    __slots__ = ('U', 'packed', 'split')
+
+    def __init__(self, U, packed, split):
+        self.U, self.packed, self.split = U, packed, split
 
 
 def _p(t):
@@ -80,9 +95,43 @@ def weights(weight: torch.Tensor):
     st = _stream(w.device)
     _call('nfi_wino_weight_transform', _p(w), _p(U), Co, Ci, 0, st)
     _call('nfi_wino_weight_transform', _p(w), _p(Ut), Co, Ci, 1, st)
-    out = ((U, _pack(U, Co, Ci, st)), (Ut, _pack(Ut, Ci, Co, st)))
+    out = (WeightSet(U, _pack(U, Co, Ci, st), _split(U, Ci, st)),
+           WeightSet(Ut, _pack(Ut, Ci, Co, st), _split(Ut, Co, st)))
     weight._nfi_winograd = (tag, out)          # cached on the (frozen) parameter itself
     return out
+
+
+def _split(U, K, st):
+    """U [36, M, K] -> (hi, lo [36, M, K] f16 bits, inverse scales [36]) for nfi_gemm_split16."""
+    if K % SPLIT16_BK:
+        return None
+    hi = torch.empty(U.shape, device=U.device, dtype=torch.int16)
+    lo = torch.empty(U.shape, device=U.device, dtype=torch.int16)
+    inv = torch.empty((U.shape[0],), device=U.device)
+    _call('nfi_split16_pack', _p(U), U.shape[0], U.shape[1] * U.shape[2], _p(hi), _p(lo), _p(inv), st)
+    return hi, lo, inv
+
+
+def _product(Uw: WeightSet, x, scale=None, relu_y=None):
+    """Input transform of x [N, K, H, W] (times scale [N, K]; through the ReLU mask of relu_y) and
+    the 36 products with the transformed weights: M [36, Mrows, P]."""
+    N, K, H, W = x.shape
+    P = N * (H // 4) * (W // 4)
+    st = _stream(x.device)
+    V = torch.empty((36, K, P), device=x.device)
+    if SPLIT16 and Uw.split is not None:
+        hi, lo, inv = Uw.split
+        vmax = torch.empty((64,), device=x.device, dtype=torch.int32)
+        _call('nfi_wino_input_transform_max', _p(x), _p(scale), _p(relu_y), _p(V), _p(vmax), N, K, H, W, st)
+        Mrows = Uw.U.shape[1]
+        M = torch.empty((36, Mrows, P), device=x.device)
+        _call('nfi_gemm_split16', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, st)
+        return M
+    if relu_y is not None:
+        _call('nfi_wino_input_transform_relu_grad', _p(x), _p(relu_y), _p(V), N, K, H, W, st)
+    else:
+        _call('nfi_wino_input_transform_scaled', _p(x), _p(scale), _p(V), N, K, H, W, st)
+    return torch.bmm(Uw.U, V)
 
 
 def _pack(U, Co, Ci, st):
@@ -98,7 +147,7 @@ def _winograd(x, Uw, bias=None, pool=False, scale=None):
     """x [N,Ci,H,W] (contiguous) with transformed weights Uw = (U [36,Co,Ci], packed or None) ->
     y [N,Co,H,W] (and the pooled map when pool).  scale [N,Ci]: convolve x * scale[n, c]
     (three-pass form: folded into the input transform)."""
-    U, Ua = Uw
+    U, Ua = Uw.U, Uw.packed
     N, Ci, H, W = x.shape
     Co = U.shape[1]
     st = _stream(x.device)
@@ -110,11 +159,7 @@ def _winograd(x, Uw, bias=None, pool=False, scale=None):
     if FUSED and Ua is not None and Ci <= FUSED_MAX_CI:
         _call('nfi_wino_conv_fused', _p(x), _p(Ua), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
         return (y, m) if pool else y
-    P = N * (H // 4) * (W // 4)
-    V = torch.empty((36, Ci, P), device=x.device)
-    _call('nfi_wino_input_transform_scaled', _p(x), _p(scale), _p(V), N, Ci, H, W, st)
-    M = torch.bmm(U, V)
-    del V
+    M = _product(Uw, x, scale)
     _call('nfi_wino_output_transform', _p(M), _p(bias), _p(y), _p(m), N, Co, H, W, st)
     return (y, m) if pool else y
 
@@ -170,14 +215,10 @@ class _ModConv(torch.autograd.Function):
         ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
         st = _stream(x.device)
         Co = g.shape[1]
-        Ut, Uta = ctx.Ut
+        Uta = ctx.Ut.packed
         if DGRAD and not (FUSED and Uta is not None and Co <= FUSED_MAX_CI):
             # three-pass data gradient, the scale backward in its output transform
-            P = B * (H // 4) * (W // 4)
-            V = torch.empty((36, Co, P), device=g.device)
-            _call('nfi_wino_input_transform_scaled', _p(g), None, _p(V), B, Co, H, W, st)
-            M = torch.bmm(Ut, V)
-            del V
+            M = _product(ctx.Ut, g)
             _call('nfi_wino_output_transform_scaled_grad', _p(M), _p(x), _p(s), _p(gx), _p(ds), B, C, H, W, st)
             return gx, ds, None
         gxs = _dgrad(g, ctx)
@@ -209,16 +250,12 @@ class _VggBlock(torch.autograd.Function):
         N, C, H, W = y.shape
         gy = None if gy is None else gy.contiguous()
         gm = None if gm is None else gm.contiguous()
-        Ut, Uta = ctx.Ut
+        Uta = ctx.Ut.packed
         if RELU_IN_TRANSFORM and gm is None and DGRAD and not (FUSED and Uta is not None and C <= FUSED_MAX_CI):
             # no pool gradient: the ReLU threshold inside the data gradient's input transform
             st = _stream(y.device)
-            P = N * (H // 4) * (W // 4)
-            V = torch.empty((36, C, P), device=y.device)
-            _call('nfi_wino_input_transform_relu_grad', _p(gy), _p(y), _p(V), N, C, H, W, st)
-            M = torch.bmm(Ut, V)
-            del V
-            Ci = Ut.shape[1]
+            M = _product(ctx.Ut, gy, relu_y=y)
+            Ci = ctx.Ut.U.shape[1]
             gx = torch.empty((N, Ci, H, W), device=y.device)
             _call('nfi_wino_output_transform', _p(M), None, _p(gx), None, N, Ci, H, W, st)
             return gx, None, None, None

@@ -17,7 +17,7 @@ for i in $(seq "${ROUNDS:-2}"); do
     if [ "$lib" = default ]; then
       timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion --no-configs "$@" > gpurun_out/ab_run.log 2>&1 || exit 1
     else
-      NFI_LIBRARY=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion --no-configs "$@" > gpurun_out/ab_run.log 2>&1 || exit 1
+      NFI_AB_OLDER=1 NFI_LIBRARY=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-inversion --no-configs "$@" > gpurun_out/ab_run.log 2>&1 || exit 1
     fi
     show "$(basename $lib)" gpurun_out/ab_run.log || exit 1
   done

@@ -14,6 +14,6 @@ while [ $# -ge 2 ]; do
     git archive "${defs#git:}" $C include | tar -x -C $d
     src=$d/$C; defs=""
   fi
-  /opt/rocm/bin/hipcc $FL $defs -o $O/libnfi_hip_$name.so $src/nfi_rays.hip $src/nfi_render.hip $src/nfi_producer.hip $src/nfi_conv.hip &
+  /opt/rocm/bin/hipcc $FL $defs -o $O/libnfi_hip_$name.so $src/nfi_rays.hip $src/nfi_render.hip $src/nfi_producer.hip $src/nfi_conv.hip $(ls $src/nfi_gemm.hip 2>/dev/null) &
 done
 wait

@@ -41,6 +41,11 @@ def main():
             conv.FUSED, conv.FUSED_MAX_CI = fused, 1 << 20
             res.append(timeit(lambda: conv._winograd(x, Uw, b, False)))
         conv.FUSED, conv.FUSED_MAX_CI = True, 64
+        # the three-pass form with hipBLASLt's fp32 GEMM instead of the split-f16 product
+        conv.FUSED, conv.SPLIT16 = False, False
+        t_bmm = timeit(lambda: conv._winograd(x, Uw, b, False))
+        conv.FUSED, conv.SPLIT16 = True, True
+        print(f'    three-pass with hipBLASLt bmm {t_bmm:.3f} ms', flush=True)
         res.append(timeit(lambda: F.relu(F.conv2d(x, w, b, padding=1))))
         gf = 2 * 9 * ci * co * hw * hw * N / 4 / 1e9       # Winograd GEMM GFLOP (4x fewer products)
         print(f'{ci:4d}->{co:4d} @{hw:3d}: fused {res[0]:.3f} ms ({gf / res[0]:.0f} TF)  three-pass {res[1]:.3f} ms  '

@@ -62,3 +62,19 @@ def test_bad_arguments_are_rejected_without_launch():
     code = lib.nfi_render_forward(ctypes.byref(args), None)
     assert code == -1
     assert b'null' in lib.nfi_last_error()
+
+
+def test_torch_ops_library_registers():
+    """nfi/libnfi_torch.so (TORCH_LIBRARY(nfi, ...), csrc/nfi_torch.cpp) loads here without a GPU and
+    registers every operator with its schema; a CPU tensor raises instead of computing."""
+    import torch
+    from nfi import torch_ops
+    torch_ops.load()
+    for name in torch_ops.OPS:
+        assert hasattr(torch.ops.nfi, name), name
+    schema = str(torch.ops.nfi.volume_render.default._schema)
+    assert schema.startswith('nfi::volume_render(Tensor planes_tm, Tensor? palette, Tensor ro, Tensor rd')
+    cu = torch.jit.CompilationUnit(torch_ops.render_script_source())
+    assert 'nfi::volume_render' in str(cu.render_rays.graph)
+    with pytest.raises(RuntimeError, match='HIP devices only'):
+        torch.ops.nfi.cumprod_exclusive(torch.ones(2, 3))

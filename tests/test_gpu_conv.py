@@ -86,7 +86,7 @@ def test_fused_kernel_matches_three_pass(N, Ci, Co, H, W, pool):
     w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
     b = torch.randn((Co,), device=DEV, generator=g) * 0.1
     Uw, _ = conv.weights(w)
-    assert Uw[1] is not None
+    assert Uw.packed is not None
     outs = []
     for fused in (True, False):
         conv.FUSED, conv.FUSED_MAX_CI = fused, 1 << 20
@@ -101,15 +101,19 @@ def test_fused_kernel_matches_three_pass(N, Ci, Co, H, W, pool):
 
 
 def test_weight_cache_follows_in_place_updates():
-    w = torch.randn((16, 16, 3, 3), device=DEV)
-    (U1, A1), _ = conv.weights(w)
+    w = torch.randn((32, 32, 3, 3), device=DEV)   # channel counts the split GEMM takes (multiples of 32)
+    ws1, _ = conv.weights(w)
+    U1, A1 = ws1.U, ws1.packed
     U1c, A1c = U1.clone(), A1.clone()
-    assert conv.weights(w)[0][0] is U1
+    assert conv.weights(w)[0].U is U1
     with torch.no_grad():
         w.mul_(2)
-    (U2, A2), _ = conv.weights(w)
-    torch.testing.assert_close(U2, 2 * U1c)
-    torch.testing.assert_close(A2, 2 * A1c)
+    ws2, _ = conv.weights(w)
+    torch.testing.assert_close(ws2.U, 2 * U1c)
+    torch.testing.assert_close(ws2.packed, 2 * A1c)
+    # the split halves follow too: x2 is a power of two, so hi / lo are equal and the scale halves
+    assert torch.equal(ws2.split[0], ws1.split[0]) and torch.equal(ws2.split[1], ws1.split[1])
+    torch.testing.assert_close(ws2.split[2], ws1.split[2] * 2)
 
 
 def test_trainable_weight_takes_the_library_path():

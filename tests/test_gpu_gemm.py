@@ -1,0 +1,82 @@
+"""The split-f16 batched GEMM (csrc/nfi_gemm.hip, nfi_gemm_split16) against fp64: C[b] = A[b] B[b]
+with fp32 operands carried as power-of-two-scaled hi + lo fp16 pairs on the f16 matrix cores
+(three products each).  Bound: the fp64-relative error of each batch entry within 4x of the fp32
+GEMM's own (torch.bmm on the device, hipBLASLt) plus a floor of 2^-22 of the entry's |A||B| scale;
+partial M / N tiles, K from 32 to 512, operands spanning magnitudes across the batch."""
+
+import ctypes
+
+import pytest
+import torch
+
+from nfi import _lib, conv
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def split_gemm(A, B):
+    lib = _lib.load()
+    st = ctypes.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    b, M, K = A.shape
+    N = B.shape[2]
+    hi = torch.empty(A.shape, device=DEV, dtype=torch.int16)
+    lo = torch.empty(A.shape, device=DEV, dtype=torch.int16)
+    inv = torch.empty((b,), device=DEV)
+    _lib.check(lib.nfi_split16_pack(_p(A), b, M * K, _p(hi), _p(lo), _p(inv), st), 'nfi_split16_pack')
+    slots = torch.empty((64,), device=DEV, dtype=torch.int32)
+    _lib.check(lib.nfi_absmax_slots(_p(B), B.numel(), _p(slots), st), 'nfi_absmax_slots')
+    C = torch.empty((b, M, N), device=DEV)
+    _lib.check(lib.nfi_gemm_split16(_p(hi), _p(lo), _p(inv), _p(B), _p(slots), _p(C), b, M, N, K, st),
+               'nfi_gemm_split16')
+    return C
+
+
+@pytest.mark.parametrize('b,M,N,K', [(4, 64, 1000, 64), (36, 128, 4096, 128), (3, 96, 257, 32), (2, 512, 1024, 512),
+                                     (36, 256, 300, 256)])
+def test_split16_gemm_matches_fp64(b, M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn((b, M, K), device=DEV, generator=g)
+    B = torch.randn((b, K, N), device=DEV, generator=g)
+    # magnitudes spread across the batch entries (A's scale is per entry, B's per call)
+    A *= torch.logspace(-3, 3, b, device=DEV)[:, None, None]
+    B *= torch.logspace(2, -2, b, device=DEV)[:, None, None]
+    C = split_gemm(A, B)
+    ref64 = torch.bmm(A.double(), B.double())
+    ref32 = torch.bmm(A, B)
+    for i in range(b):
+        scale = float((A[i].double().abs() @ B[i].double().abs()).max())
+        e_hip = float((C[i].double() - ref64[i]).abs().max()) / scale
+        e_ref = float((ref32[i].double() - ref64[i]).abs().max()) / scale
+        assert e_hip <= 4 * e_ref + 2 ** -22, (i, e_hip, e_ref)
+
+
+@pytest.mark.parametrize('Ci,Co,H', [(128, 128, 32), (256, 512, 16), (128, 64, 64)])
+def test_winograd_split16_matches_bmm(Ci, Co, H):
+    """The three-pass Winograd convolution with the split-f16 products against the same pipeline with
+    hipBLASLt's fp32 bmm, and both against an fp64 direct convolution (the 2e-5 bound of
+    tests/test_gpu_conv.py)."""
+    g = torch.Generator(device=DEV).manual_seed(Ci + Co)
+    x = torch.randn((4, Ci, H, H), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    Uw, _ = conv.weights(w)
+    assert Uw.split is not None
+    old = conv.FUSED, conv.SPLIT16
+    out = {}
+    try:
+        conv.FUSED = False
+        for mode in (True, False):
+            conv.SPLIT16 = mode
+            out[mode] = conv._winograd(x, Uw)
+    finally:
+        conv.FUSED, conv.SPLIT16 = old
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), padding=1)
+    scale = float(ref.abs().max())
+    e_split = float((out[True].double() - ref).abs().max()) / scale
+    e_bmm = float((out[False].double() - ref).abs().max()) / scale
+    print(f'  split16 {e_split:.3g}  bmm {e_bmm:.3g}')
+    assert e_split <= 2e-5 and e_split <= 2 * e_bmm + 1e-6
