@@ -219,7 +219,12 @@ int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gim
  *   bits; zeroed by the call).
  * nfi_absmax_slots: the same running maximum of any x [n] (zeroes slots[64] first).
  * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max[64] from one of the above,
- *   C [batch][M][N] fp32 (written); K a multiple of 32. */
+ *   C [batch][M][N] fp32 (written); K a multiple of 32.  N % 4 == 0 with 16-B aligned B and C takes
+ *   the wide-load kernel, else the general one (NFI_GEMM_KERNEL=1 forces the general one).
+ * nfi_gemm_split16_shared_a: the same with ONE A [M][K] (and a_inv[0]) for every batch entry — the
+ *   up-sampling convolutions' 9-tap weight matrix against each image (stylegan.py:99-101) — and K
+ *   split in ksplit ranges when ksplit > 1 (few output tiles, long K: the data gradient W9^T dP), the
+ *   partial products in work [ksplit][batch][M][N] summed in order (deterministic). */
 int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* Ah, uint16_t* Al, float* a_inv,
                          void* stream);
 int32_t nfi_wino_input_transform_max(const float* x, const float* scale, const float* relu_y, float* V,
@@ -228,6 +233,9 @@ int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* strea
 int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                          const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                          void* stream);
+int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                                  const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                                  int32_t ksplit, float* work, void* stream);
 
 #ifdef __cplusplus
 }

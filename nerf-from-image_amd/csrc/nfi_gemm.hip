@@ -21,6 +21,9 @@
 // coalesced 256-B row reads across the wave), 40 KB of LDS; the next step's global loads are in
 // flight during the step's 48 MFMAs per wave.  Rows padded by 8 halves (80 B) so the b128 operand
 // reads of 16 lanes spread over the banks.
+#include <algorithm>
+#include <cstdlib>
+
 #include "nfi_common.h"
 #include "nfi_host.h"
 #include "../../include/nfi_producer.h"
@@ -86,6 +89,9 @@ struct Args {
   const unsigned* b_max;      // [SLOTS] running maxima of |B| (float bits)
   float* C;                   // [batch][M][N]
   int M, N, K;
+  int a_shared;               // 1: one A (and scale) for every batch entry
+  int ksplit, kchunk;         // (general kernel) K in ksplit ranges of kchunk: blockIdx.z = b ksplit + s,
+  float* work;                //   range s's partial C to work[s][b][M][N] when ksplit > 1
 };
 
 __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
@@ -95,18 +101,20 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
   unsigned short* Bhs = lds + 2 * TILE_H;
   unsigned short* Bls = lds + 3 * TILE_H;
   const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
-  const int b = blockIdx.z;
+  const int b = blockIdx.z / g.ksplit, ks = blockIdx.z - b * g.ksplit;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int M = g.M, N = g.N, K = g.K;
+  const int kbeg = ks * g.kchunk, kend = min(K, kbeg + g.kchunk);
   // B's scale: the maximum over the input transform's slots
   float bm = __uint_as_float(g.b_max[l]);
   bm = wave_max(bm);
   float sb, isb;
   pow2_scale15(bm, sb, isb);
-  const float out_scale = g.a_inv[b] * isb;
+  const int ba = g.a_shared ? 0 : b;
+  const float out_scale = g.a_inv[ba] * isb;
 
-  const unsigned short* Ahg = g.Ah + (long long)b * M * K;
-  const unsigned short* Alg = g.Al + (long long)b * M * K;
+  const unsigned short* Ahg = g.Ah + (long long)ba * M * K;
+  const unsigned short* Alg = g.Al + (long long)ba * M * K;
   const float* Bg = g.B + (long long)b * K * N;
 
   // global -> register staging: A rows (row ar = tid >> 1, halves 16 (tid & 1) .. +15 of the K-step:
@@ -164,11 +172,11 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
-  for (int k0 = 0; k0 < K; k0 += BK) {
+  load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
     store();
     __syncthreads();
-    if (k0 + BK < K) load(k0 + BK);   // in flight during this step's products
+    if (k0 + BK < kend) load(k0 + BK);   // in flight during this step's products
     u4v ah[4], al[4];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
@@ -191,7 +199,7 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
     __syncthreads();
   }
   // C rows m0 + 64 wm + 16 x + 4 kg + r, column n0 + 64 wn + 16 y + i16
-  float* Cg = g.C + (long long)b * M * N;
+  float* Cg = (g.ksplit > 1 ? g.work + (long long)ks * (gridDim.z / g.ksplit) * M * N : g.C) + (long long)b * M * N;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -204,6 +212,148 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
         if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * out_scale;
       }
     }
+}
+
+// ---- the product, N % 4 == 0: wide loads and stores ----------------------------------------------
+// 128 x 128 tile, K in steps of 64 (two f16 MFMAs deep): per step the workgroup stages A's hi / lo rows
+// (32 KB, each thread one half-row: 4 + 4 b128 loads) and B's 64 x 128 fp32 slab (each thread an
+// 8 (k) x 4 (n) block: 8 float4 loads, 512-B row segments per wave; split in registers and written as
+// four B^T rows of 8 consecutive k, one b128 store per row and half — lanes 0..7 of a store take the
+// 8 k-groups of one row: distinct banks).  72-half (144-B) LDS rows: the 16 rows an MFMA operand
+// read spans start on 16 distinct 4-bank groups.  The products run as C^T = B^T A^T, so a lane's
+// accumulator holds 4 consecutive columns of one row of C: float4 stores.  74 KB of LDS, two
+// workgroups per CU; K % 64 == 32 runs a zero-padded last step.
+constexpr int BK4 = 64;
+constexpr int LK4 = BK4 + 8;
+constexpr int IMG4 = 128 * LK4;
+
+__global__ void __launch_bounds__(256, 2) split16_gemm4_kernel(Args g) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[4 * IMG4];   // A hi, A lo, Bt hi, Bt lo
+  unsigned short* Ahs = lds;
+  unsigned short* Als = lds + IMG4;
+  unsigned short* Bhs = lds + 2 * IMG4;
+  unsigned short* Bls = lds + 3 * IMG4;
+  const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
+  const int b = blockIdx.z;
+  const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
+  const int M = g.M, N = g.N, K = g.K;
+  float bm = __uint_as_float(g.b_max[l]);
+  bm = wave_max(bm);
+  float sb, isb;
+  pow2_scale15(bm, sb, isb);
+  const int ba = g.a_shared ? 0 : b;
+  const float out_scale = g.a_inv[ba] * isb;
+
+  const unsigned short* Ahg = g.Ah + (long long)ba * M * K;
+  const unsigned short* Alg = g.Al + (long long)ba * M * K;
+  const float* Bg = g.B + (long long)b * K * N;
+
+  // A: row ar, halves 32 ah2 .. +31 of the step; B: rows 8 k8 .. +7 of the step, columns 4 n4 .. +3
+  const int ar = tid >> 1, ah2 = tid & 1;
+  const int arow = min(m0 + ar, M - 1);
+  const bool a_ok = m0 + ar < M;
+  const int k8 = l & 7, n4 = 8 * wv + (l >> 3);
+  const int bcol = n0 + 4 * n4;
+  const bool b_ok = bcol < N;
+  const int bc = min(bcol, N - 4);
+  u4v ra[8];
+  f4v rb[8];
+  auto load = [&](int k0) {
+    const long long ao = (long long)arow * K + min(k0 + 32 * ah2, K - 32);
+    const u4v* ph = reinterpret_cast<const u4v*>(Ahg + ao);
+    const u4v* pl = reinterpret_cast<const u4v*>(Alg + ao);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ra[j] = ph[j];
+      ra[4 + j] = pl[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rb[i] = *reinterpret_cast<const f4v*>(Bg + (long long)min(k0 + 8 * k8 + i, K - 1) * N + bc);
+  };
+  auto store = [&](int k0) {
+    const u4v z = {0u, 0u, 0u, 0u};
+    const bool al = a_ok && k0 + 32 * ah2 < K;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lds_st(reinterpret_cast<u4v*>(Ahs + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[j] : z);
+      lds_st(reinterpret_cast<u4v*>(Als + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[4 + j] : z);
+    }
+    const bool bl = b_ok && k0 + 8 * k8 < K;   // (K % 32 == 0: a k-group is all in or all out)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u4v hv, lv;
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const float v0 = bl ? rb[i][c] * sb : 0.f, v1 = bl ? rb[i + 1][c] * sb : 0.f;
+        const unsigned short h0 = h_bits(v0), h1 = h_bits(v1);
+        const unsigned short l0 = h_bits(v0 - h_val(h0)), l1 = h_bits(v1 - h_val(h1));
+        hv[i >> 1] = (unsigned)h0 | ((unsigned)h1 << 16);
+        lv[i >> 1] = (unsigned)l0 | ((unsigned)l1 << 16);
+      }
+      lds_st(reinterpret_cast<u4v*>(Bhs + (4 * n4 + c) * LK4 + 8 * k8), hv);
+      lds_st(reinterpret_cast<u4v*>(Bls + (4 * n4 + c) * LK4 + 8 * k8), lv);
+    }
+  };
+
+  // wave (wm, wn): rows 64 wm.., columns 64 wn.. of the tile; acc[y][x] = (C^T) block (n block y,
+  // m block x): lane (i16, kg) holds C[64 wm + 16 x + i16][64 wn + 16 y + 4 kg + r]
+  const int wm = wv >> 1, wn = wv & 1;
+  const int i16 = l & 15, kg = l >> 4;
+  f4v acc[4][4];
+#pragma unroll
+  for (int y = 0; y < 4; ++y)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) acc[y][x] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += BK4) {
+    store(k0);
+    __syncthreads();
+    if (k0 + BK4 < K) load(k0 + BK4);   // in flight during this step's products
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u4v bh[4], bl[4];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int r = (64 * wn + 16 * y + i16) * LK4 + 32 * s + 8 * kg;
+        bh[y] = *reinterpret_cast<const u4v*>(Bhs + r);
+        bl[y] = *reinterpret_cast<const u4v*>(Bls + r);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int r = (64 * wm + 16 * x + i16) * LK4 + 32 * s + 8 * kg;
+        const u4v ah = *reinterpret_cast<const u4v*>(Ahs + r);
+        const u4v al = *reinterpret_cast<const u4v*>(Als + r);
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          acc[y][x] = mfma_h(bl[y], ah, acc[y][x]);   // small terms first
+          acc[y][x] = mfma_h(bh[y], al, acc[y][x]);
+          acc[y][x] = mfma_h(bh[y], ah, acc[y][x]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* Cg = g.C + (long long)b * M * N;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const int m = m0 + 64 * wm + 16 * x + i16;
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int n = n0 + 64 * wn + 16 * y + 4 * kg;
+      if (m < M && n < N) *reinterpret_cast<f4v*>(Cg + (long long)m * N + n) = acc[y][x] * out_scale;
+    }
+  }
+}
+
+// C = sum over s of work[s] (fixed order: deterministic), float4 per thread
+__global__ void __launch_bounds__(256) ksum_kernel(const float* __restrict__ work, float* __restrict__ C, long long n4,
+                                                    int ksplit) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  f4v a = reinterpret_cast<const f4v*>(work)[i];
+  for (int s = 1; s < ksplit; ++s) a += reinterpret_cast<const f4v*>(work)[(long long)s * n4 + i];
+  reinterpret_cast<f4v*>(C)[i] = a;
 }
 
 // running maximum of |x| over n floats into the 64 slots (generic callers; the Winograd input
@@ -248,9 +398,9 @@ int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* strea
   return NFI_OK;
 }
 
-int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
-                         const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                         void* stream) {
+static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                            const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                            int a_shared, int32_t ksplit, float* work, void* stream) {
   NFI_REQUIRE(Ah && Al && a_inv && B && b_max && C, "gemm_split16: null pointer");
   NFI_REQUIRE(batch > 0 && batch <= 65535 && M > 0 && N > 0 && K > 0 && K % gemm::BK == 0,
               "gemm_split16: bad shape batch=%d M=%d N=%d K=%d (K a multiple of %d)", batch, M, N, K, gemm::BK);
@@ -258,12 +408,50 @@ int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_
               "gemm_split16: matrix too large");
   NFI_REQUIRE(((uintptr_t)Ah & 15) == 0 && ((uintptr_t)Al & 15) == 0, "gemm_split16: A halves must be 16-B aligned");
   gemm::Args g{reinterpret_cast<const unsigned short*>(Ah), reinterpret_cast<const unsigned short*>(Al), a_inv, B,
-               b_max, C, M, N, K};
+               b_max, C, M, N, K, a_shared, 1, K, nullptr};
+  NFI_REQUIRE(ksplit >= 1 && (ksplit == 1 || work), "gemm_split16: ksplit=%d needs a workspace", ksplit);
   const dim3 grid((unsigned)((N + gemm::BN - 1) / gemm::BN), (unsigned)((M + gemm::BM - 1) / gemm::BM), (unsigned)batch);
   NFI_REQUIRE(grid.y <= 65535, "gemm_split16: M too large");
-  hipLaunchKernelGGL(gemm::split16_gemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
-  NFI_CHECK_LAUNCH("split16_gemm_kernel");
+  // (NFI_GEMM_KERNEL=2: the wide-load kernel where it applies — measured slower than the general one
+  //  on every Winograd shape, scripts/gemm_bench.py — kept for A/B)
+  const char* fe = getenv("NFI_GEMM_KERNEL");
+  const int forced = fe ? atoi(fe) : 0;
+  if (ksplit > 1) {   // K ranges of whole steps, partials summed in order
+    const int steps = K / gemm::BK;
+    ksplit = std::min(ksplit, steps);
+    g.ksplit = ksplit;
+    g.kchunk = (steps + ksplit - 1) / ksplit * gemm::BK;
+    g.work = work;
+    NFI_REQUIRE((long long)batch * ksplit <= 65535, "gemm_split16: batch x ksplit too large");
+    NFI_REQUIRE(((uintptr_t)work & 15) == 0 && ((uintptr_t)C & 15) == 0 && (long long)M * N % 4 == 0,
+                "gemm_split16: ksplit needs 16-B aligned work / C and M N % 4 == 0");
+    const dim3 gk(grid.x, grid.y, (unsigned)(batch * ksplit));
+    hipLaunchKernelGGL(gemm::split16_gemm_kernel, gk, dim3(256), 0, (hipStream_t)stream, g);
+    NFI_CHECK_LAUNCH("split16_gemm_kernel");
+    const long long n4 = (long long)batch * M * N / 4;
+    hipLaunchKernelGGL(gemm::ksum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, work, C,
+                       n4, ksplit);
+    NFI_CHECK_LAUNCH("ksum_kernel");
+  } else if (N % 4 == 0 && forced == 2 && ((uintptr_t)B & 15) == 0 && ((uintptr_t)C & 15) == 0) {
+    hipLaunchKernelGGL(gemm::split16_gemm4_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+    NFI_CHECK_LAUNCH("split16_gemm4_kernel");
+  } else {
+    hipLaunchKernelGGL(gemm::split16_gemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+    NFI_CHECK_LAUNCH("split16_gemm_kernel");
+  }
   return NFI_OK;
+}
+
+int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                         const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                         void* stream) {
+  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 0, 1, nullptr, stream);
+}
+
+int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                                  const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                                  int32_t ksplit, float* work, void* stream) {
+  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 1, ksplit, work, stream);
 }
 
 }  // extern "C"

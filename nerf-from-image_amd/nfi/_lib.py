@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 15
+ABI_VERSION = 16
 DEC_SIZE = 7200
 DEC_SIZE_VIEWDIR = 14384
 
@@ -122,6 +122,7 @@ SIGNATURES = {
     'nfi_wino_input_transform_max': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_absmax_slots': (ctypes.c_int32, [c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
     'nfi_gemm_split16': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 4 + [c_void_p]),
+    'nfi_gemm_split16_shared_a': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),
     'nfi_syn_act_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

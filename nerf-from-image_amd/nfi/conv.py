@@ -47,7 +47,7 @@ RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
 # the three-pass layers' 36 products on the f16 matrix cores at fp32 accuracy (csrc/nfi_gemm.hip:
 # hi / lo splits, three products each; the weights split once, V's scale from the input
 # transform's running maximum); 0: torch.bmm (hipBLASLt fp32)
-SPLIT16 = os.environ.get('NFI_SPLIT16', '0') != '0'
+SPLIT16 = os.environ.get('NFI_SPLIT16', '1') != '0'
 SPLIT16_BK = 32       # the split GEMM's K step: channel counts must be multiples of it
 
 
@@ -110,6 +110,41 @@ def _split(U, K, st):
     inv = torch.empty((U.shape[0],), device=U.device)
     _call('nfi_split16_pack', _p(U), U.shape[0], U.shape[1] * U.shape[2], _p(hi), _p(lo), _p(inv), st)
     return hi, lo, inv
+
+
+def split_matrix(A):
+    """A frozen [M, K] fp32 matrix -> its split-f16 halves for split_matmul_shared (None when K is not
+    a multiple of SPLIT16_BK, or SPLIT16 is off: the caller keeps torch.matmul)."""
+    if not SPLIT16 or A.shape[1] % SPLIT16_BK:
+        return None
+    return _split(A.detach().contiguous()[None], A.shape[1], _stream(A.device))
+
+
+def split_matmul_shared(As, X):
+    """C[b] = A X[b] for X [B, K, N] on the split GEMM, A's halves from split_matrix (one A for every
+    image: nfi_gemm_split16_shared_a); X's scale from its maximum (nfi_absmax_slots)."""
+    hi, lo, inv = As
+    X = X.contiguous()
+    B, K, N = X.shape
+    Mrows = hi.shape[1]
+    assert hi.shape[2] == K, (hi.shape, X.shape)
+    st = _stream(X.device)
+    slots = torch.empty((64,), device=X.device, dtype=torch.int32)
+    _call('nfi_absmax_slots', _p(X), X.numel(), _p(slots), st)
+    C = torch.empty((B, Mrows, N), device=X.device)
+    ks = ksplit(B * -(-Mrows // 128) * -(-N // 128), K) if (Mrows * N) % 4 == 0 else 1
+    work = torch.empty((ks, B, Mrows, N), device=X.device) if ks > 1 else None
+    _call('nfi_gemm_split16_shared_a', _p(hi), _p(lo), _p(inv), _p(X), _p(slots), _p(C), B, Mrows, N, K, ks,
+          _p(work), st)
+    return C
+
+
+def ksplit(tiles, K):
+    """K ranges for a split GEMM of `tiles` 128 x 128 output tiles: enough workgroups to cover the
+    256 CUs about twice (each range at least 8 K-steps of 32)."""
+    if tiles >= 512:
+        return 1
+    return max(1, min(K // 256, -(-512 // tiles)))
 
 
 def _product(Uw: WeightSet, x, scale=None, relu_y=None):

@@ -21,7 +21,7 @@ import ctypes
 import torch
 import torch.nn.functional as F
 
-from . import _lib
+from . import _lib, conv
 from .ops import _require_device, _stream
 
 
@@ -124,16 +124,28 @@ class _FirUpAct(torch.autograd.Function):
 
 def _up_weights(w):
     """(W9 [9*Co, Ci] = w[co, ci, ky, kx] at row (3ky+kx)*Co + co, and W9^T contiguous) of a
-    frozen w, cached on the tensor per storage version."""
-    key = (w.data_ptr(), w._version, w.device)
+    frozen w, cached on the tensor per storage version — each as (fp32 matrix, split-f16 halves for
+    conv.split_matmul_shared or None)."""
+    key = (w.data_ptr(), w._version, w.device, conv.SPLIT16)
     hit = getattr(w, '_nfi_upconv', None)
     if hit is None or hit[0] != key:
         with torch.no_grad():
             co, ci = w.shape[:2]
             W9 = w.detach().permute(2, 3, 0, 1).reshape(9 * co, ci).contiguous()
-            hit = (key, (W9, W9.t().contiguous()))
+            W9t = W9.t().contiguous()
+            hit = (key, ((W9, conv.split_matrix(W9)), (W9t, conv.split_matrix(W9t))))
         w._nfi_upconv = hit
     return hit[1]
+
+
+def _mm_shared(Wm, X):
+    """Wm[0] X[b] per image: the split GEMM when Wm carries halves and the maps have >= 1024 pixels,
+    else torch.matmul (hipBLASLt).  Below 1024 the products are launch-sized (20-60 us) and hipBLASLt's
+    small tiles fill the GPU better: scripts/gemm_bench.py, N = 16..256 split 1.1-2.4x slower, N >= 1024
+    1.3-1.9x faster."""
+    if Wm[1] is not None and X.shape[2] >= 1024:
+        return conv.split_matmul_shared(Wm[1], X)
+    return torch.matmul(Wm[0], X)
 
 
 class _UpConv(torch.autograd.Function):
@@ -141,27 +153,28 @@ class _UpConv(torch.autograd.Function):
     def forward(ctx, x, W9, W9t):
         x = x.contiguous()
         B, Ci, n, _ = x.shape
-        Co = W9.shape[0] // 9
-        P = torch.matmul(W9, x.view(B, Ci, n * n))                          # [B, 9*Co, n*n]
+        Co = W9[0].shape[0] // 9
+        P = _mm_shared(W9, x.view(B, Ci, n * n))                            # [B, 9*Co, n*n]
         t = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=x.device, dtype=x.dtype)
         _call('nfi_syn_up_conv_scatter', _p(P), _p(t), B, Co, n, _stream(x.device))
-        ctx.save_for_backward(W9t)
+        ctx.W9t = W9t            # (frozen: no saved-tensor version check needed)
         ctx.shape = (B, Ci, Co, n)
         return t
 
     @staticmethod
     def backward(ctx, gt):
-        W9t, = ctx.saved_tensors
+        W9t = ctx.W9t
         B, Ci, Co, n = ctx.shape
         gt = gt.contiguous()
         dP = torch.empty((B, 9 * Co, n * n), device=gt.device, dtype=gt.dtype)
         _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, _stream(gt.device))
-        return torch.matmul(W9t, dP).view(B, Ci, n, n), None, None         # conv_transpose2d's adjoint
+        return _mm_shared(W9t, dP).view(B, Ci, n, n), None, None           # conv_transpose2d's adjoint
 
 
 def up_conv(x, w):
     """F.conv_transpose2d(x, w.transpose(0, 1), stride=2) for w [Co, Ci, 3, 3] (stylegan.py:99-101,
-    the synthesis up-sampling layers) as GEMMs over the 9 taps: forward P = W9 x (hipBLASLt,
+    the synthesis up-sampling layers) as GEMMs over the 9 taps: forward P = W9 x (the split-f16 GEMM,
+    conv.split_matmul_shared; hipBLASLt fp32 with NFI_SPLIT16=0 or channel counts off multiples of 32 —
     125-137 TFLOP/s on the 256^2 generator's layers where MIOpen's transposed kernels reach 50-70)
     and the tap scatter nfi_syn_up_conv_scatter; data gradient W9^T dP after the tap gather
     nfi_syn_up_conv_gather.  A weight that takes gradients goes to MIOpen's conv_transpose2d."""
@@ -179,20 +192,22 @@ class _UpConvAct(torch.autograd.Function):
         x = x.contiguous()
         d = d.contiguous()
         B, Ci, n, _ = x.shape
-        Co = W9.shape[0] // 9
-        P = torch.matmul(W9, x.view(B, Ci, n * n))                          # [B, 9*Co, n*n]
+        Co = W9[0].shape[0] // 9
+        P = _mm_shared(W9, x.view(B, Ci, n * n))                            # [B, 9*Co, n*n]
         o = torch.empty((B, Co, 2 * n, 2 * n), device=x.device, dtype=x.dtype)
         y = torch.empty_like(o)
         _call('nfi_syn_up_conv_fir_act_forward', _p(P), _p(d), _p(bias), _p(o), _p(y), B, Co, n,
               ctypes.c_float(gain), _stream(x.device))
-        ctx.save_for_backward(o, d, bias, W9t)
+        ctx.save_for_backward(o, d, bias)
+        ctx.W9t = W9t
         ctx.gain = gain
         ctx.shape = (B, Ci, Co, n)
         return y
 
     @staticmethod
     def backward(ctx, g):
-        o, d, bias, W9t = ctx.saved_tensors
+        o, d, bias = ctx.saved_tensors
+        W9t = ctx.W9t
         B, Ci, Co, n = ctx.shape
         g = g.contiguous()
         dev = _stream(o.device)
@@ -208,7 +223,7 @@ class _UpConvAct(torch.autograd.Function):
             gt = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
             _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * Co, n, dev)
             _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, dev)
-        gx = torch.matmul(W9t, dP).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
+        gx = _mm_shared(W9t, dP).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
         return gx, None, None, dd, None, None
 
 

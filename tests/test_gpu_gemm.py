@@ -36,9 +36,16 @@ def split_gemm(A, B):
     return C
 
 
+@pytest.mark.parametrize('kernel', ['wide', 'general'])
 @pytest.mark.parametrize('b,M,N,K', [(4, 64, 1000, 64), (36, 128, 4096, 128), (3, 96, 257, 32), (2, 512, 1024, 512),
-                                     (36, 256, 300, 256)])
-def test_split16_gemm_matches_fp64(b, M, N, K):
+                                     (36, 256, 300, 256), (5, 160, 516, 96), (2, 200, 132, 32)])
+def test_split16_gemm_matches_fp64(b, M, N, K, kernel, monkeypatch):
+    """Both kernels of the entry: the general one (the default) and the wide one (NFI_GEMM_KERNEL=2;
+    N % 4 == 0; K % 64 == 32 as a zero-padded last step)."""
+    if kernel == 'wide':
+        if N % 4:
+            pytest.skip('the wide kernel takes N % 4 == 0')
+        monkeypatch.setenv('NFI_GEMM_KERNEL', '2')
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     A = torch.randn((b, M, K), device=DEV, generator=g)
     B = torch.randn((b, K, N), device=DEV, generator=g)
@@ -80,3 +87,27 @@ def test_winograd_split16_matches_bmm(Ci, Co, H):
     e_bmm = float((out[False].double() - ref).abs().max()) / scale
     print(f'  split16 {e_split:.3g}  bmm {e_bmm:.3g}')
     assert e_split <= 2e-5 and e_split <= 2 * e_bmm + 1e-6
+
+
+@pytest.mark.parametrize('b,M,N,K', [(4, 9 * 64, 256, 128), (2, 9 * 32, 1024, 96), (3, 64, 36, 4608),
+                                     (4, 512, 64, 4608), (2, 256, 1000, 1152)])
+def test_split16_shared_a_matches_fp64(b, M, N, K):
+    """nfi_gemm_split16_shared_a (conv.split_matmul_shared): one A for every batch entry — the
+    up-sampling convolutions' 9-tap matrix W9 [9 Co, Ci] against each image, and W9^T [Ci, 9 Co]
+    against the tap gradients (K = 9 Co; few output tiles: K split in ranges, conv.ksplit)."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + 1)
+    A = torch.randn((M, K), device=DEV, generator=g) * 1e-2
+    X = torch.randn((b, K, N), device=DEV, generator=g) * torch.logspace(1, -1, b, device=DEV)[:, None, None]
+    old = conv.SPLIT16
+    try:
+        conv.SPLIT16 = True
+        C = conv.split_matmul_shared(conv.split_matrix(A), X)
+    finally:
+        conv.SPLIT16 = old
+    ref64 = torch.matmul(A.double(), X.double())
+    ref32 = torch.matmul(A, X)
+    for i in range(b):
+        scale = float((A.double().abs() @ X[i].double().abs()).max())
+        e_hip = float((C[i].double() - ref64[i]).abs().max()) / scale
+        e_ref = float((ref32[i].double() - ref64[i]).abs().max()) / scale
+        assert e_hip <= 4 * e_ref + 2 ** -22, (i, e_hip, e_ref)
