@@ -119,6 +119,16 @@ __device__ __forceinline__ void lds_st(T* p, const T& v) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// lds_st with a scheduling barrier ahead of the store as well: in a region holding the splits of
+// several stores' data (nfi_gemm.hip's B operand), the scheduler otherwise hoisted a store above the
+// next store's arithmetic, leaving its trailing s_nop ~90 instructions later and the freed data
+// register rewritten at once (caught by scripts/isa_lint.py)
+template <class T>
+__device__ __forceinline__ void lds_st_fenced(T* p, const T& v) {
+  __builtin_amdgcn_sched_barrier(0);
+  lds_st(p, v);
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));

@@ -20,7 +20,11 @@
 // registers on its way to LDS as B^T hi / lo rows (each thread: one column, 16 consecutive k —
 // coalesced 256-B row reads across the wave), 40 KB of LDS; the next step's global loads are in
 // flight during the step's 48 MFMAs per wave.  Rows padded by 8 halves (80 B) so the b128 operand
-// reads of 16 lanes spread over the banks.
+// reads of 16 lanes spread over the banks.  Measured against the alternatives kept for A/B
+// (scripts/gemm_bench.py, profiles/r04_gemm_bench.log): 256 x 128 / 128 x 256 tiles of 8 waves
+// (NFI_GEMM_TILE=42 / 24) 0-50 % slower, two register stages of prefetch (NFI_GEMM_PF=2: occupancy
+// 2) 0-15 % slower, the wide-load kernel (NFI_GEMM_KERNEL=2) 5-25 % slower; 200-256 TFLOP/s
+// fp32-equivalent on the 256-512-channel Winograd shapes, 2x hipBLASLt's fp32 bmm.
 #include <algorithm>
 #include <cstdlib>
 
@@ -66,7 +70,7 @@ __global__ void __launch_bounds__(256) split_pack_kernel(const float* __restrict
   float m = 0.f;
   for (long long i = threadIdx.x; i < per; i += 256) m = fmaxf(m, fabsf(a[i]));
   m = wave_max(m);
-  if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
+  if (lane_id() == 0) lds_st_fenced(red + (threadIdx.x >> 6), m);
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   float s, is;
@@ -92,17 +96,44 @@ struct Args {
   int a_shared;               // 1: one A (and scale) for every batch entry
   int ksplit, kchunk;         // (general kernel) K in ksplit ranges of kchunk: blockIdx.z = b ksplit + s,
   float* work;                //   range s's partial C to work[s][b][M][N] when ksplit > 1
+  int xcd;                    // 1: XCD-major tile order (below)
 };
 
-__global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
-  __shared__ __attribute__((aligned(16))) unsigned short lds[4 * TILE_H];   // A hi, A lo, Bt hi, Bt lo
+// Workgroups are dispatched round-robin over the 8 XCDs in linear order (x fastest), each XCD with
+// its own L2.  XCD-major order: the tiles an XCD runs are a contiguous range of (n block fastest, m
+// block, batch entry), so the tiles sharing an A row block or a B column slab meet in one L2 instead of
+// eight (bijective for any tile count: the first T mod 8 XCDs take one tile more).
+__device__ __forceinline__ void tile_order(int xcd, int& bx, int& by, int& bz) {
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  bz = blockIdx.z;
+  if (!xcd) return;
+  const unsigned gx = gridDim.x, gy = gridDim.y, T = gx * gy * gridDim.z;
+  const unsigned L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const unsigned x = L & 7, q = T >> 3, r = T & 7;
+  const unsigned t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+  bx = (int)(t % gx);
+  by = (int)((t / gx) % gy);
+  bz = (int)(t / (gx * gy));
+}
+
+// WM x WN waves of 64 x 64: tile (64 WM) x (64 WN), 64 WM WN threads
+template <int WM, int WN, int PF>
+__global__ void __launch_bounds__(64 * WM * WN, WM * WN == 4 ? (PF == 1 ? 3 : 2) : 1) split16_gemm_kernel(Args g) {
+  constexpr int T = 64 * WM * WN, TBM = 64 * WM, TBN = 64 * WN;
+  constexpr int CA = 4 / WN;    // 8-half chunks of A's K-step rows per thread (hi; as many lo)
+  constexpr int KB = 32 / WM;   // k rows of B's slab per thread (one column)
+  static_assert(CA >= 1 && KB >= 8 && KB % 8 == 0, "tile shape");
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * LDK * (TBM + TBN)];   // A hi, A lo, Bt hi, Bt lo
   unsigned short* Ahs = lds;
-  unsigned short* Als = lds + TILE_H;
-  unsigned short* Bhs = lds + 2 * TILE_H;
-  unsigned short* Bls = lds + 3 * TILE_H;
+  unsigned short* Als = lds + TBM * LDK;
+  unsigned short* Bhs = lds + 2 * TBM * LDK;
+  unsigned short* Bls = Bhs + TBN * LDK;
   const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
-  const int b = blockIdx.z / g.ksplit, ks = blockIdx.z - b * g.ksplit;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int bx, by, bz;
+  tile_order(g.xcd, bx, by, bz);
+  const int b = bz / g.ksplit, ks = bz - b * g.ksplit;
+  const int m0 = by * TBM, n0 = bx * TBN;
   const int M = g.M, N = g.N, K = g.K;
   const int kbeg = ks * g.kchunk, kend = min(K, kbeg + g.kchunk);
   // B's scale: the maximum over the input transform's slots
@@ -117,38 +148,40 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
   const unsigned short* Alg = g.Al + (long long)ba * M * K;
   const float* Bg = g.B + (long long)b * K * N;
 
-  // global -> register staging: A rows (row ar = tid >> 1, halves 16 (tid & 1) .. +15 of the K-step:
-  // two b128 loads each of hi and lo), B column (bn = tid & 127, k = 16 (tid >> 7) .. +15)
-  const int ar = tid >> 1, ak = 16 * (tid & 1);
+  // global -> register staging: A (row ar, halves ak .. ak + 8 CA - 1 of the K-step: CA b128 loads
+  // each of hi and lo), B column bn, k = bk .. bk + KB - 1 (coalesced rows across the wave)
+  const int ar = tid / WN, ak = 8 * ((tid * CA) & 3);
   const int arow = min(m0 + ar, M - 1);
   const bool a_ok = m0 + ar < M;
-  const int bn = tid & 127, bk = 16 * (tid >> 7);
+  const int bn = tid % TBN, bk = (tid / TBN) * KB;
   const int bcol = min(n0 + bn, N - 1);
   const bool b_ok = n0 + bn < N;
-  u4v ra[4];
-  float rb[16];
-  auto load = [&](int k0) {
+  u4v RA[PF][2 * CA];
+  float RB[PF][KB];
+  auto load = [&](int k0, u4v (&ra)[2 * CA], float (&rb)[KB]) {
     const u4v* ph = reinterpret_cast<const u4v*>(Ahg + (long long)arow * K + k0 + ak);
     const u4v* pl = reinterpret_cast<const u4v*>(Alg + (long long)arow * K + k0 + ak);
-    ra[0] = ph[0];
-    ra[1] = ph[1];
-    ra[2] = pl[0];
-    ra[3] = pl[1];
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      ra[i] = ph[i];
+      ra[CA + i] = pl[i];
+    }
     const float* pb = Bg + (long long)(k0 + bk) * N + bcol;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) rb[i] = pb[(long long)i * N];
+    for (int i = 0; i < KB; ++i) rb[i] = pb[(long long)i * N];
   };
-  auto store = [&]() {
+  auto store = [&](const u4v (&ra)[2 * CA], const float (&rb)[KB]) {
     const u4v z = {0u, 0u, 0u, 0u};
     u4v* dh = reinterpret_cast<u4v*>(Ahs + ar * LDK + ak);
     u4v* dl = reinterpret_cast<u4v*>(Als + ar * LDK + ak);
-    lds_st(dh, a_ok ? ra[0] : z);
-    lds_st(dh + 1, a_ok ? ra[1] : z);
-    lds_st(dl, a_ok ? ra[2] : z);
-    lds_st(dl + 1, a_ok ? ra[3] : z);
-    u4v hv[2], lv[2];
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
+    for (int i = 0; i < CA; ++i) {
+      lds_st_fenced(dh + i, a_ok ? ra[i] : z);
+      lds_st_fenced(dl + i, a_ok ? ra[CA + i] : z);
+    }
+    u4v hv[KB / 8], lv[KB / 8];
+#pragma unroll
+    for (int i = 0; i < KB; i += 2) {
       const float v0 = b_ok ? rb[i] * sb : 0.f, v1 = b_ok ? rb[i + 1] * sb : 0.f;
       const unsigned short h0 = h_bits(v0), h1 = h_bits(v1);
       const unsigned short l0 = h_bits(v0 - h_val(h0)), l1 = h_bits(v1 - h_val(h1));
@@ -157,14 +190,15 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
     }
     u4v* eh = reinterpret_cast<u4v*>(Bhs + bn * LDK + bk);
     u4v* el = reinterpret_cast<u4v*>(Bls + bn * LDK + bk);
-    lds_st(eh, hv[0]);
-    lds_st(eh + 1, hv[1]);
-    lds_st(el, lv[0]);
-    lds_st(el + 1, lv[1]);
+#pragma unroll
+    for (int i = 0; i < KB / 8; ++i) {
+      lds_st_fenced(eh + i, hv[i]);
+      lds_st_fenced(el + i, lv[i]);
+    }
   };
 
   // wave (wm, wn) computes rows 64 wm.., columns 64 wn.. of the tile
-  const int wm = wv >> 1, wn = wv & 1;
+  const int wm = wv / WN, wn = wv % WN;
   const int i16 = l & 15, kg = l >> 4;
   f4v acc[4][4];
 #pragma unroll
@@ -172,11 +206,7 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    store();
-    __syncthreads();
-    if (k0 + BK < kend) load(k0 + BK);   // in flight during this step's products
+  auto compute = [&]() {
     u4v ah[4], al[4];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
@@ -196,7 +226,27 @@ __global__ void __launch_bounds__(256, 2) split16_gemm_kernel(Args g) {
         acc[x][y] = mfma_h(ah[x], bh, acc[x][y]);
       }
     }
+  };
+  // PF register stages: the loads of step k + PF are issued once step k's registers are in LDS and
+  // are in flight during PF steps' products
+  auto step = [&](int k0, u4v (&ra)[2 * CA], float (&rb)[KB]) {
+    store(ra, rb);
     __syncthreads();
+    if (k0 + PF * BK < kend) load(k0 + PF * BK, ra, rb);
+    compute();
+    __syncthreads();
+  };
+  load(kbeg, RA[0], RB[0]);
+  if constexpr (PF == 1) {
+    for (int k0 = kbeg; k0 < kend; k0 += BK) step(k0, RA[0], RB[0]);
+  } else {
+    if (kbeg + BK < kend) load(kbeg + BK, RA[PF - 1], RB[PF - 1]);
+    int k0 = kbeg;
+    for (; k0 + BK < kend; k0 += 2 * BK) {
+      step(k0, RA[0], RB[0]);
+      step(k0 + BK, RA[PF - 1], RB[PF - 1]);
+    }
+    if (k0 < kend) step(k0, RA[0], RB[0]);
   }
   // C rows m0 + 64 wm + 16 x + 4 kg + r, column n0 + 64 wn + 16 y + i16
   float* Cg = (g.ksplit > 1 ? g.work + (long long)ks * (gridDim.z / g.ksplit) * M * N : g.C) + (long long)b * M * N;
@@ -275,8 +325,8 @@ __global__ void __launch_bounds__(256, 2) split16_gemm4_kernel(Args g) {
     const bool al = a_ok && k0 + 32 * ah2 < K;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      lds_st(reinterpret_cast<u4v*>(Ahs + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[j] : z);
-      lds_st(reinterpret_cast<u4v*>(Als + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[4 + j] : z);
+      lds_st_fenced(reinterpret_cast<u4v*>(Ahs + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[j] : z);
+      lds_st_fenced(reinterpret_cast<u4v*>(Als + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[4 + j] : z);
     }
     const bool bl = b_ok && k0 + 8 * k8 < K;   // (K % 32 == 0: a k-group is all in or all out)
 #pragma unroll
@@ -290,8 +340,8 @@ __global__ void __launch_bounds__(256, 2) split16_gemm4_kernel(Args g) {
         hv[i >> 1] = (unsigned)h0 | ((unsigned)h1 << 16);
         lv[i >> 1] = (unsigned)l0 | ((unsigned)l1 << 16);
       }
-      lds_st(reinterpret_cast<u4v*>(Bhs + (4 * n4 + c) * LK4 + 8 * k8), hv);
-      lds_st(reinterpret_cast<u4v*>(Bls + (4 * n4 + c) * LK4 + 8 * k8), lv);
+      lds_st_fenced(reinterpret_cast<u4v*>(Bhs + (4 * n4 + c) * LK4 + 8 * k8), hv);
+      lds_st_fenced(reinterpret_cast<u4v*>(Bls + (4 * n4 + c) * LK4 + 8 * k8), lv);
     }
   };
 
@@ -365,7 +415,7 @@ __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ x
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     m = fmaxf(m, fabsf(x[i]));
   m = wave_max(m);
-  if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
+  if (lane_id() == 0) lds_st_fenced(red + (threadIdx.x >> 6), m);
   __syncthreads();
   if (threadIdx.x == 0)
     atomicMax(slots + blockIdx.x % SLOTS, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
@@ -408,10 +458,36 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
               "gemm_split16: matrix too large");
   NFI_REQUIRE(((uintptr_t)Ah & 15) == 0 && ((uintptr_t)Al & 15) == 0, "gemm_split16: A halves must be 16-B aligned");
   gemm::Args g{reinterpret_cast<const unsigned short*>(Ah), reinterpret_cast<const unsigned short*>(Al), a_inv, B,
-               b_max, C, M, N, K, a_shared, 1, K, nullptr};
+               b_max, C, M, N, K, a_shared, 1, K, nullptr, 1};
+  // XCD-major tile order where a row of tiles is short (<= 8 column blocks: the 512-channel layers'
+  // products, 5-12 % faster); the long rows of the large maps stream better in linear order (3-6 %,
+  // profiles/r04_gemm_bench.log).  NFI_GEMM_XCD=0/1 forces it (A/B).
+  const char* xe = getenv("NFI_GEMM_XCD");
+  g.xcd = xe ? atoi(xe) : 0;
   NFI_REQUIRE(ksplit >= 1 && (ksplit == 1 || work), "gemm_split16: ksplit=%d needs a workspace", ksplit);
-  const dim3 grid((unsigned)((N + gemm::BN - 1) / gemm::BN), (unsigned)((M + gemm::BM - 1) / gemm::BM), (unsigned)batch);
+  // tile of the general kernel: WM x WN waves (NFI_GEMM_TILE = "WMWN": 22 default, 42, 24, 41, 14)
+  const char* te = getenv("NFI_GEMM_TILE");
+  const int tile = te ? atoi(te) : 22;
+  const int WM = tile / 10, WN = tile % 10;
+  NFI_REQUIRE(tile == 22 || tile == 42 || tile == 24 || tile == 41 || tile == 14, "gemm_split16: NFI_GEMM_TILE=%d", tile);
+  const dim3 grid((unsigned)((N + 64 * WN - 1) / (64 * WN)), (unsigned)((M + 64 * WM - 1) / (64 * WM)), (unsigned)batch);
   NFI_REQUIRE(grid.y <= 65535, "gemm_split16: M too large");
+  if (!xe) g.xcd = grid.x <= 8;
+  const char* pe = getenv("NFI_GEMM_PF");   // register prefetch depth (A/B: 1 or 2)
+  const int pf = pe ? atoi(pe) : 1;
+  auto general = [&](dim3 gr) {
+    if (pf == 2) {
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 2, 2>), gr, dim3(256), 0, (hipStream_t)stream, g);
+      return;
+    }
+    switch (tile) {
+      case 42: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<4, 2, 1>), gr, dim3(512), 0, (hipStream_t)stream, g); break;
+      case 24: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 4, 1>), gr, dim3(512), 0, (hipStream_t)stream, g); break;
+      case 41: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<4, 1, 1>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
+      case 14: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<1, 4, 1>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
+      default: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 2, 1>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
+    }
+  };
   // (NFI_GEMM_KERNEL=2: the wide-load kernel where it applies — measured slower than the general one
   //  on every Winograd shape, scripts/gemm_bench.py — kept for A/B)
   const char* fe = getenv("NFI_GEMM_KERNEL");
@@ -425,18 +501,18 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
     NFI_REQUIRE((long long)batch * ksplit <= 65535, "gemm_split16: batch x ksplit too large");
     NFI_REQUIRE(((uintptr_t)work & 15) == 0 && ((uintptr_t)C & 15) == 0 && (long long)M * N % 4 == 0,
                 "gemm_split16: ksplit needs 16-B aligned work / C and M N % 4 == 0");
-    const dim3 gk(grid.x, grid.y, (unsigned)(batch * ksplit));
-    hipLaunchKernelGGL(gemm::split16_gemm_kernel, gk, dim3(256), 0, (hipStream_t)stream, g);
+    general(dim3(grid.x, grid.y, (unsigned)(batch * ksplit)));
     NFI_CHECK_LAUNCH("split16_gemm_kernel");
     const long long n4 = (long long)batch * M * N / 4;
     hipLaunchKernelGGL(gemm::ksum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, work, C,
                        n4, ksplit);
     NFI_CHECK_LAUNCH("ksum_kernel");
   } else if (N % 4 == 0 && forced == 2 && ((uintptr_t)B & 15) == 0 && ((uintptr_t)C & 15) == 0) {
-    hipLaunchKernelGGL(gemm::split16_gemm4_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+    const dim3 g4((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), (unsigned)batch);
+    hipLaunchKernelGGL(gemm::split16_gemm4_kernel, g4, dim3(256), 0, (hipStream_t)stream, g);
     NFI_CHECK_LAUNCH("split16_gemm4_kernel");
   } else {
-    hipLaunchKernelGGL(gemm::split16_gemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, g);
+    general(grid);
     NFI_CHECK_LAUNCH("split16_gemm_kernel");
   }
   return NFI_OK;

@@ -22,6 +22,10 @@ SHAPES = [(128, 128, 16384), (256, 128, 4096), (256, 256, 4096), (512, 256, 1024
           (512, 512, 256), (256, 256, 16384), (128, 128, 65536), (512, 512, 4096), (96, 96, 4100)]
 
 
+# tile:xcd:prefetch variants of the general kernel (NFI_GEMM_TILE, NFI_GEMM_XCD, NFI_GEMM_PF)
+VARIANTS = [v.split(':') for v in os.environ.get('GEMM_VARIANTS', '22:0:1 22:1:1 22:0:2 22:1:2').split()]
+
+
 def _p(t):
     return ctypes.c_void_p(t.data_ptr())
 
@@ -57,12 +61,16 @@ def main():
         ref = torch.bmm(A.double(), B.double()).float()
         t_bmm = timeit(lambda: torch.bmm(A, B))
         res = []
-        for kern in ('0', '2'):
-            os.environ['NFI_GEMM_KERNEL'] = kern
+        for tile, xcd, pf in VARIANTS:
+            os.environ['NFI_GEMM_TILE'] = tile
+            os.environ['NFI_GEMM_XCD'] = xcd
+            os.environ['NFI_GEMM_PF'] = pf
+            C.zero_()
             t = timeit(gemm)
             err = float((C - ref).abs().max())
-            res.append(f'k{kern} {t:7.3f} ms ({fl / t / 1e9:6.1f} TF, err {err:.1e})')
-        os.environ.pop('NFI_GEMM_KERNEL')
+            res.append(f't{tile}x{xcd}p{pf} {t:6.3f} ms ({fl / t / 1e9:5.1f} TF{", err %.0e" % err if err > 2e-4 else ""})')
+        for k in ('NFI_GEMM_TILE', 'NFI_GEMM_XCD', 'NFI_GEMM_PF'):
+            os.environ.pop(k)
         mb = 36 * (Ci + Co) * P * 4 / 1e6
         print(f'Co {Co:4d} Ci {Ci:4d} P {P:6d} ({mb:5.0f} MB): bmm {t_bmm:7.3f} ms ({fl / t_bmm / 1e9:6.1f} TF)  '
               + '  '.join(res) + f'  pack {t_pack:.3f} ms', flush=True)

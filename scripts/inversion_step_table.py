@@ -23,6 +23,8 @@ def dur(x):
 
 
 def group(name):
+    if 'nfi::gemm::' in name:
+        return 'GEMMs (nfi split-f16)'
     if 'nfi::syn::lpips' in name:
         return 'LPIPS distance head (nfi HIP)'
     if 'nfi::wino::' in name:
