@@ -245,7 +245,7 @@ def inversion_leg(args, dev, cfg, world, loss):
     (nfi.synthetic.cameras), a synthetic target image.  Timed like the renderer leg (barrier +
     synchronize around exactly --inv-steps steps, max over ranks); the final all_gather of the
     results is inside the timed region."""
-    from nfi import inversion, lpips, ops, parallel, producer, synthetic
+    from nfi import conv as _conv, inversion, lpips, ops, parallel, producer, synthetic
     sr, wbg, flipped, _, H, S, pose, bwd = cfg
     progress(f'inversion leg ({loss})')
     B = args.inv_batch * world      # the global step batch
@@ -300,8 +300,11 @@ def inversion_leg(args, dev, cfg, world, loss):
                                    'package offline)' if net is not None else ''),
             'loss_first_last': [round(res.losses[0], 5), round(res.losses[-1], 5)],
             'producer': 'StyleGAN2 synthesis 256^2x96 + AttentionMapper, fp32: 3x3 convs Winograd F(4,3) '
-                        '(nfi HIP transforms + hipBLASLt batched GEMM), up-sampling convs as one 9-tap GEMM + HIP FIR, '
-                        'epilogues/FIR/skip/modulation-backward nfi HIP',
+                        + ('(nfi HIP transforms + nfi split-f16 batched GEMM, fp32-accurate), up-sampling convs as one '
+                           '9-tap GEMM (split-f16 for maps >= 32^2, else hipBLASLt) + HIP FIR, '
+                           if _conv.SPLIT16 else '(nfi HIP transforms + hipBLASLt batched GEMM), up-sampling convs as '
+                                                 'one 9-tap GEMM + HIP FIR, ')
+                        + 'epilogues/FIR/skip/modulation-backward nfi HIP',
             'renderer': 'nfi HIP fwd+bwd',
             'step_replay': ('HIP graph of the whole step (captured in the warm-up batch, reused)'
                             if icfg.graph else 'eager launches')}
