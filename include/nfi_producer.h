@@ -187,6 +187,14 @@ int32_t nfi_wino_output_transform_scaled_grad(const float* M, const float* x, co
  * nfi_wino_packed_size floats).  Ci % 8 == 0, H and W multiples of 4, x and y 16-byte aligned. */
 int64_t nfi_wino_packed_size(int32_t Co, int32_t Ci);
 int32_t nfi_wino_pack_weights(const float* U, float* Ua, int32_t Co, int32_t Ci, void* stream);
+/* nfi_wino_conv_fused_split: the same convolution (+ bias/ReLU/pool epilogue) with the products on the
+ * f16 matrix cores (split-f16, fp32-level error): Uh, Ul, uinv = nfi_split16_pack of U [36][Co][Ci]
+ * (batch 36).  A workgroup: 16 x 16 outputs of one image x 64 output channels, the K reduction in
+ * chunks of 32 channels and the 36 products consumed by the output transform one Winograd row at a
+ * time.  Ci % 32 == 0, Co % 64 == 0, H and W multiples of 16. */
+int32_t nfi_wino_conv_fused_split(const float* x, const uint16_t* Uh, const uint16_t* Ul, const float* uinv,
+                                  const float* bias, float* y, float* pooled, int32_t N, int32_t Ci, int32_t Co,
+                                  int32_t H, int32_t W, void* stream);
 int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, float* y, float* pooled,
                             int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W, void* stream);
 
@@ -215,11 +223,12 @@ int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gim
  * nfi_split16_pack: A [batch][per] -> hi, lo [batch][per] (fp16 bits) and a_inv [batch] = 2^-e, with
  *   the largest |A[b]| 2^e in [2^14, 2^15) (one workgroup per batch entry; frozen operands: once).
  * nfi_wino_input_transform_max: nfi_wino_input_transform_scaled (scale may be NULL) or, with relu_y,
- *   the ReLU-masked gradient transform, also leaving the running maximum of |V| in vmax[64] (float
- *   bits; zeroed by the call).
- * nfi_absmax_slots: the same running maximum of any x [n] (zeroes slots[64] first).
- * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max[64] from one of the above,
- *   C [batch][M][N] fp32 (written); K a multiple of 32.  N % 4 == 0 with 16-B aligned B and C takes
+ *   the ReLU-masked gradient transform, also leaving the running maximum of |V| in vmax[0..63] (float
+ *   bits).  vmax[0..64] must hold zeros on entry: a zeroed buffer, or one a split GEMM has consumed.
+ * nfi_absmax_slots: the same running maximum of any x [n] (zeroes slots[0..64] first).
+ * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max[65] from one of the above,
+ *   C [batch][M][N] fp32 (written); K a multiple of 32.  b_max[64] is a completion counter: the
+ *   launch's last workgroup returns b_max[0..64] to zero (no memset before the next producer).  N % 4 == 0 with 16-B aligned B and C takes
  *   the wide-load kernel, else the general one (NFI_GEMM_KERNEL=1 forces the general one).
  * nfi_gemm_split16_shared_a: the same with ONE A [M][K] (and a_inv[0]) for every batch entry — the
  *   up-sampling convolutions' 9-tap weight matrix against each image (stylegan.py:99-101) — and K

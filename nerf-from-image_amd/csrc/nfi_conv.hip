@@ -20,6 +20,8 @@
 // F.conv2d(x, w, padding=1) as the LPIPS VGG16 trunk (lpips 0.1 via lib/metrics.py:107) and the
 // synthesis layers (models/stylegan.py:130-145) call it; the reference runs fp32 with TF32 off
 // (run.py:59-60), which this keeps (fp32 transforms, fp32 GEMM).
+#include <type_traits>
+
 #include "nfi_common.h"
 #include "nfi_host.h"
 #include "../../include/nfi_producer.h"
@@ -558,6 +560,305 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused convolution on the f16 matrix cores (round 4): input transform -> 36 products -> output
+// transform in one kernel, the products as the split-f16 GEMM's (hi + lo halves of
+// power-of-two-scaled fp32 operands, three f16 products each, fp32 accumulation: csrc/nfi_gemm.hip).
+// A workgroup owns a 4 x 4 block of tiles (16 x 16 outputs of one image) and 64 output channels
+// (wave w: channels 16w..16w+15, one 16 x 16 MFMA block of (channel, tile)).  The order is the
+// transpose of fused_kernel's: the Winograd elements e = (e1, e2) are the OUTER loop and the channel
+// chunks of 32 the outermost, so each product's accumulators are consumed by the output transform
+// as soon as they are complete — y = sum over chunks and e of A^T-weights x M_e is linear — and no
+// 36-product accumulator set is ever live (fused_kernel: 288 registers, one wave per SIMD; here
+// 64 output accumulators per lane).  Per chunk: the 32-channel 18 x 18 input region is staged in LDS
+// (rows of 28 floats: the 16 interior columns as aligned float4 at column 4, the halo at 3 and 20);
+// per e1, each thread forms row e1 of B^T d (from the 4-5 patch rows that row reads) and its six
+// B-transformed values for 2 channels of one tile, splits them (one power of two per chunk from the
+// region's largest |x|: |V| <= 49 max|x|) and writes them as the B operands of the six products
+// (e1, 0..5); the 6 x 3 MFMAs per wave follow, their results are unscaled, taken through A^T along
+// e2 and added into the 4 x 4 outputs with A^T's e1 weights.
+// MEASURED SLOWER than fused_kernel (64->64 @128^2, 64 images: 0.68 vs 0.48-0.51 ms; scripts/wino_layers.py)
+// though half its error (1e-6 vs 2e-6 of the largest output): the compiler keeps ~300 registers live
+// (one wave per SIMD) and each Winograd row's A-operand loads and two barriers are exposed.  Kept
+// behind NFI_FUSED_SPLIT=1 (conv.FUSED_SPLIT, default off) with its test.
+#ifndef NFI_FSPLIT_OCC
+#define NFI_FSPLIT_OCC 1   // workgroups per CU the register budget is set for (2: spills)
+#endif
+constexpr int XT = 16;                  // tiles per workgroup (4 x 4)
+constexpr int XKC = 32;                 // channels per chunk
+constexpr int XRW = 28;                 // LDS region row (floats): 112-B rows spread a half-wave's b128 reads
+constexpr int XRH = 18;
+constexpr int XREG = XKC * XRH * XRW;   // floats
+constexpr int XVK = XKC + 8;            // halves per V row
+constexpr int XVG = 6 * XT * XVK;       // halves per V group image
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma_h16(u4v a, u4v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ unsigned short hbits(float v) { return __builtin_bit_cast(unsigned short, (_Float16)v); }
+__device__ __forceinline__ float hval(unsigned short b) { return (float)__builtin_bit_cast(_Float16, b); }
+
+// B^T row e1 applied down the 6 patch rows: t = sum_i B^T[e1][i] d[i] (bt_col's coefficients)
+template <int E1>
+__device__ __forceinline__ float bt_row(const float (&d)[6]) {
+  if constexpr (E1 == 0) return (d[0] - 2.f * d[2] + d[4]) + 1.5f * (d[1] - d[3]);
+  if constexpr (E1 == 1) return (d[4] - d[1]) - 2.5f * d[2] - 0.5f * d[3];
+  if constexpr (E1 == 2) return (d[1] + d[4]) + 0.5f * d[2] - 2.5f * d[3];
+  if constexpr (E1 == 3) return (d[4] - d[2]) + 0.5f * (d[3] - d[1]);
+  if constexpr (E1 == 4) return (d[4] - d[2]) + 2.f * (d[1] - d[3]);
+  return (d[1] - 2.f * d[3] + d[5]) + 1.5f * (d[2] - d[4]);
+}
+// A^T[o][e] (at_col's coefficients)
+__device__ __forceinline__ constexpr float at_w(int o, int e) {
+  return o == 0 ? (e == 5 ? 0.f : 1.f)
+       : o == 1 ? (e == 0 ? 0.f : e == 1 ? 1.f : e == 2 ? -1.f : e == 3 ? 2.f : e == 4 ? -0.5f : 0.f)
+       : o == 2 ? (e == 0 ? 0.f : e == 1 ? 1.f : e == 2 ? 1.f : e == 3 ? 4.f : e == 4 ? 0.25f : 0.f)
+                : (e == 0 ? 0.f : e == 1 ? 1.f : e == 2 ? -1.f : e == 3 ? 8.f : e == 4 ? -0.125f : 1.f);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p, int bytes) {
+  const uint64_t pb = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pb), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+struct SplitConvArgs {
+  const float* x;               // [N][Ci][H][W]
+  const unsigned short* Uh;     // [36][Co][Ci] f16 bits (nfi_split16_pack of U)
+  const unsigned short* Ul;
+  const float* uinv;            // [36]
+  const float* bias;            // [Co] or null (no epilogue)
+  float* y;                     // [N][Co][H][W]
+  float* pooled;                // [N][Co][H/2][W/2] or null
+  int Ci, Co, H, W, BX, BY;     // BX, BY: 16 x 16 blocks per row / column
+};
+
+template <int E1>
+__device__ __forceinline__ void split_e1(const float* __restrict__ reg, unsigned short* __restrict__ vh,
+                                        unsigned short* __restrict__ vl, int t, int q, float sx) {
+  const int ty = t >> 2, tx = t & 3;
+  unsigned hw[6], lw[6];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float* base = reg + (2 * q + c) * (XRH * XRW) + (4 * ty) * XRW + 4 * tx + 3;
+    float d[6][6];   // the patch (rows B^T[e1] does not read are dead loads, removed)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const float* rp = base + i * XRW;
+      const f4v m = *reinterpret_cast<const f4v*>(rp + 1);
+      d[i][0] = rp[0];
+      d[i][1] = m[0];
+      d[i][2] = m[1];
+      d[i][3] = m[2];
+      d[i][4] = m[3];
+      d[i][5] = rp[5];
+    }
+    float tr[6];   // row e1 of B^T d (stage_patch's first pass, one row of it)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const float col[6] = {d[0][j], d[1][j], d[2][j], d[3][j], d[4][j], d[5][j]};
+      tr[j] = bt_row<E1>(col);
+    }
+    float v[6];    // (B^T d B)[e1][0..5]
+    bt_col(tr, v);
+#pragma unroll
+    for (int e2 = 0; e2 < 6; ++e2) {
+      const float a = v[e2] * sx;
+      const unsigned short h = hbits(a), lo = hbits(a - hval(h));
+      if (c == 0) {
+        hw[e2] = h;
+        lw[e2] = lo;
+      } else {
+        hw[e2] |= (unsigned)h << 16;
+        lw[e2] |= (unsigned)lo << 16;
+      }
+    }
+  }
+#pragma unroll
+  for (int e2 = 0; e2 < 6; ++e2) {
+    // (lds_st keeps the compiler from pairing these into ds_write2 stores, which need the gap)
+    lds_st(reinterpret_cast<unsigned*>(vh + (e2 * XT + t) * XVK + 2 * q), hw[e2]);
+    lds_st(reinterpret_cast<unsigned*>(vl + (e2 * XT + t) * XVK + 2 * q), lw[e2]);
+  }
+}
+
+template <int E1>
+__device__ __forceinline__ void products_e1(const SplitConvArgs& g, const unsigned short* __restrict__ vh,
+                                            const unsigned short* __restrict__ vl, const u4v (&ah)[6],
+                                            const u4v (&al)[6], float fsc, float (&Y)[4][4][4]) {
+  const int l = lane_id(), i16 = l & 15, kg = l >> 4;
+  // lane (i16, kg): channel 4kg + r of the wave's 16, tile i16.  S = A^T along e2, folded in per
+  // product (A^T is linear in its six inputs), then the e1 weights into the 4 x 4 outputs
+  float S[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) S[r][o] = 0.f;
+#pragma unroll
+  for (int e2 = 0; e2 < 6; ++e2) {
+    const int rr = (e2 * XT + i16) * XVK + 8 * kg;
+    const u4v bh = *reinterpret_cast<const u4v*>(vh + rr);
+    const u4v bl = *reinterpret_cast<const u4v*>(vl + rr);
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    acc = mfma_h16(al[e2], bh, acc);   // small terms first
+    acc = mfma_h16(ah[e2], bl, acc);
+    acc = mfma_h16(ah[e2], bh, acc);
+    const float f = g.uinv[6 * E1 + e2] * fsc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float m = acc[r] * f;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        const float w = at_w(o, e2);
+        if (w != 0.f) S[r][o] = fmaf(w, m, S[r][o]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int oy = 0; oy < 4; ++oy) {
+      const float w = at_w(oy, E1);
+      if (w != 0.f) {
+#pragma unroll
+        for (int ox = 0; ox < 4; ++ox) Y[r][oy][ox] = fmaf(w, S[r][ox], Y[r][oy][ox]);
+      }
+    }
+}
+
+__global__ void __launch_bounds__(256, NFI_FSPLIT_OCC) fused_split_kernel(SplitConvArgs g) {
+  __shared__ __attribute__((aligned(16))) float lds[XREG + XVG + 8];   // region, V hi + lo, 4 maxima
+  float* reg = lds;
+  unsigned short* vh = reinterpret_cast<unsigned short*>(lds + XREG);
+  unsigned short* vl = vh + XVG;
+  float* red = lds + XREG + XVG;
+  const int tid = threadIdx.x, l = lane_id(), w = tid >> 6;
+  const int blk = blockIdx.x;                      // (image, block row, block column)
+  const int bx = blk % g.BX, by = (blk / g.BX) % g.BY, n = blk / (g.BX * g.BY);
+  const int co0 = blockIdx.y * 64;
+  const int H = g.H, W = g.W, Ci = g.Ci;
+  const int64_t HW = (int64_t)H * W;
+  const float* xn = g.x + (int64_t)n * Ci * HW;
+  const int i16 = l & 15, kg = l >> 4;
+  const int t = tid & 15, q = tid >> 4;            // V role: tile t, channels 2q, 2q+1 of the chunk
+  float Y[4][4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) Y[r][a][b] = 0.f;
+  // A operands: U[e][co0 + 16w + i16][chunk + 8kg .. +7] (byte offsets: lane uoff, product ue2)
+  const int uoff = ((co0 + 16 * w + i16) * Ci + 8 * kg) * 2;
+  const int ue2 = g.Co * Ci * 2;
+  const __amdgpu_buffer_rsrc_t urs_h = wave_rsrc(g.Uh, 36 * ue2), urs_l = wave_rsrc(g.Ul, 36 * ue2);
+  const __amdgpu_buffer_rsrc_t xrs = wave_rsrc(xn, (int)(Ci * HW * 4));
+  for (int c0 = 0; c0 < Ci; c0 += XKC) {
+    // ---- stage the 32-channel region: 576 rows of 4 float4 (9 per thread) + 2 halo floats ----
+    // (all loads issued at clamped addresses before any is used; padding by selects afterwards)
+    f4v rv[9];
+    float hv[5];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int k = tid + 256 * i, r = k >> 2, ci = r / XRH, rr = r - ci * XRH;
+      const int yy = min(max(16 * by - 1 + rr, 0), H - 1);
+      rv[i] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                          xrs, ((c0 + ci) * (int)HW + yy * W + 16 * bx + 4 * (k & 3)) * 4, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = min(tid + 256 * i, 2 * XKC * XRH - 1), r = k >> 1, ci = r / XRH, rr = r - ci * XRH;
+      const int yy = min(max(16 * by - 1 + rr, 0), H - 1);
+      const int xx = (k & 1) ? min(16 * bx + 16, W - 1) : max(16 * bx - 1, 0);
+      hv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, ((c0 + ci) * (int)HW + yy * W + xx) * 4, 0, 0));
+    }
+    float mx = 0.f;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int k = tid + 256 * i, r = k >> 2, ci = r / XRH, rr = r - ci * XRH;
+      const int yy = 16 * by - 1 + rr;
+      const f4v z = (yy >= 0 && yy < H) ? rv[i] : f4v{0.f, 0.f, 0.f, 0.f};
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(z[0]), fabsf(z[1])), fmaxf(fabsf(z[2]), fabsf(z[3]))));
+      lds_st_fenced(reinterpret_cast<f4v*>(reg + (ci * XRH + rr) * XRW + 4 + 4 * (k & 3)), z);
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int k = tid + 256 * i, r = min(k, 2 * XKC * XRH - 1) >> 1, ci = r / XRH, rr = r - ci * XRH;
+      const int yy = 16 * by - 1 + rr;
+      const int xx = (k & 1) ? 16 * bx + 16 : 16 * bx - 1;
+      const float z = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? hv[i] : 0.f;
+      mx = fmaxf(mx, fabsf(z));
+      if (k < 2 * XKC * XRH) reg[(ci * XRH + rr) * XRW + ((k & 1) ? 20 : 3)] = z;
+    }
+    mx = wave_max(mx);
+    if (l == 0) red[w] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    // one power of two for the chunk: 49 max|x| (the B^T row sums squared) to [2^14, 2^15)
+    const float m49 = 49.f * mx;
+    int ex = 15 - __builtin_amdgcn_frexp_expf(m49);
+    ex = (m49 > 0.f && m49 < __builtin_inff()) ? min(max(ex, -120), 120) : 0;
+    const float sx = __builtin_ldexpf(1.f, ex), isx = __builtin_ldexpf(1.f, -ex);
+    auto group = [&](auto e1c) {
+      constexpr int E1 = decltype(e1c)::value;
+      split_e1<E1>(reg, vh, vl, t, q, sx);
+      // the six products' A operands (L2-resident U halves), in flight across the barrier.  Buffer
+      // loads (lane offset in a VGPR, product offset in an SGPR: global loads made the compiler hoist
+      // all 36 products' 64-bit addresses out of the chunk loop), the offset through an empty
+      // volatile asm that stays behind the previous barrier (no hoisting of later groups' loads)
+      int sbase = 6 * E1 * ue2;
+      asm volatile("" : "+s"(sbase));
+      u4v ah[6], al[6];
+#pragma unroll
+      for (int e2 = 0; e2 < 6; ++e2) {
+        const int so = sbase + e2 * ue2;
+        ah[e2] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(urs_h, uoff + 2 * c0, so, 0));
+        al[e2] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(urs_l, uoff + 2 * c0, so, 0));
+      }
+      __syncthreads();
+      products_e1<E1>(g, vh, vl, ah, al, isx, Y);
+      __syncthreads();
+    };
+    group(std::integral_constant<int, 0>{});
+    group(std::integral_constant<int, 1>{});
+    group(std::integral_constant<int, 2>{});
+    group(std::integral_constant<int, 3>{});
+    group(std::integral_constant<int, 4>{});
+    group(std::integral_constant<int, 5>{});
+  }
+  // ---- epilogue: lane (i16, kg) holds channels co0 + 16w + 4kg + r of tile i16 ----
+  const int ty = i16 >> 2, tx = i16 & 3;
+  const int oy0 = 16 * by + 4 * ty, ox0 = 16 * bx + 4 * tx;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = co0 + 16 * w + 4 * kg + r;
+    if (co >= g.Co) continue;
+    float o[4][4];
+    const float b = g.bias ? g.bias[co] : 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o[a][c] = g.bias ? fmaxf(Y[r][a][c] + b, 0.f) : Y[r][a][c];
+    float* dst = g.y + (((int64_t)n * g.Co + co) * H + oy0) * W + ox0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      *reinterpret_cast<float4*>(dst + (int64_t)a * W) = make_float4(o[a][0], o[a][1], o[a][2], o[a][3]);
+    if (g.pooled) {
+      const int W2 = W >> 1, H2 = H >> 1;
+      float* pd = g.pooled + (((int64_t)n * g.Co + co) * H2 + (oy0 >> 1)) * W2 + (ox0 >> 1);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        *reinterpret_cast<float2*>(pd + (int64_t)a * W2) =
+            make_float2(fmaxf(fmaxf(o[2 * a][0], o[2 * a][1]), fmaxf(o[2 * a + 1][0], o[2 * a + 1][1])),
+                        fmaxf(fmaxf(o[2 * a][2], o[2 * a][3]), fmaxf(o[2 * a + 1][2], o[2 * a + 1][3])));
+    }
+  }
+}
+
 }  // namespace wino
 }  // namespace nfi
 
@@ -611,7 +912,8 @@ int32_t nfi_wino_input_transform_max(const float* x, const float* scale, const f
               "wino_input_transform_max: bad shape (H, W multiples of 4)");
   NFI_REQUIRE(((uintptr_t)x & 15) == 0 && (relu_y == nullptr || ((uintptr_t)relu_y & 15) == 0),
               "wino_input_transform_max: misaligned");
-  NFI_REQUIRE(hipMemsetAsync(vmax, 0, 64 * 4, (hipStream_t)stream) == hipSuccess, "wino_input_transform_max: memset");
+  // (no memset: vmax holds zeros on entry — a zeroed buffer, or one a split GEMM has consumed, which
+  //  returns its 64 slots and completion counter to zero; include/nfi_producer.h)
   const int TW = W / 4, T = (H / 4) * TW;
   const int64_t P = (int64_t)N * T;
   hipLaunchKernelGGL(input_kernel, dim3((unsigned)((P + 255) / 256), C), dim3(256), 0,
@@ -695,6 +997,29 @@ int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, 
   hipLaunchKernelGGL(fused_kernel, dim3((unsigned)G), dim3(256), 0, (hipStream_t)stream, x, Ua, bias, y, pooled,
                      Ci, Co, H, W, TW, T, P, CoP / 16, bias ? 1 : 0, (int)nPB, (int)nCB);
   NFI_CHECK_LAUNCH("wino fused_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_wino_conv_fused_split(const float* x, const uint16_t* Uh, const uint16_t* Ul, const float* uinv,
+                                  const float* bias, float* y, float* pooled, int32_t N, int32_t Ci, int32_t Co,
+                                  int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(x && Uh && Ul && uinv && y, "wino_conv_fused_split: null pointer");
+  NFI_REQUIRE(N > 0 && Ci > 0 && Ci % XKC == 0 && Co > 0 && Co % 64 == 0 && H >= 16 && W >= 16 && H % 16 == 0 &&
+                  W % 16 == 0,
+              "wino_conv_fused_split: bad shape (Ci %% 32, Co %% 64, H %% 16, W %% 16 must be 0)");
+  NFI_REQUIRE(pooled == nullptr || bias != nullptr, "wino_conv_fused_split: pooling needs the bias/ReLU epilogue");
+  NFI_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && (pooled == nullptr || ((uintptr_t)pooled & 7) == 0) &&
+                  ((uintptr_t)Uh & 15) == 0 && ((uintptr_t)Ul & 15) == 0,
+              "wino_conv_fused_split: misaligned tensors");
+  const int BX = W / 16, BY = H / 16;
+  const int64_t nb = (int64_t)N * BX * BY;
+  NFI_REQUIRE(nb < (1ll << 31) && Co / 64 <= 65535 && (int64_t)Ci * H * W * 4 < (1ll << 31) &&
+                  (int64_t)36 * Co * Ci * 2 < (1ll << 31),
+              "wino_conv_fused_split: too large (32-bit buffer offsets)");
+  SplitConvArgs g{x, reinterpret_cast<const unsigned short*>(Uh), reinterpret_cast<const unsigned short*>(Ul), uinv,
+                  bias, y, pooled, Ci, Co, H, W, BX, BY};
+  hipLaunchKernelGGL(fused_split_kernel, dim3((unsigned)nb, (unsigned)(Co / 64)), dim3(256), 0, (hipStream_t)stream, g);
+  NFI_CHECK_LAUNCH("wino fused_split_kernel");
   return NFI_OK;
 }
 

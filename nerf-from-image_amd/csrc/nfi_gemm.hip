@@ -99,6 +99,23 @@ struct Args {
   int xcd;                    // 1: XCD-major tile order (below)
 };
 
+// The B maxima are consumed, not copied: b_max[0..63] (float bits) + b_max[64] (a completion counter)
+// return to zero when the launch's last workgroup finishes, so the producer of the next maxima needs
+// no memset launch.  Every workgroup read b_max at its start, before its first barrier; the one whose
+// increment completes the count runs after all of those reads.  Relaxed atomics, no fence: a
+// release fence at agent scope writes back the L2 (measured: the inversion step 16 -> 20 ms).
+__device__ __forceinline__ void release_slots(const unsigned* b_max) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* bm = const_cast<unsigned*>(b_max);
+    const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+    if (__hip_atomic_fetch_add(bm + SLOTS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+      for (int i = 0; i < SLOTS; ++i) __hip_atomic_store(bm + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bm + SLOTS, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs in linear order (x fastest), each XCD with
 // its own L2.  XCD-major order: the tiles an XCD runs are a contiguous range of (n block fastest, m
 // block, batch entry), so the tiles sharing an A row block or a B column slab meet in one L2 instead of
@@ -262,6 +279,7 @@ __global__ void __launch_bounds__(64 * WM * WN, WM * WN == 4 ? (PF == 1 ? 3 : 2)
         if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * out_scale;
       }
     }
+  release_slots(g.b_max);
 }
 
 // ---- the product, N % 4 == 0: wide loads and stores ----------------------------------------------
@@ -394,6 +412,7 @@ __global__ void __launch_bounds__(256, 2) split16_gemm4_kernel(Args g) {
       if (m < M && n < N) *reinterpret_cast<f4v*>(Cg + (long long)m * N + n) = acc[y][x] * out_scale;
     }
   }
+  release_slots(g.b_max);
 }
 
 // C = sum over s of work[s] (fixed order: deterministic), float4 per thread
@@ -440,7 +459,7 @@ int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* A
 
 int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* stream) {
   NFI_REQUIRE(x && slots && n > 0, "absmax_slots: bad arguments");
-  NFI_REQUIRE(hipMemsetAsync(slots, 0, gemm::SLOTS * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
+  NFI_REQUIRE(hipMemsetAsync(slots, 0, (gemm::SLOTS + 1) * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
   const long long blocks = std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(gemm::absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long long)n,
                      slots);

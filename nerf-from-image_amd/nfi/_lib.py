@@ -175,6 +175,7 @@ SIGNATURES = {
     'nfi_wino_output_transform': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_wino_packed_size': (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    'nfi_wino_conv_fused_split': (ctypes.c_int32, [c_void_p] * 7 + [ctypes.c_int32] * 5 + [c_void_p]),
     'nfi_wino_input_transform_relu_grad': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_wino_output_transform_scaled_grad': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_wino_pack_weights': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32, c_void_p]),

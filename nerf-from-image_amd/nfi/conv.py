@@ -41,6 +41,14 @@ FUSED = True          # one fused kernel per layer (nfi_wino_conv_fused) for lay
 # NFI_FUSED_MAX_CI=128 measured 18.9 vs 18.8 ms) — and loses on the deeper ones (512->512 @16^2: 0.32 vs
 # 0.21 ms); scripts/wino_layers.py.
 FUSED_MAX_CI = int(os.environ.get('NFI_FUSED_MAX_CI', '64'))
+# ... and output channels: with the split-f16 GEMM (round 4) the three-pass form wins 64->128 @64^2
+# (0.220 vs 0.263 ms) while the fused kernel keeps 64->64 @128^2 (0.48-0.51 vs 0.62 ms)
+FUSED_MAX_CO = int(os.environ.get('NFI_FUSED_MAX_CO', '64'))
+
+
+def _fused_ok(Uw, Ci, Co):
+    """Whether a layer with these channel counts runs as the fused kernel."""
+    return FUSED and Uw.packed is not None and Ci <= FUSED_MAX_CI and (Co <= FUSED_MAX_CO or not SPLIT16)
 # the VGG blocks' ReLU threshold_backward inside the data gradient's input transform (no pool
 # gradient; three-pass layers)
 RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
@@ -49,16 +57,21 @@ RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
 # transform's running maximum); 0: torch.bmm (hipBLASLt fp32)
 SPLIT16 = os.environ.get('NFI_SPLIT16', '1') != '0'
 SPLIT16_BK = 32       # the split GEMM's K step: channel counts must be multiples of it
+# the fused layers on the f16 matrix cores (nfi_wino_conv_fused_split: products consumed by the output
+# transform one Winograd row at a time) where the shapes allow — measured slower than fused_kernel's
+# fp32 MFMAs (0.68 vs 0.48-0.51 ms on the 64->64 @128^2 layer), so off unless NFI_FUSED_SPLIT=1
+FUSED_SPLIT = os.environ.get('NFI_FUSED_SPLIT', '0') != '0'
 
 
 class WeightSet:
     """One orientation of a frozen 3x3 weight, transformed: U [36, M, K] fp32 (the hipBLASLt
     product), `packed` (the fused kernel's MFMA operands, or None) and `split` = (hi, lo, inverse
     scales) f16 halves for the split-f16 product (or None)."""
-    __slots__ = ('U', 'packed', 'split')
+    __slots__ = ('U', 'packed', 'split', 'vmax')
 
     def __init__(self, U, packed, split):
         self.U, self.packed, self.split = U, packed, split
+        self.vmax = {}   # stream -> the split product's maxima slots (self-clearing: see _slots)
 
 
 def _p(t):
@@ -129,7 +142,7 @@ def split_matmul_shared(As, X):
     Mrows = hi.shape[1]
     assert hi.shape[2] == K, (hi.shape, X.shape)
     st = _stream(X.device)
-    slots = torch.empty((64,), device=X.device, dtype=torch.int32)
+    slots = torch.empty((128,), device=X.device, dtype=torch.int32)   # 64 maxima + the GEMM's counter
     _call('nfi_absmax_slots', _p(X), X.numel(), _p(slots), st)
     C = torch.empty((B, Mrows, N), device=X.device)
     ks = ksplit(B * -(-Mrows // 128) * -(-N // 128), K) if (Mrows * N) % 4 == 0 else 1
@@ -147,6 +160,18 @@ def ksplit(tiles, K):
     return max(1, min(K // 256, -(-512 // tiles)))
 
 
+def _slots(Uw: WeightSet, device):
+    """The maxima slots of this layer's split products on the current stream: 64 running maxima + a
+    completion counter, zeroed once; the input transform fills them and the GEMM's last workgroup
+    returns them to zero (include/nfi_producer.h), so no memset per call.  One buffer per stream: the
+    LPIPS target features run the same layers on a side stream."""
+    key = torch.cuda.current_stream(device).cuda_stream
+    buf = Uw.vmax.get(key)
+    if buf is None:
+        buf = Uw.vmax[key] = torch.zeros((128,), device=device, dtype=torch.int32)
+    return buf
+
+
 def _product(Uw: WeightSet, x, scale=None, relu_y=None):
     """Input transform of x [N, K, H, W] (times scale [N, K]; through the ReLU mask of relu_y) and
     the 36 products with the transformed weights: M [36, Mrows, P]."""
@@ -156,7 +181,7 @@ def _product(Uw: WeightSet, x, scale=None, relu_y=None):
     V = torch.empty((36, K, P), device=x.device)
     if SPLIT16 and Uw.split is not None:
         hi, lo, inv = Uw.split
-        vmax = torch.empty((64,), device=x.device, dtype=torch.int32)
+        vmax = _slots(Uw, x.device)
         _call('nfi_wino_input_transform_max', _p(x), _p(scale), _p(relu_y), _p(V), _p(vmax), N, K, H, W, st)
         Mrows = Uw.U.shape[1]
         M = torch.empty((36, Mrows, P), device=x.device)
@@ -188,11 +213,17 @@ def _winograd(x, Uw, bias=None, pool=False, scale=None):
     st = _stream(x.device)
     y = torch.empty((N, Co, H, W), device=x.device)
     m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
-    if scale is not None and FUSED and Ua is not None and Ci <= FUSED_MAX_CI:
+    fused = _fused_ok(Uw, Ci, Co)
+    if scale is not None and fused:
         x = x * scale[:, :, None, None]          # (the fused kernel takes no scale)
         scale = None
-    if FUSED and Ua is not None and Ci <= FUSED_MAX_CI:
-        _call('nfi_wino_conv_fused', _p(x), _p(Ua), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
+    if fused:
+        if FUSED_SPLIT and Uw.split is not None and Co % 64 == 0 and H % 16 == 0 and W % 16 == 0:
+            hi, lo, inv = Uw.split
+            _call('nfi_wino_conv_fused_split', _p(x), _p(hi), _p(lo), _p(inv), _p(bias), _p(y), _p(m), N, Ci, Co,
+                  H, W, st)
+        else:
+            _call('nfi_wino_conv_fused', _p(x), _p(Ua), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
         return (y, m) if pool else y
     M = _product(Uw, x, scale)
     _call('nfi_wino_output_transform', _p(M), _p(bias), _p(y), _p(m), N, Co, H, W, st)
@@ -250,8 +281,7 @@ class _ModConv(torch.autograd.Function):
         ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
         st = _stream(x.device)
         Co = g.shape[1]
-        Uta = ctx.Ut.packed
-        if DGRAD and not (FUSED and Uta is not None and Co <= FUSED_MAX_CI):
+        if DGRAD and not _fused_ok(ctx.Ut, Co, C):
             # three-pass data gradient, the scale backward in its output transform
             M = _product(ctx.Ut, g)
             _call('nfi_wino_output_transform_scaled_grad', _p(M), _p(x), _p(s), _p(gx), _p(ds), B, C, H, W, st)
@@ -285,8 +315,7 @@ class _VggBlock(torch.autograd.Function):
         N, C, H, W = y.shape
         gy = None if gy is None else gy.contiguous()
         gm = None if gm is None else gm.contiguous()
-        Uta = ctx.Ut.packed
-        if RELU_IN_TRANSFORM and gm is None and DGRAD and not (FUSED and Uta is not None and C <= FUSED_MAX_CI):
+        if RELU_IN_TRANSFORM and gm is None and DGRAD and not _fused_ok(ctx.Ut, C, ctx.Ut.U.shape[1]):
             # no pool gradient: the ReLU threshold inside the data gradient's input transform
             st = _stream(y.device)
             M = _product(ctx.Ut, gy, relu_y=y)

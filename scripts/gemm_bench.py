@@ -51,7 +51,7 @@ def main():
         hi = torch.empty(A.shape, device=DEV, dtype=torch.int16)
         lo = torch.empty(A.shape, device=DEV, dtype=torch.int16)
         inv = torch.empty((36,), device=DEV)
-        slots = torch.empty((64,), device=DEV, dtype=torch.int32)
+        slots = torch.empty((128,), device=DEV, dtype=torch.int32)   # 64 maxima + counter
         t_pack = timeit(lambda: _lib.check(lib.nfi_split16_pack(_p(A), 36, Co * Ci, _p(hi), _p(lo), _p(inv), st), 'pack'))
         _lib.check(lib.nfi_absmax_slots(_p(B), B.numel(), _p(slots), st), 'absmax')
         C = torch.empty((36, Co, P), device=DEV)

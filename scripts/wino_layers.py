@@ -38,9 +38,9 @@ def main():
         Uw, _ = conv.weights(w)
         res = []
         for fused in (True, False):
-            conv.FUSED, conv.FUSED_MAX_CI = fused, 1 << 20
+            conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO = fused, 1 << 20, 1 << 20
             res.append(timeit(lambda: conv._winograd(x, Uw, b, False)))
-        conv.FUSED, conv.FUSED_MAX_CI = True, 64
+        conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO = True, 64, 64
         # the three-pass form with hipBLASLt's fp32 GEMM instead of the split-f16 product
         conv.FUSED, conv.SPLIT16 = False, False
         t_bmm = timeit(lambda: conv._winograd(x, Uw, b, False))

@@ -89,11 +89,11 @@ def test_fused_kernel_matches_three_pass(N, Ci, Co, H, W, pool):
     assert Uw.packed is not None
     outs = []
     for fused in (True, False):
-        conv.FUSED, conv.FUSED_MAX_CI = fused, 1 << 20
+        conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO = fused, 1 << 20, 1 << 20
         try:
             r = conv._winograd(x, Uw, b if pool else None, pool)
         finally:
-            conv.FUSED, conv.FUSED_MAX_CI = True, 64
+            conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO = True, 64, 64
         outs.append(r if pool else (r,))
     for a, ref in zip(*outs):
         scale = float(ref.abs().max())
@@ -145,3 +145,40 @@ def test_modulated_conv(N, C, Co, H):
     assert _err(y, yd) < 2e-5
     assert _err(xa.grad, xd.grad) < 2e-5
     assert float((sa.grad.double().cpu() - sd.grad).norm() / sd.grad.norm()) < 1e-4
+
+
+@pytest.mark.parametrize('epilogue', ['none', 'relu', 'pool'])
+@pytest.mark.parametrize('N,Ci,Co,H,W', [(2, 64, 64, 32, 32), (1, 64, 128, 16, 48), (2, 32, 64, 16, 16),
+                                         (1, 64, 64, 128, 128)])
+def test_fused_split_kernel(N, Ci, Co, H, W, epilogue):
+    """nfi_wino_conv_fused_split (the fused layers' products on the f16 matrix cores, the 36 products
+    consumed row by row by the output transform) against an fp64 convolution + epilogue (the 2e-5
+    bar) and against fused_kernel (fp32 MFMAs) on the same inputs."""
+    g = torch.Generator(device=DEV).manual_seed(N + Ci + Co + H + W)
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    x[:, :, : H // 4] *= 1e-3                         # magnitudes spread inside a workgroup's region
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    b = 0.1 * torch.randn((Co,), device=DEV, generator=g)
+    Uw, _ = conv.weights(w)
+    assert Uw.split is not None
+    bias = None if epilogue == 'none' else b
+    pool = epilogue == 'pool'
+    old = conv.FUSED_SPLIT, conv.FUSED_MAX_CO
+    outs = {}
+    try:
+        conv.FUSED_MAX_CO = 1 << 20                      # (the fused path for every shape here)
+        for mode in (True, False):
+            conv.FUSED_SPLIT = mode
+            outs[mode] = conv._winograd(x, Uw, bias, pool)
+    finally:
+        conv.FUSED_SPLIT, conv.FUSED_MAX_CO = old
+    ref = F.conv2d(x.double(), w.double(), padding=1)
+    if bias is not None:
+        ref = torch.relu(ref + b.double()[None, :, None, None])
+    refs = (ref, F.max_pool2d(ref, 2)) if pool else (ref,)
+    for got_s, got_f, r in zip(outs[True] if pool else (outs[True],), outs[False] if pool else (outs[False],), refs):
+        scale = float(r.abs().max())
+        e_s = float((got_s.double() - r).abs().max()) / scale
+        e_f = float((got_f.double() - r).abs().max()) / scale
+        print(f'  split {e_s:.3g}  fused fp32 {e_f:.3g}')
+        assert e_s <= 2e-5, (e_s, e_f)

@@ -28,7 +28,7 @@ def split_gemm(A, B):
     lo = torch.empty(A.shape, device=DEV, dtype=torch.int16)
     inv = torch.empty((b,), device=DEV)
     _lib.check(lib.nfi_split16_pack(_p(A), b, M * K, _p(hi), _p(lo), _p(inv), st), 'nfi_split16_pack')
-    slots = torch.empty((64,), device=DEV, dtype=torch.int32)
+    slots = torch.empty((128,), device=DEV, dtype=torch.int32)   # 64 maxima + counter
     _lib.check(lib.nfi_absmax_slots(_p(B), B.numel(), _p(slots), st), 'nfi_absmax_slots')
     C = torch.empty((b, M, N), device=DEV)
     _lib.check(lib.nfi_gemm_split16(_p(hi), _p(lo), _p(inv), _p(B), _p(slots), _p(C), b, M, N, K, st),
