@@ -195,6 +195,8 @@ class NfiError(RuntimeError):
 def load(path: str = LIB_PATH):
     """Load and type the library once.  Raises NfiError if it is absent or mismatched."""
     global _lib
+    if _lib is not None:     # (fast path: every launch goes through here)
+        return _lib
     with _lock:
         if _lib is not None:
             return _lib

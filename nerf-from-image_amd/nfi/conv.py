@@ -75,12 +75,19 @@ class WeightSet:
 
 
 def _p(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    return None if t is None else t.data_ptr()
+
+
+_fns = {}
 
 
 def _call(name, *args):
-    lib = _lib.load()
-    _lib.check(getattr(lib, name)(*args), name)
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(_lib.load(), name)
+    rc = fn(*args)
+    if rc:
+        _lib.check(rc, name)
 
 
 def applicable(x: torch.Tensor, weight: torch.Tensor) -> bool:

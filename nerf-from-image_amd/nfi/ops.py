@@ -24,11 +24,16 @@ from . import _lib
 
 
 def _ptr(t: Optional[torch.Tensor]):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    # (a plain int: the ctypes prototypes declare c_void_p, which converts it — no wrapper object)
+    return None if t is None else t.data_ptr()
+
+
+_raw_stream = torch._C._cuda_getCurrentRawStream
 
 
 def _stream(dev: torch.device):
-    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    """The current HIP stream of dev as an int (the raw handle: no torch.cuda.Stream object per launch)."""
+    return _raw_stream(dev.index if dev.index is not None else torch.cuda.current_device())
 
 
 # Optional live kernel timing (bench.py): name -> list of (start, end) events recorded on the
