@@ -77,6 +77,10 @@ class _timed:
 # B=8: 7.49 vs 7.39 ms per step; the overlapped launches stretch to 2.61 / 3.39 ms from 2.27 /
 # 2.25: the two compete for the memory pipeline, not for different units), so off by default.
 BACKWARD_PIPELINE = os.environ.get('NFI_BACKWARD_PIPELINE', '0') == '1'
+# Slabs (A/B knob): the backward of NFI_BACKWARD_SLAB images at a time — bins,
+# field backward, tile pass — so a slab's gradient rows are read back by the tile pass while the
+# Infinity Cache still holds them; 0 = the whole batch in one pass of each stage
+BACKWARD_SLAB = int(os.environ.get('NFI_BACKWARD_SLAB', '0'))
 _SIDE_STREAMS: dict = {}
 
 
@@ -462,6 +466,11 @@ class _VolumeRender(torch.autograd.Function):
                 if t is not None:
                     t.record_stream(side)
             main.wait_stream(side)
+        elif 0 < BACKWARD_SLAB < B and DEBUG_BACKWARD is None:
+            for b0 in range(0, B, BACKWARD_SLAB):
+                p = part(b0, min(BACKWARD_SLAB, B - b0))
+                for k, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
+                    stage(p, k, name, main)
         else:
             p = part(0, B)
             for k, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
