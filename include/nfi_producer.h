@@ -71,6 +71,12 @@ int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const fl
  * nfi_syn_fir_up_backward, then nfi_syn_up_conv_gather, without go and gt in memory. */
 int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
                                      float* dd, int32_t B, int32_t C, int32_t n, float gain, void* stream);
+/* The same, also leaving the running maximum of |dP| in vmax[0..63] for the split-f16 product W9^T dP
+ * (nfi_gemm_split16_shared_a; vmax[0..64] zero on entry, as nfi_wino_input_transform_max): no
+ * separate maximum pass over dP. */
+int32_t nfi_syn_up_conv_act_backward_max(const float* g, const float* o, const float* d, const float* bias, float* dP,
+                                         float* dd, uint32_t* vmax, int32_t B, int32_t C, int32_t n, float gain,
+                                         void* stream);
 
 /* Its adjoint: gt [B][C][2n+1][2n+1] -> dP [B][9][C][n][n], dP[3ky+kx][c][iy][ix] =
  * gt[c][2iy+ky][2ix+kx]; the data gradient of the transposed convolution is then W9^T dP. */

@@ -27,6 +27,11 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
   return v;
 }
+__device__ __forceinline__ float wave_absmax(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
 
 // block (256) sum -> *dst: stored when the plane is one block (gridDim.x == 1: no zero-fill
 // launch before), else one atomic per block into the zero-filled *dst
@@ -284,10 +289,11 @@ constexpr int UB_RY = 2 * UB_TY + 1, UB_RX = 2 * UB_TX + 1;            // 17 x 6
 __global__ void __launch_bounds__(256) up_bwd_fused_kernel(const float* __restrict__ g, const float* __restrict__ o,
                                                            const float* __restrict__ d, const float* __restrict__ bias,
                                                            float* __restrict__ dP, float* __restrict__ dd, int C,
-                                                           int n, float gain) {
+                                                           int n, float gain, unsigned* __restrict__ vmax) {
   __shared__ float Gs[UB_GY][UB_GX + 1];
   __shared__ float Rs[UB_RY][UB_RX + 1];
   __shared__ float part[4];
+  __shared__ float pmax[4];
   const int W2 = 2 * n;
   const int tiles_x = n / UB_TX;
   const int tile = blockIdx.x, p = blockIdx.y;
@@ -341,10 +347,22 @@ __global__ void __launch_bounds__(256) up_bwd_fused_kernel(const float* __restri
   const int lx = threadIdx.x % UB_TX, ly = threadIdx.x / UB_TX;
   const int64_t nn = (int64_t)n * n;
   float* out = dP + ((int64_t)b * 9 * C + c) * nn + (int64_t)(iy0 + ly) * n + ix0 + lx;
+  float mx = 0.f;
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) out[(ky * 3 + kx) * C * nn] = Rs[2 * ly + ky][2 * lx + kx];
+    for (int kx = 0; kx < 3; ++kx) {
+      const float v = Rs[2 * ly + ky][2 * lx + kx];
+      out[(ky * 3 + kx) * C * nn] = v;
+      mx = fmaxf(mx, fabsf(v));
+    }
+  if (vmax != nullptr) {   // (block-uniform) the running maximum of |dP| for the split-f16 product
+    mx = wave_absmax(mx);
+    if ((threadIdx.x & 63) == 0) pmax[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicMax(vmax + (blockIdx.x + blockIdx.y) % 64, __float_as_uint(fmaxf(fmaxf(pmax[0], pmax[1]), fmaxf(pmax[2], pmax[3]))));
+  }
 }
 
 // Its adjoint's operand (the data gradient of the transposed convolution is W9^T dP): gt
@@ -1209,8 +1227,8 @@ int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const fl
   return NFI_OK;
 }
 
-int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
-                                     float* dd, int32_t B, int32_t C, int32_t n, float gain, void* stream) {
+static int32_t up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
+                                   float* dd, int32_t B, int32_t C, int32_t n, float gain, uint32_t* vmax, void* stream) {
   NFI_REQUIRE(g && o && d && bias && dP && dd, "syn_up_conv_act_backward: null pointer");
   NFI_REQUIRE(B > 0 && C > 0 && n > 0 && n % UB_TX == 0, "syn_up_conv_act_backward: bad shape");
   hipStream_t st = (hipStream_t)stream;
@@ -1219,9 +1237,21 @@ int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float
     return NFI_ELAUNCH;
   }
   up_bwd_fused_kernel<<<dim3((unsigned)((n / UB_TY) * (n / UB_TX)), (unsigned)(B * C)), 256, 0, st>>>(
-      g, o, d, bias, dP, dd, C, n, gain);
+      g, o, d, bias, dP, dd, C, n, gain, (unsigned*)vmax);
   NFI_CHECK_LAUNCH("up_bwd_fused_kernel");
   return NFI_OK;
+}
+
+int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
+                                     float* dd, int32_t B, int32_t C, int32_t n, float gain, void* stream) {
+  return up_conv_act_backward(g, o, d, bias, dP, dd, B, C, n, gain, nullptr, stream);
+}
+
+int32_t nfi_syn_up_conv_act_backward_max(const float* g, const float* o, const float* d, const float* bias, float* dP,
+                                         float* dd, uint32_t* vmax, int32_t B, int32_t C, int32_t n, float gain,
+                                         void* stream) {
+  NFI_REQUIRE(vmax, "syn_up_conv_act_backward_max: null vmax");
+  return up_conv_act_backward(g, o, d, bias, dP, dd, B, C, n, gain, vmax, stream);
 }
 
 int32_t nfi_syn_up_conv_gather(const float* gt, float* dP, int32_t B, int32_t C, int32_t n, void* stream) {

@@ -139,6 +139,8 @@ SIGNATURES = {
                                                 ctypes.c_int32, c_void_p]),
     'nfi_syn_up_conv_act_backward': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 3
                                      + [ctypes.c_float, c_void_p]),
+    'nfi_syn_up_conv_act_backward_max': (ctypes.c_int32, [c_void_p] * 7 + [ctypes.c_int32] * 3
+                                         + [ctypes.c_float, c_void_p]),
     'nfi_syn_up_conv_fir_act_forward': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 3
                                         + [ctypes.c_float, c_void_p]),
     'nfi_aug_sample_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p] + [ctypes.c_int32] * 6

@@ -140,17 +140,19 @@ def split_matrix(A):
     return _split(A.detach().contiguous()[None], A.shape[1], _stream(A.device))
 
 
-def split_matmul_shared(As, X):
+def split_matmul_shared(As, X, slots=None):
     """C[b] = A X[b] for X [B, K, N] on the split GEMM, A's halves from split_matrix (one A for every
-    image: nfi_gemm_split16_shared_a); X's scale from its maximum (nfi_absmax_slots)."""
+    image: nfi_gemm_split16_shared_a); X's scale from its maximum (nfi_absmax_slots), or from `slots`
+    the producer of X already filled (e.g. nfi_syn_up_conv_act_backward_max; the GEMM clears them)."""
     hi, lo, inv = As
     X = X.contiguous()
     B, K, N = X.shape
     Mrows = hi.shape[1]
     assert hi.shape[2] == K, (hi.shape, X.shape)
     st = _stream(X.device)
-    slots = torch.empty((128,), device=X.device, dtype=torch.int32)   # 64 maxima + the GEMM's counter
-    _call('nfi_absmax_slots', _p(X), X.numel(), _p(slots), st)
+    if slots is None:
+        slots = torch.empty((128,), device=X.device, dtype=torch.int32)   # 64 maxima + the GEMM's counter
+        _call('nfi_absmax_slots', _p(X), X.numel(), _p(slots), st)
     C = torch.empty((B, Mrows, N), device=X.device)
     ks = ksplit(B * -(-Mrows // 128) * -(-N // 128), K) if (Mrows * N) % 4 == 0 else 1
     work = torch.empty((ks, B, Mrows, N), device=X.device) if ks > 1 else None
@@ -165,6 +167,16 @@ def ksplit(tiles, K):
     if tiles >= 512:
         return 1
     return max(1, min(K // 256, -(-512 // tiles)))
+
+
+def stream_slots(owner: dict, device):
+    """A self-clearing maxima buffer (64 slots + the GEMM's counter, zeroed once) per stream, kept in
+    `owner` — for producers that fill the maxima of a split product's B operand themselves."""
+    key = torch.cuda.current_stream(device).cuda_stream
+    buf = owner.get(key)
+    if buf is None:
+        buf = owner[key] = torch.zeros((128,), device=device, dtype=torch.int32)
+    return buf
 
 
 def _slots(Uw: WeightSet, device):

@@ -145,6 +145,14 @@ def _up_weights(w):
     return hit[1]
 
 
+_SLOT_OWNERS = {}
+
+
+def _slot_owner(Wm):
+    """The per-stream maxima buffers of one cached split matrix (keyed by its hi-halves tensor)."""
+    return _SLOT_OWNERS.setdefault(Wm[1][0].data_ptr(), {})
+
+
 def _mm_shared(Wm, X):
     """Wm[0] X[b] per image: the split GEMM when Wm carries halves and the maps have >= 1024 pixels,
     else torch.matmul (hipBLASLt).  Below 1024 the products are launch-sized (20-60 us) and hipBLASLt's
@@ -220,7 +228,13 @@ class _UpConvAct(torch.autograd.Function):
         dev = _stream(o.device)
         dd = torch.empty_like(d)
         dP = torch.empty((B, 9 * Co, n * n), device=o.device, dtype=o.dtype)
-        if n % 32 == 0:       # epilogue backward + FIR adjoint + tap gather in one pass
+        slots = None
+        if n % 32 == 0 and W9t[1] is not None and n * n >= 1024:
+            # the fused pass also leaves max|dP| for the split product W9^T dP (no maximum pass)
+            slots = conv.stream_slots(_slot_owner(W9t), o.device)
+            _call('nfi_syn_up_conv_act_backward_max', _p(g), _p(o), _p(d), _p(bias), _p(dP), _p(dd), _p(slots), B,
+                  Co, n, ctypes.c_float(ctx.gain), dev)
+        elif n % 32 == 0:     # epilogue backward + FIR adjoint + tap gather in one pass
             _call('nfi_syn_up_conv_act_backward', _p(g), _p(o), _p(d), _p(bias), _p(dP), _p(dd), B, Co, n,
                   ctypes.c_float(ctx.gain), dev)
         else:
@@ -230,7 +244,12 @@ class _UpConvAct(torch.autograd.Function):
             gt = torch.empty((B, Co, 2 * n + 1, 2 * n + 1), device=o.device, dtype=o.dtype)
             _call('nfi_syn_fir_up_backward', _p(go), _p(gt), B * Co, n, dev)
             _call('nfi_syn_up_conv_gather', _p(gt), _p(dP), B, Co, n, dev)
-        gx = _mm_shared(W9t, dP).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
+        if slots is not None:
+            gx = conv.split_matmul_shared(W9t[1], dP, slots).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
+            if gx is None:   # (the maxima were left for a product that did not run: clear them)
+                slots.zero_()
+        else:
+            gx = _mm_shared(W9t, dP).view(B, Ci, n, n) if ctx.needs_input_grad[0] else None
         return gx, None, None, dd, None, None
 
 

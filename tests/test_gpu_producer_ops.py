@@ -107,11 +107,13 @@ def test_up_conv(B, Ci, Co, n):
     assert float((tg.double() - r64).abs().max()) <= max(1e-6 * s, 4 * err32)
 
 
-@pytest.mark.parametrize('B,Ci,Co,n', [(2, 16, 8, 32), (1, 32, 16, 64), (2, 24, 8, 4)])
+@pytest.mark.parametrize('B,Ci,Co,n', [(2, 16, 8, 32), (1, 32, 16, 64), (2, 24, 8, 4), (2, 64, 32, 32)])
 def test_up_conv_act_fused_matches_two_kernel_path(B, Ci, Co, n):
     """The fused scatter + FIR + epilogue kernel (2n % 64 == 0) matches up_conv then fir_up_act
     (the same operations; the compiler's FMA contraction may differ by an ulp), and so do the
-    gradients (same backward kernels); n = 4 takes the unfused path."""
+    gradients (same backward kernels); n = 4 takes the unfused path.  Co = 32 at n = 32: the data
+    gradient W9^T dP on the split GEMM, its scale from the maxima the fused backward pass leaves
+    (nfi_syn_up_conv_act_backward_max) on one path and from a maximum pass over dP on the other."""
     x = _rand(B, Ci, n, n, seed=23).requires_grad_()
     w = _rand(Co, Ci, 3, 3, seed=24) / (3 * Ci ** 0.5)
     d = (_rand(B, Co, seed=25).abs() + 0.1).requires_grad_()
