@@ -22,8 +22,10 @@
 // flight during the step's 48 MFMAs per wave.  Rows padded by 8 halves (80 B) so the b128 operand
 // reads of 16 lanes spread over the banks.  Measured against the alternatives kept for A/B
 // (scripts/gemm_bench.py, profiles/r04_gemm_bench.log): 256 x 128 / 128 x 256 tiles of 8 waves
-// (NFI_GEMM_TILE=42 / 24) 0-50 % slower, two register stages of prefetch (NFI_GEMM_PF=2: occupancy
-// 2) 0-15 % slower, the wide-load kernel (NFI_GEMM_KERNEL=2) 5-25 % slower; 200-256 TFLOP/s
+// (NFI_GEMM_TILE=42 / 24) 0-50 % slower, 2 x 2 waves of 128 x 128 (NFI_GEMM_TILE=88: half the LDS
+// operand bytes per MFMA, 256 accumulation registers, one wave per SIMD) 20-100 % slower, two register
+// stages of prefetch (NFI_GEMM_PF=2: occupancy 2) 0-15 % slower, the wide-load kernel
+// (NFI_GEMM_KERNEL=2) 5-25 % slower; 200-256 TFLOP/s
 // fp32-equivalent on the 256-512-channel Winograd shapes, 2x hipBLASLt's fp32 bmm.
 #include <algorithm>
 #include <cstdlib>
@@ -135,12 +137,15 @@ __device__ __forceinline__ void tile_order(int xcd, int& bx, int& by, int& bz) {
 }
 
 // WM x WN waves of 64 x 64: tile (64 WM) x (64 WN), 64 WM WN threads
-template <int WM, int WN, int PF>
-__global__ void __launch_bounds__(64 * WM * WN, WM * WN == 4 ? (PF == 1 ? 3 : 2) : 1) split16_gemm_kernel(Args g) {
-  constexpr int T = 64 * WM * WN, TBM = 64 * WM, TBN = 64 * WN;
-  constexpr int CA = 4 / WN;    // 8-half chunks of A's K-step rows per thread (hi; as many lo)
-  constexpr int KB = 32 / WM;   // k rows of B's slab per thread (one column)
-  static_assert(CA >= 1 && KB >= 8 && KB % 8 == 0, "tile shape");
+// RX x RY blocks of 16 x 16 per wave (4 x 4: 64 accumulator registers; 8 x 8: the 256 of the
+// accumulation registers, one wave per SIMD, half the LDS operand bytes per MFMA)
+template <int WM, int WN, int PF, int RX = 4, int RY = 4>
+__global__ void __launch_bounds__(64 * WM * WN, RX * RY > 16 ? 1 : (WM * WN == 4 ? (PF == 1 ? 3 : 2) : 1))
+    split16_gemm_kernel(Args g) {
+  constexpr int T = 64 * WM * WN, TBM = 16 * RX * WM, TBN = 16 * RY * WN;
+  constexpr int CA = TBM * 4 / T;    // 8-half chunks of A's K-step rows per thread (hi; as many lo)
+  constexpr int KB = 32 * TBN / T;   // k rows of B's slab per thread (one column)
+  static_assert(CA >= 1 && CA <= 4 && KB >= 8 && KB <= 32 && KB % 8 == 0, "tile shape");
   __shared__ __attribute__((aligned(16))) unsigned short lds[2 * LDK * (TBM + TBN)];   // A hi, A lo, Bt hi, Bt lo
   unsigned short* Ahs = lds;
   unsigned short* Als = lds + TBM * LDK;
@@ -167,7 +172,7 @@ __global__ void __launch_bounds__(64 * WM * WN, WM * WN == 4 ? (PF == 1 ? 3 : 2)
 
   // global -> register staging: A (row ar, halves ak .. ak + 8 CA - 1 of the K-step: CA b128 loads
   // each of hi and lo), B column bn, k = bk .. bk + KB - 1 (coalesced rows across the wave)
-  const int ar = tid / WN, ak = 8 * ((tid * CA) & 3);
+  const int ar = (tid * CA) >> 2, ak = 8 * ((tid * CA) & 3);
   const int arow = min(m0 + ar, M - 1);
   const bool a_ok = m0 + ar < M;
   const int bn = tid % TBN, bk = (tid / TBN) * KB;
@@ -214,30 +219,30 @@ __global__ void __launch_bounds__(64 * WM * WN, WM * WN == 4 ? (PF == 1 ? 3 : 2)
     }
   };
 
-  // wave (wm, wn) computes rows 64 wm.., columns 64 wn.. of the tile
+  // wave (wm, wn) computes rows 16 RX wm.., columns 16 RY wn.. of the tile
   const int wm = wv / WN, wn = wv % WN;
   const int i16 = l & 15, kg = l >> 4;
-  f4v acc[4][4];
+  f4v acc[RX][RY];
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < RX; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < RY; ++y) acc[x][y] = f4v{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&]() {
-    u4v ah[4], al[4];
+    u4v ah[RX], al[RX];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int r = (64 * wm + 16 * x + i16) * LDK + 8 * kg;
+    for (int x = 0; x < RX; ++x) {
+      const int r = (16 * RX * wm + 16 * x + i16) * LDK + 8 * kg;
       ah[x] = *reinterpret_cast<const u4v*>(Ahs + r);
       al[x] = *reinterpret_cast<const u4v*>(Als + r);
     }
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const int r = (64 * wn + 16 * y + i16) * LDK + 8 * kg;
+    for (int y = 0; y < RY; ++y) {
+      const int r = (16 * RY * wn + 16 * y + i16) * LDK + 8 * kg;
       const u4v bh = *reinterpret_cast<const u4v*>(Bhs + r);
       const u4v bl = *reinterpret_cast<const u4v*>(Bls + r);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
+      for (int x = 0; x < RX; ++x) {
         acc[x][y] = mfma_h(al[x], bh, acc[x][y]);   // small terms first
         acc[x][y] = mfma_h(ah[x], bl, acc[x][y]);
         acc[x][y] = mfma_h(ah[x], bh, acc[x][y]);
@@ -265,17 +270,17 @@ __global__ void __launch_bounds__(64 * WM * WN, WM * WN == 4 ? (PF == 1 ? 3 : 2)
     }
     if (k0 < kend) step(k0, RA[0], RB[0]);
   }
-  // C rows m0 + 64 wm + 16 x + 4 kg + r, column n0 + 64 wn + 16 y + i16
+  // C rows m0 + 16 RX wm + 16 x + 4 kg + r, column n0 + 16 RY wn + 16 y + i16
   float* Cg = (g.ksplit > 1 ? g.work + (long long)ks * (gridDim.z / g.ksplit) * M * N : g.C) + (long long)b * M * N;
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < RX; ++x)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = m0 + 64 * wm + 16 * x + 4 * kg + r;
+      const int m = m0 + 16 * RX * wm + 16 * x + 4 * kg + r;
       if (m >= M) continue;
 #pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int n = n0 + 64 * wn + 16 * y + i16;
+      for (int y = 0; y < RY; ++y) {
+        const int n = n0 + 16 * RY * wn + 16 * y + i16;
         if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * out_scale;
       }
     }
@@ -488,8 +493,11 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
   const char* te = getenv("NFI_GEMM_TILE");
   const int tile = te ? atoi(te) : 22;
   const int WM = tile / 10, WN = tile % 10;
-  NFI_REQUIRE(tile == 22 || tile == 42 || tile == 24 || tile == 41 || tile == 14, "gemm_split16: NFI_GEMM_TILE=%d", tile);
-  const dim3 grid((unsigned)((N + 64 * WN - 1) / (64 * WN)), (unsigned)((M + 64 * WM - 1) / (64 * WM)), (unsigned)batch);
+  NFI_REQUIRE(tile == 22 || tile == 42 || tile == 24 || tile == 41 || tile == 14 || tile == 88,
+              "gemm_split16: NFI_GEMM_TILE=%d", tile);
+  // (88: 2 x 2 waves of 128 x 128 — a 256 x 256 tile)
+  const int TM = tile == 88 ? 256 : 64 * WM, TN = tile == 88 ? 256 : 64 * WN;
+  const dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)batch);
   NFI_REQUIRE(grid.y <= 65535, "gemm_split16: M too large");
   if (!xe) g.xcd = grid.x <= 8;
   const char* pe = getenv("NFI_GEMM_PF");   // register prefetch depth (A/B: 1 or 2)
@@ -500,6 +508,7 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
       return;
     }
     switch (tile) {
+      case 88: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 2, 1, 8, 8>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
       case 42: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<4, 2, 1>), gr, dim3(512), 0, (hipStream_t)stream, g); break;
       case 24: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 4, 1>), gr, dim3(512), 0, (hipStream_t)stream, g); break;
       case 41: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<4, 1, 1>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
