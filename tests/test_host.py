@@ -182,3 +182,29 @@ def test_split_f16_products_carry_fp32_error():
     ref = W.astype(np.float64) @ X.astype(np.float64)
     den = np.abs(W).astype(np.float64) @ np.abs(X).astype(np.float64)
     assert np.max(np.abs(split_mm(W, X, np.float32(1), np.float32(1)) - ref) / den) > 1e-4
+
+
+def test_split_gemm_host_rules():
+    """Host rules around the split-f16 GEMM (nfi/conv.py): the K split covers the CUs about twice
+    for few output tiles and never splits below 8 K-steps of 32; the fused Winograd kernel is kept
+    for 64 -> 64 layers only while the split GEMM is on; a weight set carries its per-stream maxima
+    buffers."""
+    from nfi import conv
+    assert conv.ksplit(600, 512) == 1 and conv.ksplit(512, 4608) == 1
+    assert conv.ksplit(4, 4608) == 18 and conv.ksplit(32, 2304) == 9 and conv.ksplit(144, 512) == 2
+    assert conv.ksplit(8, 256) == 1                        # K // 256: never below 8 K-steps of 32
+    for tiles in (1, 7, 100, 511):
+        for K in (256, 512, 1152, 4608):
+            k = conv.ksplit(tiles, K)
+            assert 1 <= k <= max(1, K // 256) and (k == 1 or tiles * k >= min(512, tiles * (K // 256)))
+    ws = conv.WeightSet(torch.zeros(36, 64, 64), torch.zeros(1), None)
+    old = conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO, conv.SPLIT16
+    try:
+        conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO, conv.SPLIT16 = True, 64, 64, True
+        assert conv._fused_ok(ws, 64, 64) and not conv._fused_ok(ws, 64, 128) and not conv._fused_ok(ws, 128, 64)
+        conv.SPLIT16 = False                               # hipBLASLt products: the round-3 rule (Ci only)
+        assert conv._fused_ok(ws, 64, 128)
+        assert not conv._fused_ok(conv.WeightSet(ws.U, None, None), 64, 64)   # no packed operands
+    finally:
+        conv.FUSED, conv.FUSED_MAX_CI, conv.FUSED_MAX_CO, conv.SPLIT16 = old
+    assert ws.vmax == {}
