@@ -248,6 +248,12 @@ int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* strea
 int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                          const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                          void* stream);
+/* nfi_gemm_split16_ksplit: nfi_gemm_split16 with K split in ksplit ranges (few output tiles: the
+ * 512-channel Winograd products at 8^2 / 16^2 maps), partials in work [ksplit][batch][M][N] summed in
+ * order (deterministic). */
+int32_t nfi_gemm_split16_ksplit(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                                const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                                int32_t ksplit, float* work, void* stream);
 int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                   const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                                   int32_t ksplit, float* work, void* stream);

@@ -552,6 +552,12 @@ int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_
   return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 0, 1, nullptr, stream);
 }
 
+int32_t nfi_gemm_split16_ksplit(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                                const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                                int32_t ksplit, float* work, void* stream) {
+  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 0, ksplit, work, stream);
+}
+
 int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                   const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                                   int32_t ksplit, float* work, void* stream) {

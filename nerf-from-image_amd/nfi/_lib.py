@@ -123,6 +123,7 @@ SIGNATURES = {
     'nfi_absmax_slots': (ctypes.c_int32, [c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
     'nfi_gemm_split16': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_gemm_split16_shared_a': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
+    'nfi_gemm_split16_ksplit': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),
     'nfi_syn_act_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

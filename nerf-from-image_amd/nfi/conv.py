@@ -57,6 +57,7 @@ RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
 # transform's running maximum); 0: torch.bmm (hipBLASLt fp32)
 SPLIT16 = os.environ.get('NFI_SPLIT16', '1') != '0'
 SPLIT16_BK = 32       # the split GEMM's K step: channel counts must be multiples of it
+KSPLIT = os.environ.get('NFI_KSPLIT', '1') != '0'   # K split of the Winograd products with few tiles
 # the fused layers on the f16 matrix cores (nfi_wino_conv_fused_split: products consumed by the output
 # transform one Winograd row at a time) where the shapes allow — measured slower than fused_kernel's
 # fp32 MFMAs (0.68 vs 0.48-0.51 ms on the 64->64 @128^2 layer), so off unless NFI_FUSED_SPLIT=1
@@ -204,7 +205,13 @@ def _product(Uw: WeightSet, x, scale=None, relu_y=None):
         _call('nfi_wino_input_transform_max', _p(x), _p(scale), _p(relu_y), _p(V), _p(vmax), N, K, H, W, st)
         Mrows = Uw.U.shape[1]
         M = torch.empty((36, Mrows, P), device=x.device)
-        _call('nfi_gemm_split16', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, st)
+        ks = ksplit(36 * -(-Mrows // 128) * -(-P // 128), K) if KSPLIT and (Mrows * P) % 4 == 0 else 1
+        if ks > 1:
+            work = torch.empty((ks, 36, Mrows, P), device=x.device)
+            _call('nfi_gemm_split16_ksplit', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, ks,
+                  _p(work), st)
+        else:
+            _call('nfi_gemm_split16', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, st)
         return M
     if relu_y is not None:
         _call('nfi_wino_input_transform_relu_grad', _p(x), _p(relu_y), _p(V), N, K, H, W, st)

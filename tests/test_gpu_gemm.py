@@ -62,11 +62,12 @@ def test_split16_gemm_matches_fp64(b, M, N, K, kernel, monkeypatch):
         assert e_hip <= 4 * e_ref + 2 ** -22, (i, e_hip, e_ref)
 
 
-@pytest.mark.parametrize('Ci,Co,H', [(128, 128, 32), (256, 512, 16), (128, 64, 64)])
+@pytest.mark.parametrize('Ci,Co,H', [(128, 128, 32), (256, 512, 16), (128, 64, 64), (512, 512, 16), (512, 512, 8)])
 def test_winograd_split16_matches_bmm(Ci, Co, H):
     """The three-pass Winograd convolution with the split-f16 products against the same pipeline with
     hipBLASLt's fp32 bmm, and both against an fp64 direct convolution (the 2e-5 bound of
-    tests/test_gpu_conv.py)."""
+    tests/test_gpu_conv.py).  512 -> 512 at 16^2 / 8^2: few output tiles, K split in two
+    (nfi_gemm_split16_ksplit)."""
     g = torch.Generator(device=DEV).manual_seed(Ci + Co)
     x = torch.randn((4, Ci, H, H), device=DEV, generator=g)
     w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
