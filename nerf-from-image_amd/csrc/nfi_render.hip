@@ -158,10 +158,13 @@ __device__ __forceinline__ void gather_records(const PlaneView& pv, const PointP
     const int o1 = o0 + (((t >> 20) & 1) ? st4 : 0);
     const int dy = ((t >> 21) & 1) ? rowb : 0;
     const float w = P.pl[q].w, n = P.pl[q].n, e = 1.f - w, s = 1.f - n;
+    // record (weight row 0, offset row 0, weight row 1, offset row 1): the weights land in even
+    // registers of the b128 read, where the packed interpolation takes them as aligned pairs (with
+    // (offset, offset, weight, weight) the odd-register weight took a v_mov per plane and group)
     lds_st(reinterpret_cast<float4*>(row + 8 * q),
-           make_float4(__int_as_float(o0), __int_as_float(o0 + dy), (s * e) * (1.f / 3.f), (n * e) * (1.f / 3.f)));
+           make_float4((s * e) * (1.f / 3.f), __int_as_float(o0), (n * e) * (1.f / 3.f), __int_as_float(o0 + dy)));
     lds_st(reinterpret_cast<float4*>(row + 8 * q + 4),
-           make_float4(__int_as_float(o1), __int_as_float(o1 + dy), (s * w) * (1.f / 3.f), (n * w) * (1.f / 3.f)));
+           make_float4((s * w) * (1.f / 3.f), __int_as_float(o1), (n * w) * (1.f / 3.f), __int_as_float(o1 + dy)));
   }
 }
 
@@ -172,12 +175,12 @@ __device__ __forceinline__ void gather_issue(__amdgpu_buffer_rsrc_t rsrc, const 
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const float4 R = *reinterpret_cast<const float4*>(rec + 8 * q);
-    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __float_as_int(R.x) + 16 * q4, 0, 0);
-    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __float_as_int(R.y) + 16 * q4, 0, 0);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __float_as_int(R.y) + 16 * q4, 0, 0);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, __float_as_int(R.w) + 16 * q4, 0, 0);
     V0[q] = make_float4(__int_as_float(v0[0]), __int_as_float(v0[1]), __int_as_float(v0[2]), __int_as_float(v0[3]));
     V1[q] = make_float4(__int_as_float(v1[0]), __int_as_float(v1[1]), __int_as_float(v1[2]), __int_as_float(v1[3]));
-    W0[q] = R.z;
-    W1[q] = R.w;
+    W0[q] = R.x;
+    W1[q] = R.z;
   }
 }
 
