@@ -140,7 +140,7 @@ __device__ __forceinline__ void tile_order(int xcd, int& bx, int& by, int& bz) {
 // RX x RY blocks of 16 x 16 per wave (4 x 4: 64 accumulator registers; 8 x 8: the 256 of the
 // accumulation registers, one wave per SIMD, half the LDS operand bytes per MFMA)
 template <int WM, int WN, int PF, int RX = 4, int RY = 4>
-__global__ void __launch_bounds__(64 * WM * WN, RX * RY > 16 ? 1 : (WM * WN == 4 ? (PF == 1 ? 3 : 2) : 1))
+__global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 ? 2 : (WM * WN == 4 ? (PF == 1 ? 3 : 2) : 1))
     split16_gemm_kernel(Args g) {
   constexpr int T = 64 * WM * WN, TBM = 16 * RX * WM, TBN = 16 * RY * WN;
   constexpr int CA = TBM * 4 / T;    // 8-half chunks of A's K-step rows per thread (hi; as many lo)
@@ -491,12 +491,16 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
   NFI_REQUIRE(ksplit >= 1 && (ksplit == 1 || work), "gemm_split16: ksplit=%d needs a workspace", ksplit);
   // tile of the general kernel: WM x WN waves (NFI_GEMM_TILE = "WMWN": 22 default, 42, 24, 41, 14)
   const char* te = getenv("NFI_GEMM_TILE");
+  // (48: 64 x 128 waves, a 128 x 256 tile at occupancy 2 with a quarter fewer LDS bytes per MFMA:
+  //  3-9 % faster than 22 alone on the long products (N >= 16384), 10-20 % slower on the rest, and
+  //  the vgg inversion step with it on those products 15.76-15.82 vs 15.58-15.64 ms: not the default)
   const int tile = te ? atoi(te) : 22;
   const int WM = tile / 10, WN = tile % 10;
-  NFI_REQUIRE(tile == 22 || tile == 42 || tile == 24 || tile == 41 || tile == 14 || tile == 88,
+  NFI_REQUIRE(tile == 22 || tile == 42 || tile == 24 || tile == 41 || tile == 14 || tile == 88 || tile == 48,
               "gemm_split16: NFI_GEMM_TILE=%d", tile);
-  // (88: 2 x 2 waves of 128 x 128 — a 256 x 256 tile)
-  const int TM = tile == 88 ? 256 : 64 * WM, TN = tile == 88 ? 256 : 64 * WN;
+  // (88: 2 x 2 waves of 128 x 128 — a 256 x 256 tile; 48: 2 x 2 waves of 64 x 128)
+  const int TM = tile == 88 ? 256 : tile == 48 ? 128 : 64 * WM;
+  const int TN = tile == 88 || tile == 48 ? 256 : 64 * WN;
   const dim3 grid((unsigned)((N + TN - 1) / TN), (unsigned)((M + TM - 1) / TM), (unsigned)batch);
   NFI_REQUIRE(grid.y <= 65535, "gemm_split16: M too large");
   if (!xe) g.xcd = grid.x <= 8;
@@ -509,6 +513,7 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
     }
     switch (tile) {
       case 88: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 2, 1, 8, 8>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
+      case 48: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 2, 1, 4, 8>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
       case 42: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<4, 2, 1>), gr, dim3(512), 0, (hipStream_t)stream, g); break;
       case 24: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 4, 1>), gr, dim3(512), 0, (hipStream_t)stream, g); break;
       case 41: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<4, 1, 1>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
