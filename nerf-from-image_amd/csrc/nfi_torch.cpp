@@ -15,6 +15,10 @@
 //   nfi::sample_pdf, nfi::compute_near_far_planes, nfi::cumprod_exclusive,
 //   nfi::render_volume_density_weights_only           the nerf_utils seams (nerf_utils.py:20-25,
 //                                                     166-182, 185-224, 227-275)
+//   nfi::render_fwd / nfi::render_bwd                 SURVEY §8(b)'s names on the reference layouts
+//                                                     (channel-major planes, gain-scaled W1s/W2s)
+//   nfi::composite_fwd/_bwd, nfi::triplane_mlp_fwd/_bwd  per-stage ops (nerf_utils.py:125-163;
+//                                                     generator.py:587-681)
 #include <cmath>
 #include <string>
 #include <vector>
@@ -121,8 +125,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> rays(const Tensor& cam, const c10::op
 }
 
 // ---- decoder -------------------------------------------------------------------------------------
-Tensor pack_decoder(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, const Tensor& b2_in) {
+// g1 / g2 < 0: the EqualizedLinear gains 1/sqrt(fan_in); 1: weights already scaled (W1s, W2s)
+Tensor pack_with_gains(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, const Tensor& b2_in, bool scaled) {
   require(w1, "w1");
+  require(b1, "b1");
+  require(w2_in, "w2");
+  require(b2_in, "b2");
+  TORCH_CHECK(w1.dim() == 2 && w1.size(0) == 64 && w1.size(1) == 32 && b1.numel() == 64 && w2_in.dim() == 2 &&
+                  w2_in.size(1) == 64 && b2_in.numel() == w2_in.size(0),
+              "nfi: decoder w1 [64,32], b1 [64], w2 [nout,64], b2 [nout] expected");
   const c10::DeviceGuard guard(w1.device());
   Tensor w2 = w2_in.detach(), b2 = b2_in.detach();
   const int32_t nout = w2.size(0) == 33 ? 33 : 11;
@@ -132,13 +143,17 @@ Tensor pack_decoder(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, con
   }
   TORCH_CHECK(w2.size(0) == nout, "nfi: decoder output layer must have <= 11 or 33 rows, got ", w2.size(0));
   Tensor dec = torch::empty({nfi_decoder_size(nout)}, w1.options());
-  const float g1 = (float)(1.0 / std::sqrt((double)w1.size(1)));
-  const float g2 = (float)(1.0 / std::sqrt((double)w2.size(1)));
+  const float g1 = scaled ? 1.0f : (float)(1.0 / std::sqrt((double)w1.size(1)));
+  const float g2 = scaled ? 1.0f : (float)(1.0 / std::sqrt((double)w2.size(1)));
   Tensor w1c = w1.detach().contiguous(), b1c = b1.detach().contiguous(), w2c = w2.contiguous(), b2c = b2.contiguous();
   check(nfi_decoder_pack_n(w1c.data_ptr<float>(), b1c.data_ptr<float>(), w2c.data_ptr<float>(), b2c.data_ptr<float>(),
                            nout, g1, g2, 1.0f, dec.data_ptr<float>(), stream_of(w1)),
         "nfi_decoder_pack_n");
   return dec;
+}
+
+Tensor pack_decoder(const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2) {
+  return pack_with_gains(w1, b1, w2, b2, false);
 }
 
 // ---- fused render --------------------------------------------------------------------------------
@@ -203,12 +218,12 @@ void check_render_inputs(const Tensor& planes_tm, const c10::optional<Tensor>& p
 
 // volume_render_fwd -> (rgb [B,H,W,3], depth, mask [B,H,W], t, sigma, rgb_s, y, perm, x, tile_counts);
 // keep_state false: a forward-only render (the saved-state outputs are empty)
-std::vector<Tensor> volume_render_fwd(const Tensor& planes_tm, const c10::optional<Tensor>& palette_o, const Tensor& ro,
-                                      const Tensor& rd, const Tensor& nr, const Tensor& fr, const Tensor& dec,
-                                      int64_t samples, bool fine, bool white, bool randomize, double scene_range,
-                                      double inv_alpha, double beta, int64_t heads, int64_t seed,
-                                      const c10::optional<Tensor>& u_coarse, const c10::optional<Tensor>& u_fine,
-                                      bool keep_state) {
+std::vector<Tensor> render_forward_impl(const Tensor& planes_tm, const c10::optional<Tensor>& palette_o, const Tensor& ro,
+                                        const Tensor& rd, const Tensor& nr, const Tensor& fr, const Tensor& dec,
+                                        int64_t samples, bool fine, bool white, bool randomize, double scene_range,
+                                        double inv_alpha, double beta, int64_t heads, int64_t seed,
+                                        const c10::optional<Tensor>& u_coarse, const c10::optional<Tensor>& u_fine,
+                                        bool keep_state, int64_t offset) {
   check_render_inputs(planes_tm, palette_o, ro, rd, nr, fr, dec, heads);
   const c10::DeviceGuard guard(ro.device());
   const Tensor palette = (palette_o && palette_o->defined()) ? palette_o->contiguous() : Tensor();
@@ -224,6 +239,7 @@ std::vector<Tensor> volume_render_fwd(const Tensor& planes_tm, const c10::option
   Tensor t_s, s_s, c_s, y_s, perm, x_s, tc;
   RenderCfg c{samples, heads, seed, fine, white, randomize, scene_range, inv_alpha, beta};
   nfi_render_args a = render_args(planes_tm, palette, ro, rd, nr, fr, dec, c);
+  a.offset = (uint64_t)offset;
   a.u_coarse = fptr(u_coarse);
   a.u_fine = fptr(u_fine);
   a.rgb = rgb.data_ptr<float>();
@@ -252,6 +268,16 @@ std::vector<Tensor> volume_render_fwd(const Tensor& planes_tm, const c10::option
   return {rgb, depth, mask, keep_state ? t_s : e, keep_state ? s_s : e, keep_state ? c_s : e,
           keep_state ? y_s : e, keep_state ? perm : e.to(torch::kInt16), keep_state ? x_s : e,
           keep_state ? tc : e.to(torch::kInt32)};
+}
+
+std::vector<Tensor> volume_render_fwd(const Tensor& planes_tm, const c10::optional<Tensor>& palette, const Tensor& ro,
+                                      const Tensor& rd, const Tensor& nr, const Tensor& fr, const Tensor& dec,
+                                      int64_t samples, bool fine, bool white, bool randomize, double scene_range,
+                                      double inv_alpha, double beta, int64_t heads, int64_t seed,
+                                      const c10::optional<Tensor>& u_coarse, const c10::optional<Tensor>& u_fine,
+                                      bool keep_state) {
+  return render_forward_impl(planes_tm, palette, ro, rd, nr, fr, dec, samples, fine, white, randomize, scene_range,
+                             inv_alpha, beta, heads, seed, u_coarse, u_fine, keep_state, 0);
 }
 
 // volume_render_bwd -> (d_planes (planes_tm's strides), d_palette [B,10,3] or empty, d_ro, d_rd or empty)
@@ -467,6 +493,221 @@ Tensor render_volume_density_weights_only(const Tensor& sigma, const Tensor& ro,
   return WeightsFn::apply(sigma, rd, t);
 }
 
+// ---- SURVEY §8(b) names: the render / per-stage ops on the reference's own layouts -----------------
+// planes channel-major [B,3,32,R,R] (generator.py:476-477), the decoder as gain-scaled W1s [64,32], b1,
+// W2s [nout,64], b2 (stylegan.py:173-176: W * gain folded on the host).  Each op converts to the
+// kernels' layouts (texel-major planes, the packed decoder) on the caller's stream and launches the
+// same C-ABI entries volume_render_fwd / _bwd, nfi_composite_*, nfi_sampler_* do.
+Tensor to_texel_major(const Tensor& planes) {
+  require(planes, "planes");
+  TORCH_CHECK(planes.dim() == 5 && planes.size(1) == 3 && planes.size(2) == 32 && planes.size(3) == planes.size(4),
+              "nfi: planes [B,3,32,R,R] expected");
+  const Tensor p = planes.contiguous();
+  const int64_t B = p.size(0), R = p.size(3);
+  Tensor tm = torch::empty({B, 3, R, R, 32}, p.options());
+  check(nfi_planes_to_texel_major(p.data_ptr<float>(), (int32_t)B, (int32_t)R, tm.data_ptr<float>(), stream_of(p)),
+        "nfi_planes_to_texel_major");
+  return tm;
+}
+
+Tensor to_channel_major(const Tensor& tm) {
+  const int64_t B = tm.size(0), R = tm.size(2);
+  Tensor p = torch::empty({B, 3, 32, R, R}, tm.options());
+  check(nfi_planes_to_channel_major(tm.data_ptr<float>(), (int32_t)B, (int32_t)R, p.data_ptr<float>(), stream_of(tm)),
+        "nfi_planes_to_channel_major");
+  return p;
+}
+
+// render_fwd -> (rgb [B,H,W,3], depth, mask [B,H,W], t_sorted [B,H,W,N], saved_state); N = 2S with fine
+// sampling.  saved_state = (planes_tm, dec, t, sigma, rgb_s, y, perm, x, tile_counts): render_bwd's input.
+std::tuple<Tensor, Tensor, Tensor, Tensor, std::vector<Tensor>> render_fwd(
+    const Tensor& planes, const Tensor& W1s, const Tensor& b1, const Tensor& W2s, const Tensor& b2,
+    const c10::optional<Tensor>& palette, double inv_alpha, double beta, const Tensor& ro, const Tensor& rd,
+    const Tensor& nr, const Tensor& fr, int64_t S, double scene_range, bool white_bg, bool randomize, int64_t seed,
+    int64_t offset, const c10::optional<Tensor>& u_coarse, const c10::optional<Tensor>& u_fine, bool fine,
+    int64_t heads) {
+  const c10::DeviceGuard guard(planes.device());
+  const Tensor tm = to_texel_major(planes);
+  const Tensor dec = pack_with_gains(W1s, b1, W2s, b2, true);
+  auto r = render_forward_impl(tm, palette, ro.contiguous(), rd.contiguous(), nr.contiguous(), fr.contiguous(), dec, S,
+                               fine, white_bg, randomize, scene_range, inv_alpha, beta, heads, seed, u_coarse, u_fine,
+                               true, offset);
+  const int64_t N = fine ? 2 * S : S;
+  Tensor t_sorted = r[3].view({ro.size(0), ro.size(1), ro.size(2), N});
+  return {r[0], r[1], r[2], t_sorted, {tm, dec, r[3], r[4], r[5], r[6], r[7], r[8], r[9]}};
+}
+
+// render_bwd -> (d_planes [B,3,32,R,R], d_palette [B,10,3] (empty without a palette), d_ro, d_rd [B,H,W,3]
+// (empty unless coords))
+std::tuple<Tensor, Tensor, Tensor, Tensor> render_bwd(
+    const c10::optional<Tensor>& g_rgb, const c10::optional<Tensor>& g_mask, at::TensorList saved,
+    const c10::optional<Tensor>& palette, double inv_alpha, double beta, const Tensor& ro, const Tensor& rd,
+    const Tensor& nr, const Tensor& fr, int64_t S, double scene_range, bool white_bg, bool randomize, bool fine,
+    int64_t heads, bool coords) {
+  TORCH_CHECK(saved.size() == 9, "nfi::render_bwd: saved_state is render_fwd's 9-tensor list");
+  const c10::DeviceGuard guard(ro.device());
+  const int64_t n = ro.size(0) * ro.size(1) * ro.size(2);
+  const Tensor gr = (g_rgb && g_rgb->defined()) ? g_rgb->contiguous().view({n, 3}) : Tensor();
+  const Tensor gm = (g_mask && g_mask->defined()) ? g_mask->contiguous().view({n}) : Tensor();
+  auto r = volume_render_bwd(gr, gm, saved[0], palette, ro.contiguous(), rd.contiguous(), nr.contiguous(),
+                             fr.contiguous(), saved[1], S, fine, white_bg, randomize, scene_range, inv_alpha, beta,
+                             heads, saved[2], saved[3], saved[4], saved[5], saved[6], saved[7], saved[8], coords);
+  return {to_channel_major(r[0]), r[1], r[2], r[3]};
+}
+
+// composite_fwd: render_volume_density (nerf_utils.py:125-163) -> (rgb_map [...,3], depth, mask [...],
+// weights [...,N]); sigma [...,N], rgb [...,N,3], rd [...,3], t [...,N]
+std::tuple<Tensor, Tensor, Tensor, Tensor> composite_fwd(const Tensor& sigma, const Tensor& rgb, const Tensor& rd,
+                                                         const Tensor& t, bool white_bg) {
+  for (auto p : {std::make_pair(&sigma, "sigma"), std::make_pair(&rgb, "rgb"), std::make_pair(&rd, "rd"),
+                 std::make_pair(&t, "t")})
+    require(*p.first, p.second);
+  const int64_t N = sigma.size(-1), n = sigma.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(N >= 1 && N <= 1024 && rgb.numel() == n * N * 3 && rgb.size(-1) == 3 && rd.numel() == n * 3 &&
+                  t.sizes() == sigma.sizes(),
+              "nfi::composite_fwd: sigma [...,N <= 1024], rgb [...,N,3], rd [...,3], t [...,N] expected");
+  const c10::DeviceGuard guard(sigma.device());
+  const Tensor sc = sigma.contiguous(), cc = rgb.contiguous(), rc = rd.contiguous(), tc = t.contiguous();
+  auto lead = sigma.sizes().slice(0, sigma.dim() - 1).vec();
+  auto lead3 = lead;
+  lead3.push_back(3);
+  auto o = sigma.options();
+  Tensor rgb_map = torch::empty(lead3, o), depth = torch::empty(lead, o), mask = torch::empty(lead, o);
+  Tensor w = torch::empty_like(sc);
+  check(nfi_composite_forward(sc.data_ptr<float>(), cc.data_ptr<float>(), rc.data_ptr<float>(), tc.data_ptr<float>(),
+                              n, (int32_t)N, white_bg, rgb_map.data_ptr<float>(), depth.data_ptr<float>(),
+                              mask.data_ptr<float>(), w.data_ptr<float>(), stream_of(sigma)),
+        "nfi_composite_forward");
+  return {rgb_map, depth, mask, w};
+}
+
+// composite_bwd -> (d_sigma, d_rgb, d_rd, d_t) in the inputs' shapes; absent gradients count as zero
+std::tuple<Tensor, Tensor, Tensor, Tensor> composite_bwd(const Tensor& sigma, const Tensor& rgb, const Tensor& rd,
+                                                         const Tensor& t, bool white_bg,
+                                                         const c10::optional<Tensor>& g_rgb,
+                                                         const c10::optional<Tensor>& g_mask,
+                                                         const c10::optional<Tensor>& g_weights) {
+  for (auto p : {std::make_pair(&sigma, "sigma"), std::make_pair(&rgb, "rgb"), std::make_pair(&rd, "rd"),
+                 std::make_pair(&t, "t")})
+    require(*p.first, p.second);
+  const int64_t N = sigma.size(-1), n = sigma.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(N >= 1 && N <= 1024 && rgb.numel() == n * N * 3 && rd.numel() == n * 3 && t.sizes() == sigma.sizes(),
+              "nfi::composite_bwd: sigma [...,N <= 1024], rgb [...,N,3], rd [...,3], t [...,N] expected");
+  const c10::DeviceGuard guard(sigma.device());
+  const Tensor sc = sigma.contiguous(), cc = rgb.contiguous(), rc = rd.contiguous(), tc = t.contiguous();
+  auto o = sigma.options();
+  const Tensor gr = (g_rgb && g_rgb->defined()) ? g_rgb->contiguous() : torch::zeros({n, 3}, o);
+  const Tensor gm = (g_mask && g_mask->defined()) ? g_mask->contiguous() : torch::zeros({n}, o);
+  const Tensor gw = (g_weights && g_weights->defined()) ? g_weights->contiguous() : Tensor();
+  TORCH_CHECK(gr.numel() == n * 3 && gm.numel() == n && (!gw.defined() || gw.numel() == n * N),
+              "nfi::composite_bwd: gradient shapes differ from the outputs'");
+  Tensor d_sigma = torch::empty_like(sc), d_rgb = torch::empty_like(cc), d_rd = torch::empty_like(rc),
+         d_t = torch::empty_like(tc);
+  check(nfi_composite_backward(sc.data_ptr<float>(), cc.data_ptr<float>(), rc.data_ptr<float>(), tc.data_ptr<float>(),
+                               n, (int32_t)N, white_bg, gr.data_ptr<float>(), gm.data_ptr<float>(), mptr(gw),
+                               d_sigma.data_ptr<float>(), d_rgb.data_ptr<float>(), d_rd.data_ptr<float>(),
+                               d_t.data_ptr<float>(), stream_of(sigma)),
+        "nfi_composite_backward");
+  return {d_sigma.view(sigma.sizes()), d_rgb.view(rgb.sizes()), d_rd.view(rd.sizes()), d_t.view(t.sizes())};
+}
+
+// triplane_mlp: the sampler closure (generator.py:587-681, TriplanarDecoder :301-331) at world points
+// x [B,P,3] on planes [B,3,32,R,R]
+struct MlpInputs {
+  Tensor tm, dec, palette, x;
+  nfi_field f;
+};
+
+MlpInputs mlp_inputs(const Tensor& planes, const Tensor& W1s, const Tensor& b1, const Tensor& W2s, const Tensor& b2,
+                     const c10::optional<Tensor>& palette, const Tensor& x, double inv_alpha, double beta,
+                     double scene_range, int64_t heads) {
+  require(x, "x");
+  TORCH_CHECK(x.dim() == 3 && x.size(0) == planes.size(0) && x.size(2) == 3, "nfi::triplane_mlp: x [B,P,3] expected");
+  TORCH_CHECK(heads == 0 || heads == NFI_HEAD_RGB_SIGMOID || heads == NFI_HEAD_NERF_DENSITY ||
+                  heads == (NFI_HEAD_RGB_SIGMOID | NFI_HEAD_NERF_DENSITY),
+              "nfi::triplane_mlp: heads 0, NFI_HEAD_RGB_SIGMOID, NFI_HEAD_NERF_DENSITY");
+  const bool has_pal = palette && palette->defined();
+  TORCH_CHECK(has_pal == !(heads & NFI_HEAD_RGB_SIGMOID),
+              "nfi: a palette is required exactly when the colour head is the attention head");
+  MlpInputs m;
+  m.tm = to_texel_major(planes);
+  m.dec = pack_with_gains(W1s, b1, W2s, b2, true);
+  if (has_pal) {
+    require(*palette, "palette");
+    TORCH_CHECK(palette->sizes() == torch::IntArrayRef({planes.size(0), 10, 3}), "nfi: palette [B,10,3] expected");
+    m.palette = palette->contiguous();
+  }
+  m.x = x.contiguous();
+  m.f = nfi_field{};
+  m.f.planes = m.tm.data_ptr<float>();
+  m.f.sb = m.tm.stride(0);
+  m.f.sq = m.tm.stride(1);
+  m.f.st = m.tm.stride(3);
+  m.f.R = (int32_t)m.tm.size(2);
+  m.f.dec = m.dec.data_ptr<float>();
+  m.f.palette = has_pal ? m.palette.data_ptr<float>() : nullptr;
+  m.f.inv_alpha = (float)inv_alpha;
+  m.f.beta = (float)beta;
+  m.f.scene_range = (float)scene_range;
+  m.f.heads = (int32_t)heads;
+  return m;
+}
+
+// triplane_mlp_fwd -> (sigma [B,P], rgb [B,P,3], y [B,P,11] decoder outputs)
+std::tuple<Tensor, Tensor, Tensor> triplane_mlp_fwd(const Tensor& planes, const Tensor& W1s, const Tensor& b1,
+                                                    const Tensor& W2s, const Tensor& b2,
+                                                    const c10::optional<Tensor>& palette, const Tensor& x,
+                                                    double inv_alpha, double beta, double scene_range, int64_t heads) {
+  const c10::DeviceGuard guard(x.device());
+  MlpInputs m = mlp_inputs(planes, W1s, b1, W2s, b2, palette, x, inv_alpha, beta, scene_range, heads);
+  const int64_t B = x.size(0), P = x.size(1);
+  auto o = x.options();
+  Tensor sigma = torch::empty({B, P}, o), rgb = torch::empty({B, P, 3}, o), y = torch::empty({B, P, 11}, o);
+  check(nfi_sampler_forward(&m.f, m.x.data_ptr<float>(), (int32_t)B, P, sigma.data_ptr<float>(), rgb.data_ptr<float>(),
+                            y.data_ptr<float>(), stream_of(x)),
+        "nfi_sampler_forward");
+  return {sigma, rgb, y};
+}
+
+// triplane_mlp_bwd -> (d_planes [B,3,32,R,R], d_palette [B,10,3] (empty without a palette), d_x [B,P,3])
+std::tuple<Tensor, Tensor, Tensor> triplane_mlp_bwd(const Tensor& planes, const Tensor& W1s, const Tensor& b1,
+                                                    const Tensor& W2s, const Tensor& b2,
+                                                    const c10::optional<Tensor>& palette, const Tensor& x,
+                                                    double inv_alpha, double beta, double scene_range, int64_t heads,
+                                                    const c10::optional<Tensor>& g_sigma,
+                                                    const c10::optional<Tensor>& g_rgb,
+                                                    const c10::optional<Tensor>& g_y) {
+  const c10::DeviceGuard guard(x.device());
+  MlpInputs m = mlp_inputs(planes, W1s, b1, W2s, b2, palette, x, inv_alpha, beta, scene_range, heads);
+  const int64_t B = x.size(0), P = x.size(1);
+  auto o = x.options();
+  auto grad = [&](const c10::optional<Tensor>& g, int64_t k, const char* name) {
+    if (!g || !g->defined()) return Tensor();
+    require(*g, name);
+    TORCH_CHECK(g->numel() == B * P * k, "nfi::triplane_mlp_bwd: ", name, " has the wrong size");
+    return g->contiguous();
+  };
+  const Tensor gs = grad(g_sigma, 1, "g_sigma"), gr = grad(g_rgb, 3, "g_rgb"), gy = grad(g_y, 11, "g_y");
+  Tensor d_tm = torch::zeros_like(m.tm), d_x = torch::empty({B, P, 3}, o);
+  const int64_t chunks = nfi_sampler_chunks((int32_t)B, P);
+  Tensor d_part = m.palette.defined() ? torch::empty({chunks, 30}, o) : Tensor();
+  void* st = stream_of(x);
+  check(nfi_sampler_backward(&m.f, m.x.data_ptr<float>(), (int32_t)B, P, gs.defined() ? gs.data_ptr<float>() : nullptr,
+                             gr.defined() ? gr.data_ptr<float>() : nullptr, gy.defined() ? gy.data_ptr<float>() : nullptr,
+                             d_tm.data_ptr<float>(), mptr(d_part), d_x.data_ptr<float>(), st),
+        "nfi_sampler_backward");
+  Tensor d_pal = torch::empty({0}, o);
+  if (m.palette.defined()) {
+    d_pal = torch::empty({B, 30}, o);
+    Tensor ws = torch::empty({B * 64 * 30}, o);
+    check(nfi_segment_sum(d_part.data_ptr<float>(), (int32_t)B, (int32_t)(chunks / B), 30, d_pal.data_ptr<float>(),
+                          ws.data_ptr<float>(), st),
+          "nfi_segment_sum");
+    d_pal = d_pal.view({B, 10, 3});
+  }
+  return {to_channel_major(d_tm), d_pal, d_x};
+}
+
 // ---- Meta kernels (shape propagation for the tracing front ends; no computation) ------------------
 std::vector<Tensor> volume_render_fwd_meta(const Tensor& planes_tm, const c10::optional<Tensor>&, const Tensor& ro,
                                            const Tensor&, const Tensor&, const Tensor&, const Tensor&, int64_t samples,
@@ -525,6 +766,22 @@ TORCH_LIBRARY(nfi, m) {
   m.def("cumprod_exclusive(Tensor tensor) -> Tensor");
   m.def("render_volume_density_weights_only(Tensor sigma_a, Tensor ray_origins, Tensor ray_directions, "
         "Tensor depth_values) -> Tensor");
+  m.def("render_fwd(Tensor planes, Tensor W1s, Tensor b1, Tensor W2s, Tensor b2, Tensor? palette, float inv_alpha, "
+        "float beta, Tensor ro, Tensor rd, Tensor near, Tensor far, int S, float scene_range, bool white_bg, "
+        "bool randomize, int seed, int offset, Tensor? u_coarse=None, Tensor? u_fine=None, bool fine=True, "
+        "int heads=0) -> (Tensor, Tensor, Tensor, Tensor, Tensor[])");
+  m.def("render_bwd(Tensor? grad_rgb, Tensor? grad_mask, Tensor[] saved_state, Tensor? palette, float inv_alpha, "
+        "float beta, Tensor ro, Tensor rd, Tensor near, Tensor far, int S, float scene_range, bool white_bg, "
+        "bool randomize, bool fine=True, int heads=0, bool coords=True) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("composite_fwd(Tensor sigma, Tensor rgb, Tensor rd, Tensor t, bool white_bg) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("composite_bwd(Tensor sigma, Tensor rgb, Tensor rd, Tensor t, bool white_bg, Tensor? g_rgb, Tensor? g_mask, "
+        "Tensor? g_weights=None) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("triplane_mlp_fwd(Tensor planes, Tensor W1s, Tensor b1, Tensor W2s, Tensor b2, Tensor? palette, Tensor x, "
+        "float inv_alpha, float beta, float scene_range, int heads=0) -> (Tensor, Tensor, Tensor)");
+  m.def("triplane_mlp_bwd(Tensor planes, Tensor W1s, Tensor b1, Tensor W2s, Tensor b2, Tensor? palette, Tensor x, "
+        "float inv_alpha, float beta, float scene_range, int heads, Tensor? g_sigma, Tensor? g_rgb, "
+        "Tensor? g_y=None) -> (Tensor, Tensor, Tensor)");
 }
 
 // the autograd-carrying ops decompose into their torch::autograd::Function (which records the graph)
@@ -542,6 +799,12 @@ TORCH_LIBRARY_IMPL(nfi, CUDA, m) {
   m.impl("volume_render_bwd", &volume_render_bwd);
   m.impl("sample_pdf", &sample_pdf);
   m.impl("compute_near_far_planes", &compute_near_far_planes);
+  m.impl("render_fwd", &render_fwd);
+  m.impl("render_bwd", &render_bwd);
+  m.impl("composite_fwd", &composite_fwd);
+  m.impl("composite_bwd", &composite_bwd);
+  m.impl("triplane_mlp_fwd", &triplane_mlp_fwd);
+  m.impl("triplane_mlp_bwd", &triplane_mlp_bwd);
 }
 
 TORCH_LIBRARY_IMPL(nfi, Meta, m) {

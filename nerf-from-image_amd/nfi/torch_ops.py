@@ -24,7 +24,8 @@ from . import _lib
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBRARY = os.path.join(HERE, 'libnfi_torch.so')
 OPS = ('rays', 'pack_decoder', 'volume_render', 'volume_render_fwd', 'volume_render_bwd', 'sample_pdf',
-       'compute_near_far_planes', 'cumprod_exclusive', 'render_volume_density_weights_only')
+       'compute_near_far_planes', 'cumprod_exclusive', 'render_volume_density_weights_only',
+       'render_fwd', 'render_bwd', 'composite_fwd', 'composite_bwd', 'triplane_mlp_fwd', 'triplane_mlp_bwd')
 _loaded = False
 
 

@@ -95,3 +95,104 @@ def test_seam_ops_match_stages():
     t = torch.sort(torch.rand(4, 5, 24, generator=g), dim=-1)[0].to(DEV) + 1
     assert torch.equal(torch.ops.nfi.render_volume_density_weights_only(sig, ro, rd, t),
                        stages.render_volume_density_weights_only(sig, ro, rd, t))
+
+
+def _channel_major(tm):
+    return tm.permute(0, 1, 4, 2, 3)
+
+
+def _scaled_decoder(inp):
+    """EqualizedLinear's gains folded on the host (stylegan.py:173-176), the render_fwd convention."""
+    w1, b1, w2, b2 = (inp[k].to(DEV) for k in ('w1', 'b1', 'w2', 'b2'))
+    return w1 * (1 / w1.shape[1] ** 0.5), b1, w2 * (1 / w2.shape[1] ** 0.5), b2
+
+
+def test_render_fwd_bwd_match_volume_render_ops():
+    """nfi::render_fwd / render_bwd (SURVEY §8(b): channel-major planes, scaled decoder) against
+    volume_render_fwd / _bwd on the converted layouts: the same launches, so equal outputs."""
+    torch_ops.load()
+    inp, planes_tm, dec = _inputs(seed=9, B=2, H=8, S=16)
+    cam, focal = inp['cam'].to(DEV), inp['focal'].to(DEV)
+    ro, rd, near, far = torch.ops.nfi.rays(cam, focal, None, None, 8, 8, 1.4)
+    pal = inp['palette'].to(DEV)
+    planes = inp['planes'].to(DEV)
+    rgb, depth, mask, t_sorted, saved = torch.ops.nfi.render_fwd(
+        planes, *_scaled_decoder(inp), pal, 1.0, 0.1, ro, rd, near, far, 16, 1.4, False, True, 11, 0)
+    ref = torch.ops.nfi.volume_render_fwd(planes_tm, pal, ro, rd, near, far, dec, 16, True, False, True, 1.4, 1.0,
+                                          0.1, 0, 11, None, None, True)
+    torch.testing.assert_close(rgb, ref[0], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(mask, ref[2], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(t_sorted.reshape(-1, 32), ref[3], rtol=1e-6, atol=1e-7)
+    assert t_sorted.shape == (2, 8, 8, 32) and len(saved) == 9
+    assert bool((t_sorted[..., 1:] >= t_sorted[..., :-1]).all())
+    g = torch.Generator().manual_seed(3)
+    g_rgb = torch.randn(2, 8, 8, 3, generator=g).to(DEV)
+    g_mask = torch.randn(2, 8, 8, generator=g).to(DEV)
+    d_planes, d_pal, d_ro, d_rd = torch.ops.nfi.render_bwd(g_rgb, g_mask, saved, pal, 1.0, 0.1, ro, rd, near, far,
+                                                          16, 1.4, False, True)
+    rb = torch.ops.nfi.volume_render_bwd(g_rgb.reshape(-1, 3), g_mask.reshape(-1), planes_tm, pal, ro, rd, near,
+                                         far, dec, 16, True, False, True, 1.4, 1.0, 0.1, 0, *ref[3:10], True)
+    assert d_planes.shape == planes.shape
+    assert rel_l2(d_planes, _channel_major(rb[0])) < 1e-5
+    assert rel_l2(d_pal, rb[1]) < 1e-5
+    assert rel_l2(d_ro, rb[2]) < 1e-5 and rel_l2(d_rd, rb[3]) < 1e-5
+
+
+def test_composite_ops_match_stages():
+    torch_ops.load()
+    g = torch.Generator().manual_seed(12)
+    sig = (torch.rand(3, 7, 40, generator=g) * 4).to(DEV)
+    rgb = torch.rand(3, 7, 40, 3, generator=g).to(DEV)
+    rd = torch.nn.functional.normalize(torch.randn(3, 7, 3, generator=g), dim=-1).to(DEV) * 1.3
+    t = (torch.sort(torch.rand(3, 7, 40, generator=g), dim=-1)[0] * 2 + 1).to(DEV)
+    for white in (False, True):
+        out = torch.ops.nfi.composite_fwd(sig, rgb, rd, t, white)
+        leaves = [x.clone().requires_grad_() for x in (sig, rgb, rd, t)]
+        ref = stages._Composite.apply(*leaves, white, True)
+        for a, b in zip(out, ref):
+            assert torch.equal(a, b.detach())
+        g_rgb = torch.randn(3, 7, 3, generator=g).to(DEV)
+        g_mask = torch.randn(3, 7, generator=g).to(DEV)
+        g_w = torch.randn(3, 7, 40, generator=g).to(DEV)
+        d = torch.ops.nfi.composite_bwd(sig, rgb, rd, t, white, g_rgb, g_mask, g_w)
+        torch.autograd.backward([ref[0], ref[2], ref[3]], [g_rgb, g_mask, g_w])
+        for a, leaf in zip(d, leaves):
+            assert torch.equal(a, leaf.grad)
+
+
+@pytest.mark.parametrize('heads', [0, 1])
+def test_triplane_mlp_ops_match_sampler(heads):
+    """triplane_mlp_fwd / _bwd (the sampler closure on world points) against nfi.stages' sampler
+    Function on the texel-major planes and the packed decoder."""
+    torch_ops.load()
+    inp, planes_tm, _ = _inputs(seed=13, B=2, H=8, S=8)
+    w1s, b1, w2s, b2 = _scaled_decoder(inp)
+    if heads == 1:                                     # RGB_SIGMOID: a 4-row colour head, no palette
+        w2s, b2 = w2s[:4].contiguous(), b2[:4].contiguous()
+        pal = None
+    else:
+        pal = inp['palette'].to(DEV)
+    dec = ops.pack_decoder(inp['w1'].to(DEV), inp['b1'].to(DEV), inp['w2'].to(DEV)[:w2s.shape[0]],
+                           inp['b2'].to(DEV)[:w2s.shape[0]])
+    g = torch.Generator().manual_seed(4)
+    x = ((torch.rand(2, 300, 3, generator=g) * 2 - 1) * 1.3).to(DEV)
+    planes = inp['planes'].to(DEV)
+    sigma, rgb, y = torch.ops.nfi.triplane_mlp_fwd(planes, w1s, b1, w2s, b2, pal, x, 1.0, 0.1, 1.4, heads)
+    pl = planes_tm.clone().requires_grad_()
+    pa = None if pal is None else pal.clone().requires_grad_()
+    xx = x.clone().requires_grad_()
+    rs, rr, ry = stages._Sampler.apply(pl, pa, xx, dec, heads, 1.4, 1.0, 0.1)
+    for a, b in ((sigma, rs), (rgb, rr), (y, ry)):
+        torch.testing.assert_close(a, b.detach(), rtol=1e-6, atol=1e-7)
+    gs = torch.randn(2, 300, generator=g).to(DEV)
+    gr = torch.randn(2, 300, 3, generator=g).to(DEV)
+    d_planes, d_pal, d_x = torch.ops.nfi.triplane_mlp_bwd(planes, w1s, b1, w2s, b2, pal, x, 1.0, 0.1, 1.4, heads,
+                                                          gs, gr)
+    torch.autograd.backward([rs, rr], [gs, gr])
+    assert d_planes.shape == planes.shape
+    assert rel_l2(d_planes, _channel_major(pl.grad)) < 1e-5
+    assert rel_l2(d_x, xx.grad) < 1e-5
+    if pal is None:
+        assert d_pal.numel() == 0
+    else:
+        assert rel_l2(d_pal, pa.grad) < 1e-5
