@@ -41,6 +41,7 @@ enum {
   NFI_OK = 0,
   NFI_EINVAL = -1,   /* bad argument / unsupported configuration */
   NFI_ELAUNCH = -2,  /* HIP launch error */
+  NFI_ECHECK = -3,   /* integrity check of an -DNFI_TILE_CHECK debug build failed (never in the product) */
 };
 
 /* Camera batch (nerf_utils.py:28-93): cam2world [B,4,4]; focal [B] (NULL = orthographic
@@ -200,6 +201,9 @@ int32_t nfi_render_forward(const nfi_render_args* a, void* stream);
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a);
 int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * beams * 3 * ((R-2)/7+1) * ((R-2)/4+1),
                                                             beams = 1 unless built with NFI_BEAM_SAMPLES */
+/* The same size from the shapes alone (B images of H x W rays, N samples per ray, planes R x R): for
+ * shape-only callers (the TORCH_LIBRARY Meta kernels) that hold no argument block; -1 on bad shapes. */
+int64_t nfi_tile_count_size_shape(int32_t B, int32_t R, int32_t H, int32_t W, int32_t N);
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 /* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
  * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,

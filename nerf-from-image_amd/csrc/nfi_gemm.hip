@@ -472,9 +472,9 @@ int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* strea
   return NFI_OK;
 }
 
-static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
-                            const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                            int a_shared, int32_t ksplit, float* work, void* stream) {
+static int32_t gemm_split16_impl(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                                 const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                                 int a_shared, int32_t ksplit, float* work, void* stream) {
   NFI_REQUIRE(Ah && Al && a_inv && B && b_max && C, "gemm_split16: null pointer");
   NFI_REQUIRE(batch > 0 && batch <= 65535 && M > 0 && N > 0 && K > 0 && K % gemm::BK == 0,
               "gemm_split16: bad shape batch=%d M=%d N=%d K=%d (K a multiple of %d)", batch, M, N, K, gemm::BK);
@@ -527,9 +527,13 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
   const int forced = fe ? atoi(fe) : 0;
   if (ksplit > 1) {   // K ranges of whole steps, partials summed in order
     const int steps = K / gemm::BK;
-    ksplit = std::min(ksplit, steps);
+    // ranges of ceil(steps / ksplit) steps, and only as many ranges as that covers: no range is
+    // empty (K = 160, ksplit 4: 5 steps -> 3 ranges of 2, 2, 1 steps; the kernel's first load of a
+    // range reads at its start unconditionally)
+    const int per = (steps + std::min(ksplit, steps) - 1) / std::min(ksplit, steps);
+    ksplit = (steps + per - 1) / per;
     g.ksplit = ksplit;
-    g.kchunk = (steps + ksplit - 1) / ksplit * gemm::BK;
+    g.kchunk = per * gemm::BK;
     g.work = work;
     NFI_REQUIRE((long long)batch * ksplit <= 65535, "gemm_split16: batch x ksplit too large");
     NFI_REQUIRE(((uintptr_t)work & 15) == 0 && ((uintptr_t)C & 15) == 0 && (long long)M * N % 4 == 0,
@@ -549,6 +553,20 @@ static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float*
     NFI_CHECK_LAUNCH("split16_gemm_kernel");
   }
   return NFI_OK;
+}
+
+// The maxima slots are consumed by the launch's last workgroup.  A call that returns an error has
+// not consumed them (rejected before the launch) or may not have (a failed launch): they are zeroed
+// here on the same stream, so the next producer's maxima start from zero instead of max(stale, new) —
+// a stale larger maximum would silently coarsen the next product's B scale
+// (tests/test_gpu_gemm.py::test_maxima_slots_back_to_back_and_after_rejection).
+static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
+                            const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
+                            int a_shared, int32_t ksplit, float* work, void* stream) {
+  const int32_t rc = gemm_split16_impl(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, a_shared, ksplit, work, stream);
+  if (rc != NFI_OK && b_max)
+    (void)hipMemsetAsync(const_cast<uint32_t*>(b_max), 0, (gemm::SLOTS + 1) * sizeof(uint32_t), (hipStream_t)stream);
+  return rc;
 }
 
 int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,

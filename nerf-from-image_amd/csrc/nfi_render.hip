@@ -2198,9 +2198,48 @@ struct TileArgs {
   int sq, st;
   int R;
   TileGrid tg;
+  // integrity checks of the -DNFI_TILE_CHECK debug build (unused by the product kernels)
+  const int* cursor;      // [K] bin cursors after the append: must equal offsets + counts
+  int* check;             // [64] violation counters / first-failure record (tile_fail)
+  float* shadow;          // d planes summed a second way (per-entry float atomics), same strides
+  long long nsamp;
+  int K;
 };
 
 typedef float img32 __attribute__((ext_vector_type(32)));
+
+// ---- -DNFI_TILE_CHECK: device-side integrity checks of the tile pass ----
+// Every global index the pass derives from loaded or shuffled data, every LDS region it stages
+// and reads back, and the bin lists themselves are checked; a violation increments
+// check[code] and records the first failure (code, chunk, tile, lane, value, expected) in
+// check[32..37] instead of trapping, and the index is clamped so the launch still completes (a
+// faulting kernel would take the GPU down).  The host reads the counters after the launch and
+// fails the call with NFI_ECHECK.  Codes:
+//   1 chunk / tile / entry range      2 bin list incomplete (cursor != offsets + counts)
+//   3 record sample index >= nsamp    4 record slot > 30 or unknown flag bits
+//   5 shuffled row index != record    6 scalar entry record != vector record
+//   7 gradient-row stage read back    8 tile texels read back after staging
+//   9 wave-image dump read back      10 record weights not in [0, 1]
+//  11 tile texels changed during the chunk   12 gradient-row stage changed during the entry loop
+#ifndef NFI_TILE_CHECK
+#define NFI_TILE_CHECK 0
+#endif
+#if NFI_TILE_CHECK
+__device__ __noinline__ void tile_fail(int* check, int code, int c, int tile, int lane, long long v,
+                                       long long expect) {
+  atomicAdd(check + code, 1);
+  if (atomicCAS(check + 31, 0, code) == 0) {
+    check[32] = code;
+    check[33] = c;
+    check[34] = tile;
+    check[35] = lane;
+    check[36] = (int)v;
+    check[37] = (int)expect;
+  }
+}
+#define NFI_TCHK(cond, code, c, tile, lane, v, e) \
+  if (!(cond)) tile_fail(A.check, code, c, tile, lane, (long long)(v), (long long)(e))
+#endif
 typedef int iv4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(4))) iv4* cint4_p;
 
@@ -2216,8 +2255,14 @@ constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 __device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
 // the tile's 8x5 plane texels x 32 channels (pose gradients), texel rows of XS floats (per-lane
-// b128 reads of different texels conflict only for texels 16 slots apart)
-constexpr int TEXF = TTX * TTY * XS;            // 1,440 floats
+// b128 reads of different texels conflict only for texels 16 slots apart); a tile row of 8
+// texels is TEXR floats (NFI_TEX_ROW_PAD floats after each row: the layout experiment of round 4)
+#ifndef NFI_TEX_ROW_PAD
+#define NFI_TEX_ROW_PAD 0
+#endif
+constexpr int TEXR = TTX * XS + NFI_TEX_ROW_PAD;
+constexpr int TEXF = TTY * TEXR;                // 1,440 floats
+__device__ __forceinline__ int tex_at(int texel) { return (texel / TTX) * TEXR + (texel % TTX) * XS; }
 // (the wave images are dumped over the stages and texels at the end of a chunk: >= 4 x 2,048)
 constexpr int TILE_LDS = (4 * TROWS + TEXF > 4 * 2048) ? 4 * TROWS + TEXF : 4 * 2048;   // 38,016 B at BATCH 56
 
@@ -2292,26 +2337,74 @@ __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, floa
 // with T_yx the cell's texels (row y0 + y, column x0 + x), e = 1 - w, s = 1 - n, and the
 // multipliers gxm / gym = (R-1)/2 strictly inside, else 0 (record flags).  A border-clipped
 // point (x0 = R-1, w = 0, gxm = 0) normalized to (R-2, w = 1) gives the same gy, and likewise in y.
+//
+// NFI_TILE_GG 1 (default): the same sums as three channel dot products of first differences,
+//   SA = sum_c g_c (T01 - T00),  SB = sum_c g_c (T11 - T10),  SC = sum_c g_c (T10 - T00),
+//   gx = gxm (SA + n (SB - SA)),  gy = gym (SC + w (SB - SA))
+// (s (T01 - T00) + n (T11 - T10) = A + n (B - A) and e (T10 - T00) + w (T11 - T01) = C + w (B - A),
+// as T11 - T01 - T10 + T00 = B - A): per channel 3 differences + 3 FMAs on aligned register pairs
+// (packed fp32, the float4 quads straight from the b128 reads) instead of ATen's 10 operations
+// per channel with the cell weights broadcast into pairs (~30 register moves per quad pair).
+// The differences are taken before any product, as ATen does; four partial sums per dot product
+// (channel c mod 4) replace ATen's sequential channel order.  NFI_TILE_GG 0: ATen's form.
+#ifndef NFI_TILE_GG
+#define NFI_TILE_GG 1
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f4v pk_sub(f4v a, f4v b, float m1) {
+  f4v r;
+  r.xy = __builtin_elementwise_fma((f2v){b.x, b.y}, (f2v){m1, m1}, (f2v){a.x, a.y});
+  r.zw = __builtin_elementwise_fma((f2v){b.z, b.w}, (f2v){m1, m1}, (f2v){a.z, a.w});
+  return r;
+}
+#ifndef NFI_TILE_GG_UNROLL
+#define NFI_TILE_GG_UNROLL 2
+#endif
 __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, const float* __restrict__ Tex,
                                                 int l, int4 rec, int q, float half, float* __restrict__ dpc) {
   const int slot = rec.y & 31;
   const float w = __int_as_float(rec.z), n = __int_as_float(rec.w);
-  const float e = 1.f - w, s = 1.f - n;
   float gx = 0.f, gy = 0.f;
+  const float* tb = Tex + tex_at(slot);
+#if NFI_TILE_GG
+  f4v SA = {0.f, 0.f, 0.f, 0.f}, SB = SA, SC = SA;
+  // -1 from an SGPR the compiler cannot see through: a - b as fma(b, -1, a) (one rounding, the
+  // same value) stays a packed v_pk_fma_f32; hipcc scalarises a packed fsub into four v_sub_f32
+  float m1;
+  asm("s_mov_b32 %0, -1.0" : "=s"(m1));
+#pragma unroll NFI_TILE_GG_UNROLL
+  for (int k = 0; k < NC / 4; ++k) {
+    const f4v g4 = *reinterpret_cast<const f4v*>(G + stage_q(l, k));
+    const float* t = tb + 4 * k;
+    const f4v t00 = *reinterpret_cast<const f4v*>(t);
+    const f4v t01 = *reinterpret_cast<const f4v*>(t + XS);
+    const f4v t10 = *reinterpret_cast<const f4v*>(t + TEXR);
+    const f4v t11 = *reinterpret_cast<const f4v*>(t + TEXR + XS);
+    SA += g4 * pk_sub(t01, t00, m1);
+    SB += g4 * pk_sub(t11, t10, m1);
+    SC += g4 * pk_sub(t10, t00, m1);
+  }
+  const float sa = (SA.x + SA.y) + (SA.z + SA.w), sb = (SB.x + SB.y) + (SB.z + SB.w);
+  const float sc = (SC.x + SC.y) + (SC.z + SC.w);
+  gx = fmaf(n, sb - sa, sa);
+  gy = fmaf(w, sb - sa, sc);
+#else
+  const float e = 1.f - w, s = 1.f - n;
 #pragma unroll 2
   for (int k = 0; k < NC / 4; ++k) {
     const float4 g4 = *reinterpret_cast<const float4*>(G + stage_q(l, k));
-    const float* t = Tex + slot * XS + 4 * k;
+    const float* t = tb + 4 * k;
     const float4 t00 = *reinterpret_cast<const float4*>(t);
     const float4 t01 = *reinterpret_cast<const float4*>(t + XS);
-    const float4 t10 = *reinterpret_cast<const float4*>(t + TTX * XS);
-    const float4 t11 = *reinterpret_cast<const float4*>(t + (TTX + 1) * XS);
+    const float4 t10 = *reinterpret_cast<const float4*>(t + TEXR);
+    const float4 t11 = *reinterpret_cast<const float4*>(t + TEXR + XS);
 #define NFI_GG(C)                                                     \
   gx = fmaf(g4.C, fmaf(s, t01.C - t00.C, n * (t11.C - t10.C)), gx);   \
   gy = fmaf(g4.C, fmaf(e, t10.C - t00.C, w * (t11.C - t01.C)), gy);
     NFI_GG(x) NFI_GG(y) NFI_GG(z) NFI_GG(w)
 #undef NFI_GG
   }
+#endif
   const float2 out = make_float2((rec.y & 0x100) ? gx * half : 0.f, (rec.y & 0x200) ? gy * half : 0.f);
   *reinterpret_cast<float2*>(dpc + ((long long)rec.x * 3 + q) * 2) = out;
 }
@@ -2329,23 +2422,53 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     // (wave-uniform scalars: readfirstlane keeps the entry loop's control and the register-image
     // index in SGPRs)
     const int tile = __builtin_amdgcn_readfirstlane(A.chunk_tile[c]);
+#if NFI_TILE_CHECK
+    if (tid == 0) {
+      NFI_TCHK(c >= 0 && c < A.meta[0] && tile >= 0 && tile < A.K, 1, c, tile, 0, c, A.meta[0]);
+    }
+    if (tile < 0 || tile >= A.K) return;
+#endif
     const int first = __builtin_amdgcn_readfirstlane(A.offsets[tile] + (c - A.chunk_start[tile]) * CHUNK);
     const int last = __builtin_amdgcn_readfirstlane(min(A.offsets[tile] + A.counts[tile], first + CHUNK));
+#if NFI_TILE_CHECK
+    if (tid == 0) {
+      NFI_TCHK(first >= A.offsets[tile] && first < last && A.offsets[tile] + A.counts[tile] <= A.offsets[A.K],
+               1, c, tile, 0, first, last);
+      NFI_TCHK(A.cursor[tile] == A.offsets[tile] + A.counts[tile], 2, c, tile, 0, A.cursor[tile],
+               A.offsets[tile] + A.counts[tile]);
+    }
+#endif
     int b, q, tx, ty;
     tile_decode(tile, A.tg, b, q, tx, ty);
+    const float* src = A.planes + (long long)b * A.sb + (long long)q * A.sq;
     if (A.dpc) {
       // the tile's texels of plane q (texels past the plane edge are never referenced: cells
       // are normalized to x0, y0 <= R-2)
-      const float* src = A.planes + (long long)b * A.sb + (long long)q * A.sq;
       for (int k = tid; k < TTX * TTY * (NC / 4); k += 256) {
         const int texel = k / (NC / 4), c4 = k % (NC / 4);
         const int gy = ty * TSY + texel / TTX, gx = tx * TSX + texel % TTX;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (gy < A.R && gx < A.R) v = *reinterpret_cast<const float4*>(src + (long long)(gy * A.R + gx) * A.st + 4 * c4);
-        *reinterpret_cast<float4*>(Tex + texel * XS + 4 * c4) = v;
+        *reinterpret_cast<float4*>(Tex + tex_at(texel) + 4 * c4) = v;
       }
       __syncthreads();
     }
+#if NFI_TILE_CHECK
+    // code 8 / 11: the staged texels read back against the planes (k = 8: after staging, 11: at
+    // the end of the chunk's entry loops)
+#define NFI_TEX_VERIFY(CODE)                                                                          \
+    if (A.dpc) {                                                                                      \
+      for (int k = tid; k < TTX * TTY * (NC / 4); k += 256) {                                         \
+        const int texel = k / (NC / 4), c4 = k % (NC / 4);                                            \
+        const int gy = ty * TSY + texel / TTX, gx = tx * TSX + texel % TTX;                           \
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);                                                   \
+        if (gy < A.R && gx < A.R) v = *reinterpret_cast<const float4*>(src + (long long)(gy * A.R + gx) * A.st + 4 * c4); \
+        const float4 s = *reinterpret_cast<const float4*>(Tex + tex_at(texel) + 4 * c4);              \
+        NFI_TCHK(s.x == v.x && s.y == v.y && s.z == v.z && s.w == v.w, CODE, c, tile, tid, texel, c4); \
+      }                                                                                               \
+    }
+    NFI_TEX_VERIFY(8)
+#endif
     const float half = (float)(A.R - 1) / 2.f;
     // each wave sums a contiguous quarter of the chunk (runs of one ray stay together)
     const int per = (((last - first) + 3) / 4 + 7) & ~7;
@@ -2367,6 +2490,18 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #define NFI_ENTRY(R, K)                                                                              \
   tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(R[K].y) & 31, __int_as_float(R[K].z), \
              __int_as_float(R[K].w), gv[K], wsgn, woff)
+#if NFI_TILE_CHECK
+      // code 6: each scalar record of the entry loop against the batch's vector record (lane U + k)
+#define NFI_STEP_CHECK(U, RUSE)                                                                      \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) if ((U) + k < n) {                                 \
+      const int vx = __shfl(crec.x, (U) + k), vy = __shfl(crec.y, (U) + k);                          \
+      const int vz = __shfl(crec.z, (U) + k), vw = __shfl(crec.w, (U) + k);                          \
+      NFI_TCHK(RUSE[k].x == vx && RUSE[k].y == vy && RUSE[k].z == vz && RUSE[k].w == vw, 6, c, tile, \
+               (U) + k, RUSE[k].x, vx);                                                              \
+    }
+#else
+#define NFI_STEP_CHECK(U, RUSE)
+#endif
 #define NFI_STEP(U, RUSE, RNEXT)                                                                     \
   {                                                                                                  \
     float gv[8];                                                                                     \
@@ -2374,26 +2509,70 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
                  "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];                \
+    NFI_STEP_CHECK(U, RUSE)                                                                          \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
   }
       // Rows loaded coalesced: lane l holds float4 (l & 7) of entry 8j + (l >> 3), j = 0..6 (the
       // entry's row index comes from its lane's record by ds_bpermute): each b128 load reads 8
       // whole 128-B rows instead of one 16-B piece of 56 different rows.
-#define NFI_LD1(J, V, SX)                                                                            \
+#if NFI_TILE_CHECK
+      // codes 3 / 5: the shuffled row index against the record loaded directly; clamped into range
+#define NFI_ROW_CHECK(J, RB)                                                                         \
+    {                                                                                                \
+      const int want_ = A.list[min((RB) + 8 * (J) + (l >> 3), b1 - 1)].x;                            \
+      NFI_TCHK(row_ == want_, 5, c, tile, l, row_, want_);                                           \
+      NFI_TCHK(row_ >= 0 && row_ < A.nsamp, 3, c, tile, l, row_, A.nsamp);                          \
+      row_ = (row_ >= 0 && row_ < A.nsamp) ? row_ : 0;                                               \
+    }
+#else
+#define NFI_ROW_CHECK(J, RB)
+#endif
+#define NFI_LD1(J, V, SX, RB)                                                                        \
   {                                                                                                  \
-    const int row_ = __shfl((SX), 8 * (J) + (l >> 3));                                              \
+    int row_ = __shfl((SX), 8 * (J) + (l >> 3));                                                    \
+    NFI_ROW_CHECK(J, RB)                                                                             \
     V = *reinterpret_cast<const float4*>(A.gfeat + (long long)row_ * NC + 4 * (l & 7));             \
   }
-#define NFI_LOAD_ROWC(REC)                                                                           \
+#define NFI_LOAD_ROWC(REC, RB)                                                                       \
   {                                                                                                  \
     const int sx_ = (REC).x;                                                                         \
-    _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_LD1(j, rc[j], sx_)                     \
+    _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_LD1(j, rc[j], sx_, RB)                 \
   }
 #define NFI_ST1(J, V)                                                                                \
   {                                                                                                  \
     const int e_ = 8 * (J) + (l >> 3);                                                               \
     lds_st(reinterpret_cast<float4*>(G + e_ * XS + 4 * (l & 7)), e_ < n ? V : make_float4(0.f, 0.f, 0.f, 0.f)); \
   }
+#if NFI_TILE_CHECK
+      // code 7: the stored gradient rows read back; code 12 (after the entry loop): the rows
+      // against gfeat itself; codes 3 / 4 / 10: the batch's records
+#define NFI_G_VERIFY(CODE)                                                                           \
+    _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) {                                          \
+      const int e_ = 8 * j + (l >> 3);                                                               \
+      const float4 s_ = *reinterpret_cast<const float4*>(G + e_ * XS + 4 * (l & 7));                 \
+      float4 w_ = make_float4(0.f, 0.f, 0.f, 0.f);                                                   \
+      if (e_ < n) {                                                                                  \
+        const int rx_ = A.list[base_ + e_].x;                                                        \
+        if (rx_ >= 0 && rx_ < A.nsamp) w_ = *reinterpret_cast<const float4*>(A.gfeat + (long long)rx_ * NC + 4 * (l & 7)); \
+      }                                                                                              \
+      NFI_TCHK(s_.x == w_.x && s_.y == w_.y && s_.z == w_.z && s_.w == w_.w, CODE, c, tile, l, base_ + e_, j); \
+    }
+#define NFI_BATCH_CHECK()                                                                            \
+    NFI_G_VERIFY(7)                                                                                  \
+    if (l < n) {                                                                                     \
+      const int4 d_ = A.list[base_ + l];                                                             \
+      NFI_TCHK(d_.x == crec.x && d_.y == crec.y && d_.z == crec.z && d_.w == crec.w, 6, c, tile, l, crec.x, d_.x); \
+      NFI_TCHK(crec.x >= 0 && crec.x < A.nsamp, 3, c, tile, l, crec.x, A.nsamp);                    \
+      NFI_TCHK((crec.y & 31) <= 30 && (crec.y & ~0x31f) == 0, 4, c, tile, l, crec.y, 30);           \
+      const float w_ = __int_as_float(crec.z), n_ = __int_as_float(crec.w);                          \
+      NFI_TCHK(w_ >= 0.f && w_ <= 1.f && n_ >= 0.f && n_ <= 1.f, 10, c, tile, l, crec.z, crec.w);  \
+    }
+#define NFI_CREC(VREC) const int4 crec = VREC;
+#else
+#define NFI_BATCH_CHECK()
+#define NFI_G_VERIFY(CODE)
+#define NFI_CREC(VREC)
+#endif
 #define NFI_NEXT_REC(VREC, AHEAD)                                                                    \
     VREC = vnext;                                                                                    \
     vnext = A.list[min(base_ + 2 * (AHEAD) + l, b1 - 1)];
@@ -2403,9 +2582,11 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int n = min(BATCH, b1 - base_);                                                            \
     _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_ST1(j, rc[j])                         \
     wave_lds_sync();                                                                                 \
+    NFI_CREC(VREC)                                                                                   \
+    NFI_BATCH_CHECK()                                                                                \
     if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
     NFI_NEXT_REC(VREC, AHEAD)                                                                        \
-    NFI_LOAD_ROWC(VREC)                                                                              \
+    NFI_LOAD_ROWC(VREC, base_ + (AHEAD))                                                             \
     NFI_STAMP(24)                                                                                    \
     iv4 ra[8], rb[8];                                                                                \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];                             \
@@ -2414,6 +2595,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       if (u + 8 >= n) break;                                                                         \
       NFI_STEP(u + 8, rb, ra)                                                                        \
     }                                                                                                \
+    NFI_G_VERIFY(12)                                                                                 \
     wave_lds_sync();                                                                                 \
     NFI_STAMP(25)                                                                                    \
   }
@@ -2423,7 +2605,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       // the next batch's records are already in registers when its rows are issued (the row
       // loads do not wait a record round trip)
       int4 vnext = A.list[min(b0 + BATCH + l, b1 - 1)];
-      NFI_LOAD_ROWC(vrec)
+      NFI_LOAD_ROWC(vrec, b0)
       for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
 #undef NFI_BATCHC
 #undef NFI_NEXT_REC
@@ -2432,14 +2614,28 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #undef NFI_LD1
 #undef NFI_STEP
 #undef NFI_ENTRY
+#undef NFI_STEP_CHECK
+#undef NFI_ROW_CHECK
+#undef NFI_BATCH_CHECK
+#undef NFI_G_VERIFY
+#undef NFI_CREC
       NFI_TILE_FLUSH(img, cur, a0, a1);
     }
     NFI_STAMP(26)
+#if NFI_TILE_CHECK
+    NFI_TEX_VERIFY(11)
+#undef NFI_TEX_VERIFY
+#endif
     __syncthreads();   // every wave is done with its row stage
     // wave images -> LDS [wave][half][slot][channel]
 #pragma unroll
     for (int r = 0; r < 32; ++r) lds[wv * 2048 + (h * 32 + r) * NC + cl] = img[r];
     __syncthreads();
+#if NFI_TILE_CHECK
+    // code 9: the dumped wave images read back
+#pragma unroll
+    for (int r = 0; r < 32; ++r) NFI_TCHK(lds[wv * 2048 + (h * 32 + r) * NC + cl] == img[r], 9, c, tile, l, r, wv);
+#endif
     float* dq = A.dplanes + (long long)b * A.sb + (long long)q * A.sq;
     for (int k = tid; k < TTX * TTY * NC; k += 256) {
       const int texel = k / NC, ch = k % NC;
@@ -2454,6 +2650,26 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       const int gy = ty * TSY + yl, gx = tx * TSX + xl;
       if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
     }
+#if NFI_TILE_CHECK
+    // the second sum of d planes (compared with the first by tile_shadow_compare_kernel): every
+    // entry of this wave's range again, straight from the list and gfeat in global memory, one
+    // float atomic per (entry, texel, channel) — no LDS stage, scalar records, register image or dump
+    if (A.shadow) {
+      float* sq_ = A.shadow + (long long)b * A.sb + (long long)q * A.sq;
+      for (int e = b0; e < b1; ++e) {
+        const int4 r_ = A.list[e];
+        if (r_.x < 0 || r_.x >= A.nsamp) continue;
+        const int slot = r_.y & 31, ly = slot / TTX, lx = slot % TTX;
+        const float w = __int_as_float(r_.z), nn = __int_as_float(r_.w);
+        const float g = A.gfeat[(long long)r_.x * NC + cl] * (h ? nn : 1.f - nn);
+        const int gy = ty * TSY + ly + h, gx = tx * TSX + lx;
+        if (gy < A.R && gx + 1 < A.R) {
+          unsafeAtomicAdd(sq_ + (gy * A.R + gx) * A.st + cl, g * (1.f - w));
+          unsafeAtomicAdd(sq_ + (gy * A.R + gx + 1) * A.st + cl, g * w);
+        }
+      }
+    }
+#endif
     __syncthreads();
     NFI_STAMP(27)
   }
@@ -2687,6 +2903,28 @@ constexpr int TILE_WGS = 2048;   // >= 256 CUs x NFI_TILE_OCC workgroups residen
 #ifndef NFI_TILE_REV
 #define NFI_TILE_REV 0   // 1: last key first (the beams the field backward wrote last)
 #endif
+#if NFI_TILE_CHECK
+// sum over d planes of (d planes - snapshot - shadow)^2 and shadow^2 (the tile pass's added d planes
+// against the per-entry atomics of the same entries), into two doubles
+__global__ void __launch_bounds__(256) tile_shadow_compare_kernel(const float* __restrict__ dp, const float* __restrict__ snap,
+                                                                  const float* __restrict__ sh, long long n, double* out) {
+  double d2 = 0.0, s2 = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double d = (double)dp[i] - (double)snap[i] - (double)sh[i];
+    d2 += d * d;
+    s2 += (double)sh[i] * (double)sh[i];
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    d2 += __shfl_xor(d2, m);
+    s2 += __shfl_xor(s2, m);
+  }
+  if (lane_id() == 0) {
+    atomicAdd(out, d2);
+    atomicAdd(out + 1, s2);
+  }
+}
+#endif
+
 __global__ void __launch_bounds__(256, NFI_TILE_OCC) tile_kernel(TileArgs A) {
   __shared__ __attribute__((aligned(16))) float lds[TILE_LDS];
   __shared__ int next;
@@ -3300,6 +3538,9 @@ struct Workspace {
   int* part;
   int4* list;
   float* dpc;
+  int* check;        // -DNFI_TILE_CHECK builds: counters + first failure + two double sums
+  float* shadow;     // -DNFI_TILE_CHECK builds: the second d-planes sum and a snapshot of d planes
+  float* snapshot;
   long long bytes;
 };
 
@@ -3329,6 +3570,13 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.chunk_tile = reinterpret_cast<int*>(take((3 * nsamp / CHUNK + K + 1) * 4));
   w.list = reinterpret_cast<int4*>(take((3 * nsamp + 128) * 16));   // + padding read by tile_chunk
   w.dpc = reinterpret_cast<float*>(take(nsamp * 6 * 4));
+  w.check = nullptr;
+  w.shadow = w.snapshot = nullptr;
+#if NFI_TILE_CHECK
+  w.check = reinterpret_cast<int*>(take(64 * 4));
+  w.shadow = reinterpret_cast<float*>(take((long long)a->B * a->field.sb * 4));
+  w.snapshot = reinterpret_cast<float*>(take((long long)a->B * a->field.sb * 4));
+#endif
   w.bytes = p - static_cast<char*>(base);
   return w;
 }
@@ -3418,14 +3666,45 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
 #endif
   TileArgs TA{a->field.planes, dpc_used, w.gfeat, counts, w.offsets, w.chunk_start,
               w.chunk_tile, w.meta, w.list, g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st,
-              a->field.R, tg};
+              a->field.R, tg, w.cursor, w.check, w.shadow, nsamp, K};
   if (do_tiles) {
     // 3) per-tile register accumulation of d planes (+ per-entry grid gradients for the pose)
     // (a bound on the chunk count meta[0]; the chunk queue meta[1] starts at 0)
     const long long TB = 3 * nsamp / CHUNK + K + 1;
     NFI_REQUIRE(hipMemsetAsync(w.meta + 1, 0, 4, s) == hipSuccess, "render_backward: memset failed");
+#if NFI_TILE_CHECK
+    const size_t dpb = (size_t)a->B * a->field.sb * 4;
+    NFI_REQUIRE(hipMemsetAsync(w.check, 0, 64 * 4, s) == hipSuccess && hipMemsetAsync(w.shadow, 0, dpb, s) == hipSuccess &&
+                    hipMemcpyAsync(w.snapshot, g->d_planes, dpb, hipMemcpyDeviceToDevice, s) == hipSuccess,
+                "render_backward: check-build setup failed");
+#endif
     tile_kernel<<<(unsigned)std::min<long long>(TB, TILE_WGS), 256, 0, s>>>(TA);
     NFI_CHECK_LAUNCH("tile_kernel");
+#if NFI_TILE_CHECK
+    {
+      const long long ne = (long long)a->B * a->field.sb;
+      tile_shadow_compare_kernel<<<(unsigned)std::min<long long>((ne + 255) / 256, 4096), 256, 0, s>>>(
+          g->d_planes, w.snapshot, w.shadow, ne, reinterpret_cast<double*>(w.check + 40));
+      NFI_CHECK_LAUNCH("tile_shadow_compare_kernel");
+      int hc[64];
+      NFI_REQUIRE(hipMemcpyAsync(hc, w.check, sizeof(hc), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                      hipStreamSynchronize(s) == hipSuccess,
+                  "render_backward: check readback failed");
+      double sums[2];
+      memcpy(sums, hc + 40, sizeof(sums));
+      const double rel = sums[1] > 0 ? sqrt(sums[0] / sums[1]) : sqrt(sums[0]);
+      int nbad = 0;
+      for (int k = 1; k < 31; ++k) nbad += hc[k];
+      if (nbad || !(rel <= 1e-5)) {
+        set_error("tile check: %d violations (first: code %d chunk %d tile %d lane %d value %d expected %d; "
+                  "per code 1..12: %d %d %d %d %d %d %d %d %d %d %d %d); d planes vs the per-entry sum: "
+                  "rel L2 %.3g",
+                  nbad, hc[32], hc[33], hc[34], hc[35], hc[36], hc[37], hc[1], hc[2], hc[3], hc[4], hc[5], hc[6],
+                  hc[7], hc[8], hc[9], hc[10], hc[11], hc[12], rel);
+        return NFI_ECHECK;
+      }
+    }
+#endif
     // 4) ray-coordinate gradients
 #if defined(NFI_ABLATE) && (NFI_ABLATE == 5 || NFI_ABLATE == 6)
     if (false) {   // experiment: no reduce launch
@@ -3521,6 +3800,12 @@ int64_t nfi_tile_count_size(const nfi_render_args* a) {
   if (nfi::validate(a)) return -1;
   const nfi::TileGrid tg = nfi::tile_grid(a->field.R, a->HW, a->W, a->fine ? 2 * a->S : a->S);
   return (int64_t)a->B * nfi::beams_per_image(tg) * 3 * tg.nx * tg.ny;
+}
+
+int64_t nfi_tile_count_size_shape(int32_t B, int32_t R, int32_t H, int32_t W, int32_t N) {
+  if (B <= 0 || R < 2 || H <= 0 || W <= 0 || N <= 0) return -1;
+  const nfi::TileGrid tg = nfi::tile_grid(R, H * W, W, N);
+  return (int64_t)B * nfi::beams_per_image(tg) * 3 * tg.nx * tg.ny;
 }
 
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {

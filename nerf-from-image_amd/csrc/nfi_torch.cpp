@@ -6,7 +6,7 @@
 //
 //   nfi::rays(cam, focal?, center?, bbox?, H, W, scene_range) -> (ro, rd, near, far)
 //       get_ray_bundle + F.normalize + compute_near_far_planes (run.py:193-200); autograd to cam, focal
-//   nfi::pack_decoder(w1, b1, w2, b2) -> dec          EqualizedLinear gains folded (stylegan.py:173-176)
+//   nfi::pack_decoder(w1, b1, w2, b2, attention_values=-1) -> dec   EqualizedLinear gains folded (stylegan.py:173-176)
 //   nfi::volume_render(planes_tm, palette?, ro, rd, near, far, dec, samples, fine, white_background,
 //                      randomize, scene_range, inv_alpha, beta, heads, seed, u_coarse?, u_fine?)
 //       -> (rgb, depth, mask)                         run.py:202-348 fused; autograd to planes_tm,
@@ -125,8 +125,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> rays(const Tensor& cam, const c10::op
 }
 
 // ---- decoder -------------------------------------------------------------------------------------
-// g1 / g2 < 0: the EqualizedLinear gains 1/sqrt(fan_in); 1: weights already scaled (W1s, W2s)
-Tensor pack_with_gains(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, const Tensor& b2_in, bool scaled) {
+// scaled false: the EqualizedLinear gains 1/sqrt(fan_in) are folded here; true: weights already scaled
+// (W1s, W2s).  attention_values: 0 = the wide-sigmoid colour head (w2 [4,64]: distance + 3 features,
+// zero-padded to the kernels' 11 rows: rows the head never reads); 1..10 = the attention head with
+// that many logits (w2 [N+1,64]): for N < 10 the missing logits get zero weights and a -1e30 bias, so
+// their softmax terms exp(-1e30 - max) are exactly 0 and the head is the N-value one (render.py
+// attention_padded does the same; a ZERO-biased padded logit would put exp(-max) of mass on palette
+// rows N..9); -1 = inferred from the rows: 11 -> 10 attention values, 4 -> the colour head, 33 -> the
+// view-direction decoder; any other row count needs attention_values.
+Tensor pack_with_gains(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, const Tensor& b2_in, bool scaled,
+                       int64_t attention_values) {
   require(w1, "w1");
   require(b1, "b1");
   require(w2_in, "w2");
@@ -136,12 +144,23 @@ Tensor pack_with_gains(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, 
               "nfi: decoder w1 [64,32], b1 [64], w2 [nout,64], b2 [nout] expected");
   const c10::DeviceGuard guard(w1.device());
   Tensor w2 = w2_in.detach(), b2 = b2_in.detach();
-  const int32_t nout = w2.size(0) == 33 ? 33 : 11;
-  if (w2.size(0) < 11) {   // attention_values 0: [4, 64] zero-padded to the kernels' 11 rows
-    w2 = torch::cat({w2, torch::zeros({11 - w2.size(0), w2.size(1)}, w2.options())});
-    b2 = torch::cat({b2, torch::zeros({11 - b2.size(0)}, b2.options())});
+  const int64_t rows = w2.size(0);
+  if (attention_values < 0) {
+    TORCH_CHECK(rows == 11 || rows == 4 || rows == 33,
+                "nfi: a decoder output layer of ", rows, " rows is ambiguous: pass attention_values (0 = colour "
+                "head [4,64], 1..10 = attention head [N+1,64])");
+    attention_values = rows == 4 ? 0 : 10;
   }
-  TORCH_CHECK(w2.size(0) == nout, "nfi: decoder output layer must have <= 11 or 33 rows, got ", w2.size(0));
+  const int32_t nout = rows == 33 ? 33 : 11;
+  if (rows != 33) {
+    TORCH_CHECK(attention_values <= 10 && rows == (attention_values == 0 ? 4 : attention_values + 1),
+                "nfi: decoder output layer of ", rows, " rows does not match attention_values=", attention_values);
+    if (rows < 11) {
+      const double fill = attention_values == 0 ? 0.0 : -1e30;
+      w2 = torch::cat({w2, torch::zeros({11 - rows, w2.size(1)}, w2.options())});
+      b2 = torch::cat({b2.reshape({-1}), torch::full({11 - rows}, fill, b2.options())});
+    }
+  }
   Tensor dec = torch::empty({nfi_decoder_size(nout)}, w1.options());
   const float g1 = scaled ? 1.0f : (float)(1.0 / std::sqrt((double)w1.size(1)));
   const float g2 = scaled ? 1.0f : (float)(1.0 / std::sqrt((double)w2.size(1)));
@@ -152,8 +171,13 @@ Tensor pack_with_gains(const Tensor& w1, const Tensor& b1, const Tensor& w2_in, 
   return dec;
 }
 
-Tensor pack_decoder(const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2) {
-  return pack_with_gains(w1, b1, w2, b2, false);
+Tensor pack_decoder(const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2, int64_t attention_values) {
+  return pack_with_gains(w1, b1, w2, b2, false, attention_values);
+}
+
+// the attention count of a render / triplane_mlp call: 0 for the colour head, else W2s's logits
+int64_t attention_of(const Tensor& W2s, int64_t heads) {
+  return (heads & NFI_HEAD_RGB_SIGMOID) ? 0 : W2s.size(0) - 1;
 }
 
 // ---- fused render --------------------------------------------------------------------------------
@@ -528,7 +552,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, std::vector<Tensor>> render_fwd(
     int64_t heads) {
   const c10::DeviceGuard guard(planes.device());
   const Tensor tm = to_texel_major(planes);
-  const Tensor dec = pack_with_gains(W1s, b1, W2s, b2, true);
+  const Tensor dec = pack_with_gains(W1s, b1, W2s, b2, true, attention_of(W2s, heads));
   auto r = render_forward_impl(tm, palette, ro.contiguous(), rd.contiguous(), nr.contiguous(), fr.contiguous(), dec, S,
                                fine, white_bg, randomize, scene_range, inv_alpha, beta, heads, seed, u_coarse, u_fine,
                                true, offset);
@@ -631,7 +655,7 @@ MlpInputs mlp_inputs(const Tensor& planes, const Tensor& W1s, const Tensor& b1, 
               "nfi: a palette is required exactly when the colour head is the attention head");
   MlpInputs m;
   m.tm = to_texel_major(planes);
-  m.dec = pack_with_gains(W1s, b1, W2s, b2, true);
+  m.dec = pack_with_gains(W1s, b1, W2s, b2, true, attention_of(W2s, heads));
   if (has_pal) {
     require(*palette, "palette");
     TORCH_CHECK(palette->sizes() == torch::IntArrayRef({planes.size(0), 10, 3}), "nfi: palette [B,10,3] expected");
@@ -720,11 +744,11 @@ std::vector<Tensor> volume_render_fwd_meta(const Tensor& planes_tm, const c10::o
   auto e = [&](std::vector<int64_t> s, c10::ScalarType t = torch::kFloat) {
     return torch::empty(keep_state ? s : std::vector<int64_t>{0}, o.dtype(t));
   };
-  (void)planes_tm;
   return {torch::empty({B, H, W, 3}, o), torch::empty({B, H, W}, o), torch::empty({B, H, W}, o), e({n, N}),
           e({n, N}), e({n, 3, N}), e({n, 11, N}), e({n, N}, torch::kInt16), e({n * N, 32}),
-          // the tile count size depends on the plane resolution only: 3 planes x 37 x 64 tiles at 256
-          e({B * 3 * ((planes_tm.size(2) - 2) / 7 + 1) * ((planes_tm.size(2) - 2) / 4 + 1)}, torch::kInt32)};
+          // the library's own rule (beams included when it was built with NFI_BEAM_SAMPLES)
+          e({nfi_tile_count_size_shape((int32_t)B, (int32_t)planes_tm.size(2), (int32_t)H, (int32_t)W, (int32_t)N)},
+            torch::kInt32)};
 }
 
 std::vector<Tensor> volume_render_bwd_meta(const Tensor&, const Tensor&, const Tensor& planes_tm,
@@ -746,7 +770,7 @@ std::vector<Tensor> volume_render_bwd_meta(const Tensor&, const Tensor&, const T
 TORCH_LIBRARY(nfi, m) {
   m.def("rays(Tensor cam, Tensor? focal, Tensor? center, Tensor? bbox, int H, int W, float scene_range) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
-  m.def("pack_decoder(Tensor w1, Tensor b1, Tensor w2, Tensor b2) -> Tensor");
+  m.def("pack_decoder(Tensor w1, Tensor b1, Tensor w2, Tensor b2, int attention_values=-1) -> Tensor");
   m.def("volume_render(Tensor planes_tm, Tensor? palette, Tensor ro, Tensor rd, Tensor near, Tensor far, "
         "Tensor dec, int samples, bool fine, bool white_background, bool randomize, float scene_range, "
         "float inv_alpha, float beta, int heads, int seed, Tensor? u_coarse=None, Tensor? u_fine=None) "

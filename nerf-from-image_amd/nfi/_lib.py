@@ -79,6 +79,7 @@ SIGNATURES = {
     'nfi_render_forward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs), c_void_p]),
     'nfi_render_backward_workspace_bytes': (ctypes.c_int64, [ctypes.POINTER(NfiRenderArgs)]),
     'nfi_tile_count_size': (ctypes.c_int64, [ctypes.POINTER(NfiRenderArgs)]),
+    'nfi_tile_count_size_shape': (ctypes.c_int64, [ctypes.c_int32] * 5),
     'nfi_render_backward': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),
                                              ctypes.POINTER(NfiRenderGradArgs), c_void_p]),
     'nfi_render_backward_stage': (ctypes.c_int32, [ctypes.POINTER(NfiRenderArgs),

@@ -71,12 +71,14 @@ def build_torch_ops(force: bool = False, verbose: bool = True) -> str:
 
 def build(force: bool = False, verbose: bool = True, variant: str = '') -> str:
     """variant 'stamps': profiling library libnfi_hip_stamps.so with per-phase cycle counters
-    (-DNFI_STAMPS, loaded via NFI_LIBRARY by scripts/stamps.py); never the product build."""
+    (-DNFI_STAMPS, loaded via NFI_LIBRARY by scripts/stamps.py); 'tilecheck': the tile pass's
+    integrity-check build libnfi_hip_tilecheck.so (-DNFI_TILE_CHECK=1, tests/test_gpu_tile_check.py);
+    never the product build."""
     out = OUT if not variant else OUT.replace('.so', f'_{variant}.so')
     if not force and not variant and not _stale():
         return out
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-    extra = {'': [], 'stamps': ['-DNFI_STAMPS']}.get(variant)
+    extra = {'': [], 'stamps': ['-DNFI_STAMPS'], 'tilecheck': ['-DNFI_TILE_CHECK=1']}.get(variant)
     if extra is None:   # experiment builds: 'D<NAME>=<value>' -> -D<NAME>=<value>
         extra = ['-' + variant] if variant.startswith('D') else []
     cmd = [hipcc] + FLAGS + extra + ['-o', out + '.tmp'] + [os.path.join(CSRC, s) for s in SOURCES]

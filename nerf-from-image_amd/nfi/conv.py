@@ -55,6 +55,14 @@ RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
 # the three-pass layers' 36 products on the f16 matrix cores at fp32 accuracy (csrc/nfi_gemm.hip:
 # hi / lo splits, three products each; the weights split once, V's scale from the input
 # transform's running maximum); 0: torch.bmm (hipBLASLt fp32)
+# Batch coupling: V's power-of-two scale is ONE per call, from the maximum over all 36 x K
+# x P entries, and P spans every image of the batch.  An image whose activations / gradients sit 2^k
+# below the batch maximum gets 2^-(39-k) of its own magnitude as operand precision (fp32-level for k up
+# to ~15), so per-image results depend on the rest of the batch beyond that; the inversion's producer
+# batches images of one dataset (activations within a few powers of two of each other) and a sharded
+# run feeds each rank its own chunk, which can differ from the unsharded batch's rounding.  The
+# decoder's split (nfi_render.hip) scales per point / per wave instead; a per-image column-block scale
+# here would need one maximum slot set per image (not built).
 SPLIT16 = os.environ.get('NFI_SPLIT16', '1') != '0'
 SPLIT16_BK = 32       # the split GEMM's K step: channel counts must be multiples of it
 KSPLIT = os.environ.get('NFI_KSPLIT', '1') != '0'   # K split of the Winograd products with few tiles

@@ -242,24 +242,29 @@ HEAD_NERF_DENSITY = 2            # include/nfi.h NFI_HEAD_NERF_DENSITY
 HEAD_VIEWDIR = 4                 # include/nfi.h NFI_HEAD_VIEWDIR
 
 
-def pack_decoder(w1, b1, w2, b2, lr_multiplier: float = 1.0) -> torch.Tensor:
+def pack_decoder(w1, b1, w2, b2, lr_multiplier: float = 1.0, key_tensors=None) -> torch.Tensor:
     """EqualizedLinear gains (stylegan.py:173-176) folded into the packed decoder buffer.  A
     [4, 64] output layer (attention_values 0: distance + 3 colour features) is zero-padded to the
     kernels' 11 rows; a [33, 64] layer (the view-direction mapper's decoder, generator.py:376-377)
-    is packed in its own layout (nfi_decoder_pack_n, nout 33)."""
+    is packed in its own layout (nfi_decoder_pack_n, nout 33).
+    `key_tensors`: the caller's own (w1, b1, w2, b2) when w2 / b2 here are padded copies of them
+    (render.attention_padded): the cache is keyed on the tensors whose in-place updates bump a version,
+    never on a fresh copy whose storage the allocator may hand out again."""
     _require_device(w1, b1, w2, b2)
     nout = 33 if w2.shape[0] == 33 else 11
+    # a pure function of the four tensors' values: cached on w1 per (storage, version) of the caller's
+    # four tensors, taken before any padding — the inversion packs the same frozen decoder every step
+    # (one kernel + host work saved per step)
+    kt = tuple(key_tensors) if key_tensors is not None else (w1, b1, w2, b2)
+    key = tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in kt) + (float(lr_multiplier), w1.device)
+    hit = getattr(w1, '_nfi_dec', None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
     if w2.shape[0] < 11:
         w2 = torch.cat([w2.detach(), w2.new_zeros(11 - w2.shape[0], w2.shape[1])])
         b2 = torch.cat([b2.detach(), b2.new_zeros(11 - b2.shape[0])])
     if w2.shape[0] != nout:
         raise ValueError(f'decoder output layer must have <= 11 or 33 rows, got {w2.shape[0]}')
-    # a pure function of the four tensors' values: cached on w1 per (storage, version) of all four —
-    # the inversion packs the same frozen decoder every step (one kernel + host work saved per step)
-    key = tuple((t.data_ptr(), t._version) for t in (w1, b1, w2, b2)) + (float(lr_multiplier), w1.device)
-    hit = getattr(w1, '_nfi_dec', None)
-    if hit is not None and hit[0] == key:
-        return hit[1]
     lib = _lib.load()
     dec = torch.empty((int(lib.nfi_decoder_size(nout)),), device=w1.device)
     g1 = float(torch.tensor(lr_multiplier / math.sqrt(w1.shape[1]), dtype=torch.float32))

@@ -26,13 +26,27 @@ def world() -> Tuple[int, int]:
     return 0, 1
 
 
-def init_from_env(backend: str = 'nccl') -> Tuple[int, int, int]:
+# Test-only switch: run the collectives of gather_rows / sum_across / invert_sharded even in a
+# 1-rank group (they return early at world size 1), so a single-GPU box executes the RCCL branch
+# (tests/test_gpu_rccl.py).  Never set by the product.
+FORCE_COLLECTIVES = False
+
+
+def _collective() -> bool:
+    """True when a collective must run: a group of > 1 ranks, or any group under FORCE_COLLECTIVES."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or FORCE_COLLECTIVES
+
+
+def init_from_env(backend: str = 'nccl', force: bool = False) -> Tuple[int, int, int]:
     """torchrun-style init (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*); returns (rank, local, world).
-    Binds the process to its local GPU when backend is nccl (RCCL)."""
+    Binds the process to its local GPU when backend is nccl (RCCL).  A 1-rank world creates no
+    group unless `force` (the RCCL test on a one-GPU box)."""
     ws = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if ws > 1 and not dist.is_initialized():
+    if (ws > 1 or force) and not dist.is_initialized():
         if backend == 'nccl':
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device('cuda', local))
@@ -66,7 +80,7 @@ def shard(tensors: Dict[str, torch.Tensor], rank: int, world_size: int) -> Dict[
 def sum_scalars(values: Sequence[float], device) -> List[float]:
     """Optional per-step logging reduction (loss, sum psnr, sum lpips): one all_reduce."""
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if _collective():
         dist.all_reduce(t)
     return t.tolist()
 
@@ -82,7 +96,7 @@ def gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
     """Reassemble per-image results [n_local, ...] of every rank into [n_total, ...] in batch
     order (end-of-run report, run.py:2329-2404).  Ranks with empty chunks contribute nothing.
     The result is on `local`'s device (the collective itself runs where the backend needs it)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _collective():
         return local
     ws = dist.get_world_size()
     bounds = chunk_bounds(n_total, ws)
@@ -100,7 +114,7 @@ def gather_rows(local: torch.Tensor, n_total: int) -> torch.Tensor:
 
 def sum_across(values: torch.Tensor) -> torch.Tensor:
     """all_reduce(SUM) of a small tensor (per-step logging terms), returned on its own device."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _collective():
         return values
     t = values.detach().to(_comm_device(values), torch.float64).clone()
     dist.all_reduce(t)
@@ -174,7 +188,7 @@ def invert_sharded(generator, target_img: torch.Tensor, cam2world: torch.Tensor,
             loc = getattr(parts, name)
         else:
             loc = torch.zeros((0,) + like_shape, device=dev)
-        return gather_rows(loc, b) if ws > 1 else loc
+        return gather_rows(loc, b) if (ws > 1 or FORCE_COLLECTIVES) else loc
 
     ws_all = gathered('ws', (15, w_init.shape[-1]))
     z0_all = None if focal is None else gathered('z0', ())

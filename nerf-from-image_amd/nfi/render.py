@@ -253,7 +253,7 @@ def render(target_model, height, width, tform_cam2world, focal_length, center, b
         vhead = ops.pack_viewdir_head(vw, vb)
     planes_tm = ops.planes_texel_major(f.planes)
     w2, b2, palette = attention_padded(f)
-    dec = ops.pack_decoder(f.w1, f.b1, w2, b2)
+    dec = ops.pack_decoder(f.w1, f.b1, w2, b2, key_tensors=(f.w1, f.b1, f.w2, f.b2))
     opts = ops.RenderOptions(samples=int(depth_samples_per_ray), fine=bool(cfg.fine_sampling),
                              white_background=bool(cfg.white_background), randomize=bool(randomize),
                              scene_range=float(cfg.scene_range), inv_alpha=1.0 / float(f.alpha),

@@ -417,7 +417,7 @@ def make_sampler(field, scene_range: Optional[float] = None):
     planes_tm = planes_texel_major(field.planes)
     w2, b2, pal_padded = attention_padded(field)     # 1..9 attention values: padded to the kernels' 10
     nattn = int(field.attention_values)
-    dec = pack_decoder(field.w1, field.b1, w2, b2)
+    dec = pack_decoder(field.w1, field.b1, w2, b2, key_tensors=(field.w1, field.b1, field.w2, field.b2))
     palette = pal_padded if nattn else None
     inv_alpha = 1.0 / float(field.alpha) if field.use_sdf else 1.0
     beta = float(field.beta) if field.use_sdf else 0.1

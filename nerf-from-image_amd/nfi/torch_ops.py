@@ -4,7 +4,7 @@ reference's nerf_utils functions are @torch.jit.script) and the C++ frontend.  S
 arguments as nfi.ops / nfi.stages; load() fails loudly when the library is missing.
 
   torch.ops.nfi.rays(cam, focal, center, bbox, H, W, scene_range) -> (ro, rd, near, far)
-  torch.ops.nfi.pack_decoder(w1, b1, w2, b2) -> dec
+  torch.ops.nfi.pack_decoder(w1, b1, w2, b2, attention_values=-1) -> dec
   torch.ops.nfi.volume_render(planes_tm, palette, ro, rd, near, far, dec, samples, fine,
                               white_background, randomize, scene_range, inv_alpha, beta, heads,
                               seed, u_coarse=None, u_fine=None) -> (rgb, depth, mask)
@@ -43,7 +43,8 @@ def load() -> None:
 
 def render_script_source() -> str:
     """A TorchScript-able render (run.py:193-348 without the producer): rays + fused volume render,
-    for tests and callers that script their step."""
+    for tests and callers that script their step.  render_rays draws its randomness from the Philox
+    seed; render_rays_u takes the reference's draws (u_coarse / u_fine, or deterministic mode)."""
     return '''
 def render_rays(planes_tm: torch.Tensor, palette: Optional[torch.Tensor], dec: torch.Tensor,
                 cam: torch.Tensor, focal: Optional[torch.Tensor], H: int, W: int, S: int,
@@ -51,4 +52,14 @@ def render_rays(planes_tm: torch.Tensor, palette: Optional[torch.Tensor], dec: t
     ro, rd, near, far = torch.ops.nfi.rays(cam, focal, None, None, H, W, scene_range)
     return torch.ops.nfi.volume_render(planes_tm, palette, ro, rd, near, far, dec, S, True,
                                        white_background, True, scene_range, inv_alpha, beta, 0, seed)
+
+
+def render_rays_u(planes_tm: torch.Tensor, palette: Optional[torch.Tensor], dec: torch.Tensor,
+                  cam: torch.Tensor, focal: Optional[torch.Tensor], H: int, W: int, S: int,
+                  scene_range: float, inv_alpha: float, beta: float, white_background: bool,
+                  randomize: bool, u_coarse: Optional[torch.Tensor], u_fine: Optional[torch.Tensor]):
+    ro, rd, near, far = torch.ops.nfi.rays(cam, focal, None, None, H, W, scene_range)
+    return torch.ops.nfi.volume_render(planes_tm, palette, ro, rd, near, far, dec, S, True,
+                                       white_background, randomize, scene_range, inv_alpha, beta, 0, 0,
+                                       u_coarse, u_fine)
 '''

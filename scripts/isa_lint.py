@@ -164,6 +164,53 @@ def lint_gpr_idx(path: str):
     return bad
 
 
+DS_ANY = re.compile(r'^\s*(ds_(?:write|read|bpermute|permute|add|swizzle)\w*)\s+(.*)$')
+
+
+def ds_addr_rewrites(path: str, window: int = 2, kernel_re: str = ''):
+    """Report-only rule 3: DS instructions (stores, loads, permutes) whose ADDRESS VGPR an
+    instruction rewrites within `window` wait states after issue — the address-side analogue of
+    rule 1, the one pattern round 4's padded tile layout added to the tile pass's staging store
+    (DESIGN.md §3).  Not a documented hazard (rule 1's data hazard was found by measurement); listed
+    so a layout change that introduces one is visible in review.  Returns (kernel, line, insn, writer)."""
+    out = []
+    lines = open(path).read().splitlines()
+    kernel = None
+    for i, ln in enumerate(lines):
+        if re.match(r'^_Z\S+:', ln):
+            kernel = ln.split(':')[0]
+        if kernel_re and not (kernel and re.search(kernel_re, kernel)):
+            continue
+        m = DS_ANY.match(ln.split(';')[0])
+        if not m:
+            continue
+        ops = split_ops(m.group(2))
+        mnem = m.group(1)
+        # address = first operand for stores / atomics without return, second for loads and permutes
+        aidx = 1 if mnem.startswith(('ds_read', 'ds_bpermute', 'ds_permute', 'ds_swizzle')) or '_rtn' in mnem else 0
+        if len(ops) <= aidx or not ops[aidx].startswith('v'):
+            continue
+        addr = regs(ops[aidx])
+        n, j = 0, i + 1
+        while j < len(lines) and n < window:
+            t = lines[j].split(';')[0].rstrip()
+            j += 1
+            if not t.strip() or t.strip().endswith(':') or t.strip().startswith('.'):
+                continue
+            im = INSN.match(t)
+            if not im:
+                continue
+            n += 1
+            if im.group(1) == 's_nop':
+                n += int((im.group(2) or '0').strip(), 0)
+            if vdst(im.group(1), im.group(2) or '') & addr:
+                out.append((kernel, i + 1, ln.strip(), t.strip()))
+                break
+            if STOP.match(t):
+                break
+    return out
+
+
 def compile_asm(src: str, out: str, extra=()):
     from nfi.build import FLAGS
     flags = [f for f in FLAGS if f not in ('-shared', '-fPIC')]

@@ -112,3 +112,80 @@ def test_split16_shared_a_matches_fp64(b, M, N, K):
         e_hip = float((C[i].double() - ref64[i]).abs().max()) / scale
         e_ref = float((ref32[i].double() - ref64[i]).abs().max()) / scale
         assert e_hip <= 4 * e_ref + 2 ** -22, (i, e_hip, e_ref)
+
+
+def test_maxima_slots_back_to_back_and_after_rejection():
+    """The split product's self-clearing maxima slots (nfi_gemm.hip release_slots: the input transform
+    fills 64 running maxima, the GEMM's last workgroup returns them to zero).  (1) One layer's
+    three-pass Winograd convolution back to back on inputs whose maxima shrink by 2^10 and 2^20 and
+    grow back: each call within the fp64 bound on its OWN scale (a slot still holding the previous
+    call's larger maximum would coarsen the next B scale by that factor).  (2) The input transform
+    fills the slots from a large input, then the GEMM call is rejected (K not a multiple of 32): the
+    rejection zeroes the slots, so the next call on an input 2^30 smaller keeps its precision (a stale
+    maximum would put its operands 2^30 below the scale: fp16 underflow, error ~1)."""
+    g = torch.Generator(device=DEV).manual_seed(7)
+    Ci, Co, H = 64, 128, 32
+    x = torch.randn((2, Ci, H, H), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    Uw, _ = conv.weights(w)
+    assert Uw.split is not None
+
+    def check(xs):
+        y = conv._winograd(xs, Uw)
+        ref = torch.nn.functional.conv2d(xs.double(), w.double(), padding=1)
+        e = float((y.double() - ref).abs().max() / ref.abs().max())
+        assert e <= 2e-5, e
+
+    old = conv.FUSED, conv.SPLIT16
+    try:
+        conv.FUSED, conv.SPLIT16 = False, True
+        for s in (1.0, 2.0 ** -10, 2.0 ** -20, 1.0):
+            check(x * s)
+        lib = _lib.load()
+        st = ctypes.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+        vmax = conv._slots(Uw, DEV)
+        P = 2 * (H // 4) * (H // 4)
+        V = torch.empty((36, Ci, P), device=DEV)
+        big = x * 2.0 ** 10
+        _lib.check(lib.nfi_wino_input_transform_max(_p(big), None, None, _p(V), _p(vmax), 2, Ci, H, H, st),
+                   'nfi_wino_input_transform_max')
+        assert int(vmax[:64].abs().sum()) > 0
+        hi, lo, inv = Uw.split
+        M = torch.empty((36, Co, P), device=DEV)
+        rc = lib.nfi_gemm_split16(_p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Co, P, Ci + 1, st)
+        assert rc != 0, 'K % 32 != 0 must be rejected'
+        torch.cuda.synchronize()
+        assert int(vmax.abs().sum()) == 0, 'a rejected call must leave the maxima slots zeroed'
+        check(x * 2.0 ** -20)
+    finally:
+        conv.FUSED, conv.SPLIT16 = old
+
+
+@pytest.mark.parametrize('K,ks', [(160, 4), (96, 3), (224, 5)])
+def test_ksplit_ranges_never_empty(K, ks):
+    """nfi_gemm_split16_ksplit with a split the K steps do not fill evenly (K = 160 = 5 steps in 4
+    ranges used to leave range 3 empty and load past the operands): the ranges are re-cut so that none
+    is empty, and the result stays within the fp64 bound."""
+    g = torch.Generator(device=DEV).manual_seed(K + ks)
+    b, M, N = 3, 96, 200
+    A = torch.randn((b, M, K), device=DEV, generator=g)
+    B = torch.randn((b, K, N), device=DEV, generator=g)
+    lib = _lib.load()
+    st = ctypes.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    hi = torch.empty(A.shape, device=DEV, dtype=torch.int16)
+    lo = torch.empty(A.shape, device=DEV, dtype=torch.int16)
+    inv = torch.empty((b,), device=DEV)
+    _lib.check(lib.nfi_split16_pack(_p(A), b, M * K, _p(hi), _p(lo), _p(inv), st), 'nfi_split16_pack')
+    slots = torch.empty((128,), device=DEV, dtype=torch.int32)
+    _lib.check(lib.nfi_absmax_slots(_p(B), B.numel(), _p(slots), st), 'nfi_absmax_slots')
+    C = torch.empty((b, M, N), device=DEV)
+    work = torch.empty((ks, b, M, N), device=DEV)
+    _lib.check(lib.nfi_gemm_split16_ksplit(_p(hi), _p(lo), _p(inv), _p(B), _p(slots), _p(C), b, M, N, K, ks,
+                                           _p(work), st), 'nfi_gemm_split16_ksplit')
+    ref64 = torch.bmm(A.double(), B.double())
+    ref32 = torch.bmm(A, B)
+    for i in range(b):
+        scale = float((A[i].double().abs() @ B[i].double().abs()).max())
+        e_hip = float((C[i].double() - ref64[i]).abs().max()) / scale
+        e_ref = float((ref32[i].double() - ref64[i]).abs().max()) / scale
+        assert e_hip <= 4 * e_ref + 2 ** -22, (i, e_hip, e_ref)

@@ -2,13 +2,15 @@
 trajectory (tests/golden/inversion.npz: run.py:1960-2310 around the reference Generator, render()
 and pose_utils; 3 Adam steps, L1 loss, pose optimised, injected random draws).
 
-The producer runs in PyTorch-ROCm on the GPU; the volume render (forward + backward to planes,
-palette and the camera) is the HIP path.  Tolerances: losses to 1e-4 relative (the HIP render
-matches the reference to fp32 rounding, tests/test_gpu_parity.py); latent and pose within 3%
-of the distance the reference moved them (tests/test_producer.py::check_trajectory): the fp32
-differences of the GPU producer (MIOpen; d_ws 4e-4 relative L2) and renderer in the gradient
-feed Adam's normalised steps, where small gradient coordinates count as much as large ones
-(measured 1.1-1.25%; the CPU oracle in the same loop stays below 0.1%).
+The producer runs on the GPU through nfi's HIP operators (split-f16 Winograd and up-sampling
+products, fused epilogues; nfi/producer.py); the volume render (forward + backward to planes, palette
+and the camera) is the HIP path.  Tolerances: losses to 1e-4 relative (the HIP render matches the
+reference to fp32 rounding, tests/test_gpu_parity.py); latent and pose within 1.5% of the distance
+the reference moved them (tests/test_producer.py::check_trajectory): the fp32-level differences of
+the GPU producer (d ws within 4x of torch fp32's error against fp64, tests/test_gpu_producer_ops.py)
+and of the renderer in the gradient feed Adam's normalised first steps, where small gradient
+coordinates count as much as large ones (measured 1.1-1.25%; the CPU oracle in the same loop stays
+below 0.1%).
 """
 
 import pytest
@@ -30,7 +32,7 @@ def test_inversion_trajectory_hip():
                   fine_sampling=True, use_sdf=True, attention_values=10, use_viewdir=False)
     res = inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg,
                            uniforms=lambda it: (d['u_coarse'][it], d['u_fine'][it]))
-    rel = check_trajectory(res, d, loss_rtol=1e-4, w_rel=3e-2)
+    rel = check_trajectory(res, d, loss_rtol=1e-4, w_rel=1.5e-2)
     print(f'latent distance / reference displacement: {rel:.2e}')
 
 
@@ -48,7 +50,7 @@ def test_inversion_adam_forms_agree():
         cfg.adam = form
         res[form] = inversion.invert(gen, d['target'], d['cam0'], d['focal0'], d['w_init'], cfg,
                                      uniforms=lambda it: (d['u_coarse'][it], d['u_fine'][it]))
-        check_trajectory(res[form], d, loss_rtol=1e-4, w_rel=3e-2)
+        check_trajectory(res[form], d, loss_rtol=1e-4, w_rel=1.5e-2)
     disp = float((res['foreach'].ws - d['w_init'].to(dev)).norm())
     dist = float((res['fused'].ws - res['foreach'].ws).norm())
     print(f'fused vs foreach latent distance / displacement: {dist / disp:.2e}')

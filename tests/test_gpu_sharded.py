@@ -82,7 +82,7 @@ def test_sharded_hip_inversion(tmp_path):
     dev = torch.device('cuda:0')
     gen, d, meta, cfg = inversion_setup(dev)
     d_cpu = {k: v.cpu() for k, v in d.items()}
-    rel = check_trajectory(res, d_cpu, loss_rtol=1e-4, w_rel=3e-2)
+    rel = check_trajectory(res, d_cpu, loss_rtol=1e-4, w_rel=1.5e-2)
     print(f'sharded HIP inversion: latent distance / reference displacement {rel:.2e}')
     # the same chunks inverted one after the other in this process
     nfi.configure(scene_range=float(meta['scene_range']), white_background=False, fine_sampling=True,

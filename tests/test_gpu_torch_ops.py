@@ -196,3 +196,121 @@ def test_triplane_mlp_ops_match_sampler(heads):
         assert d_pal.numel() == 0
     else:
         assert rel_l2(d_pal, pa.grad) < 1e-5
+
+
+@pytest.mark.parametrize('case', ['p3d', 'shapenet'])
+def test_dispatcher_ops_match_goldens(case):
+    """SURVEY §8(b)'s operators on the reference's own golden vectors, with the
+    parity bounds of tests/test_gpu_parity.py::check (fp64 oracle + directly against the golden):
+    (1) nfi::rays -> nfi::render_fwd / nfi::render_bwd on the reference layouts (channel-major planes,
+    gain-scaled decoder W1s = W1/sqrt(32), W2s = W2/sqrt(64) as EqualizedLinear forms them,
+    stylegan.py:173-176), d cam / d focal through nfi::rays' autograd from render_bwd's d ro / d rd;
+    (2) the scripted render (TorchScript: nfi::rays + nfi::volume_render with nfi::pack_decoder) with
+    the reference's draws.  p3d: random draws, pose gradients; shapenet: deterministic mode, white
+    background, pose frozen (force_no_cam_grad)."""
+    from golden_io import load
+    from gpu_helpers import run_oracle64
+    from test_gpu_parity import check
+    torch_ops.load()
+    d, meta = load(f'render_{case}')
+    H, W, S = int(meta['H']), int(meta['W']), int(meta['S'])
+    sr, white, rnd = float(meta['scene_range']), bool(meta['white_bg']), bool(meta['randomize'])
+    ncg = bool(meta['force_no_cam_grad'])
+    inv_alpha, beta = 1.0 / float(d['alpha']), float(d['beta'])
+    uc = d['u_coarse'].to(DEV).contiguous() if rnd else None
+    uf = d['u_fine'].to(DEV).contiguous() if rnd else None
+    g_rgb, g_mask = d['g_rgb'].to(DEV), d['g_mask'].to(DEV)
+    ref64 = run_oracle64(d, meta)
+
+    # (1) render_fwd / render_bwd
+    w1s, b1, w2s, b2 = _scaled_decoder(d)
+    cam = d['cam'].to(DEV).requires_grad_(not ncg)
+    focal = d['focal'].to(DEV).requires_grad_(not ncg)
+    ro, rd, near, far = torch.ops.nfi.rays(cam, focal, None, None, H, W, sr)
+    pal = d['palette'].to(DEV)
+    planes = d['planes'].to(DEV)
+    rgb, depth, mask, t_sorted, saved = torch.ops.nfi.render_fwd(
+        planes, w1s, b1, w2s, b2, pal, inv_alpha, beta, ro.detach(), rd.detach(), near, far, S, sr, white, rnd, 0, 0,
+        uc, uf)
+    d_planes, d_pal, d_ro, d_rd = torch.ops.nfi.render_bwd(g_rgb, g_mask, saved, pal, inv_alpha, beta, ro.detach(),
+                                                          rd.detach(), near, far, S, sr, white, rnd, True, 0,
+                                                          not ncg)
+    hip = dict(rgb=rgb.cpu(), depth=depth.cpu(), mask=mask.cpu(), d_planes=d_planes.cpu(), d_palette=d_pal.cpu())
+    if not ncg:
+        torch.autograd.backward([ro, rd], [d_ro, d_rd])
+        hip.update(d_cam=cam.grad.cpu(), d_focal=focal.grad.cpu())
+    assert ncg or 'd_cam' in d
+    print(f'  render_fwd / render_bwd ({case})')
+    check(hip, d, ref64)
+
+    # (2) the scripted render with the reference's draws
+    cu = torch.jit.CompilationUnit(torch_ops.render_script_source())
+    pl = d['planes'].to(DEV).requires_grad_()
+    pa = d['palette'].to(DEV).requires_grad_()
+    cam2 = d['cam'].to(DEV).requires_grad_(not ncg)
+    focal2 = d['focal'].to(DEV).requires_grad_(not ncg)
+    dec = torch.ops.nfi.pack_decoder(*(d[k].to(DEV) for k in ('w1', 'b1', 'w2', 'b2')))
+    rgb2, depth2, mask2 = cu.render_rays_u(ops.planes_texel_major(pl), pa, dec, cam2, focal2, H, W, S, sr, inv_alpha,
+                                           beta, white, rnd, uc, uf)
+    ((rgb2 * g_rgb).sum() + (mask2 * g_mask).sum()).backward()
+    hip2 = dict(rgb=rgb2.detach().cpu(), depth=depth2.cpu(), mask=mask2.detach().cpu(), d_planes=pl.grad.cpu(),
+                d_palette=pa.grad.cpu())
+    if not ncg:
+        hip2.update(d_cam=cam2.grad.cpu(), d_focal=focal2.grad.cpu())
+    print(f'  scripted render ({case})')
+    check(hip2, d, ref64)
+
+
+@pytest.mark.parametrize('nattn', [1, 5, 9])
+def test_render_fwd_attention_counts(nattn):
+    """ADVICE r04 (medium): nfi::render_fwd with a decoder of N < 10 attention values ([N+1, 64] output
+    layer; palette [B,10,3] whose rows N..9 the head must not reach) equals nfi.render's N-value head
+    (render.attention_padded: zero rows + a -1e30 bias on the missing logits) — and so the reference's
+    softmax over N logits; a zero-biased padded logit would put exp(-max) of mass on rows N..9."""
+    torch_ops.load()
+    inp, meta = synthetic_inputs(B=2, H=8, W=8, S=16, R=32, scene_range=1.4, seed=60 + nattn)
+    w1s, b1, w2s, b2 = _scaled_decoder(inp)
+    w2s, b2 = w2s[:nattn + 1].contiguous(), b2[:nattn + 1].contiguous()
+    pal = inp['palette'].to(DEV).clone()
+    pal[:, nattn:] = 5.0                              # rows the N-value head must never reach
+    cam, focal = inp['cam'].to(DEV), inp['focal'].to(DEV)
+    ro, rd, near, far = torch.ops.nfi.rays(cam, focal, None, None, 8, 8, 1.4)
+    uc, uf = inp['u_coarse'].to(DEV).contiguous(), inp['u_fine'].to(DEV).contiguous()
+    rgb, depth, mask, _, saved = torch.ops.nfi.render_fwd(inp['planes'].to(DEV), w1s, b1, w2s, b2, pal, 1.0, 0.1,
+                                                           ro, rd, near, far, 16, 1.4, False, True, 0, 0, uc, uf)
+    g = torch.Generator().manual_seed(1)
+    g_rgb = torch.randn(2, 8, 8, 3, generator=g).to(DEV)
+    d_planes, d_pal, _, _ = torch.ops.nfi.render_bwd(g_rgb, None, saved, pal, 1.0, 0.1, ro, rd, near, far, 16, 1.4,
+                                                     False, True, True, 0, False)
+    nfi.configure(scene_range=1.4, white_background=False, fine_sampling=True, use_sdf=True, attention_values=nattn,
+                  use_viewdir=False)
+    pl = inp['planes'].to(DEV).requires_grad_()
+    pa = inp['palette'].to(DEV)[:, :nattn].clone().requires_grad_()
+    f = nfi.TriplaneField(planes=pl, palette=pa, w1=inp['w1'].to(DEV), b1=inp['b1'].to(DEV),
+                          w2=inp['w2'].to(DEV)[:nattn + 1], b2=inp['b2'].to(DEV)[:nattn + 1], alpha=1.0, beta=0.1,
+                          attention_values=nattn)
+    rgb2, depth2, mask2, _, _, _ = nfi.render(f, 8, 8, cam, focal, None, None, None, 16, randomize=True,
+                                              u_coarse=uc, u_fine=uf)
+    (rgb2 * g_rgb).sum().backward()
+    nfi.configure(attention_values=10)
+    torch.testing.assert_close(rgb, rgb2.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(mask, mask2.detach(), rtol=1e-6, atol=1e-7)
+    assert rel_l2(d_planes, pl.grad) < 1e-5
+    assert rel_l2(d_pal[:, :nattn], pa.grad) < 1e-5
+    assert float(d_pal[:, nattn:].abs().max()) == 0.0
+
+
+def test_pack_decoder_rejects_ambiguous_rows():
+    """nfi::pack_decoder: 11 rows = 10 attention values, 4 = the colour head, 33 = view-direction; any
+    other row count needs attention_values (a guessed zero-biased padding would be wrong)."""
+    torch_ops.load()
+    inp, _, _ = _inputs(seed=3, B=1, H=8, S=8)
+    w1, b1 = inp['w1'].to(DEV), inp['b1'].to(DEV)
+    w2, b2 = inp['w2'].to(DEV), inp['b2'].to(DEV)
+    with pytest.raises(RuntimeError, match='ambiguous'):
+        torch.ops.nfi.pack_decoder(w1, b1, w2[:6], b2[:6])
+    with pytest.raises(RuntimeError, match='does not match'):
+        torch.ops.nfi.pack_decoder(w1, b1, w2[:6], b2[:6], 3)
+    a = torch.ops.nfi.pack_decoder(w1, b1, w2[:6], b2[:6], 5)
+    b = ops.pack_decoder(w1, b1, torch.cat([w2[:6], w2.new_zeros(5, 64)]), torch.cat([b2[:6], b2.new_full((5,), -1e30)]))
+    assert torch.equal(a, b)
