@@ -2297,7 +2297,7 @@ __device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1
 #ifndef NFI_TILE_AB
 #define NFI_TILE_AB 1
 #endif
-#if NFI_TILE_AB
+#if NFI_TILE_AB == 1
 // A run of one cell is kept as (A, B) = (sum gw, sum gw w): the texel x0 gets A - B, x0 + 1 gets B
 // when the run ends.  Per entry 4 VALU (the row weight, gw, A, B with w read from its SGPR) instead of
 // building the (1 - w, w) register pair for a packed fma each time (6).
@@ -2312,6 +2312,53 @@ __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, floa
   }
   a0 += gw;
   a1 = fmaf(gw, w, a1);
+}
+#define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0 - a1, a1)
+#elif NFI_TILE_AB == 2
+// Every entry straight into the register image, no run merging and no branch: per entry the row
+// weight, gw, 1 - w and two M0-indexed FMAs (SRC2 | DST indexed: img[slot] += gw (1 - w),
+// img[slot + 1] += gw w) — 5 VALU + 4 SALU whatever the cell sequence.
+__device__ __forceinline__ void img_fma2(img32& img, int slot, float gw, float omw, float w) {
+  slot = min(slot, 30);
+  asm volatile(
+      "s_set_gpr_idx_on %1, gpr_idx(SRC2,DST)\n\t"
+      "v_fma_f32 v40, %2, %3, v40\n\t"
+      "v_fma_f32 v41, %2, %4, v41\n\t"
+      "s_set_gpr_idx_off"
+      : "+{v[40:71]}"(img)
+      : "s"(slot), "v"(gw), "v"(omw), "s"(w)
+      : "m0");
+}
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
+                                           float nn, float g, float wsgn, float woff) {
+  const float gw = g * fmaf(nn, wsgn, woff);
+  img_fma2(img, slot, gw, 1.f - w, w);
+}
+#define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
+#elif NFI_TILE_AB == 4
+// As 2 (every entry straight into the image, branch-free) but with the product's indexed form —
+// VOP2 v_add_f32 under gpr_idx(SRC0,DST) — on the two products: 7 VALU per entry.  (2's VOP3 v_fma
+// under gpr_idx(SRC2,DST) gave wrong d planes and a faulting launch on MI355X)
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
+                                           float nn, float g, float wsgn, float woff) {
+  const float gw = g * fmaf(nn, wsgn, woff);
+  img_add(img, slot, gw * (1.f - w), gw * w);
+}
+#define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
+#elif NFI_TILE_AB == 3
+// (A, B) run sums as in 1, a new run starting from the entry's own (gw, gw w) instead of zeroed sums
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
+                                           float nn, float g, float wsgn, float woff) {
+  const float gw = g * fmaf(nn, wsgn, woff);
+  if (slot != cur) {
+    img_add(img, cur, a0 - a1, a1);
+    a0 = gw;
+    a1 = gw * w;
+    cur = slot;
+  } else {
+    a0 += gw;
+    a1 = fmaf(gw, w, a1);
+  }
 }
 #define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0 - a1, a1)
 #else

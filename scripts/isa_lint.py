@@ -133,9 +133,11 @@ def lint_asm(path: str, window: int):
 
 
 def lint_gpr_idx(path: str):
-    """Rule 2 (the tile pass's register image, nfi_render.hip img_add): every M0-indexed region
-    (s_set_gpr_idx_on .. s_set_gpr_idx_off) holds only 32-bit v_add_f32 on the pinned image base
-    v40 / v41 (no packed or 64-bit operand: an odd index would address an unaligned VGPR pair), and
+    """Rule 2 (the tile pass's register image, nfi_render.hip img_add / img_fma2): every M0-indexed
+    region (s_set_gpr_idx_on .. s_set_gpr_idx_off) holds only 32-bit VOP2 v_add_f32 vD, vD, vX under
+    gpr_idx(SRC0,DST) on the pinned image base vD = v40 / v41 (no packed or 64-bit operand: an odd
+    index would address an unaligned VGPR pair; no VOP3 form: a VOP3 v_fma_f32 under gpr_idx(SRC2,DST)
+    broke the pass on MI355X), and
     its index SGPR was clamped to <= 30 by an s_min just before (v40 + 31 + 1 = v72 is outside the
     image), so no index reaches past v71."""
     bad = []
@@ -148,7 +150,7 @@ def lint_gpr_idx(path: str):
         if not m:
             continue
         idx = m.group(1)
-        prev = [x.split(';')[0].strip() for x in lines[max(0, i - 12):i]]
+        prev = [x.split(';')[0].strip() for x in lines[max(0, i - 30):i]]
         prev = [x for x in prev if x and not x.startswith('.') and not x.endswith(':')]
         if not any(re.match(rf's_min_[iu]32\s+{idx},\s*{idx},\s*30$', x) or
                    re.match(rf's_min_[iu]32\s+{idx},\s*s\d+,\s*30$', x) for x in prev):
@@ -159,8 +161,13 @@ def lint_gpr_idx(path: str):
             j += 1
             if not t or t.startswith('.'):
                 continue
-            if not re.match(r'v_add_f32(_e32)?\s+v4[01],\s*v4[01],\s*v\d+$', t):
-                bad.append((kernel, j, f'unexpected instruction in an indexed region: {t}'))
+            mode = re.search(r'gpr_idx\(([A-Z0-9,]+)\)', ln)
+            mode = mode.group(1) if mode else ''
+            ok_add = mode == 'SRC0,DST' and re.match(r'v_add_f32(_e32)?\s+(v4[01]),\s*\2,\s*v\d+$', t)
+            # (rejected: NFI_TILE_AB 2's VOP3 v_fma_f32 vD, vA, vB, vD under gpr_idx(SRC2,DST) gave wrong
+            #  d planes and a faulting launch on MI355X — DESIGN.md §3)
+            if not ok_add:
+                bad.append((kernel, j, f'unexpected instruction in an indexed region ({mode}): {t}'))
     return bad
 
 
