@@ -2345,6 +2345,40 @@ __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, floa
   img_add(img, slot, gw * (1.f - w), gw * w);
 }
 #define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
+#elif NFI_TILE_AB == 5 || NFI_TILE_AB == 6
+// Experiments on 4's failure: 5 = each region followed, inside the asm, by two VOP1 moves (the
+// product's instruction mix after s_set_gpr_idx_off); 6 = each region followed by s_nop 4.
+__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
+                                           float nn, float g, float wsgn, float woff) {
+  const float gw = g * fmaf(nn, wsgn, woff);
+  const float x0 = gw * (1.f - w), x1 = gw * w;
+  slot = min(slot, 30);
+#if NFI_TILE_AB == 5
+  float d0, d1;
+  asm volatile(
+      "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
+      "v_add_f32 v40, v40, %4\n\t"
+      "v_add_f32 v41, v41, %5\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "v_mov_b32 %1, 0\n\t"
+      "v_mov_b32 %2, 0"
+      : "+{v[40:71]}"(img), "=&v"(d0), "=&v"(d1)
+      : "s"(slot), "v"(x0), "v"(x1)
+      : "m0");
+  asm volatile("" ::"v"(d0), "v"(d1));
+#else
+  asm volatile(
+      "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
+      "v_add_f32 v40, v40, %2\n\t"
+      "v_add_f32 v41, v41, %3\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_nop 4"
+      : "+{v[40:71]}"(img)
+      : "s"(slot), "v"(x0), "v"(x1)
+      : "m0");
+#endif
+}
+#define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
 #elif NFI_TILE_AB == 3
 // (A, B) run sums as in 1, a new run starting from the entry's own (gw, gw w) instead of zeroed sums
 __device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
@@ -2408,7 +2442,8 @@ __device__ __forceinline__ f4v pk_sub(f4v a, f4v b, float m1) {
 #define NFI_TILE_GG_UNROLL 2
 #endif
 __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, const float* __restrict__ Tex,
-                                                int l, int4 rec, int q, float half, float* __restrict__ dpc) {
+                                                int l, int4 rec, int q, float half, float* __restrict__ dpc,
+                                                long long nsamp_chk = 0) {
   const int slot = rec.y & 31;
   const float w = __int_as_float(rec.z), n = __int_as_float(rec.w);
   float gx = 0.f, gy = 0.f;
@@ -2453,6 +2488,9 @@ __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, con
   }
 #endif
   const float2 out = make_float2((rec.y & 0x100) ? gx * half : 0.f, (rec.y & 0x200) ? gy * half : 0.f);
+#if NFI_TILE_CHECK
+  if (rec.x < 0 || rec.x >= nsamp_chk) return;   // (code 3 counts it; never store out of range)
+#endif
   *reinterpret_cast<float2*>(dpc + ((long long)rec.x * 3 + q) * 2) = out;
 }
 
@@ -2631,7 +2669,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     wave_lds_sync();                                                                                 \
     NFI_CREC(VREC)                                                                                   \
     NFI_BATCH_CHECK()                                                                                \
-    if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc);                            \
+    if (A.dpc && l < n) entry_grid_grad(G, Tex, l, VREC, q, half, A.dpc, A.nsamp);                   \
     NFI_NEXT_REC(VREC, AHEAD)                                                                        \
     NFI_LOAD_ROWC(VREC, base_ + (AHEAD))                                                             \
     NFI_STAMP(24)                                                                                    \
