@@ -173,6 +173,18 @@ int32_t nfi_decoder_pack_n(const float* w1, const float* b1, const float* w2, co
 /* [B,3,32,R,R] channel-major planes (generator.py:476-477) <-> texel-major [B,3,R,R,32]. */
 int32_t nfi_planes_to_texel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream);
 int32_t nfi_planes_to_channel_major(const float* src, int32_t B, int32_t R, float* dst, void* stream);
+/* The inversion step's pose algebra (run.py:2262: pose_to_matrix(z0, t2, s, F.normalize(q)),
+ * lib/pose_utils.py:48-78) and its backward, one launch each; [B] z0 (NULL: no focal, orthographic
+ * branch), [B,2] t2, [B] s, [B,4] q (w, x, y, z; normalised inside) -> cam2world [B,4,4], focal [B]
+ * (= (1 + exp z0) / 2).  The backward writes (not accumulates) d z0 / d t2 / d s / d q from
+ * d cam2world and d focal (NULL: zero).  nfi_pose_project: the post-step projections in place
+ * (run.py:2300-2306): q <- F.normalize(q), z0 <- clamp(z0, -4, 4), s <- |s| (z0 / s may be NULL). */
+int32_t nfi_pose_forward(const float* z0, const float* t2, const float* s, const float* q, int32_t B,
+                         int32_t camera_flipped, float* cam2world, float* focal, void* stream);
+int32_t nfi_pose_backward(const float* z0, const float* t2, const float* s, const float* q, int32_t B,
+                          int32_t camera_flipped, const float* g_cam2world, const float* g_focal, float* d_z0,
+                          float* d_t2, float* d_s, float* d_q, void* stream);
+int32_t nfi_pose_project(float* z0, float* s, float* q, int32_t B, void* stream);
 
 /* get_ray_bundle + F.normalize + compute_near_far_planes (run.py:193-200).
  * Outputs ro, rd (unit) [B*H*W,3], near, far [B*H*W].  ws: 2 + B*H*W uint32 of device scratch. */

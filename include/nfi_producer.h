@@ -258,6 +258,17 @@ int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const 
                                   const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                                   int32_t ksplit, float* work, void* stream);
 
+/* AttentionMapper conditional norm + activation (generator.py:42-60 ConditionalLayerNorm, then the
+ * leaky ReLU of :173-178): x = lrelu(beta + gamma1 * layer_norm(h), 0.2) per row of C channels
+ * (C <= 1024; layer_norm without affine, eps 1e-5; gamma1 = 1 + gamma, beta with row stride ld,
+ * h and x contiguous [B][C]); stats [B][2] = (mean, rstd) for the backward, which writes d h,
+ * d gamma1 and d beta ([B][C] contiguous). */
+int32_t nfi_syn_cond_norm_act_forward(const float* h, const float* gamma1, const float* beta, int32_t B, int32_t C,
+                                      int32_t ld, float* x, float* stats, void* stream);
+int32_t nfi_syn_cond_norm_act_backward(const float* gx, const float* h, const float* gamma1, const float* beta,
+                                       const float* stats, int32_t B, int32_t C, int32_t ld, float* dh,
+                                       float* dgamma1, float* dbeta, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1160,6 +1160,102 @@ __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ 
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+
+// ---------------------------------------------------------------------------------------
+// AttentionMapper conditional norm layer (generator.py:42-60, 160-178):
+//   x = leaky_relu(beta + gamma1 * layer_norm(h), 0.2),  layer_norm without affine, eps 1e-5
+// one workgroup per row (C <= 1024 channels, 256 threads x 4), mean / rstd saved for the backward:
+//   gz = gx * slope(z); d beta = gz; d gamma1 = gz * y; gy = gz * gamma1;
+//   d h = rstd * (gy - mean(gy) - y * mean(gy * y))   (ATen's layer_norm backward)
+// (the mapper's 4 norms: 3 ATen kernels forward and ~6 backward each -> 1 + 1)
+// ---------------------------------------------------------------------------------------
+constexpr int CLN_PER = 4;   // channels per thread (C <= 1024)
+__device__ __forceinline__ void block_sum2(float& a, float& b) {
+  __shared__ float red[2][4];
+  a = wave_sum(a);
+  b = wave_sum(b);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = a;
+    red[1][threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  a = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  b = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+}
+
+__global__ void __launch_bounds__(256) cln_act_fwd_kernel(const float* __restrict__ h, const float* __restrict__ g1,
+                                                          const float* __restrict__ be, int ld, int C,
+                                                          float* __restrict__ x, float* __restrict__ stats) {
+  const int row = blockIdx.x;
+  const float* hr = h + (long long)row * C;
+  float v[CLN_PER], s1 = 0.f, s0 = 0.f;
+#pragma unroll
+  for (int k = 0; k < CLN_PER; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    v[k] = c < C ? hr[c] : 0.f;
+    s1 += v[k];
+  }
+  block_sum2(s1, s0);
+  const float mean = s1 / (float)C;
+  float s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < CLN_PER; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    const float d = c < C ? v[k] - mean : 0.f;
+    s2 += d * d;
+  }
+  s0 = 0.f;
+  block_sum2(s2, s0);
+  const float rstd = rsqrtf(s2 / (float)C + 1e-5f);
+#pragma unroll
+  for (int k = 0; k < CLN_PER; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    if (c < C) {
+      const float z = be[(long long)row * ld + c] + g1[(long long)row * ld + c] * ((v[k] - mean) * rstd);
+      x[(long long)row * C + c] = z > 0.f ? z : 0.2f * z;
+    }
+  }
+  if (threadIdx.x == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = rstd;
+  }
+}
+
+__global__ void __launch_bounds__(256) cln_act_bwd_kernel(const float* __restrict__ gx, const float* __restrict__ h,
+                                                          const float* __restrict__ g1, const float* __restrict__ be,
+                                                          int ld, int C, const float* __restrict__ stats,
+                                                          float* __restrict__ dh, float* __restrict__ dg1,
+                                                          float* __restrict__ dbe) {
+  const int row = blockIdx.x;
+  const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+  float y[CLN_PER], gy[CLN_PER], a = 0.f, b = 0.f;
+#pragma unroll
+  for (int k = 0; k < CLN_PER; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    y[k] = gy[k] = 0.f;
+    if (c < C) {
+      const long long i = (long long)row * C + c, ic = (long long)row * ld + c;
+      y[k] = (h[i] - mean) * rstd;
+      const float gam = g1[ic];
+      const float z = be[ic] + gam * y[k];
+      const float gz = z > 0.f ? gx[i] : 0.2f * gx[i];
+      dbe[i] = gz;
+      dg1[i] = gz * y[k];
+      gy[k] = gz * gam;
+      a += gy[k];
+      b += gy[k] * y[k];
+    }
+  }
+  block_sum2(a, b);
+  const float ma = a / (float)C, mb = b / (float)C;
+#pragma unroll
+  for (int k = 0; k < CLN_PER; ++k) {
+    const int c = threadIdx.x + 256 * k;
+    if (c < C) dh[(long long)row * C + c] = rstd * (gy[k] - ma - y[k] * mb);
+  }
+}
+
 }  // namespace syn
 }  // namespace nfi
 
@@ -1457,6 +1553,28 @@ int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gim
   const int64_t total = (int64_t)B * H * W;
   aug_bwd_kernel<<<blocks(total * 16), 256, 0, (hipStream_t)stream>>>(gout, grid, gimg, total, K, H, W, Ho, Wo);
   NFI_CHECK_LAUNCH("aug_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_cond_norm_act_forward(const float* h, const float* gamma1, const float* beta, int32_t B, int32_t C,
+                                      int32_t ld, float* x, float* stats, void* stream) {
+  NFI_REQUIRE(h && gamma1 && beta && x && stats, "syn_cond_norm_act_forward: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && C <= 256 * CLN_PER && ld >= C, "syn_cond_norm_act_forward: bad shape B=%d C=%d ld=%d",
+              B, C, ld);
+  cln_act_fwd_kernel<<<B, 256, 0, (hipStream_t)stream>>>(h, gamma1, beta, ld, C, x, stats);
+  NFI_CHECK_LAUNCH("cln_act_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_syn_cond_norm_act_backward(const float* gx, const float* h, const float* gamma1, const float* beta,
+                                       const float* stats, int32_t B, int32_t C, int32_t ld, float* dh,
+                                       float* dgamma1, float* dbeta, void* stream) {
+  NFI_REQUIRE(gx && h && gamma1 && beta && stats && dh && dgamma1 && dbeta,
+              "syn_cond_norm_act_backward: null pointer");
+  NFI_REQUIRE(B > 0 && C > 0 && C <= 256 * CLN_PER && ld >= C, "syn_cond_norm_act_backward: bad shape B=%d C=%d ld=%d",
+              B, C, ld);
+  cln_act_bwd_kernel<<<B, 256, 0, (hipStream_t)stream>>>(gx, h, gamma1, beta, ld, C, stats, dh, dgamma1, dbeta);
+  NFI_CHECK_LAUNCH("cln_act_bwd_kernel");
   return NFI_OK;
 }
 

@@ -535,6 +535,145 @@ __global__ void __launch_bounds__(256) planes_t2c_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The inversion step's pose algebra (run.py:2262-2266 -> pose_utils.py:48-78) in one launch each way:
+// cam2world [b,4,4] and focal [b] from the optimised (z0, t2, s, q), q through F.normalize first;
+// and the post-step projections (run.py:2300-2306).  One thread per image (the batch is a handful
+// of images: this replaces ~35 scalar-sized ATen kernels per step, forward and backward).
+// ---------------------------------------------------------------------------------------
+// r = the row-major rotation matrix of the unit quaternion (w, x, y, z); the reference's matrix is
+// its transpose (pose_utils.py:41-45 rotates the rows of the identity): R[i][j] = r[3j + i].
+__device__ __forceinline__ void quat_r(const float n[4], float r[9]) {
+  const float w = n[0], x = n[1], y = n[2], z = n[3];
+  r[0] = 1.f - 2.f * (y * y + z * z);
+  r[1] = 2.f * (x * y - w * z);
+  r[2] = 2.f * (x * z + w * y);
+  r[3] = 2.f * (x * y + w * z);
+  r[4] = 1.f - 2.f * (x * x + z * z);
+  r[5] = 2.f * (y * z - w * x);
+  r[6] = 2.f * (x * z - w * y);
+  r[7] = 2.f * (y * z + w * x);
+  r[8] = 1.f - 2.f * (x * x + y * y);
+}
+
+struct PoseIn {
+  float n[4];      // F.normalize(q)
+  float qnorm;     // max(||q||, 1e-12)
+  float t3[3];     // (t2 / s, f / s) or (t2, 1) / s
+  float ez;        // exp(z0) (0 without z0)
+  float R[3][3];
+};
+
+__device__ __forceinline__ PoseIn pose_in(const float* z0, const float* t2, const float* s, const float* q, int b) {
+  PoseIn P;
+  const float q0 = q[4 * b], q1 = q[4 * b + 1], q2 = q[4 * b + 2], q3 = q[4 * b + 3];
+  P.qnorm = fmaxf(sqrtf(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3), 1e-12f);
+  P.n[0] = q0 / P.qnorm;
+  P.n[1] = q1 / P.qnorm;
+  P.n[2] = q2 / P.qnorm;
+  P.n[3] = q3 / P.qnorm;
+  float r[9];
+  quat_r(P.n, r);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) P.R[i][j] = r[3 * j + i];
+  const float sv = s[b];
+  P.ez = z0 ? expf(z0[b]) : 0.f;
+  const float f = z0 ? 1.f + P.ez : 1.f;
+  P.t3[0] = t2[2 * b] / sv;
+  P.t3[1] = t2[2 * b + 1] / sv;
+  P.t3[2] = f / sv;
+  return P;
+}
+
+__global__ void pose_fwd_kernel(const float* __restrict__ z0, const float* __restrict__ t2,
+                                const float* __restrict__ s, const float* __restrict__ q, int B, int flipped,
+                                float* __restrict__ cam, float* __restrict__ focal) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const PoseIn P = pose_in(z0, t2, s, q, b);
+  float* m = cam + 16 * b;
+  const float sg = flipped ? -1.f : 1.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float c3 = P.R[i][0] * P.t3[0] + P.R[i][1] * P.t3[1] + P.R[i][2] * P.t3[2];
+    m[4 * i + 0] = P.R[i][0];
+    m[4 * i + 1] = sg * P.R[i][1];
+    m[4 * i + 2] = sg * P.R[i][2];
+    m[4 * i + 3] = sg * c3;
+  }
+  m[12] = 0.f;
+  m[13] = 0.f;
+  m[14] = 0.f;
+  m[15] = 1.f;
+  if (z0 && focal) focal[b] = (1.f + P.ez) / 2.f;
+}
+
+// d cam2world [b,4,4] (+ d focal [b]) -> d z0, d t2, d s, d q (each written, not accumulated)
+__global__ void pose_bwd_kernel(const float* __restrict__ z0, const float* __restrict__ t2,
+                                const float* __restrict__ s, const float* __restrict__ q, int B, int flipped,
+                                const float* __restrict__ g_cam, const float* __restrict__ g_focal,
+                                float* __restrict__ d_z0, float* __restrict__ d_t2, float* __restrict__ d_s,
+                                float* __restrict__ d_q) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const PoseIn P = pose_in(z0, t2, s, q, b);
+  float G[3][4];
+  const float sg = flipped ? -1.f : 1.f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) G[i][j] = (j == 0 ? 1.f : sg) * g_cam[16 * b + 4 * i + j];
+  // mat[i][3] = sum_j R[i][j] t3[j]
+  float dr[9], dt3[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      dr[3 * j + i] = G[i][j] + G[i][3] * P.t3[j];
+      dt3[j] += G[i][3] * P.R[i][j];
+    }
+  const float sv = s[b];
+  d_t2[2 * b] = dt3[0] / sv;
+  d_t2[2 * b + 1] = dt3[1] / sv;
+  d_s[b] = -(dt3[0] * P.t3[0] + dt3[1] * P.t3[1] + dt3[2] * P.t3[2]) / sv;
+  if (z0 && d_z0) {
+    const float df = dt3[2] / sv + (g_focal ? 0.5f * g_focal[b] : 0.f);
+    d_z0[b] = df * P.ez;
+  }
+  // r(n): d r / d n of the quadratic forms in quat_r
+  const float w = P.n[0], x = P.n[1], y = P.n[2], z = P.n[3];
+  const float dw = 2.f * (-z * dr[1] + y * dr[2] + z * dr[3] - y * dr[6] - x * dr[5] + x * dr[7]);
+  const float dx = 2.f * (y * dr[1] + z * dr[2] + y * dr[3] - 2.f * x * dr[4] - w * dr[5] + z * dr[6] +
+                          w * dr[7] - 2.f * x * dr[8]);
+  const float dy = 2.f * (-2.f * y * dr[0] + x * dr[1] + w * dr[2] + x * dr[3] + z * dr[5] - w * dr[6] +
+                          z * dr[7] - 2.f * y * dr[8]);
+  const float dz = 2.f * (-2.f * z * dr[0] - w * dr[1] + x * dr[2] + w * dr[3] - 2.f * z * dr[4] + y * dr[5] +
+                          x * dr[6] + y * dr[7]);
+  // F.normalize backward: (g - n (n . g)) / max(||q||, eps) (the clamp passes no gradient below eps)
+  const float dn = w * dw + x * dx + y * dy + z * dz;
+  const bool above = P.qnorm > 1e-12f;
+  d_q[4 * b + 0] = (dw - (above ? w * dn : 0.f)) / P.qnorm;
+  d_q[4 * b + 1] = (dx - (above ? x * dn : 0.f)) / P.qnorm;
+  d_q[4 * b + 2] = (dy - (above ? y * dn : 0.f)) / P.qnorm;
+  d_q[4 * b + 3] = (dz - (above ? z * dn : 0.f)) / P.qnorm;
+}
+
+// after the optimiser step (run.py:2300-2306): q <- F.normalize(q), z0 <- clamp(z0, -4, 4), s <- |s|
+__global__ void pose_project_kernel(float* __restrict__ z0, float* __restrict__ s, float* __restrict__ q, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float q0 = q[4 * b], q1 = q[4 * b + 1], q2 = q[4 * b + 2], q3 = q[4 * b + 3];
+  const float n = fmaxf(sqrtf(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3), 1e-12f);
+  q[4 * b] = q0 / n;
+  q[4 * b + 1] = q1 / n;
+  q[4 * b + 2] = q2 / n;
+  q[4 * b + 3] = q3 / n;
+  if (z0) z0[b] = fminf(fmaxf(z0[b], -4.f), 4.f);
+  if (s) s[b] = fabsf(s[b]);
+}
+
 }  // namespace nfi
 
 using namespace nfi;
@@ -671,6 +810,34 @@ int32_t nfi_planes_to_channel_major(const float* src, int32_t B, int32_t R, floa
   const int RR = R * R;
   planes_t2c_kernel<<<dim3((RR + 63) / 64, B * 3), 256, 0, (hipStream_t)stream>>>(src, RR, dst);
   NFI_CHECK_LAUNCH("planes_t2c_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_pose_forward(const float* z0, const float* t2, const float* s, const float* q, int32_t B,
+                         int32_t camera_flipped, float* cam2world, float* focal, void* stream) {
+  NFI_REQUIRE(t2 && s && q && cam2world && B > 0, "pose_forward: bad args (B=%d)", B);
+  NFI_REQUIRE(!z0 || focal, "pose_forward: z0 given without a focal output");
+  pose_fwd_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>(z0, t2, s, q, B, camera_flipped != 0, cam2world,
+                                                                 focal);
+  NFI_CHECK_LAUNCH("pose_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_pose_backward(const float* z0, const float* t2, const float* s, const float* q, int32_t B,
+                          int32_t camera_flipped, const float* g_cam2world, const float* g_focal, float* d_z0,
+                          float* d_t2, float* d_s, float* d_q, void* stream) {
+  NFI_REQUIRE(t2 && s && q && g_cam2world && d_t2 && d_s && d_q && B > 0, "pose_backward: bad args (B=%d)", B);
+  NFI_REQUIRE(!z0 || d_z0, "pose_backward: z0 given without a d_z0 output");
+  pose_bwd_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>(z0, t2, s, q, B, camera_flipped != 0,
+                                                                 g_cam2world, g_focal, d_z0, d_t2, d_s, d_q);
+  NFI_CHECK_LAUNCH("pose_bwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_pose_project(float* z0, float* s, float* q, int32_t B, void* stream) {
+  NFI_REQUIRE(q && B > 0, "pose_project: bad args (B=%d)", B);
+  pose_project_kernel<<<(B + 63) / 64, 64, 0, (hipStream_t)stream>>>(z0, s, q, B);
+  NFI_CHECK_LAUNCH("pose_project_kernel");
   return NFI_OK;
 }
 

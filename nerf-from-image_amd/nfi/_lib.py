@@ -70,6 +70,9 @@ SIGNATURES = {
                                                    c_void_p, c_void_p]),
     'nfi_planes_to_channel_major': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                      c_void_p, c_void_p]),
+    'nfi_pose_forward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 2 + [c_void_p] * 3),
+    'nfi_pose_backward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 2 + [c_void_p] * 7),
+    'nfi_pose_project': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int32, c_void_p]),
     'nfi_rays_forward': (ctypes.c_int32, [ctypes.POINTER(NfiCamera), ctypes.c_float, c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'nfi_rays_backward': (ctypes.c_int32, [ctypes.POINTER(NfiCamera), c_void_p, c_void_p,
@@ -125,6 +128,8 @@ SIGNATURES = {
     'nfi_gemm_split16': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_gemm_split16_shared_a': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
     'nfi_gemm_split16_ksplit': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
+    'nfi_syn_cond_norm_act_forward': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int32] * 3 + [c_void_p] * 3),
+    'nfi_syn_cond_norm_act_backward': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 3 + [c_void_p] * 4),
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_float, c_void_p]),
     'nfi_syn_act_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

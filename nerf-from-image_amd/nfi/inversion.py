@@ -91,6 +91,68 @@ def pose_to_matrix(z0, t2, s, q, camera_flipped: bool):
     return _flip(torch.cat([top, bottom.expand(b, 1, 4)], dim=1), camera_flipped), focal
 
 
+class _PoseHIP(torch.autograd.Function):
+    """pose_to_matrix(z0, t2, s, F.normalize(q)) on device tensors as one HIP launch each way
+    (nfi_pose_forward / nfi_pose_backward: the ~35 scalar-sized ATen kernels of the torch form)."""
+
+    @staticmethod
+    def forward(ctx, z0, t2, s, q, flipped: bool):
+        from . import _lib
+        from .ops import _ptr, _stream
+        b = q.shape[0]
+        z0c, t2c, sc, qc = (None if z0 is None else z0.contiguous()), t2.contiguous(), s.contiguous(), q.contiguous()
+        cam = torch.empty((b, 4, 4), device=q.device)
+        focal = torch.empty((b,), device=q.device) if z0 is not None else None
+        _lib.check(_lib.load().nfi_pose_forward(_ptr(z0c), _ptr(t2c), _ptr(sc), _ptr(qc), b, int(flipped), _ptr(cam),
+                                                _ptr(focal), _stream(q.device)), 'nfi_pose_forward')
+        ctx.save_for_backward(*(t for t in (z0c, t2c, sc, qc) if t is not None))
+        ctx.has_z0, ctx.flipped = z0 is not None, flipped
+        return cam, focal
+
+    @staticmethod
+    def backward(ctx, g_cam, g_focal):
+        from . import _lib
+        from .ops import _ptr, _stream
+        saved = ctx.saved_tensors
+        z0, t2, s, q = saved if ctx.has_z0 else (None,) + tuple(saved)
+        b = q.shape[0]
+        g_cam = torch.zeros((b, 4, 4), device=q.device) if g_cam is None else g_cam.contiguous()
+        d_z0 = torch.empty_like(z0) if z0 is not None else None
+        d_t2, d_s, d_q = torch.empty_like(t2), torch.empty_like(s), torch.empty_like(q)
+        _lib.check(_lib.load().nfi_pose_backward(
+            _ptr(z0), _ptr(t2), _ptr(s), _ptr(q), b, int(ctx.flipped), _ptr(g_cam),
+            _ptr(None if g_focal is None else g_focal.contiguous()), _ptr(d_z0), _ptr(d_t2), _ptr(d_s), _ptr(d_q),
+            _stream(q.device)), 'nfi_pose_backward')
+        return d_z0, d_t2, d_s, d_q, None
+
+
+def pose_matrix(z0, t2, s, q, camera_flipped: bool):
+    """pose_to_matrix(z0, t2, s, F.normalize(q, dim=-1), camera_flipped) (run.py:2262): the HIP
+    kernels for device tensors, the torch formulation on the CPU."""
+    if q.is_cuda:
+        return _PoseHIP.apply(z0, t2, s, q, camera_flipped)
+    return pose_to_matrix(z0, t2, s, F.normalize(q, dim=-1), camera_flipped)
+
+
+def project_pose(z0, s, q):
+    """The post-step projections (run.py:2300-2306), in place, no grad: q <- F.normalize(q),
+    z0 <- clamp(z0, -4, 4), s <- |s|."""
+    with torch.no_grad():
+        if q.is_cuda:
+            from . import _lib
+            from .ops import _ptr, _stream
+            _lib.check(_lib.load().nfi_pose_project(_ptr(z0), _ptr(s), _ptr(q), q.shape[0], _stream(q.device)),
+                       'nfi_pose_project')
+            for t in (z0, s, q):       # written in place behind autograd's back: mark them modified
+                if t is not None:
+                    torch.autograd.graph.increment_version(t)
+            return
+        q.copy_(F.normalize(q, dim=-1))
+        if z0 is not None:
+            z0.clamp_(-4, 4)
+        s.abs_()
+
+
 def invert_space(mat: torch.Tensor) -> torch.Tensor:
     """pose_utils.py:20-27: cam2world <-> world2cam of a scaled rigid transform."""
     scale = mat[:, 3:4, 3:4]
@@ -426,7 +488,7 @@ class _State:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 prepared = vgg_target(cfg.loss, self.target, self.lpips_net, cfg.white_background)
-        cam, foc = pose_to_matrix(self.z0_, self.t2_, self.s_, F.normalize(self.q_, dim=-1), cfg.camera_flipped)
+        cam, foc = pose_matrix(self.z0_, self.t2_, self.s_, self.q_, cfg.camera_flipped)
         ws = self.z_ * cfg.gain_z
         if cfg.no_split:
             ws = ws.expand(-1, 15, -1)
@@ -440,11 +502,7 @@ class _State:
         loss.backward()
         self.opt.step()
         self.opt.zero_grad()
-        with torch.no_grad():
-            self.q_.copy_(F.normalize(self.q_, dim=-1))
-            if self.z0_ is not None:
-                self.z0_.clamp_(-4, 4)
-            self.s_.abs_()
+        project_pose(self.z0_, self.s_, self.q_)
         return loss
 
     def result(self, losses, secs):

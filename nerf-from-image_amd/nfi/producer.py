@@ -374,7 +374,10 @@ class PaletteMapper(nn.Module):
                 h = getattr(self, f'fc{i}')(x)
                 # (1 + gamma_i(c)) and beta_i(c) from the one batched projection
                 g1, b = cond[2 * (i - 1)], cond[2 * (i - 1) + 1]
-                x = F.leaky_relu(torch.addcmul(b, g1, F.layer_norm(h, (h.shape[-1],))), 0.2)
+                if h.is_cuda and h.shape[-1] <= 1024:
+                    x = _hip().cond_norm_act(h, g1, b)        # one HIP kernel each way
+                else:
+                    x = F.leaky_relu(torch.addcmul(b, g1, F.layer_norm(h, (h.shape[-1],))), 0.2)
             x = (x + shortcut) * scale
         x = F.leaky_relu(self.fc5(x), 0.2)
         return wide_sigmoid_rescaled(self.fc_values(x).view(-1, self.num_values, 3))

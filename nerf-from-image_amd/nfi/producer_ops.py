@@ -554,6 +554,42 @@ def vgg_epilogue(x, bias, pool: bool = False):
     return _VggEpilogue.apply(x, bias, pool)
 
 
+class _CondNormAct(torch.autograd.Function):
+    """lrelu(beta + gamma1 * layer_norm(h), 0.2) (generator.py:42-60, 173-178): one HIP kernel each
+    way (nfi_syn_cond_norm_act_*) instead of layer_norm / addcmul / leaky_relu and their backwards.
+    gamma1 and beta may be row-strided views of one [B, k*C] projection (their last dim contiguous)."""
+
+    @staticmethod
+    def forward(ctx, h, gamma1, beta):
+        _require_device(h, gamma1, beta)
+        h = h.contiguous()
+        B, C = h.shape
+        if gamma1.stride(-1) != 1 or beta.stride(-1) != 1 or gamma1.stride(0) != beta.stride(0):
+            gamma1, beta = gamma1.contiguous(), beta.contiguous()
+        ld = gamma1.stride(0)
+        x = torch.empty_like(h)
+        stats = torch.empty((B, 2), device=h.device)
+        _call('nfi_syn_cond_norm_act_forward', _p(h), _p(gamma1), _p(beta), B, C, ld, _p(x), _p(stats),
+              _stream(h.device))
+        ctx.save_for_backward(h, gamma1, beta, stats)
+        ctx.ld = ld
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        h, gamma1, beta, stats = ctx.saved_tensors
+        B, C = h.shape
+        dh, dg1, db = torch.empty_like(h), torch.empty_like(h), torch.empty_like(h)
+        _call('nfi_syn_cond_norm_act_backward', _p(gx.contiguous()), _p(h), _p(gamma1), _p(beta), _p(stats), B, C,
+              ctx.ld, _p(dh), _p(dg1), _p(db), _stream(h.device))
+        return dh, dg1, db
+
+
+def cond_norm_act(h, gamma1, beta):
+    """F.leaky_relu(torch.addcmul(beta, gamma1, F.layer_norm(h, (C,))), 0.2) for [B, C] rows."""
+    return _CondNormAct.apply(h, gamma1, beta)
+
+
 def lpips_head(f0, f1, w):
     """[N] = mean_hw sum_c w_c (n(f0) - n(f1))_c^2 (lpips distance of one layer)."""
     return _LpipsHead.apply(f0, f1, w)
