@@ -1178,6 +1178,11 @@ __device__ __forceinline__ void block_sum2(float& a, float& b) {
   if ((threadIdx.x & 63) == 0) {
     red[0][threadIdx.x >> 6] = a;
     red[1][threadIdx.x >> 6] = b;
+    // (wait states behind the paired LDS store before its data registers are rewritten: the
+    //  wide-store data hazard nfi_common.h's lds_st guards, checked by scripts/isa_lint.py)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
   a = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);

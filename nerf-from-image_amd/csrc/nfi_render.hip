@@ -1289,9 +1289,16 @@ __device__ __forceinline__ void field_eval(const nfi_render_args& a, const Plane
     float4* xs = reinterpret_cast<float4*>(a.x_saved + (R.r * N + eval_base) * NC);
     const int l = lane_id();
     const float* src = X + (l >> 3) * XS + 4 * (l & 7);   // row k*8 + l/8: a constant offset per k
+    if (npts == 64) {
+      // (the common full chunk: no per-store lane mask, so the eight LDS reads issue together
+      //  instead of one exec-masked read + wait + store at a time)
 #pragma unroll
-    for (int k = 0; k < NC / 4; ++k)
-      if (8 * k + (l >> 3) < npts) nt_store4(xs + k * 64 + l, *reinterpret_cast<const float4*>(src + k * 8 * XS));
+      for (int k = 0; k < NC / 4; ++k) nt_store4(xs + k * 64 + l, *reinterpret_cast<const float4*>(src + k * 8 * XS));
+    } else {
+#pragma unroll
+      for (int k = 0; k < NC / 4; ++k)
+        if (8 * k + (l >> 3) < npts) nt_store4(xs + k * 64 + l, *reinterpret_cast<const float4*>(src + k * 8 * XS));
+    }
   }
   NFI_STAMP(1)
   float y[NOUT];
