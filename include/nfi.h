@@ -216,6 +216,14 @@ int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * beams * 3 * ((
 /* The same size from the shapes alone (B images of H x W rays, N samples per ray, planes R x R): for
  * shape-only callers (the TORCH_LIBRARY Meta kernels) that hold no argument block; -1 on bad shapes. */
 int64_t nfi_tile_count_size_shape(int32_t B, int32_t R, int32_t H, int32_t W, int32_t N);
+/* Deterministic backward for the calling host thread (on = 1), the default atomics form (0), or
+ * query only (-1); returns the previous setting (initially from the environment variable
+ * NFI_DETERMINISTIC).  Deterministic: every tile's bin entries are sorted by sample index before the
+ * tile pass and the d planes are summed from per-chunk partial tile images in a fixed order instead
+ * of float atomics, so d planes (and every other output) are bitwise reproducible run to run; the
+ * workspace (nfi_render_backward_workspace_bytes, which follows this setting) grows by ~40 B per
+ * (sample, plane) entry.  The reference's grid_sample backward itself accumulates with atomics. */
+int32_t nfi_set_deterministic(int32_t on);
 int32_t nfi_render_backward(const nfi_render_args* a, const nfi_render_grad_args* g, void* stream);
 /* The same backward one stage at a time, in order 0, 1, 2 on one stream with one workspace
  * (lets a caller time or overlap the stages): 0 = tile binning of the saved samples,

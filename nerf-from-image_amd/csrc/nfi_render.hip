@@ -2190,6 +2190,89 @@ __global__ void __launch_bounds__(256) chunk_map_kernel(const int* __restrict__ 
   for (int j = 0; j < nc; ++j) chunk_tile[c0 + j] = k;
 }
 
+// ---- deterministic mode (nfi_set_deterministic): the entries of every tile ordered by sample
+// index (their append order otherwise follows the cursor atomics), and the d planes summed from the
+// chunks' partial tile images in a fixed order (no float atomics): a backward whose results are
+// bitwise reproducible run to run.
+// One workgroup per chunk (the tile pass's chunks: <= CHUNK entries of one tile): each of its
+// entries' rank = the number of the tile's entries with a smaller sample index (unique within a
+// tile: one entry per sample and plane), counted against the tile's keys staged through LDS 1,024
+// at a time; the entry is copied to its rank.  O(CHUNK n / 256) per chunk of an n-entry tile — a
+// reproducibility mode, not the product path.
+constexpr int DET_PER = CHUNK / 256;
+__global__ void __launch_bounds__(256) det_sort_kernel(const int4* __restrict__ list, const int* __restrict__ offsets,
+                                                       const int* __restrict__ chunk_start,
+                                                       const int* __restrict__ chunk_tile, const int* __restrict__ meta,
+                                                       int4* __restrict__ sorted) {
+  const int c = blockIdx.x;
+  if (c >= meta[0]) return;
+  const int tile = chunk_tile[c];
+  const int a = offsets[tile], n = offsets[tile + 1] - a;
+  const int first = (c - chunk_start[tile]) * CHUNK, last = min(n, first + CHUNK);
+  __shared__ int ks[1024];
+  const int tid = threadIdx.x;
+  int my[DET_PER], rank[DET_PER];
+#pragma unroll
+  for (int j = 0; j < DET_PER; ++j) {
+    const int e = first + tid + 256 * j;
+    my[j] = e < last ? list[a + e].x : 0x7fffffff;
+    rank[j] = 0;
+  }
+  for (int j0 = 0; j0 < n; j0 += 1024) {
+    const int m = min(1024, n - j0);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = tid + 256 * j;
+      if (t < m) ks[t] = list[a + j0 + t].x;
+    }
+    __syncthreads();
+    for (int t = 0; t < m; ++t) {
+      const int v = ks[t];
+#pragma unroll
+      for (int j = 0; j < DET_PER; ++j) rank[j] += v < my[j] ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < DET_PER; ++j) {
+    const int e = first + tid + 256 * j;
+    if (e < last) sorted[a + rank[j]] = list[a + e];
+  }
+}
+// the 64 zeroed records after the last entry that the tile pass's record prefetch reads
+__global__ void det_pad_kernel(const int* __restrict__ offsets, int K, int4* __restrict__ sorted) {
+  sorted[offsets[K] + threadIdx.x] = make_int4(0, 0, 0, 0);
+}
+// d planes += the partial tile images [chunk][TTX*TTY][NC] of every tile covering the texel: tiles
+// by (beam, ty, tx) ascending, each tile's chunks ascending.  One thread per (b, q, y, x, channel).
+__global__ void __launch_bounds__(256) dplanes_reduce_kernel(const float* __restrict__ part,
+                                                             const int* __restrict__ chunk_start, TileGrid G, int B,
+                                                             int R, long long sb, int sq, int st,
+                                                             float* __restrict__ dplanes) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * 3 * R * R * NC) return;
+  const int ch = (int)(i % NC);
+  long long t = i / NC;
+  const int x = (int)(t % R);
+  t /= R;
+  const int y = (int)(t % R);
+  t /= R;
+  const int q = (int)(t % 3), b = (int)(t / 3);
+  // tiles whose 8 x 5 texels hold (x, y): x - TSX tx in [0, TSX], y - TSY ty in [0, TSY]
+  const int tx0 = max(0, (x - TSX + TSX - 1) / TSX), tx1 = min(G.nx - 1, x / TSX);
+  const int ty0 = max(0, (y - TSY + TSY - 1) / TSY), ty1 = min(G.ny - 1, y / TSY);
+  float v = 0.f;
+  const int nb = beams_per_image(G);
+  for (int bm = 0; bm < nb; ++bm)
+    for (int ty = ty0; ty <= ty1; ++ty)
+      for (int tx = tx0; tx <= tx1; ++tx) {
+        const int key = tile_key(b * nb + bm, q, tx, ty, G);
+        const int slot = ((y - TSY * ty) * TTX + (x - TSX * tx)) * NC + ch;
+        for (int c = chunk_start[key]; c < chunk_start[key + 1]; ++c) v += part[(long long)c * (TTX * TTY * NC) + slot];
+      }
+  if (v != 0.f) dplanes[(long long)b * sb + (long long)q * sq + (long long)(y * R + x) * st + ch] += v;
+}
+
 struct TileArgs {
   const float* planes;    // texel-major, strides sb / sq / st as dplanes
   float* dpc;             // [nsamp][3 planes][2] grid gradients (NULL: no pose gradients)
@@ -2211,6 +2294,9 @@ struct TileArgs {
   float* shadow;          // d planes summed a second way (per-entry float atomics), same strides
   long long nsamp;
   int K;
+  // deterministic mode (nfi_set_deterministic): each chunk's merged tile image [TTX*TTY][NC] is
+  // stored here instead of flushed with float atomics; dplanes_reduce_kernel sums them in order
+  float* part;
 };
 
 typedef float img32 __attribute__((ext_vector_type(32)));
@@ -2740,7 +2826,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
         if (yl >= 1) v += im[(32 + (yl - 1) * TTX + xl) * NC + ch];
       }
       const int gy = ty * TSY + yl, gx = tx * TSX + xl;
-      if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
+      if (A.part) A.part[(long long)c * (TTX * TTY * NC) + k] = v;
+      else if (v != 0.f && gy < A.R && gx < A.R) unsafeAtomicAdd(dq + (gy * A.R + gx) * A.st + ch, v);
     }
 #if NFI_TILE_CHECK
     // the second sum of d planes (compared with the first by tile_shadow_compare_kernel): every
@@ -3633,8 +3720,22 @@ struct Workspace {
   int* check;        // -DNFI_TILE_CHECK builds: counters + first failure + two double sums
   float* shadow;     // -DNFI_TILE_CHECK builds: the second d-planes sum and a snapshot of d planes
   float* snapshot;
+  // deterministic mode
+  int4* det_list;    // the entries in tile, sample order (+ 64 zeroed records)
+  float* tpart;      // per-chunk partial tile images
   long long bytes;
 };
+
+// deterministic mode of the backward, per host thread (nfi_set_deterministic; default from the
+// environment variable NFI_DETERMINISTIC)
+static thread_local int g_det = -1;
+static bool deterministic() {
+  if (g_det < 0) {
+    const char* e = std::getenv("NFI_DETERMINISTIC");
+    g_det = (e && e[0] && std::strcmp(e, "0") != 0) ? 1 : 0;
+  }
+  return g_det != 0;
+}
 
 static Workspace carve(const nfi_render_args* a, void* base) {
   const long long nrays = (long long)a->B * a->HW;
@@ -3664,6 +3765,12 @@ static Workspace carve(const nfi_render_args* a, void* base) {
   w.dpc = reinterpret_cast<float*>(take(nsamp * 6 * 4));
   w.check = nullptr;
   w.shadow = w.snapshot = nullptr;
+  w.det_list = nullptr;
+  w.tpart = nullptr;
+  if (deterministic()) {
+    w.det_list = reinterpret_cast<int4*>(take((3 * nsamp + 128) * 16));
+    w.tpart = reinterpret_cast<float*>(take((3 * nsamp / CHUNK + K + 1) * (TTX * TTY * NC) * 4));
+  }
 #if NFI_TILE_CHECK
   w.check = reinterpret_cast<int*>(take(64 * 4));
   w.shadow = reinterpret_cast<float*>(take((long long)a->B * a->field.sb * 4));
@@ -3756,9 +3863,10 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
 #else
   float* const dpc_used = g->g_ro ? w.dpc : nullptr;
 #endif
+  const bool det = w.tpart != nullptr;
   TileArgs TA{a->field.planes, dpc_used, w.gfeat, counts, w.offsets, w.chunk_start,
-              w.chunk_tile, w.meta, w.list, g->d_planes, a->field.sb, (int)a->field.sq, (int)a->field.st,
-              a->field.R, tg, w.cursor, w.check, w.shadow, nsamp, K};
+              w.chunk_tile, w.meta, det ? w.det_list : w.list, g->d_planes, a->field.sb, (int)a->field.sq,
+              (int)a->field.st, a->field.R, tg, w.cursor, w.check, w.shadow, nsamp, K, w.tpart};
   if (do_tiles) {
     // 3) per-tile register accumulation of d planes (+ per-entry grid gradients for the pose)
     // (a bound on the chunk count meta[0]; the chunk queue meta[1] starts at 0)
@@ -3770,8 +3878,23 @@ static int launch_bwd(const nfi_render_args* a, const nfi_render_grad_args* g, h
                     hipMemcpyAsync(w.snapshot, g->d_planes, dpb, hipMemcpyDeviceToDevice, s) == hipSuccess,
                 "render_backward: check-build setup failed");
 #endif
+    if (det) {
+      // the bins' entries in sample order per tile (their append order follows the cursor atomics)
+      det_sort_kernel<<<(unsigned)(3 * nsamp / CHUNK + K + 1), 256, 0, s>>>(w.list, w.offsets, w.chunk_start,
+                                                                             w.chunk_tile, w.meta, w.det_list);
+      NFI_CHECK_LAUNCH("det_sort_kernel");
+      det_pad_kernel<<<1, 64, 0, s>>>(w.offsets, K, w.det_list);
+      NFI_CHECK_LAUNCH("det_pad_kernel");
+    }
     tile_kernel<<<(unsigned)std::min<long long>(TB, TILE_WGS), 256, 0, s>>>(TA);
     NFI_CHECK_LAUNCH("tile_kernel");
+    if (det) {
+      const long long n = (long long)a->B * 3 * a->field.R * a->field.R * NC;
+      dplanes_reduce_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(w.tpart, w.chunk_start, tg, a->B, a->field.R,
+                                                                         a->field.sb, (int)a->field.sq,
+                                                                         (int)a->field.st, g->d_planes);
+      NFI_CHECK_LAUNCH("dplanes_reduce_kernel");
+    }
 #if NFI_TILE_CHECK
     {
       const long long ne = (long long)a->B * a->field.sb;
@@ -3898,6 +4021,12 @@ int64_t nfi_tile_count_size_shape(int32_t B, int32_t R, int32_t H, int32_t W, in
   if (B <= 0 || R < 2 || H <= 0 || W <= 0 || N <= 0) return -1;
   const nfi::TileGrid tg = nfi::tile_grid(R, H * W, W, N);
   return (int64_t)B * nfi::beams_per_image(tg) * 3 * tg.nx * tg.ny;
+}
+
+int32_t nfi_set_deterministic(int32_t on) {
+  const int32_t prev = nfi::deterministic() ? 1 : 0;
+  if (on >= 0) nfi::g_det = on ? 1 : 0;
+  return prev;
 }
 
 int64_t nfi_render_backward_workspace_bytes(const nfi_render_args* a) {

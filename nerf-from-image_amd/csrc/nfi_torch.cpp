@@ -19,6 +19,8 @@
 //                                                     (channel-major planes, gain-scaled W1s/W2s)
 //   nfi::composite_fwd/_bwd, nfi::triplane_mlp_fwd/_bwd  per-stage ops (nerf_utils.py:125-163;
 //                                                     generator.py:587-681)
+#include <cstring>
+#include <cstdlib>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -334,6 +336,13 @@ std::vector<Tensor> volume_render_bwd(const Tensor& g_rgb_in, const Tensor& g_ma
   a.y_saved = y_s.data_ptr<float>();
   a.perm = perm.data_ptr<int16_t>();
   a.x_saved = x_s.data_ptr<float>();
+  {
+    // torch.use_deterministic_algorithms() (or NFI_DETERMINISTIC) selects the bitwise-reproducible
+    // backward: sorted bins, d planes without float atomics (nfi_set_deterministic)
+    const char* env = std::getenv("NFI_DETERMINISTIC");
+    const bool det = at::globalContext().deterministicAlgorithms() || (env && env[0] && std::strcmp(env, "0") != 0);
+    nfi_set_deterministic(det ? 1 : 0);
+  }
   const int64_t nbytes = nfi_render_backward_workspace_bytes(&a);
   check(nbytes < 0 ? -1 : 0, "nfi_render_backward_workspace_bytes");
   Tensor ws = torch::empty({nbytes}, o.dtype(torch::kUInt8));

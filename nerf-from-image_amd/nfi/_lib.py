@@ -70,6 +70,7 @@ SIGNATURES = {
                                                    c_void_p, c_void_p]),
     'nfi_planes_to_channel_major': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                      c_void_p, c_void_p]),
+    'nfi_set_deterministic': (ctypes.c_int32, [ctypes.c_int32]),
     'nfi_pose_forward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 2 + [c_void_p] * 3),
     'nfi_pose_backward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 2 + [c_void_p] * 7),
     'nfi_pose_project': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int32, c_void_p]),

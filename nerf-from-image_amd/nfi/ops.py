@@ -42,6 +42,17 @@ def _stream(dev: torch.device):
 # False the backward counts them itself (both paths are covered by tests/test_gpu_parity.py).
 FORWARD_TILE_COUNTS = True
 
+# Bitwise-reproducible backward (nfi_set_deterministic): tile bins sorted by sample, d planes summed
+# in a fixed order without float atomics.  None: follow torch.use_deterministic_algorithms() (and the
+# NFI_DETERMINISTIC environment variable, read by the library); True / False: force.
+DETERMINISTIC: Optional[bool] = None
+
+
+def _deterministic() -> bool:
+    if DETERMINISTIC is not None:
+        return bool(DETERMINISTIC)
+    return torch.are_deterministic_algorithms_enabled() or os.environ.get('NFI_DETERMINISTIC', '0') not in ('', '0')
+
 KERNEL_TIMERS: Optional[dict] = None
 
 # randomized renders draw their uniforms with torch.rand on the device (graph-safe) instead of the
@@ -417,6 +428,7 @@ class _VolumeRender(torch.autograd.Function):
         per_img = None
         if tile_counts is not None:
             per_img = tile_counts.numel() // B
+        lib.nfi_set_deterministic(1 if _deterministic() else 0)   # (workspace size and launches follow it)
 
         def part(b0, nb):
             """C-ABI arguments of the backward of images b0 .. b0+nb-1 (every per-image / per-ray
