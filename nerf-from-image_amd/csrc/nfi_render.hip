@@ -2275,7 +2275,7 @@ __global__ void __launch_bounds__(256) dplanes_reduce_kernel(const float* __rest
 
 struct TileArgs {
   const float* planes;    // texel-major, strides sb / sq / st as dplanes
-  float* dpc;             // [nsamp][3 planes][2] grid gradients (NULL: no pose gradients)
+  float* dpc;             // grid gradients, dpc_at() layout (NULL: no pose gradients)
   const float* gfeat;     // [nsamp][32]
   const int* counts;
   const int* offsets;
@@ -2534,9 +2534,18 @@ __device__ __forceinline__ f4v pk_sub(f4v a, f4v b, float m1) {
 #ifndef NFI_TILE_GG_UNROLL
 #define NFI_TILE_GG_UNROLL 2
 #endif
+// dpc layout: NFI_DPC_PLANAR 1 (default) [3 planes][nsamp][2] — a chunk's entries (one plane,
+// runs of consecutive samples) write consecutive 8-B pairs; 0: [nsamp][3][2] (each entry's pair
+// 24 B apart, three tile passes' partial writes per line)
+#ifndef NFI_DPC_PLANAR
+#define NFI_DPC_PLANAR 1
+#endif
+__device__ __forceinline__ long long dpc_at(long long s, int q, long long nsamp) {
+  return NFI_DPC_PLANAR ? ((long long)q * nsamp + s) * 2 : (s * 3 + q) * 2;
+}
 __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, const float* __restrict__ Tex,
                                                 int l, int4 rec, int q, float half, float* __restrict__ dpc,
-                                                long long nsamp_chk = 0) {
+                                                long long nsamp) {
   const int slot = rec.y & 31;
   const float w = __int_as_float(rec.z), n = __int_as_float(rec.w);
   float gx = 0.f, gy = 0.f;
@@ -2582,9 +2591,9 @@ __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, con
 #endif
   const float2 out = make_float2((rec.y & 0x100) ? gx * half : 0.f, (rec.y & 0x200) ? gy * half : 0.f);
 #if NFI_TILE_CHECK
-  if (rec.x < 0 || rec.x >= nsamp_chk) return;   // (code 3 counts it; never store out of range)
+  if (rec.x < 0 || rec.x >= nsamp) return;   // (code 3 counts it; never store out of range)
 #endif
-  *reinterpret_cast<float2*>(dpc + ((long long)rec.x * 3 + q) * 2) = out;
+  *reinterpret_cast<float2*>(dpc + dpc_at(rec.x, q, nsamp)) = out;
 }
 
 // One workgroup-chunk c (< meta[0]) of a tile's entries; lds: TILE_LDS floats.
@@ -3143,10 +3152,10 @@ __global__ void __launch_bounds__(256) dcoord_reduce_kernel(nfi_render_args a, B
   for (int e = 0; e < NPL; ++e) {
     const int ic = min(e * 64 + l, N - 1);
     ts[e] = a.t_saved[r * N + ic];
-    const float2* p = reinterpret_cast<const float2*>(dpc + (r * N + ic) * 6);
-    xy[e] = p[0];
-    xz[e] = p[1];
-    yz[e] = p[2];
+    const long long si = r * N + ic, ns = nrays * N;
+    xy[e] = *reinterpret_cast<const float2*>(dpc + dpc_at(si, 0, ns));
+    xz[e] = *reinterpret_cast<const float2*>(dpc + dpc_at(si, 1, ns));
+    yz[e] = *reinterpret_cast<const float2*>(dpc + dpc_at(si, 2, ns));
   }
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, u0 = 0.f, u1 = 0.f, u2 = 0.f;
 #pragma unroll
