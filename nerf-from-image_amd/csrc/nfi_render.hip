@@ -2596,6 +2596,22 @@ __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, con
   *reinterpret_cast<float2*>(dpc + dpc_at(rec.x, q, nsamp)) = out;
 }
 
+// the gradient-row gathers: NFI_ROW_NT 1 marks them non-temporal (a row's three reads are a third of
+// the pass apart, so the idea was to leave the L2 to the records, whose scalar re-read in the entry
+// loop follows the vector read by one batch) — measured slower: tile pass 2.03 vs 1.83-1.86 ms
+// (gpurun_out/r05/ab_rownt.log), so plain loads
+#ifndef NFI_ROW_NT
+#define NFI_ROW_NT 0
+#endif
+__device__ __forceinline__ float4 tile_row_load(const float4* p) {
+#if NFI_ROW_NT
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(v[0], v[1], v[2], v[3]);
+#else
+  return *p;
+#endif
+}
+
 // One workgroup-chunk c (< meta[0]) of a tile's entries; lds: TILE_LDS floats.
 __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict__ lds, int c) {
   const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = lane_id();
@@ -2718,7 +2734,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
   {                                                                                                  \
     int row_ = __shfl((SX), 8 * (J) + (l >> 3));                                                    \
     NFI_ROW_CHECK(J, RB)                                                                             \
-    V = *reinterpret_cast<const float4*>(A.gfeat + (long long)row_ * NC + 4 * (l & 7));             \
+    V = tile_row_load(reinterpret_cast<const float4*>(A.gfeat + (long long)row_ * NC + 4 * (l & 7))); \
   }
 #define NFI_LOAD_ROWC(REC, RB)                                                                       \
   {                                                                                                  \
