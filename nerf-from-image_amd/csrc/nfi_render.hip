@@ -2344,6 +2344,12 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 #define NFI_TILE_BATCH 56
 #endif
 constexpr int BATCH = NFI_TILE_BATCH;
+// NFI_TILE_LDSREC 1: the entry loop takes each entry's record from the pad columns of its stage row
+// (written there with the row) instead of re-reading the list with scalar loads
+#ifndef NFI_TILE_LDSREC
+#define NFI_TILE_LDSREC 0
+#endif
+static_assert(XS >= NC + 4, "the stage rows' pad holds a record");
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 __device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
@@ -2705,6 +2711,37 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #else
 #define NFI_STEP_CHECK(U, RUSE)
 #endif
+#if NFI_TILE_LDSREC
+      // the entries' records from the stage rows' pad columns (written with the rows): one broadcast
+      // b128 LDS read per entry, no scalar loads (the list is read once, by the vector loads)
+#if NFI_TILE_CHECK
+      // code 6: the LDS records against the batch's vector records (lane U + k)
+#define NFI_LDSREC_CHECK(U, HH, R)                                                                   \
+    _Pragma("unroll") for (int k = (HH); k < (HH) + 4; ++k) if ((U) + k < n) {                       \
+      const int vy = __shfl(crec.y, (U) + k), vz = __shfl(crec.z, (U) + k), vw = __shfl(crec.w, (U) + k); \
+      NFI_TCHK(R[k].x == vy && R[k].y == vz && R[k].z == vw, 6, c, tile, (U) + k, R[k].x, vy);       \
+    }
+#else
+#define NFI_LDSREC_CHECK(U, HH, R)
+#endif
+#define NFI_LDSREC_ENTRY(R, K)                                                                       \
+  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(R[K].x) & 31, __int_as_float(R[K].y), \
+             __int_as_float(R[K].z), gv[K], wsgn, woff)
+#define NFI_STEP(U, RUSE, RNEXT)                                                                     \
+  {                                                                                                  \
+    float gv[8];                                                                                     \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) gv[k] = G[stage_at((U) + k, cl)];                 \
+    asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
+                 "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
+    _Pragma("unroll") for (int hh = 0; hh < 8; hh += 4) {                                            \
+      int3 rk[8];   /* (slot | flags, w, n) of entries hh..hh+3: b96 broadcast reads */             \
+      _Pragma("unroll") for (int k = hh; k < hh + 4; ++k)                                           \
+        rk[k] = *reinterpret_cast<const int3*>(G + ((U) + k) * XS + NC);                             \
+      NFI_LDSREC_CHECK(U, hh, rk)                                                                    \
+      _Pragma("unroll") for (int k = hh; k < hh + 4; ++k) NFI_LDSREC_ENTRY(rk, k);                  \
+    }                                                                                                \
+  }
+#else
 #define NFI_STEP(U, RUSE, RNEXT)                                                                     \
   {                                                                                                  \
     float gv[8];                                                                                     \
@@ -2715,6 +2752,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     NFI_STEP_CHECK(U, RUSE)                                                                          \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
   }
+#endif
       // Rows loaded coalesced: lane l holds float4 (l & 7) of entry 8j + (l >> 3), j = 0..6 (the
       // entry's row index comes from its lane's record by ds_bpermute): each b128 load reads 8
       // whole 128-B rows instead of one 16-B piece of 56 different rows.
@@ -2776,6 +2814,15 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #define NFI_G_VERIFY(CODE)
 #define NFI_CREC(VREC)
 #endif
+#if NFI_TILE_LDSREC
+#define NFI_REC_ST(VREC) if (l < BATCH) lds_st(reinterpret_cast<int4*>(G + l * XS + NC), make_int4((VREC).y, (VREC).z, (VREC).w, (VREC).x));
+#define NFI_REC_FIRST()
+#else
+#define NFI_REC_ST(VREC)
+#define NFI_REC_FIRST()                                                                              \
+    iv4 ra[8], rb[8];                                                                                \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];
+#endif
 #define NFI_NEXT_REC(VREC, AHEAD)                                                                    \
     VREC = vnext;                                                                                    \
     vnext = A.list[min(base_ + 2 * (AHEAD) + l, b1 - 1)];
@@ -2784,6 +2831,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int base_ = (BASE);                                                                        \
     const int n = min(BATCH, b1 - base_);                                                            \
     _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_ST1(j, rc[j])                         \
+    NFI_REC_ST(VREC)                                                                                 \
     wave_lds_sync();                                                                                 \
     NFI_CREC(VREC)                                                                                   \
     NFI_BATCH_CHECK()                                                                                \
@@ -2791,8 +2839,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     NFI_NEXT_REC(VREC, AHEAD)                                                                        \
     NFI_LOAD_ROWC(VREC, base_ + (AHEAD))                                                             \
     NFI_STAMP(24)                                                                                    \
-    iv4 ra[8], rb[8];                                                                                \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];                             \
+    NFI_REC_FIRST()                                                                                  \
     for (int u = 0; u < n; u += 16) {                                                                \
       NFI_STEP(u, ra, rb)                                                                            \
       if (u + 8 >= n) break;                                                                         \
@@ -2812,6 +2859,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
 #undef NFI_BATCHC
 #undef NFI_NEXT_REC
+#undef NFI_REC_ST
+#undef NFI_REC_FIRST
 #undef NFI_ST1
 #undef NFI_LOAD_ROWC
 #undef NFI_LD1
