@@ -1093,16 +1093,20 @@ __global__ void __launch_bounds__(256) aug_fwd_kernel(const float* __restrict__ 
   for (int c = 0; c < 3; ++c) op[c * HWo] = acc[c] + shift;
 }
 
-// Adjoint, gathered (no atomics): 16 lanes per input pixel (b, Y, X), lane k taking copies k,
-// k + 16, ...; for each copy the output pixels whose sample has (Y, X) as a corner lie in the
-// preimage of the 2x2 box around (Y, X) under the copy's affine map (read off the grid itself:
-// its value at (0,0), (0,1), (1,0)), enumerated over that preimage's bounding box + 1 and tested
-// with the forward's exact arithmetic; the 16 lanes' sums are combined by shuffles.
+// Adjoint, gathered (no atomics): a workgroup takes 64 consecutive input pixels (b, Y, X), one per
+// lane, and its four waves the copies k = wave, wave + 4, ...; for each copy the output pixels whose
+// sample has (Y, X) as a corner lie in the preimage of the 2x2 box around (Y, X) under the copy's
+// affine map (read off the grid itself: its value at (0,0), (0,1), (1,0)), enumerated over that
+// preimage's bounding box + 1 and tested with the forward's exact arithmetic; the four waves' sums
+// are combined in LDS in wave order.  The lanes of a wave hold neighbouring pixels of ONE copy, so an
+// enumeration step's grid and gradient reads are neighbouring addresses (round 4 had 16 lanes per
+// pixel on 16 copies: every read a separate line, 110 us per vgg step).
 __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ grid,
                                                       float* __restrict__ gimg, int64_t total, int K, int H, int W,
                                                       int Ho, int Wo) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;   // input pixel
-  const int kl = threadIdx.x & 15;
+  __shared__ float part[3][4][64];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + l;   // input pixel
   const bool live = i < total;
   const int64_t ic = live ? i : total - 1;
   const int64_t HW = (int64_t)H * W, HWo = (int64_t)Ho * Wo;
@@ -1110,7 +1114,7 @@ __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ 
   const int pix = (int)(ic - (int64_t)b * HW);
   const int Y = pix / W, X = pix - Y * W;
   float acc[3] = {0.f, 0.f, 0.f};
-  for (int k = kl; k < K; k += 16) {
+  for (int k = wv; k < K; k += 4) {
     const int64_t j = (int64_t)b * K + k;
     const float* gj = grid + j * HWo * 2;
     // source position as an affine function of the output pixel, s(x, y) = s00 + x dx + y dy,
@@ -1150,12 +1154,20 @@ __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ 
     }
   }
 #pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) {
-    acc[0] += __shfl_xor(acc[0], m, 64);
-    acc[1] += __shfl_xor(acc[1], m, 64);
-    acc[2] += __shfl_xor(acc[2], m, 64);
+  for (int c = 0; c < 3; ++c) part[c][wv][l] = acc[c];
+  // (wait states behind the LDS stores before their data registers are rewritten: the wide-store
+  //  data hazard nfi_common.h's lds_st guards, checked by scripts/isa_lint.py)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 1" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __syncthreads();
+  // 64 pixels x 3 channels, contiguous in gimg [B][H][W][3]
+  const int t = threadIdx.x;
+  if (t < 192) {
+    const int p = t / 3, c = t - 3 * p;
+    const int64_t o = (int64_t)blockIdx.x * 64 + p;
+    if (o < total) gimg[o * 3 + c] = (part[c][0][p] + part[c][1][p]) + (part[c][2][p] + part[c][3][p]);
   }
-  if (live && kl < 3) gimg[i * 3 + kl] = kl == 0 ? acc[0] : (kl == 1 ? acc[1] : acc[2]);
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -1556,7 +1568,7 @@ int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gim
   NFI_REQUIRE(gout && grid && gimg, "aug_sample_backward: null pointer");
   NFI_REQUIRE(B > 0 && K > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, "aug_sample_backward: bad shape");
   const int64_t total = (int64_t)B * H * W;
-  aug_bwd_kernel<<<blocks(total * 16), 256, 0, (hipStream_t)stream>>>(gout, grid, gimg, total, K, H, W, Ho, Wo);
+  aug_bwd_kernel<<<(unsigned)((total + 63) / 64), 256, 0, (hipStream_t)stream>>>(gout, grid, gimg, total, K, H, W, Ho, Wo);
   NFI_CHECK_LAUNCH("aug_bwd_kernel");
   return NFI_OK;
 }
