@@ -336,7 +336,11 @@ __global__ void __launch_bounds__(256) output_scaled_kernel(const float* __restr
 // buffers' space) and each thread transforms two (channel, tile) outputs with the same bias /
 // ReLU / max-pool epilogue as output_kernel.
 // ---------------------------------------------------------------------------------------
-constexpr int FP = 32, FC = 64, FK = 8;
+#ifndef NFI_WINO_FC
+#define NFI_WINO_FC 64   // output channels per workgroup: 64 (one workgroup per CU) or 32 (two)
+#endif
+constexpr int FP = 32, FC = NFI_WINO_FC, FK = 8;
+static_assert(FC == 32 || FC == 64, "fused_kernel: 32 or 64 output channels per workgroup");
 constexpr int HB = FC / 16;                   // 16-channel MFMA row blocks per workgroup
 constexpr int VIMG = 36 * FK * FP;            // floats per V image
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -419,7 +423,7 @@ __device__ __forceinline__ void emit_tile(float (&m)[6][6], float b, int mode, f
 // grid (ceil(P / FP), CoP / FC), 256 threads, one workgroup per CU (occupancy 1: 288
 // accumulator registers per lane, the next chunk's A operands and patch prefetched a whole
 // chunk ahead).  Ci % FK == 0.
-__global__ void __launch_bounds__(256, 1) fused_kernel(const float* __restrict__ x, const float* __restrict__ Ua,
+__global__ void __launch_bounds__(256, 64 / FC) fused_kernel(const float* __restrict__ x, const float* __restrict__ Ua,
                                                        const float* __restrict__ bias, float* __restrict__ y,
                                                        float* __restrict__ pooled, int Ci, int Co, int H, int W,
                                                        int TW, int T, int64_t P, int CB, int mode, int nPB,
@@ -537,7 +541,7 @@ __global__ void __launch_bounds__(256, 1) fused_kernel(const float* __restrict__
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          lds[((9 * w + xl) * 16 + 4 * kk + i) * FP + 16 * g + cc] = acc[xl][h][g][i];
+          lds_st(lds + ((9 * w + xl) * 16 + 4 * kk + i) * FP + 16 * g + cc, acc[xl][h][g][i]);
     __syncthreads();
 #pragma unroll
     for (int rep = 0; rep < 2; ++rep) {
