@@ -382,6 +382,31 @@ __device__ __forceinline__ void stage_patch(float (&d)[6][6], float* __restrict_
   }
 }
 
+// stage_patch in pieces: B^T applied to columns [J0, J1), then rows [R0, R1) transformed and stored
+// (NFI_WINO_INTERLEAVE: the next chunk's staging spread over the current chunk's products)
+template <int J0, int J1>
+__device__ __forceinline__ void stage_cols(float (&d)[6][6]) {
+#pragma unroll
+  for (int j = J0; j < J1; ++j) {
+    float col[6], o[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) col[r] = d[r][j];
+    bt_col(col, o);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) d[r][j] = o[r];
+  }
+}
+template <int R0, int R1>
+__device__ __forceinline__ void stage_rows(float (&d)[6][6], float* __restrict__ dst) {
+#pragma unroll
+  for (int r = R0; r < R1; ++r) {
+    float o[6];
+    bt_col(d[r], o);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) lds_st(dst + (r * 6 + j) * (FK * FP), o[j]);
+  }
+}
+
 // A^T m A of one tile plus the epilogue, stored to y (and pooled)
 __device__ __forceinline__ void emit_tile(float (&m)[6][6], float b, int mode, float* __restrict__ dst, int W,
                                           float* __restrict__ pd, int W2) {
@@ -416,6 +441,9 @@ __device__ __forceinline__ void emit_tile(float (&m)[6][6], float b, int mode, f
   }
 }
 
+#ifndef NFI_WINO_INTERLEAVE
+#define NFI_WINO_INTERLEAVE 0   // 1: the next chunk's patch staging inside products 3..8 of this chunk
+#endif
 #ifndef NFI_WINO_ADEPTH
 #define NFI_WINO_ADEPTH 3   // 1: the previous one-product-ahead A loads
 #endif
@@ -525,9 +553,24 @@ __global__ void __launch_bounds__(256, 64 / FC) fused_kernel(const float* __rest
 #pragma unroll
           for (int g = 0; g < 2; ++g)
             acc[xl][h][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[h][s2], b[s2][g], acc[xl][h][g], 0, 0, 0);
+#if NFI_WINO_INTERLEAVE
+      // the next chunk's staging beside this product's MFMAs (its patch loads, issued at the top of
+      // the chunk, have had three products to arrive; the other V buffer is free since the barrier)
+      if (c + 1 < nk) {
+        float* nv = vdst + (cur ^ 1) * VIMG;
+        if (xl == 3) stage_cols<0, 2>(d);
+        if (xl == 4) stage_cols<2, 4>(d);
+        if (xl == 5) stage_cols<4, 6>(d);
+        if (xl == 6) stage_rows<0, 2>(d, nv);
+        if (xl == 7) stage_rows<2, 4>(d, nv);
+        if (xl == 8) stage_rows<4, 6>(d, nv);
+      }
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
+#if !NFI_WINO_INTERLEAVE
     if (c + 1 < nk) stage_patch(d, vdst + (cur ^ 1) * VIMG);
+#endif
     __syncthreads();
   }
 
