@@ -221,6 +221,13 @@ int32_t nfi_aug_sample_forward(const float* img, const float* grid, float* out, 
 int32_t nfi_aug_sample_backward(const float* gout, const float* grid, float* gimg, int32_t B, int32_t K, int32_t H,
                                 int32_t W, int32_t Ho, int32_t Wo, void* stream);
 
+/* The augmentation's sampling grid: F.affine_grid(theta, [N, C, H, W], align_corners=False)
+ * (run.py:749 in augment_impl, :720-767) for theta [N][2][3]: grid [N][H][W][2] =
+ * theta[n] . (x_i, y_j, 1) with x_i = linspace(-1, 1, W)_i (W - 1) / W (y_j likewise), the
+ * products summed in ATen's order (x, y, then the translation).  One launch instead of ATen's
+ * linspace / base-grid / bmm sequence. */
+int32_t nfi_aug_affine_grid(const float* theta, int32_t N, int32_t H, int32_t W, float* grid, void* stream);
+
 /* ---- Split-f16 batched GEMM (csrc/nfi_gemm.hip): C[b] = A[b] . B[b] in fp32 on the f16 matrix cores
  * (v_mfma_f32_16x16x32_f16), each fp32 operand a power-of-two-scaled hi + lo fp16 pair and each
  * product lo.hi + hi.lo + hi.hi on an fp32 accumulator (fp32-level error).  Replaces the

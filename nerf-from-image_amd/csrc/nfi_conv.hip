@@ -584,7 +584,7 @@ __global__ void __launch_bounds__(256, 64 / FC) fused_kernel(const float* __rest
       for (int g = 0; g < 2; ++g)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          lds_st(lds + ((9 * w + xl) * 16 + 4 * kk + i) * FP + 16 * g + cc, acc[xl][h][g][i]);
+          lds[((9 * w + xl) * 16 + 4 * kk + i) * FP + 16 * g + cc] = acc[xl][h][g][i];
     __syncthreads();
 #pragma unroll
     for (int rep = 0; rep < 2; ++rep) {

@@ -1093,6 +1093,31 @@ __global__ void __launch_bounds__(256) aug_fwd_kernel(const float* __restrict__ 
   for (int c = 0; c < 3; ++c) op[c * HWo] = acc[c] + shift;
 }
 
+// F.affine_grid(theta, [N, C, H, W], align_corners=False): ATen's base grid (linspace(-1, 1, n) scaled
+// by (n - 1) / n; linspace's two-sided form: start + step i below the middle, end - step (n - 1 - i)
+// above) times theta^T, the three products accumulated x, y, translation
+__device__ __forceinline__ float affine_base(int i, int n) {
+  if (n == 1) return 0.f;   // linspace(-1, 1, 1) = [-1], times 0 / 1
+  const float step = 2.f / (float)(n - 1);
+  const float v = i < n / 2 ? -1.f + step * (float)i : 1.f - step * (float)(n - 1 - i);
+  return v * (float)(n - 1) / (float)n;
+}
+__global__ void __launch_bounds__(256) affine_grid_kernel(const float* __restrict__ theta, int64_t total, int H, int W,
+                                                          float* __restrict__ grid) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t HW = (int64_t)H * W;
+  const int64_t n = i / HW;
+  const int pix = (int)(i - n * HW);
+  const int y = pix / W, x = pix - y * W;
+  const float bx = affine_base(x, W), by = affine_base(y, H);
+  const float* t = theta + n * 6;
+  float2 g;
+  g.x = fmaf(1.f, t[2], fmaf(by, t[1], bx * t[0]));
+  g.y = fmaf(1.f, t[5], fmaf(by, t[4], bx * t[3]));
+  reinterpret_cast<float2*>(grid)[i] = g;
+}
+
 // Adjoint, gathered (no atomics): a workgroup takes 64 consecutive input pixels (b, Y, X), one per
 // lane, and its four waves the copies k = wave, wave + 4, ...; for each copy the output pixels whose
 // sample has (Y, X) as a corner lie in the preimage of the 2x2 box around (Y, X) under the copy's
@@ -1560,6 +1585,16 @@ int32_t nfi_aug_sample_forward(const float* img, const float* grid, float* out, 
   const int64_t total = (int64_t)B * K * Ho * Wo;
   aug_fwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(img, grid, out, total, K, H, W, Ho, Wo, shift);
   NFI_CHECK_LAUNCH("aug_fwd_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_aug_affine_grid(const float* theta, int32_t N, int32_t H, int32_t W, float* grid, void* stream) {
+  NFI_REQUIRE(theta && grid, "aug_affine_grid: null pointer");
+  NFI_REQUIRE(N > 0 && H > 0 && W > 0, "aug_affine_grid: bad shape N=%d H=%d W=%d", N, H, W);
+  NFI_REQUIRE(((uintptr_t)grid & 7) == 0, "aug_affine_grid: grid must be 8-B aligned");
+  const int64_t total = (int64_t)N * H * W;
+  affine_grid_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(theta, total, H, W, grid);
+  NFI_CHECK_LAUNCH("affine_grid_kernel");
   return NFI_OK;
 }
 

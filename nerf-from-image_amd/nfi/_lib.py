@@ -155,6 +155,7 @@ SIGNATURES = {
                                + [ctypes.c_float, c_void_p]),
     'nfi_aug_sample_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p] + [ctypes.c_int32] * 6
                                 + [c_void_p]),
+    'nfi_aug_affine_grid': (ctypes.c_int32, [c_void_p] + [ctypes.c_int32] * 3 + [c_void_p, c_void_p]),
     'nfi_syn_up_add_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_vgg_first_forward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 4 + [c_void_p]),

@@ -274,6 +274,8 @@ def augment_grid(shape, p: float, dev, disable_scale: bool = False,
     rotm = torch.stack([torch.stack([c, -s], -1), torch.stack([s, c], -1)], 1)   # [bs,2,2]
     t = torch.stack([translation[:, 0], -translation[:, 1]], -1) * scale[:, None]
     theta = torch.cat([rotm * scale[:, None, None], (rotm * t[:, None, :]).sum(-1, keepdim=True)], -1)
+    if theta.is_cuda and producer_ops.AFFINE_GRID_HIP:
+        return producer_ops.affine_grid(theta, list(shape))
     return F.affine_grid(theta, list(shape), align_corners=False)
 
 

@@ -17,6 +17,7 @@ the inversion (run.py:630-632), so biases never receive gradients (asking for on
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -266,6 +267,13 @@ def up_conv_act(x, w, d, bias, gain: float):
     return _UpConvAct.apply(x, W9, W9t, d, bias, gain)
 
 
+# the planes layer's backward as one K = 96 product (round 5) instead of one product per plane plus
+# in-place accumulations; NFI_PLANES_BWD_ONE=0 restores the per-plane form (A/B)
+PLANES_BWD_ONE = os.environ.get('NFI_PLANES_BWD_ONE', '1') != '0'
+# the augmentation grid in one launch (nfi_aug_affine_grid); NFI_AFFINE_GRID_HIP=0: F.affine_grid
+AFFINE_GRID_HIP = os.environ.get('NFI_AFFINE_GRID_HIP', '1') != '0'
+
+
 class _ModConv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, s, Wf, Wt, layout: str):
@@ -287,12 +295,16 @@ class _ModConv1x1(torch.autograd.Function):
     def backward(ctx, gy):
         x, s, Wt = ctx.saved_tensors
         B, C, H, W = x.shape
-        if gy.dim() == 5:     # texel-major planes [B, Q, 32, H, W]: one product per plane, accumulated
+        if gy.dim() == 5 and not PLANES_BWD_ONE:   # (the round-4 form: one product per plane, accumulated)
             gxs = None
             for q in range(gy.shape[1]):
                 gq = gy[:, q].reshape(B, 32, H * W)
                 Wq = Wt[:, 32 * q:32 * (q + 1)]
                 gxs = torch.matmul(Wq, gq) if gxs is None else gxs.baddbmm_(Wq.expand(B, -1, -1), gq)
+        elif gy.dim() == 5:   # texel-major planes [B, Q, 32, H, W]: the Q planes' channels are one
+            # K = 32 Q contraction (a view: plane and channel strides merge in the texel-major layout) —
+            # one product instead of a product + Q - 1 in-place accumulations over the [B, C, HW] result
+            gxs = torch.matmul(Wt, gy.reshape(B, gy.shape[1] * gy.shape[2], H * W))
         elif gy.is_contiguous():
             gxs = torch.matmul(Wt, gy.view(B, -1, H * W))
         else:                 # channels-last: [B, HW, O] seen as [B, O, HW] (a transposed operand, no copy)
@@ -350,6 +362,20 @@ class _AugSample(torch.autograd.Function):
         gimg = torch.empty((B, H, W, 3), device=gout.device, dtype=gout.dtype)
         _call('nfi_aug_sample_backward', _p(gout), _p(grid), _p(gimg), B, K, H, W, Ho, Wo, _stream(gout.device))
         return gimg, None, None, None
+
+
+def affine_grid(theta, size):
+    """F.affine_grid(theta, size, align_corners=False) for theta [N, 2, 3] on the device, size
+    [N, C, H, W] (augment_impl's grid, run.py:749): one launch (nfi_aug_affine_grid) instead of ATen's
+    base grid + batched product.  No gradient (the augmentation parameters are random draws)."""
+    _require_device(theta)
+    N, _, H, W = size
+    if theta.shape != (N, 2, 3) or theta.dtype != torch.float32:
+        raise ValueError(f'affine_grid: theta {tuple(theta.shape)} {theta.dtype} for size {tuple(size)}')
+    theta = theta.detach().contiguous()
+    grid = torch.empty((N, H, W, 2), device=theta.device, dtype=theta.dtype)
+    _call('nfi_aug_affine_grid', _p(theta), N, H, W, _p(grid), _stream(theta.device))
+    return grid
 
 
 def aug_sample(img, grid, copies: int, white_background: bool = False):

@@ -1,6 +1,6 @@
 """Device time of the inversion step's generic PyTorch GEMMs (mm / bmm / addmm / baddbmm / linear)
 by input shapes (GPU box), to find the small products that run on a few workgroups for long.
-Usage: python scripts/gemm_shapes_probe.py [loss] [steps]"""
+Usage: python scripts/gemm_shapes_probe.py [loss] [steps] [all]  ('all': every op, not only GEMMs)"""
 import collections
 import os
 import sys
@@ -20,6 +20,7 @@ GEMMS = ('aten::mm', 'aten::bmm', 'aten::addmm', 'aten::baddbmm', 'aten::baddbmm
 def main():
     loss = sys.argv[1] if len(sys.argv) > 1 else 'l1'
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    every = len(sys.argv) > 3 and sys.argv[3] == 'all'
     dev = torch.device('cuda:0')
     B = 4
     cfg = bench.CONFIGS['p3d_fwdbwd']
@@ -40,11 +41,11 @@ def main():
         torch.cuda.synchronize()
     agg = collections.defaultdict(lambda: [0, 0.0])
     for e in prof.key_averages(group_by_input_shape=True):
-        if e.key in GEMMS:
+        if e.key in GEMMS or (every and e.key.startswith('aten::') and e.device_time_total > 0):
             k = (e.key, str(e.input_shapes))
             agg[k][0] += e.count
             agg[k][1] += e.device_time_total
-    for (name, shapes), (cnt, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:30]:
+    for (name, shapes), (cnt, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:60 if every else 30]:
         print(f'{t / steps / 1e3:8.3f} ms/step  {cnt / steps:5.1f}/step  {name:14s} {shapes}')
 
 

@@ -151,6 +151,22 @@ def test_aug_sample_matches_grid_sample(B, H, W, white, scale):
     assert gerr <= max(1e-6 * float(gr.abs().max()), 4 * gerr32), (gerr, gerr32)
 
 
+@pytest.mark.parametrize('N,H,W', [(60, 128, 128), (3, 7, 5), (2, 1, 4), (1, 6, 1)])
+def test_affine_grid_matches_aten(N, H, W):
+    """nfi_aug_affine_grid (the augmentation's grid, run.py:749) against F.affine_grid(align_corners=
+    False) on the same device: ATen's base grid and product order, so equal to an ulp of the grid's
+    magnitude (the batched product's accumulation order is hipBLASLt's); sizes 1 included."""
+    g = torch.Generator(device=DEV).manual_seed(N * 100 + H)
+    theta = torch.randn((N, 2, 3), device=DEV, generator=g)
+    ours = producer_ops.affine_grid(theta, [N, 6, H, W])
+    ref = torch.nn.functional.affine_grid(theta, [N, 6, H, W], align_corners=False)
+    assert ours.shape == ref.shape
+    tol = 2.5e-7 * (1.0 + float(theta.abs().amax()) * 3)
+    assert float((ours - ref).abs().max()) <= tol
+    grid = inversion.augment_grid((4, 6, 16, 16), 1.0, DEV, generator=g)   # the inversion's call
+    assert grid.shape == (4, 16, 16, 2) and torch.isfinite(grid).all()
+
+
 @pytest.mark.parametrize('N,Co,H,W', [(2, 64, 16, 64), (3, 64, 32, 128), (1, 8, 48, 64)])
 def test_vgg_first_layer(N, Co, H, W):
     """The fused first VGG layer (direct 3x3 conv + bias + ReLU; backward threshold + data gradient)
