@@ -9,6 +9,10 @@ wide DS store whose data registers are rewritten within WINDOW instructions (str
 labels do not stop the scan, an unconditional branch or s_endpgm does), says whether the writer sits
 inside an inline-asm block (;;#ASMSTART .. ;;#ASMEND), and exits 1 if any is found.
 Rule 2 (lint_gpr_idx): the M0-indexed register-image regions of the tile pass.
+Rule 4 (lds_return_in_region): no LDS instruction that returns data to VGPRs may be outstanding at
+an s_set_gpr_idx_on — LDS data returning while GPR-index mode is on corrupts registers outside its
+destination (round 5: scripts/ubench/gpr_idx_probe.hip pattern 15 faults the GPU; the same with a
+global load, pattern 14, is exact).
 
 Usage: python scripts/isa_lint.py [--window N] [--keep DIR] [source.hip ...]
 (default: every nfi_*.hip in nerf-from-image_amd/csrc, compiled exactly as nfi/build.py compiles them,
@@ -171,6 +175,84 @@ def lint_gpr_idx(path: str):
     return bad
 
 
+LDS_RET = ('ds_read', 'ds_load', 'ds_bpermute', 'ds_permute', 'ds_swizzle', 'ds_consume', 'ds_append')
+
+
+def lds_return_in_region(path: str, depth: int = 600):
+    """Rule 4: for every s_set_gpr_idx_on, walk back (along the fall-through path and, at a loop
+    header, from each backward branch to it) to the wait that covers it: an LDS load issued after the
+    last s_waitcnt lgkmcnt(0) — or among the N most recent lgkm instructions before an lgkmcnt(N) —
+    may still return its data while the region's index mode is on.  Returns (kernel, line, load)."""
+    lines = open(path).read().splitlines()
+    out = []
+    # kernel bodies: (name, [(line no, kind, text)])
+    bodies, cur = [], None
+    for i, ln in enumerate(lines):
+        if re.match(r'^_Z\S+:', ln):
+            cur = (ln.split(':')[0], [])
+            bodies.append(cur)
+            continue
+        if cur is None:
+            continue
+        if ln.startswith('.Lfunc_end'):
+            cur = None
+            continue
+        m = re.match(r'^(\.LBB\w+):', ln)
+        if m:
+            cur[1].append((i + 1, 'label', m.group(1)))
+            continue
+        t = ln.split(';')[0].strip()
+        if t and not t.startswith('.') and ln.startswith('\t'):
+            cur[1].append((i + 1, 'op', t))
+    for kernel, ins in bodies:
+        if not any(k == 'op' and t.startswith('s_set_gpr_idx_on') for _, k, t in ins):
+            continue
+        labels = {t: j for j, (_, k, t) in enumerate(ins) if k == 'label'}
+        back = {}
+        for j, (_, k, t) in enumerate(ins):
+            if k == 'op':
+                m = re.match(r's_(?:cbranch_\w+|branch)\s+(\.LBB\w+)', t)
+                if m and m.group(1) in labels and labels[m.group(1)] < j:
+                    back.setdefault(labels[m.group(1)], []).append(j)
+
+        def lgkm(t):
+            return t.startswith(('ds_', 's_load', 's_buffer_load'))
+
+        for j, (lno, k, t) in enumerate(ins):
+            if k != 'op' or not t.startswith('s_set_gpr_idx_on'):
+                continue
+            stack, seen, hit = [(j - 1, 0)], set(), None
+            while stack and hit is None:
+                p, n = stack.pop()
+                while p >= 0 and n < depth and hit is None:
+                    _, kk, tt = ins[p]
+                    if kk == 'label':
+                        for b in back.get(p, []):
+                            if b not in seen:
+                                seen.add(b)
+                                stack.append((b, n))
+                        p -= 1
+                        continue
+                    if tt.startswith('s_waitcnt'):
+                        mm = re.search(r'lgkmcnt\((\d+)\)', tt)
+                        if mm:
+                            left, q = int(mm.group(1)), p - 1
+                            while left > 0 and q >= 0:
+                                if ins[q][1] == 'op' and lgkm(ins[q][2]):
+                                    left -= 1
+                                    if ins[q][2].startswith(LDS_RET):
+                                        hit = ins[q]
+                                q -= 1
+                            break
+                    if tt.startswith(LDS_RET):
+                        hit = ins[p]
+                    n += 1
+                    p -= 1
+            if hit:
+                out.append((kernel, lno, f'LDS load possibly in flight at the region: line {hit[0]} {hit[2]}'))
+    return out
+
+
 DS_ANY = re.compile(r'^\s*(ds_(?:write|read|bpermute|permute|add|swizzle)\w*)\s+(.*)$')
 
 
@@ -249,7 +331,7 @@ def main():
                   f"      -> +{x['distance']} {x['writer']}"
                   f"{'  [writer inside inline asm]' if x['writer_in_inline_asm'] else ''}")
         total += f
-        g = lint_gpr_idx(out)
+        g = lint_gpr_idx(out) + lds_return_in_region(out)
         nreg = sum(1 for ln in open(out) if 's_set_gpr_idx_on' in ln)
         print(f'{os.path.basename(s)}: {nreg} M0-indexed regions, {len(g)} violations')
         for k, ln, msg in g:
