@@ -2737,6 +2737,11 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       int3 rk[8];   /* (slot | flags, w, n) of entries hh..hh+3: b96 broadcast reads */             \
       _Pragma("unroll") for (int k = hh; k < hh + 4; ++k)                                           \
         rk[k] = *reinterpret_cast<const int3*>(G + ((U) + k) * XS + NC);                             \
+      /* consumed before any region opens: LDS data must not return under GPR-index mode (lint    \
+         rule 4) */                                                                    \
+      asm volatile("" ::"v"(rk[hh].x), "v"(rk[hh].y), "v"(rk[hh].z), "v"(rk[hh + 1].x), "v"(rk[hh + 1].y), \
+                   "v"(rk[hh + 1].z), "v"(rk[hh + 2].x), "v"(rk[hh + 2].y), "v"(rk[hh + 2].z),        \
+                   "v"(rk[hh + 3].x), "v"(rk[hh + 3].y), "v"(rk[hh + 3].z) : "memory");              \
       NFI_LDSREC_CHECK(U, hh, rk)                                                                    \
       _Pragma("unroll") for (int k = hh; k < hh + 4; ++k) NFI_LDSREC_ENTRY(rk, k);                  \
     }                                                                                                \
