@@ -1163,18 +1163,25 @@ __global__ void __launch_bounds__(256) aug_bwd_kernel(const float* __restrict__ 
     const int ylo = max((int)floorf(cy - ey), 0), yhi = min((int)ceilf(cy + ey), Ho - 1);
     const float* go = gout + j * 3 * HWo;
     for (int y = ylo; y <= yhi; ++y) {
-      for (int x = xlo; x <= xhi; ++x) {
-        const int64_t o = (int64_t)y * Wo + x;
-        const Samp s = samp_at(gj + o * 2, W, H);
-        const int dxc = X - s.x0, dyc = Y - s.y0;
-        if (dxc < 0 || dxc > 1 || dyc < 0 || dyc > 1) continue;
-        const float fx = (float)s.x0, fy = (float)s.y0;
-        const float wxv = dxc ? (s.ix - fx) : (fx + 1.f - s.ix);
-        const float wyv = dyc ? (s.iy - fy) : (fy + 1.f - s.iy);
-        const float w = wxv * wyv;
-        acc[0] += w * go[o];
-        acc[1] += w * go[HWo + o];
-        acc[2] += w * go[2 * HWo + o];
+      // four box columns per pass: their grid reads issued together (the walk is a chain of dependent
+      // grid read -> test -> gradient read; one column at a time exposes each read's latency)
+      for (int x = xlo; x <= xhi; x += 4) {
+        Samp s[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s[u] = samp_at(gj + ((int64_t)y * Wo + min(x + u, xhi)) * 2, W, H);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t o = (int64_t)y * Wo + x + u;
+          const int dxc = X - s[u].x0, dyc = Y - s[u].y0;
+          if (x + u > xhi || dxc < 0 || dxc > 1 || dyc < 0 || dyc > 1) continue;
+          const float fx = (float)s[u].x0, fy = (float)s[u].y0;
+          const float wxv = dxc ? (s[u].ix - fx) : (fx + 1.f - s[u].ix);
+          const float wyv = dyc ? (s[u].iy - fy) : (fy + 1.f - s[u].iy);
+          const float w = wxv * wyv;
+          acc[0] += w * go[o];
+          acc[1] += w * go[HWo + o];
+          acc[2] += w * go[2 * HWo + o];
+        }
       }
     }
   }
