@@ -25,3 +25,35 @@ def test_isa_lint_product_build(tmp_path):
     # the lint saw the kernels it is about (a silently empty compile would pass trivially)
     assert 'nfi_render.hip: 0 wide' not in r.stdout
     assert 'M0-indexed regions, 0 violations' in r.stdout
+
+
+def _lint_mod():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('isa_lint', os.path.join(ROOT, 'scripts', 'isa_lint.py'))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+REGION = '\ts_set_gpr_idx_on s5, gpr_idx(SRC0,DST)\n\tv_add_f32 v40, v40, v2\n\ts_set_gpr_idx_off\n'
+
+
+def test_rule4_lds_return_in_region(tmp_path):
+    """Rule 4 on synthetic assembler text: an LDS load not yet waited for when a region opens is
+    reported (straight-line, through an lgkmcnt(N) that leaves it outstanding, and around a loop's
+    back edge); one covered by lgkmcnt(0) is not."""
+    lint = _lint_mod()
+
+    def run(body):
+        p = tmp_path / 'k.s'
+        p.write_text('_Z1kv:\n' + body + '\ts_endpgm\n.Lfunc_end0:\n')
+        return lint.lds_return_in_region(str(p))
+
+    assert run('\tds_read_b32 v1, v0\n' + REGION)                                   # in flight
+    assert not run('\tds_read_b32 v1, v0\n\ts_waitcnt lgkmcnt(0)\n' + REGION)         # waited
+    assert run('\tds_read_b32 v1, v0\n\tds_read_b32 v3, v0\n\ts_waitcnt lgkmcnt(1)\n' + REGION)
+    assert not run('\tds_write_b32 v0, v1\n' + REGION)                                # a store returns nothing
+    loop = ('.LBB0_1:\n' + REGION + '\tds_read_b32 v1, v0\n\ts_cbranch_scc1 .LBB0_1\n')
+    assert run(loop)                                                                   # issued at the loop bottom
+    loop_ok = ('.LBB0_1:\n' + REGION + '\tds_read_b32 v1, v0\n\ts_waitcnt lgkmcnt(0)\n\ts_cbranch_scc1 .LBB0_1\n')
+    assert not run(loop_ok)
