@@ -2346,6 +2346,9 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 constexpr int BATCH = NFI_TILE_BATCH;
 // NFI_TILE_LDSREC 1: the entry loop takes each entry's record from the pad columns of its stage row
 // (written there with the row) instead of re-reading the list with scalar loads
+#ifndef NFI_TILE_SMEM_SAFE
+#define NFI_TILE_SMEM_SAFE 0   // 1: no scalar record load in flight across an indexed region
+#endif
 #ifndef NFI_TILE_LDSREC
 #define NFI_TILE_LDSREC 0
 #endif
@@ -2753,10 +2756,23 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     _Pragma("unroll") for (int k = 0; k < 8; ++k) gv[k] = G[stage_at((U) + k, cl)];                 \
     asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
                  "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];                \
+    NFI_RNEXT_EARLY(U, RNEXT)                                                                        \
     NFI_STEP_CHECK(U, RUSE)                                                                          \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
+    NFI_RNEXT_LATE(U, RNEXT)                                                                         \
   }
+#if NFI_TILE_SMEM_SAFE
+// the next step's records issued after this step's last region (a memory clobber keeps them there):
+// no scalar load is in flight while an indexed region is open — the next step's row wait
+// (lgkmcnt(0): scalar loads return out of order) completes them first (probe pattern 19)
+#define NFI_RNEXT_EARLY(U, RNEXT)
+#define NFI_RNEXT_LATE(U, RNEXT)                                                                     \
+    asm volatile("" ::: "memory");                                                                   \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];
+#else
+#define NFI_RNEXT_EARLY(U, RNEXT) _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];
+#define NFI_RNEXT_LATE(U, RNEXT)
+#endif
 #endif
       // Rows loaded coalesced: lane l holds float4 (l & 7) of entry 8j + (l >> 3), j = 0..6 (the
       // entry's row index comes from its lane's record by ds_bpermute): each b128 load reads 8
@@ -2870,6 +2886,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #undef NFI_LOAD_ROWC
 #undef NFI_LD1
 #undef NFI_STEP
+#undef NFI_RNEXT_EARLY
+#undef NFI_RNEXT_LATE
 #undef NFI_ENTRY
 #undef NFI_STEP_CHECK
 #undef NFI_ROW_CHECK

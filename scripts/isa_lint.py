@@ -178,7 +178,10 @@ def lint_gpr_idx(path: str):
 LDS_RET = ('ds_read', 'ds_load', 'ds_bpermute', 'ds_permute', 'ds_swizzle', 'ds_consume', 'ds_append')
 
 
-def lds_return_in_region(path: str, depth: int = 600):
+SMEM_RET = ('s_load', 's_buffer_load')
+
+
+def lds_return_in_region(path: str, depth: int = 600, smem: bool = False):
     """Rule 4: for every s_set_gpr_idx_on, walk back (along the fall-through path and, at a loop
     header, from each backward branch to it) to the wait that covers it: an LDS load issued after the
     last s_waitcnt lgkmcnt(0) — or among the N most recent lgkm instructions before an lgkmcnt(N) —
@@ -237,6 +240,10 @@ def lds_return_in_region(path: str, depth: int = 600):
                         mm = re.search(r'lgkmcnt\((\d+)\)', tt)
                         if mm:
                             left, q = int(mm.group(1)), p - 1
+                            if left and smem:   # scalar loads return out of order: only lgkmcnt(0) completes them
+                                n += 1
+                                p -= 1
+                                continue
                             while left > 0 and q >= 0:
                                 if ins[q][1] == 'op' and lgkm(ins[q][2]):
                                     left -= 1
@@ -244,12 +251,13 @@ def lds_return_in_region(path: str, depth: int = 600):
                                         hit = ins[q]
                                 q -= 1
                             break
-                    if tt.startswith(LDS_RET):
+                    if tt.startswith(LDS_RET) or (smem and tt.startswith(SMEM_RET)):
                         hit = ins[p]
                     n += 1
                     p -= 1
             if hit:
-                out.append((kernel, lno, f'LDS load possibly in flight at the region: line {hit[0]} {hit[2]}'))
+                what = 'scalar' if hit[2].startswith(SMEM_RET) else 'LDS'
+                out.append((kernel, lno, f'{what} load possibly in flight at the region: line {hit[0]} {hit[2]}'))
     return out
 
 
