@@ -9,10 +9,10 @@ wide DS store whose data registers are rewritten within WINDOW instructions (str
 labels do not stop the scan, an unconditional branch or s_endpgm does), says whether the writer sits
 inside an inline-asm block (;;#ASMSTART .. ;;#ASMEND), and exits 1 if any is found.
 Rule 2 (lint_gpr_idx): the M0-indexed register-image regions of the tile pass.
-Rule 4 (lds_return_in_region): no LDS instruction that returns data to VGPRs may be outstanding at
-an s_set_gpr_idx_on — LDS data returning while GPR-index mode is on corrupts registers outside its
-destination (round 5: scripts/ubench/gpr_idx_probe.hip pattern 15 faults the GPU; the same with a
-global load, pattern 14, is exact).
+Rule 4 (lds_return_in_region): no LDS load and no scalar load may be outstanding at an
+s_set_gpr_idx_on — data returning while GPR-index mode is on corrupts registers outside its
+destination (round 5: scripts/ubench/gpr_idx_probe.hip patterns 15 (LDS) and 19 (scalar) fault the
+GPU; the same with a global load, pattern 14, is exact).
 
 Usage: python scripts/isa_lint.py [--window N] [--keep DIR] [source.hip ...]
 (default: every nfi_*.hip in nerf-from-image_amd/csrc, compiled exactly as nfi/build.py compiles them,
@@ -339,7 +339,7 @@ def main():
                   f"      -> +{x['distance']} {x['writer']}"
                   f"{'  [writer inside inline asm]' if x['writer_in_inline_asm'] else ''}")
         total += f
-        g = lint_gpr_idx(out) + lds_return_in_region(out)
+        g = lint_gpr_idx(out) + lds_return_in_region(out, smem=True)
         nreg = sum(1 for ln in open(out) if 's_set_gpr_idx_on' in ln)
         print(f'{os.path.basename(s)}: {nreg} M0-indexed regions, {len(g)} violations')
         for k, ln, msg in g:
