@@ -9,6 +9,7 @@ wide DS store whose data registers are rewritten within WINDOW instructions (str
 labels do not stop the scan, an unconditional branch or s_endpgm does), says whether the writer sits
 inside an inline-asm block (;;#ASMSTART .. ;;#ASMEND), and exits 1 if any is found.
 Rule 2 (lint_gpr_idx): the M0-indexed register-image regions of the tile pass.
+Rule 5 (valu_sgpr_near_region): no v_readfirstlane / v_readlane shortly before a region (probes 16-18).
 Rule 4 (lds_return_in_region): no LDS load and no scalar load may be outstanding at an
 s_set_gpr_idx_on — data returning while GPR-index mode is on corrupts registers outside its
 destination (round 5: scripts/ubench/gpr_idx_probe.hip patterns 15 (LDS) and 19 (scalar) fault the
@@ -261,6 +262,64 @@ def lds_return_in_region(path: str, depth: int = 600, smem: bool = False):
     return out
 
 
+def valu_sgpr_near_region(path: str, window: int = 30):
+    """Rule 5: no VALU instruction writing an SGPR from a VGPR lane (v_readfirstlane / v_readlane)
+    within `window` instructions before an s_set_gpr_idx_on, along the fall-through path and loop back
+    edges — an index SGPR made that way gave wrong register images in a region train (probe patterns
+    16-18).  Returns (kernel, line, message)."""
+    lines = open(path).read().splitlines()
+    out, bodies, cur = [], [], None
+    for i, ln in enumerate(lines):
+        if re.match(r'^_Z\S+:', ln):
+            cur = (ln.split(':')[0], [])
+            bodies.append(cur)
+            continue
+        if cur is None:
+            continue
+        if ln.startswith('.Lfunc_end'):
+            cur = None
+            continue
+        m = re.match(r'^(\.LBB\w+):', ln)
+        if m:
+            cur[1].append((i + 1, 'label', m.group(1)))
+            continue
+        t = ln.split(';')[0].strip()
+        if t and not t.startswith('.') and ln.startswith('\t'):
+            cur[1].append((i + 1, 'op', t))
+    for kernel, ins in bodies:
+        labels = {t: j for j, (_, k, t) in enumerate(ins) if k == 'label'}
+        back = {}
+        for j, (_, k, t) in enumerate(ins):
+            if k == 'op':
+                m = re.match(r's_(?:cbranch_\w+|branch)\s+(\.LBB\w+)', t)
+                if m and m.group(1) in labels and labels[m.group(1)] < j:
+                    back.setdefault(labels[m.group(1)], []).append(j)
+        for j, (lno, k, t) in enumerate(ins):
+            if k != 'op' or not t.startswith('s_set_gpr_idx_on'):
+                continue
+            stack, seen, hit = [(j - 1, 0)], set(), None
+            while stack and hit is None:
+                p, n = stack.pop()
+                while p >= 0 and n < window:
+                    _, kk, tt = ins[p]
+                    if kk == 'label':
+                        for b in back.get(p, []):
+                            if b not in seen:
+                                seen.add(b)
+                                stack.append((b, n))
+                        p -= 1
+                        continue
+                    if tt.startswith(('v_readfirstlane', 'v_readlane')):
+                        hit = ins[p]
+                        break
+                    n += 1
+                    p -= 1
+            if hit:
+                out.append((kernel, lno, f'VALU-written SGPR {window} instructions or fewer before the region: '
+                                         f'line {hit[0]} {hit[2]}'))
+    return out
+
+
 DS_ANY = re.compile(r'^\s*(ds_(?:write|read|bpermute|permute|add|swizzle)\w*)\s+(.*)$')
 
 
@@ -339,7 +398,7 @@ def main():
                   f"      -> +{x['distance']} {x['writer']}"
                   f"{'  [writer inside inline asm]' if x['writer_in_inline_asm'] else ''}")
         total += f
-        g = lint_gpr_idx(out) + lds_return_in_region(out, smem=True)
+        g = lint_gpr_idx(out) + lds_return_in_region(out, smem=True) + valu_sgpr_near_region(out)
         nreg = sum(1 for ln in open(out) if 's_set_gpr_idx_on' in ln)
         print(f'{os.path.basename(s)}: {nreg} M0-indexed regions, {len(g)} violations')
         for k, ln, msg in g:

@@ -57,3 +57,17 @@ def test_rule4_lds_return_in_region(tmp_path):
     assert run(loop)                                                                   # issued at the loop bottom
     loop_ok = ('.LBB0_1:\n' + REGION + '\tds_read_b32 v1, v0\n\ts_waitcnt lgkmcnt(0)\n\ts_cbranch_scc1 .LBB0_1\n')
     assert not run(loop_ok)
+
+
+def test_rule5_valu_sgpr_index(tmp_path):
+    """Rule 5 on synthetic assembler text: a v_readfirstlane shortly before a region (the index path
+    probe patterns 16-18 showed unreliable) is reported, one far before it is not."""
+    lint = _lint_mod()
+
+    def run(body):
+        p = tmp_path / 'k.s'
+        p.write_text('_Z1kv:\n' + body + '\ts_endpgm\n.Lfunc_end0:\n')
+        return lint.valu_sgpr_near_region(str(p))
+
+    assert run('\tv_readfirstlane_b32 s5, v1\n\ts_and_b32 s5, s5, 31\n' + REGION)
+    assert not run('\tv_readfirstlane_b32 s5, v1\n' + '\tv_add_f32 v3, v3, v4\n' * 40 + REGION)
