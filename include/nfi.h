@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 16
+#define NFI_ABI_VERSION 17
 #define NFI_DEC_SIZE 7200   /* floats in the packed decoder buffer (11 outputs: split-f16 tables) */
 #define NFI_DEC_SIZE_VIEWDIR 14384 /* ... with the view-direction mapper (33 outputs) */
 
@@ -218,7 +218,11 @@ int64_t nfi_tile_count_size(const nfi_render_args* a);   /* = B * beams * 3 * ((
 int64_t nfi_tile_count_size_shape(int32_t B, int32_t R, int32_t H, int32_t W, int32_t N);
 /* Deterministic backward for the calling host thread (on = 1), the default atomics form (0), or
  * query only (-1); returns the previous setting (initially from the environment variable
- * NFI_DETERMINISTIC).  Deterministic: every tile's bin entries are sorted by sample index before the
+ * NFI_DETERMINISTIC).  The setting is PER HOST THREAD and is read by the thread that calls
+ * nfi_render_backward[_stage] / nfi_render_backward_workspace_bytes: a caller that sets it on one
+ * thread does not change a backward another thread runs (PyTorch autograd runs .backward() on its
+ * device thread; nfi.ops sets it there from nfi.ops.DETERMINISTIC / torch.use_deterministic_algorithms
+ * around each backward and restores that thread's previous value).  Deterministic: every tile's bin entries are sorted by sample index before the
  * tile pass and the d planes are summed from per-chunk partial tile images in a fixed order instead
  * of float atomics, so d planes (and every other output) are bitwise reproducible run to run; the
  * workspace (nfi_render_backward_workspace_bytes, which follows this setting) grows by ~40 B per

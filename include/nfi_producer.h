@@ -71,9 +71,9 @@ int32_t nfi_syn_up_conv_fir_act_forward(const float* P, const float* d, const fl
  * nfi_syn_fir_up_backward, then nfi_syn_up_conv_gather, without go and gt in memory. */
 int32_t nfi_syn_up_conv_act_backward(const float* g, const float* o, const float* d, const float* bias, float* dP,
                                      float* dd, int32_t B, int32_t C, int32_t n, float gain, void* stream);
-/* The same, also leaving the running maximum of |dP| in vmax[0..63] for the split-f16 product W9^T dP
- * (nfi_gemm_split16_shared_a; vmax[0..64] zero on entry, as nfi_wino_input_transform_max): no
- * separate maximum pass over dP. */
+/* The same, also leaving each image's running maximum of |dP| in its slots of vmax for the split-f16
+ * product W9^T dP (nfi_gemm_split16_shared_a; vmax zero on entry, as nfi_wino_input_transform_max):
+ * no separate maximum pass over dP. */
 int32_t nfi_syn_up_conv_act_backward_max(const float* g, const float* o, const float* d, const float* bias, float* dP,
                                          float* dd, uint32_t* vmax, int32_t B, int32_t C, int32_t n, float gain,
                                          void* stream);
@@ -235,32 +235,40 @@ int32_t nfi_aug_affine_grid(const float* theta, int32_t N, int32_t H, int32_t W,
  * lpips VGG16 via metrics.py:107).
  * nfi_split16_pack: A [batch][per] -> hi, lo [batch][per] (fp16 bits) and a_inv [batch] = 2^-e, with
  *   the largest |A[b]| 2^e in [2^14, 2^15) (one workgroup per batch entry; frozen operands: once).
+ * Maxima slots (b_max / vmax / slots below): NFI_SPLIT16_SLOT_WORDS uint32 (= nfi_split16_slot_words()):
+ *   image i's running maximum of |B| in words [4 (i mod 256), 4 (i mod 256) + 4) (float bits), a
+ *   completion counter in word 1024.  B's power-of-two scale is PER IMAGE, so an image's operand
+ *   precision (and result) does not depend on the other images of its batch (sharded = unsharded).
  * nfi_wino_input_transform_max: nfi_wino_input_transform_scaled (scale may be NULL) or, with relu_y,
- *   the ReLU-masked gradient transform, also leaving the running maximum of |V| in vmax[0..63] (float
- *   bits).  vmax[0..64] must hold zeros on entry: a zeroed buffer, or one a split GEMM has consumed.
- * nfi_absmax_slots: the same running maximum of any x [n] (zeroes slots[0..64] first).
- * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max[65] from one of the above,
- *   C [batch][M][N] fp32 (written); K a multiple of 32.  b_max[64] is a completion counter: the
- *   launch's last workgroup returns b_max[0..64] to zero (no memset before the next producer).  N % 4 == 0 with 16-B aligned B and C takes
- *   the wide-load kernel, else the general one (NFI_GEMM_KERNEL=1 forces the general one).
- * nfi_gemm_split16_shared_a: the same with ONE A [M][K] (and a_inv[0]) for every batch entry — the
- *   up-sampling convolutions' 9-tap weight matrix against each image (stylegan.py:99-101) — and K
- *   split in ksplit ranges when ksplit > 1 (few output tiles, long K: the data gradient W9^T dP), the
- *   partial products in work [ksplit][batch][M][N] summed in order (deterministic). */
+ *   the ReLU-masked gradient transform, also leaving each image's running maximum of |V| in its
+ *   slots.  vmax must hold zeros on entry: a zeroed buffer, or one a split GEMM has consumed.
+ * nfi_absmax_slots: the same per-image maxima of any x [nimg][per_image] (zeroes the slots first).
+ * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max from one of the above, C
+ *   [batch][M][N] fp32 (written); K a multiple of 32; column n of every B[b] belongs to image
+ *   n / cols_per_image (cols_per_image divides N; the Winograd products: tiles per image; N: one image).
+ *   The launch's last workgroup returns the used slots and the counter to zero (no memset before the
+ *   next producer).
+ * nfi_gemm_split16_shared_a: the same with ONE A [M][K] (and a_inv[0]) for every batch entry, batch
+ *   entry b being image b — the up-sampling convolutions' 9-tap weight matrix against each image
+ *   (stylegan.py:99-101) — and K split in ksplit ranges when ksplit > 1 (few output tiles, long K: the
+ *   data gradient W9^T dP), the partial products in work [ksplit][batch][M][N] summed in order
+ *   (deterministic). */
+#define NFI_SPLIT16_SLOT_WORDS 1025
+int32_t nfi_split16_slot_words(void);
 int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* Ah, uint16_t* Al, float* a_inv,
                          void* stream);
 int32_t nfi_wino_input_transform_max(const float* x, const float* scale, const float* relu_y, float* V,
                                      uint32_t* vmax, int32_t N, int32_t C, int32_t H, int32_t W, void* stream);
-int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* stream);
+int32_t nfi_absmax_slots(const float* x, int32_t nimg, int64_t per_image, uint32_t* slots, void* stream);
 int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                          const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                         void* stream);
+                         int32_t cols_per_image, void* stream);
 /* nfi_gemm_split16_ksplit: nfi_gemm_split16 with K split in ksplit ranges (few output tiles: the
  * 512-channel Winograd products at 8^2 / 16^2 maps), partials in work [ksplit][batch][M][N] summed in
  * order (deterministic). */
 int32_t nfi_gemm_split16_ksplit(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                 const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                                int32_t ksplit, float* work, void* stream);
+                                int32_t cols_per_image, int32_t ksplit, float* work, void* stream);
 int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                   const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                                   int32_t ksplit, float* work, void* stream);

@@ -141,8 +141,10 @@ __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ w
 // grid (ceil(P / 256), C).  scale (optional, [N][C]): the transform of x * scale[n][c] (the
 // modulation of the synthesis layers, stylegan.py:130, applied to the input of the convolution;
 // the transform is linear, so the per-(image, channel) factor multiplies the 36 outputs)
-// vmax (optional, 64 slots of float bits): the running maximum of |V| for the split-f16 product
-// (nfi_gemm.hip), one atomic per workgroup into slot (x + y) % 64
+// vmax (optional, the split-f16 product's per-image slots, split_slot in nfi_host.h): each image's
+// running maximum of |V| (nfi_gemm.hip).  A workgroup inside one image: one atomic; one that straddles
+// images (small maps, T < 256): the per-image maxima reduced in LDS, one atomic per image of the block
+// (per-lane global atomics measured +0.9 ms per inversion step on the LPIPS 8^2-32^2 layers).
 __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x, const float* __restrict__ scale,
                                                     const float* __restrict__ mask, float* __restrict__ V, int C,
                                                     int H, int W, int TW, int T, int64_t P,
@@ -198,13 +200,28 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
     }
   }
   if (vmax != nullptr) {
-    __shared__ float red[4];
-    m = wave_max(live ? m : 0.f);
-    if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
-    __syncthreads();
-    if (threadIdx.x == 0)
-      atomicMax(vmax + (blockIdx.x + blockIdx.y) % 64,
-                __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    m = live ? m : 0.f;
+    const int64_t pb = (int64_t)blockIdx.x * 256;
+    const int nb0 = (int)(pb / T), nb1 = (int)(min(pb + 255, P - 1) / T);
+    if (nb0 == nb1) {   // (block-uniform)
+      __shared__ float red[4];
+      m = wave_max(m);
+      if (lane_id() == 0) lds_st(red + (threadIdx.x >> 6), m);
+      __syncthreads();
+      if (threadIdx.x == 0)
+        atomicMax(vmax + split_slot(nb0, blockIdx.x + blockIdx.y),
+                  __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    } else {   // (block-uniform) the block straddles images: per-image maxima in LDS, then one
+               // global atomic per image of the block
+      __shared__ unsigned ired[257];   // images of 256 consecutive columns: at most 256 / T + 1
+      const int ni = nb1 - nb0 + 1;
+      for (int i = threadIdx.x; i < ni; i += 256) ired[i] = 0u;
+      __syncthreads();
+      if (m > 0.f) atomicMax(ired + (n - nb0), __float_as_uint(m));
+      __syncthreads();
+      for (int i = threadIdx.x; i < ni; i += 256)
+        if (ired[i] != 0u) atomicMax(vmax + split_slot(nb0 + i, blockIdx.y), ired[i]);
+    }
   }
 }
 

@@ -9,10 +9,14 @@
 // (3 2^-22 |a||b| per product at worst, below the K 2^-24 accumulation bound for K >= 12; K here is
 // the channel count, 64..512).  Scales: A (frozen Winograd weights U) per batch entry, computed once
 // when A is split (nfi_split16_pack: largest |A[b]| to [2^14, 2^15)); B (the input transform V) one
-// scale for the whole call, from the running maximum the input transform leaves in 64 slots
-// (nfi_wino_input_transform_max; slots combined in the prologue).  An operand 2^-k below its scale's
-// maximum is exact to 2^-(39-k) of itself — fp32-level to k ~ 15 and, beyond, below the Winograd
-// transform's own rounding (a few 1e-6 of the largest output, tests/test_gpu_conv.py).
+// scale PER IMAGE, from the running maxima its producer leaves in that image's slots (split_slot,
+// nfi_common.h; nfi_wino_input_transform_max, nfi_absmax_slots): column n of B[b] belongs to image
+// n / cols_per_image (the Winograd products: the image's tiles), or to image b (shared-A products: one
+// image per batch entry).  Each thread splits its own column with its image's scale and the epilogue
+// unscales per column, so an image's result does not depend on the other images of its batch (a
+// sharded run gives each image the operand precision of the unsharded one).  An operand 2^-k below its
+// image's maximum is exact to 2^-(39-k) of itself — fp32-level to k ~ 15 and, beyond, below the
+// Winograd transform's own rounding (a few 1e-6 of the largest output, tests/test_gpu_conv.py).
 //
 // Tiling: a 256-thread workgroup computes a 128 x 128 tile of C, each wave 64 x 64 (4 x 4 blocks of
 // 16 x 16, 16 accumulators of 4 floats); K in steps of 32 (one f16 MFMA deep).  Per step the
@@ -24,8 +28,8 @@
 // (scripts/gemm_bench.py, profiles/r04_gemm_bench.log): 256 x 128 / 128 x 256 tiles of 8 waves
 // (NFI_GEMM_TILE=42 / 24) 0-50 % slower, 2 x 2 waves of 128 x 128 (NFI_GEMM_TILE=88: half the LDS
 // operand bytes per MFMA, 256 accumulation registers, one wave per SIMD) 20-100 % slower, two register
-// stages of prefetch (NFI_GEMM_PF=2: occupancy 2) 0-15 % slower, the wide-load kernel
-// (NFI_GEMM_KERNEL=2) 5-25 % slower; 200-256 TFLOP/s
+// stages of prefetch (NFI_GEMM_PF=2: occupancy 2) 0-15 % slower, a wide-load kernel (8 x 4 B blocks
+// per thread, removed in round 6) 5-25 % slower; 200-256 TFLOP/s
 // fp32-equivalent on the 256-512-channel Winograd shapes, 2x hipBLASLt's fp32 bmm.
 #include <algorithm>
 #include <cstdlib>
@@ -44,7 +48,6 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int BM = 128, BN = 128, BK = 32;
 constexpr int LDK = BK + 8;                    // halves per LDS row (80 B)
 constexpr int TILE_H = BM * LDK;               // halves per operand image (A and B^T: BM == BN)
-constexpr int SLOTS = 64;                      // running-maximum slots of B
 
 __device__ __forceinline__ f4v mfma_h(u4v a, u4v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
@@ -92,29 +95,44 @@ struct Args {
   const unsigned short* Al;
   const float* a_inv;         // [batch]
   const float* B;             // [batch][K][N]
-  const unsigned* b_max;      // [SLOTS] running maxima of |B| (float bits)
+  const unsigned* b_max;      // [SPLIT_SLOTS + 1] per-image running maxima of |B| (float bits) + counter
   float* C;                   // [batch][M][N]
   int M, N, K;
   int a_shared;               // 1: one A (and scale) for every batch entry
   int ksplit, kchunk;         // (general kernel) K in ksplit ranges of kchunk: blockIdx.z = b ksplit + s,
   float* work;                //   range s's partial C to work[s][b][M][N] when ksplit > 1
   int xcd;                    // 1: XCD-major tile order (below)
+  int cpi;                    // columns per image (image of column n: n / cpi; a_shared: image b)
+  int nslot;                  // slots the last workgroup returns to zero (images used x SPLIT_ISLOTS)
 };
 
-// The B maxima are consumed, not copied: b_max[0..63] (float bits) + b_max[64] (a completion counter)
-// return to zero when the launch's last workgroup finishes, so the producer of the next maxima needs
-// no memset launch.  Every workgroup read b_max at its start, before its first barrier; the one whose
-// increment completes the count runs after all of those reads.  Relaxed atomics, no fence: a
-// release fence at agent scope writes back the L2 (measured: the inversion step 16 -> 20 ms).
-__device__ __forceinline__ void release_slots(const unsigned* b_max) {
+// B's scale for one image: the largest of its slots
+__device__ __forceinline__ void image_scale(const unsigned* b_max, int img, float& s, float& inv) {
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < SPLIT_ISLOTS; ++j) m = fmaxf(m, __uint_as_float(b_max[split_slot(img, j)]));
+  pow2_scale15(m, s, inv);
+}
+
+// The B maxima are consumed, not copied: the used slots of b_max (float bits) + b_max[SPLIT_SLOTS] (a
+// completion counter) return to zero when the launch's last workgroup finishes, so the producer of the
+// next maxima needs no memset launch.  Every workgroup read b_max at its start, before its first
+// barrier; the one whose increment completes the count runs after all of those reads.  Relaxed
+// atomics, no fence: a release fence at agent scope writes back the L2 (measured: the inversion step
+// 16 -> 20 ms).
+__device__ __forceinline__ void release_slots(const unsigned* b_max, int nslot) {
+  __shared__ int last;
   __syncthreads();
+  unsigned* bm = const_cast<unsigned*>(b_max);
   if (threadIdx.x == 0) {
-    unsigned* bm = const_cast<unsigned*>(b_max);
     const unsigned total = gridDim.x * gridDim.y * gridDim.z;
-    if (__hip_atomic_fetch_add(bm + SLOTS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-      for (int i = 0; i < SLOTS; ++i) __hip_atomic_store(bm + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(bm + SLOTS, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    last = __hip_atomic_fetch_add(bm + SPLIT_SLOTS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1;
+  }
+  __syncthreads();
+  if (last) {
+    for (int i = threadIdx.x; i < nslot; i += blockDim.x)
+      __hip_atomic_store(bm + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(bm + SPLIT_SLOTS, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -158,13 +176,7 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
   const int m0 = by * TBM, n0 = bx * TBN;
   const int M = g.M, N = g.N, K = g.K;
   const int kbeg = ks * g.kchunk, kend = min(K, kbeg + g.kchunk);
-  // B's scale: the maximum over the input transform's slots
-  float bm = __uint_as_float(g.b_max[l]);
-  bm = wave_max(bm);
-  float sb, isb;
-  pow2_scale15(bm, sb, isb);
   const int ba = g.a_shared ? 0 : b;
-  const float out_scale = g.a_inv[ba] * isb;
 
   const unsigned short* Ahg = g.Ah + (long long)ba * M * K;
   const unsigned short* Alg = g.Al + (long long)ba * M * K;
@@ -178,6 +190,11 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
   const int bn = tid % TBN, bk = (tid / TBN) * KB;
   const int bcol = min(n0 + bn, N - 1);
   const bool b_ok = n0 + bn < N;
+  // B's scale: this thread's column's image; the epilogue unscales each column by its own
+  __shared__ float col_scale[TBN];
+  float sb, isb;
+  image_scale(g.b_max, g.a_shared ? b : bcol / g.cpi, sb, isb);
+  if (tid < TBN) col_scale[bn] = g.a_inv[ba] * isb;   // (read after the K loop's barriers)
   u4v RA[PF][2 * CA];
   float RB[PF][KB];
   auto load = [&](int k0, u4v (&ra)[2 * CA], float (&rb)[KB]) {
@@ -281,143 +298,10 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
 #pragma unroll
       for (int y = 0; y < RY; ++y) {
         const int n = n0 + 16 * RY * wn + 16 * y + i16;
-        if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * out_scale;
+        if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * col_scale[n - n0];
       }
     }
-  release_slots(g.b_max);
-}
-
-// ---- the product, N % 4 == 0: wide loads and stores ----------------------------------------------
-// 128 x 128 tile, K in steps of 64 (two f16 MFMAs deep): per step the workgroup stages A's hi / lo rows
-// (32 KB, each thread one half-row: 4 + 4 b128 loads) and B's 64 x 128 fp32 slab (each thread an
-// 8 (k) x 4 (n) block: 8 float4 loads, 512-B row segments per wave; split in registers and written as
-// four B^T rows of 8 consecutive k, one b128 store per row and half — lanes 0..7 of a store take the
-// 8 k-groups of one row: distinct banks).  72-half (144-B) LDS rows: the 16 rows an MFMA operand
-// read spans start on 16 distinct 4-bank groups.  The products run as C^T = B^T A^T, so a lane's
-// accumulator holds 4 consecutive columns of one row of C: float4 stores.  74 KB of LDS, two
-// workgroups per CU; K % 64 == 32 runs a zero-padded last step.
-constexpr int BK4 = 64;
-constexpr int LK4 = BK4 + 8;
-constexpr int IMG4 = 128 * LK4;
-
-__global__ void __launch_bounds__(256, 2) split16_gemm4_kernel(Args g) {
-  __shared__ __attribute__((aligned(16))) unsigned short lds[4 * IMG4];   // A hi, A lo, Bt hi, Bt lo
-  unsigned short* Ahs = lds;
-  unsigned short* Als = lds + IMG4;
-  unsigned short* Bhs = lds + 2 * IMG4;
-  unsigned short* Bls = lds + 3 * IMG4;
-  const int tid = threadIdx.x, l = lane_id(), wv = tid >> 6;
-  const int b = blockIdx.z;
-  const int m0 = blockIdx.y * 128, n0 = blockIdx.x * 128;
-  const int M = g.M, N = g.N, K = g.K;
-  float bm = __uint_as_float(g.b_max[l]);
-  bm = wave_max(bm);
-  float sb, isb;
-  pow2_scale15(bm, sb, isb);
-  const int ba = g.a_shared ? 0 : b;
-  const float out_scale = g.a_inv[ba] * isb;
-
-  const unsigned short* Ahg = g.Ah + (long long)ba * M * K;
-  const unsigned short* Alg = g.Al + (long long)ba * M * K;
-  const float* Bg = g.B + (long long)b * K * N;
-
-  // A: row ar, halves 32 ah2 .. +31 of the step; B: rows 8 k8 .. +7 of the step, columns 4 n4 .. +3
-  const int ar = tid >> 1, ah2 = tid & 1;
-  const int arow = min(m0 + ar, M - 1);
-  const bool a_ok = m0 + ar < M;
-  const int k8 = l & 7, n4 = 8 * wv + (l >> 3);
-  const int bcol = n0 + 4 * n4;
-  const bool b_ok = bcol < N;
-  const int bc = min(bcol, N - 4);
-  u4v ra[8];
-  f4v rb[8];
-  auto load = [&](int k0) {
-    const long long ao = (long long)arow * K + min(k0 + 32 * ah2, K - 32);
-    const u4v* ph = reinterpret_cast<const u4v*>(Ahg + ao);
-    const u4v* pl = reinterpret_cast<const u4v*>(Alg + ao);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ra[j] = ph[j];
-      ra[4 + j] = pl[j];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) rb[i] = *reinterpret_cast<const f4v*>(Bg + (long long)min(k0 + 8 * k8 + i, K - 1) * N + bc);
-  };
-  auto store = [&](int k0) {
-    const u4v z = {0u, 0u, 0u, 0u};
-    const bool al = a_ok && k0 + 32 * ah2 < K;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lds_st_fenced(reinterpret_cast<u4v*>(Ahs + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[j] : z);
-      lds_st_fenced(reinterpret_cast<u4v*>(Als + ar * LK4 + 32 * ah2 + 8 * j), al ? ra[4 + j] : z);
-    }
-    const bool bl = b_ok && k0 + 8 * k8 < K;   // (K % 32 == 0: a k-group is all in or all out)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      u4v hv, lv;
-#pragma unroll
-      for (int i = 0; i < 8; i += 2) {
-        const float v0 = bl ? rb[i][c] * sb : 0.f, v1 = bl ? rb[i + 1][c] * sb : 0.f;
-        const unsigned short h0 = h_bits(v0), h1 = h_bits(v1);
-        const unsigned short l0 = h_bits(v0 - h_val(h0)), l1 = h_bits(v1 - h_val(h1));
-        hv[i >> 1] = (unsigned)h0 | ((unsigned)h1 << 16);
-        lv[i >> 1] = (unsigned)l0 | ((unsigned)l1 << 16);
-      }
-      lds_st_fenced(reinterpret_cast<u4v*>(Bhs + (4 * n4 + c) * LK4 + 8 * k8), hv);
-      lds_st_fenced(reinterpret_cast<u4v*>(Bls + (4 * n4 + c) * LK4 + 8 * k8), lv);
-    }
-  };
-
-  // wave (wm, wn): rows 64 wm.., columns 64 wn.. of the tile; acc[y][x] = (C^T) block (n block y,
-  // m block x): lane (i16, kg) holds C[64 wm + 16 x + i16][64 wn + 16 y + 4 kg + r]
-  const int wm = wv >> 1, wn = wv & 1;
-  const int i16 = l & 15, kg = l >> 4;
-  f4v acc[4][4];
-#pragma unroll
-  for (int y = 0; y < 4; ++y)
-#pragma unroll
-    for (int x = 0; x < 4; ++x) acc[y][x] = f4v{0.f, 0.f, 0.f, 0.f};
-
-  load(0);
-  for (int k0 = 0; k0 < K; k0 += BK4) {
-    store(k0);
-    __syncthreads();
-    if (k0 + BK4 < K) load(k0 + BK4);   // in flight during this step's products
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      u4v bh[4], bl[4];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int r = (64 * wn + 16 * y + i16) * LK4 + 32 * s + 8 * kg;
-        bh[y] = *reinterpret_cast<const u4v*>(Bhs + r);
-        bl[y] = *reinterpret_cast<const u4v*>(Bls + r);
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int r = (64 * wm + 16 * x + i16) * LK4 + 32 * s + 8 * kg;
-        const u4v ah = *reinterpret_cast<const u4v*>(Ahs + r);
-        const u4v al = *reinterpret_cast<const u4v*>(Als + r);
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-          acc[y][x] = mfma_h(bl[y], ah, acc[y][x]);   // small terms first
-          acc[y][x] = mfma_h(bh[y], al, acc[y][x]);
-          acc[y][x] = mfma_h(bh[y], ah, acc[y][x]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  float* Cg = g.C + (long long)b * M * N;
-#pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    const int m = m0 + 64 * wm + 16 * x + i16;
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const int n = n0 + 64 * wn + 16 * y + 4 * kg;
-      if (m < M && n < N) *reinterpret_cast<f4v*>(Cg + (long long)m * N + n) = acc[y][x] * out_scale;
-    }
-  }
-  release_slots(g.b_max);
+  release_slots(g.b_max, g.nslot);
 }
 
 // C = sum over s of work[s] (fixed order: deterministic), float4 per thread
@@ -430,19 +314,20 @@ __global__ void __launch_bounds__(256) ksum_kernel(const float* __restrict__ wor
   reinterpret_cast<f4v*>(C)[i] = a;
 }
 
-// running maximum of |x| over n floats into the 64 slots (generic callers; the Winograd input
-// transform keeps its own, nfi_conv.hip)
-__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ x, long long n,
+// running maximum of |x| per image, x [nimg][per], into the images' slots (generic callers; the
+// Winograd input transform keeps its own, nfi_conv.hip).  grid (blocks per image, nimg)
+__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ x, long long per,
                                                      unsigned* __restrict__ slots) {
   __shared__ float red[4];
+  const float* xi = x + (long long)blockIdx.y * per;
   float m = 0.f;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-    m = fmaxf(m, fabsf(x[i]));
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < per; i += (long long)gridDim.x * 256)
+    m = fmaxf(m, fabsf(xi[i]));
   m = wave_max(m);
   if (lane_id() == 0) lds_st_fenced(red + (threadIdx.x >> 6), m);
   __syncthreads();
   if (threadIdx.x == 0)
-    atomicMax(slots + blockIdx.x % SLOTS, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+    atomicMax(slots + split_slot(blockIdx.y, blockIdx.x), __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 }  // namespace gemm
@@ -462,27 +347,33 @@ int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* A
   return NFI_OK;
 }
 
-int32_t nfi_absmax_slots(const float* x, int64_t n, uint32_t* slots, void* stream) {
-  NFI_REQUIRE(x && slots && n > 0, "absmax_slots: bad arguments");
-  NFI_REQUIRE(hipMemsetAsync(slots, 0, (gemm::SLOTS + 1) * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
-  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(gemm::absmax_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long long)n,
-                     slots);
+static_assert(NFI_SPLIT16_SLOT_WORDS == SPLIT_SLOTS + 1, "include/nfi_producer.h slot words");
+int32_t nfi_split16_slot_words(void) { return SPLIT_SLOTS + 1; }
+
+int32_t nfi_absmax_slots(const float* x, int32_t nimg, int64_t per_image, uint32_t* slots, void* stream) {
+  NFI_REQUIRE(x && slots && nimg > 0 && nimg <= 65535 && per_image > 0, "absmax_slots: bad arguments");
+  NFI_REQUIRE(hipMemsetAsync(slots, 0, (SPLIT_SLOTS + 1) * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
+  const long long blocks = std::max<long long>(1, std::min<long long>((per_image + 255) / 256, 4096 / nimg));
+  hipLaunchKernelGGL(gemm::absmax_kernel, dim3((unsigned)blocks, (unsigned)nimg), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)per_image, slots);
   NFI_CHECK_LAUNCH("absmax_kernel");
   return NFI_OK;
 }
 
 static int32_t gemm_split16_impl(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                  const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                                 int a_shared, int32_t ksplit, float* work, void* stream) {
+                                 int32_t cpi, int a_shared, int32_t ksplit, float* work, void* stream) {
   NFI_REQUIRE(Ah && Al && a_inv && B && b_max && C, "gemm_split16: null pointer");
+  NFI_REQUIRE(a_shared || (cpi > 0 && N % cpi == 0), "gemm_split16: cols_per_image=%d must divide N=%d", cpi, N);
   NFI_REQUIRE(batch > 0 && batch <= 65535 && M > 0 && N > 0 && K > 0 && K % gemm::BK == 0,
               "gemm_split16: bad shape batch=%d M=%d N=%d K=%d (K a multiple of %d)", batch, M, N, K, gemm::BK);
   NFI_REQUIRE((long long)M * K < (1ll << 31) && (long long)K * N < (1ll << 31) && (long long)M * N < (1ll << 31),
               "gemm_split16: matrix too large");
   NFI_REQUIRE(((uintptr_t)Ah & 15) == 0 && ((uintptr_t)Al & 15) == 0, "gemm_split16: A halves must be 16-B aligned");
   gemm::Args g{reinterpret_cast<const unsigned short*>(Ah), reinterpret_cast<const unsigned short*>(Al), a_inv, B,
-               b_max, C, M, N, K, a_shared, 1, K, nullptr, 1};
+               b_max, C, M, N, K, a_shared, 1, K, nullptr, 1, a_shared ? N : cpi, 0};
+  const int nimg = a_shared ? batch : N / cpi;
+  g.nslot = std::min(nimg, SPLIT_IMAGES) * SPLIT_ISLOTS;
   // XCD-major tile order where a row of tiles is short (<= 8 column blocks: the 512-channel layers'
   // products, 5-12 % faster); the long rows of the large maps stream better in linear order (3-6 %,
   // profiles/r04_gemm_bench.log).  NFI_GEMM_XCD=0/1 forces it (A/B).
@@ -521,10 +412,6 @@ static int32_t gemm_split16_impl(const uint16_t* Ah, const uint16_t* Al, const f
       default: hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::split16_gemm_kernel<2, 2, 1>), gr, dim3(256), 0, (hipStream_t)stream, g); break;
     }
   };
-  // (NFI_GEMM_KERNEL=2: the wide-load kernel where it applies — measured slower than the general one
-  //  on every Winograd shape, scripts/gemm_bench.py — kept for A/B)
-  const char* fe = getenv("NFI_GEMM_KERNEL");
-  const int forced = fe ? atoi(fe) : 0;
   if (ksplit > 1) {   // K ranges of whole steps, partials summed in order
     const int steps = K / gemm::BK;
     // ranges of ceil(steps / ksplit) steps, and only as many ranges as that covers: no range is
@@ -544,10 +431,6 @@ static int32_t gemm_split16_impl(const uint16_t* Ah, const uint16_t* Al, const f
     hipLaunchKernelGGL(gemm::ksum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, work, C,
                        n4, ksplit);
     NFI_CHECK_LAUNCH("ksum_kernel");
-  } else if (N % 4 == 0 && forced == 2 && ((uintptr_t)B & 15) == 0 && ((uintptr_t)C & 15) == 0) {
-    const dim3 g4((unsigned)((N + 127) / 128), (unsigned)((M + 127) / 128), (unsigned)batch);
-    hipLaunchKernelGGL(gemm::split16_gemm4_kernel, g4, dim3(256), 0, (hipStream_t)stream, g);
-    NFI_CHECK_LAUNCH("split16_gemm4_kernel");
   } else {
     general(grid);
     NFI_CHECK_LAUNCH("split16_gemm_kernel");
@@ -562,29 +445,29 @@ static int32_t gemm_split16_impl(const uint16_t* Ah, const uint16_t* Al, const f
 // (tests/test_gpu_gemm.py::test_maxima_slots_back_to_back_and_after_rejection).
 static int32_t gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                             const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                            int a_shared, int32_t ksplit, float* work, void* stream) {
-  const int32_t rc = gemm_split16_impl(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, a_shared, ksplit, work, stream);
+                            int32_t cpi, int a_shared, int32_t ksplit, float* work, void* stream) {
+  const int32_t rc = gemm_split16_impl(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, cpi, a_shared, ksplit, work, stream);
   if (rc != NFI_OK && b_max)
-    (void)hipMemsetAsync(const_cast<uint32_t*>(b_max), 0, (gemm::SLOTS + 1) * sizeof(uint32_t), (hipStream_t)stream);
+    (void)hipMemsetAsync(const_cast<uint32_t*>(b_max), 0, (SPLIT_SLOTS + 1) * sizeof(uint32_t), (hipStream_t)stream);
   return rc;
 }
 
 int32_t nfi_gemm_split16(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                          const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                         void* stream) {
-  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 0, 1, nullptr, stream);
+                         int32_t cols_per_image, void* stream) {
+  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, cols_per_image, 0, 1, nullptr, stream);
 }
 
 int32_t nfi_gemm_split16_ksplit(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                 const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
-                                int32_t ksplit, float* work, void* stream) {
-  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 0, ksplit, work, stream);
+                                int32_t cols_per_image, int32_t ksplit, float* work, void* stream) {
+  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, cols_per_image, 0, ksplit, work, stream);
 }
 
 int32_t nfi_gemm_split16_shared_a(const uint16_t* Ah, const uint16_t* Al, const float* a_inv, const float* B,
                                   const uint32_t* b_max, float* C, int32_t batch, int32_t M, int32_t N, int32_t K,
                                   int32_t ksplit, float* work, void* stream) {
-  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 1, ksplit, work, stream);
+  return gemm_split16(Ah, Al, a_inv, B, b_max, C, batch, M, N, K, 0, 1, ksplit, work, stream);
 }
 
 }  // extern "C"

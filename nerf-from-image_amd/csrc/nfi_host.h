@@ -1,4 +1,5 @@
-// Host-side helpers shared by the C-ABI entry points (error reporting, launch checks).
+// Helpers shared by the C-ABI entry points (error reporting, launch checks) and the split-f16
+// product's slot layout (used by its producers in three sources).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
@@ -8,6 +9,14 @@
 
 namespace nfi {
 void set_error(const char* fmt, ...);
+// Running-maximum slots of the split-f16 product's B operand (nfi_gemm.hip), PER IMAGE: image i's
+// maximum of |B| lives in slots [i mod SPLIT_IMAGES][0..SPLIT_ISLOTS) (float bits, atomicMax'ed by
+// its producer), the completion counter at [SPLIT_SLOTS].  One power-of-two scale per image, so an
+// image's operand precision never depends on the other images of its batch (include/nfi_producer.h).
+constexpr int SPLIT_IMAGES = 256, SPLIT_ISLOTS = 4, SPLIT_SLOTS = SPLIT_IMAGES * SPLIT_ISLOTS;
+__host__ __device__ __forceinline__ int split_slot(int img, int j) {
+  return (img & (SPLIT_IMAGES - 1)) * SPLIT_ISLOTS + (j & (SPLIT_ISLOTS - 1));
+}
 }
 
 #define NFI_REQUIRE(cond, ...)        \

@@ -227,8 +227,8 @@ __device__ __forceinline__ void gather_features(const PlaneView& pv, const Point
 // the plane its bilinear cell lies in, and a workgroup sums a chunk of one tile's entries in
 // REGISTERS: lane (h, c) of a wave holds channel c of texel rows ly + h of the tile's 8x5 texels
 // as a 32-float vector (half h = 1 stores row y at slot y - 1, so an entry's two rows sit at the
-// same wave-uniform slot ly*8 + lx in both halves), updated through M0-indexed VGPR moves
-// (s_set_gpr_idx).  No LDS atomics (gfx950 ds_add_f32: ~200 cycles per wave-instruction per CU)
+// same wave-uniform slot ly*8 + lx in both halves), updated through a wave-uniform jump table of
+// static-register FMAs (tile_entry).  No LDS atomics (gfx950 ds_add_f32: ~200 cycles per wave-instruction per CU)
 // and no LDS read-modify-write chain; the waves' images are merged once through LDS and flushed
 // with one global float atomic per nonzero texel channel.
 //
@@ -2200,6 +2200,7 @@ __global__ void __launch_bounds__(256) chunk_map_kernel(const int* __restrict__ 
 // at a time; the entry is copied to its rank.  O(CHUNK n / 256) per chunk of an n-entry tile — a
 // reproducibility mode, not the product path.
 constexpr int DET_PER = CHUNK / 256;
+static_assert(CHUNK % 256 == 0 && CHUNK >= 256, "det_sort_kernel ranks CHUNK / 256 entries per thread");
 __global__ void __launch_bounds__(256) det_sort_kernel(const int4* __restrict__ list, const int* __restrict__ offsets,
                                                        const int* __restrict__ chunk_start,
                                                        const int* __restrict__ chunk_tile, const int* __restrict__ meta,
@@ -2344,174 +2345,54 @@ typedef const __attribute__((address_space(4))) iv4* cint4_p;
 #define NFI_TILE_BATCH 56
 #endif
 constexpr int BATCH = NFI_TILE_BATCH;
-// NFI_TILE_LDSREC 1: the entry loop takes each entry's record from the pad columns of its stage row
-// (written there with the row) instead of re-reading the list with scalar loads
-#ifndef NFI_TILE_SMEM_SAFE
-#define NFI_TILE_SMEM_SAFE 1   // 0: the next records issued before the step's regions (round-5 form, 9 % faster tile pass)
-#endif
-#ifndef NFI_TILE_LDSREC
-#define NFI_TILE_LDSREC 0
-#endif
-static_assert(XS >= NC + 4, "the stage rows' pad holds a record");
 constexpr int TROWS = BATCH * XS;   // floats per wave
 __device__ __forceinline__ int stage_at(int u, int c) { return u * XS + c; }
 __device__ __forceinline__ int stage_q(int u, int k) { return u * XS + 4 * k; }
 // the tile's 8x5 plane texels x 32 channels (pose gradients), texel rows of XS floats (per-lane
 // b128 reads of different texels conflict only for texels 16 slots apart); a tile row of 8
-// texels is TEXR floats (NFI_TEX_ROW_PAD floats after each row: the layout experiment of round 4)
-#ifndef NFI_TEX_ROW_PAD
-#define NFI_TEX_ROW_PAD 0
-#endif
-constexpr int TEXR = TTX * XS + NFI_TEX_ROW_PAD;
+// texels is TEXR floats
+constexpr int TEXR = TTX * XS;
 constexpr int TEXF = TTY * TEXR;                // 1,440 floats
 __device__ __forceinline__ int tex_at(int texel) { return (texel / TTX) * TEXR + (texel % TTX) * XS; }
 // (the wave images are dumped over the stages and texels at the end of a chunk: >= 4 x 2,048)
 constexpr int TILE_LDS = (4 * TROWS + TEXF > 4 * 2048) ? 4 * TROWS + TEXF : 4 * 2048;   // 38,016 B at BATCH 56
 
-// img[slot] += a0, img[slot + 1] += a1 for a wave-uniform slot: M0-indexed source AND
-// destination (s_set_gpr_idx_on SRC0|DST), one v_add per element.  The image is pinned to
-// v[40:71] at these points so the asm can name its base register.
-__device__ __forceinline__ void img_add(img32& img, int slot, float a0, float a1) {
-  slot = min(slot, 30);   // (cells are slots 0..30; never index past v71, whatever the record)
-#if defined(NFI_ABLATE) && NFI_ABLATE == 1
-  img[0] += a0 + a1 + (float)slot;   // experiment: no indexed update
-  return;
-#endif
-#ifdef NFI_IMG_NATIVE
-  img[slot] += a0;       // experiment: the compiler's indirect register addressing
-  img[slot + 1] += a1;
-  return;
-#endif
-  asm volatile(
-      "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
-      "v_add_f32 v40, v40, %2\n\t"
-      "v_add_f32 v41, v41, %3\n\t"
-      "s_set_gpr_idx_off"
-      : "+{v[40:71]}"(img)
-      : "s"(slot), "v"(a0), "v"(a1)
-      : "m0");   // s_set_gpr_idx_on writes the index into M0.  M0 is reserved in LLVM's AMDGPU
-                 // backend (hence the compiler's note on this clobber): it materialises M0 right
-                 // before each instruction that reads it and keeps nothing live in it across
-                 // statements (this file's code uses M0 nowhere else: checked in the ISA dump)
-}
-
-// One entry: run-merge into (a0, a1) while the cell repeats, else flush to the image.
-#ifndef NFI_TILE_AB
-#define NFI_TILE_AB 1
-#endif
-#if NFI_TILE_AB == 1
-// A run of one cell is kept as (A, B) = (sum gw, sum gw w): the texel x0 gets A - B, x0 + 1 gets B
-// when the run ends.  Per entry 4 VALU (the row weight, gw, A, B with w read from its SGPR) instead of
-// building the (1 - w, w) register pair for a packed fma each time (6).
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff) {
+// One entry into the register image: img[slot] += gw (1 - w), img[slot + 1] += gw w, for a
+// wave-uniform slot (0..30), through a wave-uniform JUMP TABLE — 31 static cases, one per slot, each
+// two VOP2 v_fmac_f32 on fixed registers of the image (pinned to v[40:71] so the cases can name them),
+// a branch to the common exit and padding to 16 B.  The case address is PC-relative: s_getpc_b64 +
+// slot * 16 + the table's offset (an assembler-resolved label difference, s_lshl4_add_u32), then
+// s_setpc_b64.  No GPR-index mode (s_set_gpr_idx_on) and no M0: register writes returning from loads
+// in flight are never redirected (round 5 measured that hazard class under index mode).
+// Per entry: gw, 1 - w and the case's two FMAs (5 VALU) plus one table jump, whatever the cell
+// sequence; scripts/isa_lint.py rule 6 checks every table of the build against its slot registers.
+// (y-weights: half 0 of the wave holds texel row ly with weight 1 - n, half 1 row ly + 1 with n.)
+__device__ __forceinline__ void tile_entry(img32& img, int slot, float w, float nn, float g, float wsgn,
+                                           float woff) {
   const float gw = g * fmaf(nn, wsgn, woff);
-  if (slot != cur) {
-    img_add(img, cur, a0 - a1, a1);
-    a0 = 0.f;
-    a1 = 0.f;
-    cur = slot;
-  }
-  a0 += gw;
-  a1 = fmaf(gw, w, a1);
-}
-#define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0 - a1, a1)
-#elif NFI_TILE_AB == 2
-// Every entry straight into the register image, no run merging and no branch: per entry the row
-// weight, gw, 1 - w and two M0-indexed FMAs (SRC2 | DST indexed: img[slot] += gw (1 - w),
-// img[slot + 1] += gw w) — 5 VALU + 4 SALU whatever the cell sequence.
-__device__ __forceinline__ void img_fma2(img32& img, int slot, float gw, float omw, float w) {
-  slot = min(slot, 30);
+  const float omw = 1.f - w;
+  slot = min((unsigned)slot, 30u);   // (cells are slots 0..30; never leave the table, whatever the record)
+#define NFI_JF(D0, D1) "v_fmac_f32 v" #D0 ", %2, %3\n\tv_fmac_f32 v" #D1 ", %4, %2\n\ts_branch 3f\n\ts_nop 0\n\t"
   asm volatile(
-      "s_set_gpr_idx_on %1, gpr_idx(SRC2,DST)\n\t"
-      "v_fma_f32 v40, %2, %3, v40\n\t"
-      "v_fma_f32 v41, %2, %4, v41\n\t"
-      "s_set_gpr_idx_off"
+      "s_getpc_b64 s[88:89]\n"
+      "1:\n\t"
+      "s_lshl4_add_u32 s90, %1, 2f-1b\n\t"
+      "s_add_u32 s88, s88, s90\n\t"
+      "s_addc_u32 s89, s89, 0\n\t"
+      "s_setpc_b64 s[88:89]\n"
+      "2:\n\t"
+      NFI_JF(40, 41) NFI_JF(41, 42) NFI_JF(42, 43) NFI_JF(43, 44) NFI_JF(44, 45) NFI_JF(45, 46)
+      NFI_JF(46, 47) NFI_JF(47, 48) NFI_JF(48, 49) NFI_JF(49, 50) NFI_JF(50, 51) NFI_JF(51, 52)
+      NFI_JF(52, 53) NFI_JF(53, 54) NFI_JF(54, 55) NFI_JF(55, 56) NFI_JF(56, 57) NFI_JF(57, 58)
+      NFI_JF(58, 59) NFI_JF(59, 60) NFI_JF(60, 61) NFI_JF(61, 62) NFI_JF(62, 63) NFI_JF(63, 64)
+      NFI_JF(64, 65) NFI_JF(65, 66) NFI_JF(66, 67) NFI_JF(67, 68) NFI_JF(68, 69) NFI_JF(69, 70)
+      NFI_JF(70, 71)
+      "3:"
       : "+{v[40:71]}"(img)
       : "s"(slot), "v"(gw), "v"(omw), "s"(w)
-      : "m0");
+      : "s88", "s89", "s90", "scc");
+#undef NFI_JF
 }
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff) {
-  const float gw = g * fmaf(nn, wsgn, woff);
-  img_fma2(img, slot, gw, 1.f - w, w);
-}
-#define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
-#elif NFI_TILE_AB == 4
-// As 2 (every entry straight into the image, branch-free) but with the product's indexed form —
-// VOP2 v_add_f32 under gpr_idx(SRC0,DST) — on the two products: 7 VALU per entry.  (2's VOP3 v_fma
-// under gpr_idx(SRC2,DST) gave wrong d planes and a faulting launch on MI355X)
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff) {
-  const float gw = g * fmaf(nn, wsgn, woff);
-  img_add(img, slot, gw * (1.f - w), gw * w);
-}
-#define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
-#elif NFI_TILE_AB == 5 || NFI_TILE_AB == 6
-// Experiments on 4's failure: 5 = each region followed, inside the asm, by two VOP1 moves (the
-// product's instruction mix after s_set_gpr_idx_off); 6 = each region followed by s_nop 4.
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff) {
-  const float gw = g * fmaf(nn, wsgn, woff);
-  const float x0 = gw * (1.f - w), x1 = gw * w;
-  slot = min(slot, 30);
-#if NFI_TILE_AB == 5
-  float d0, d1;
-  asm volatile(
-      "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\t"
-      "v_add_f32 v40, v40, %4\n\t"
-      "v_add_f32 v41, v41, %5\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "v_mov_b32 %1, 0\n\t"
-      "v_mov_b32 %2, 0"
-      : "+{v[40:71]}"(img), "=&v"(d0), "=&v"(d1)
-      : "s"(slot), "v"(x0), "v"(x1)
-      : "m0");
-  asm volatile("" ::"v"(d0), "v"(d1));
-#else
-  asm volatile(
-      "s_set_gpr_idx_on %1, gpr_idx(SRC0,DST)\n\t"
-      "v_add_f32 v40, v40, %2\n\t"
-      "v_add_f32 v41, v41, %3\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "s_nop 4"
-      : "+{v[40:71]}"(img)
-      : "s"(slot), "v"(x0), "v"(x1)
-      : "m0");
-#endif
-}
-#define NFI_TILE_FLUSH(img, cur, a0, a1) (void)0
-#elif NFI_TILE_AB == 3
-// (A, B) run sums as in 1, a new run starting from the entry's own (gw, gw w) instead of zeroed sums
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff) {
-  const float gw = g * fmaf(nn, wsgn, woff);
-  if (slot != cur) {
-    img_add(img, cur, a0 - a1, a1);
-    a0 = gw;
-    a1 = gw * w;
-    cur = slot;
-  } else {
-    a0 += gw;
-    a1 = fmaf(gw, w, a1);
-  }
-}
-#define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0 - a1, a1)
-#else
-__device__ __forceinline__ void tile_entry(img32& img, int& cur, float& a0, float& a1, int slot, float w,
-                                           float nn, float g, float wsgn, float woff) {
-  const float gw = g * fmaf(nn, wsgn, woff);
-  if (slot != cur) {
-    img_add(img, cur, a0, a1);
-    a0 = 0.f;
-    a1 = 0.f;
-    cur = slot;
-  }
-  a0 = fmaf(gw, 1.f - w, a0);
-  a1 = fmaf(gw, w, a1);
-}
-#define NFI_TILE_FLUSH(img, cur, a0, a1) img_add(img, cur, a0, a1)
-#endif
 
 // Grid gradient of one (sample, plane) entry from its gradient row g (stage row l of G) and the
 // tile texels: grid_sampler_2d_backward (generator.py:312-326 through ATen, border padding,
@@ -2605,22 +2486,6 @@ __device__ __forceinline__ void entry_grid_grad(const float* __restrict__ G, con
   *reinterpret_cast<float2*>(dpc + dpc_at(rec.x, q, nsamp)) = out;
 }
 
-// the gradient-row gathers: NFI_ROW_NT 1 marks them non-temporal (a row's three reads are a third of
-// the pass apart, so the idea was to leave the L2 to the records, whose scalar re-read in the entry
-// loop follows the vector read by one batch) — measured slower: tile pass 2.03 vs 1.83-1.86 ms
-// (gpurun_out/r05/ab_rownt.log), so plain loads
-#ifndef NFI_ROW_NT
-#define NFI_ROW_NT 0
-#endif
-__device__ __forceinline__ float4 tile_row_load(const float4* p) {
-#if NFI_ROW_NT
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-  return make_float4(v[0], v[1], v[2], v[3]);
-#else
-  return *p;
-#endif
-}
-
 // One workgroup-chunk c (< meta[0]) of a tile's entries; lds: TILE_LDS floats.
 __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict__ lds, int c) {
   const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), l = lane_id();
@@ -2687,10 +2552,6 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int b0 = first + wv * per, b1 = min(last, b0 + per);
     img32 img = 0.f;
     if (b0 < b1) {
-      // consecutive entries of one cell (a ray's samples) are merged in a0/a1 before the
-      // indexed update (cur starts at slot 0 with nothing pending)
-      int cur = 0;
-      float a0 = 0.f, a1 = 0.f;
       const cint4_p L = (cint4_p)A.list;
       // 8 entries per step.  Scalar (record) and LDS (row) loads share lgkmcnt and scalar loads
       // return out of order, so a step that waits for its LDS rows also waits for every scalar load
@@ -2700,8 +2561,8 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       // entries of the last step read the next tile's records or the zeroed list padding
       // (chunk_map_kernel): valid cells, and their zeroed rows add 0.
 #define NFI_ENTRY(R, K)                                                                              \
-  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(R[K].y) & 31, __int_as_float(R[K].z), \
-             __int_as_float(R[K].w), gv[K], wsgn, woff)
+  tile_entry(img, __builtin_amdgcn_readfirstlane(R[K].y) & 31, __int_as_float(R[K].z), __int_as_float(R[K].w), \
+             gv[K], wsgn, woff)
 #if NFI_TILE_CHECK
       // code 6: each scalar record of the entry loop against the batch's vector record (lane U + k)
 #define NFI_STEP_CHECK(U, RUSE)                                                                      \
@@ -2714,66 +2575,16 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #else
 #define NFI_STEP_CHECK(U, RUSE)
 #endif
-#if NFI_TILE_LDSREC
-      // the entries' records from the stage rows' pad columns (written with the rows): one broadcast
-      // b128 LDS read per entry, no scalar loads (the list is read once, by the vector loads)
-#if NFI_TILE_CHECK
-      // code 6: the LDS records against the batch's vector records (lane U + k)
-#define NFI_LDSREC_CHECK(U, HH, R)                                                                   \
-    _Pragma("unroll") for (int k = (HH); k < (HH) + 4; ++k) if ((U) + k < n) {                       \
-      const int vy = __shfl(crec.y, (U) + k), vz = __shfl(crec.z, (U) + k), vw = __shfl(crec.w, (U) + k); \
-      NFI_TCHK(R[k].x == vy && R[k].y == vz && R[k].z == vw, 6, c, tile, (U) + k, R[k].x, vy);       \
-    }
-#else
-#define NFI_LDSREC_CHECK(U, HH, R)
-#endif
-#define NFI_LDSREC_ENTRY(R, K)                                                                       \
-  tile_entry(img, cur, a0, a1, __builtin_amdgcn_readfirstlane(R[K].x) & 31, __int_as_float(R[K].y), \
-             __int_as_float(R[K].z), gv[K], wsgn, woff)
 #define NFI_STEP(U, RUSE, RNEXT)                                                                     \
   {                                                                                                  \
     float gv[8];                                                                                     \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) gv[k] = G[stage_at((U) + k, cl)];                 \
     asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
                  "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
-    _Pragma("unroll") for (int hh = 0; hh < 8; hh += 4) {                                            \
-      int3 rk[8];   /* (slot | flags, w, n) of entries hh..hh+3: b96 broadcast reads */             \
-      _Pragma("unroll") for (int k = hh; k < hh + 4; ++k)                                           \
-        rk[k] = *reinterpret_cast<const int3*>(G + ((U) + k) * XS + NC);                             \
-      /* consumed before any region opens: LDS data must not return under GPR-index mode (lint    \
-         rule 4) */                                                                    \
-      asm volatile("" ::"v"(rk[hh].x), "v"(rk[hh].y), "v"(rk[hh].z), "v"(rk[hh + 1].x), "v"(rk[hh + 1].y), \
-                   "v"(rk[hh + 1].z), "v"(rk[hh + 2].x), "v"(rk[hh + 2].y), "v"(rk[hh + 2].z),        \
-                   "v"(rk[hh + 3].x), "v"(rk[hh + 3].y), "v"(rk[hh + 3].z) : "memory");              \
-      NFI_LDSREC_CHECK(U, hh, rk)                                                                    \
-      _Pragma("unroll") for (int k = hh; k < hh + 4; ++k) NFI_LDSREC_ENTRY(rk, k);                  \
-    }                                                                                                \
-  }
-#else
-#define NFI_STEP(U, RUSE, RNEXT)                                                                     \
-  {                                                                                                  \
-    float gv[8];                                                                                     \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) gv[k] = G[stage_at((U) + k, cl)];                 \
-    asm volatile("" ::"v"(gv[0]), "v"(gv[1]), "v"(gv[2]), "v"(gv[3]), "v"(gv[4]), "v"(gv[5]),       \
-                 "v"(gv[6]), "v"(gv[7]) : "memory");                                                 \
-    NFI_RNEXT_EARLY(U, RNEXT)                                                                        \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];                 \
     NFI_STEP_CHECK(U, RUSE)                                                                          \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) NFI_ENTRY(RUSE, k);                               \
-    NFI_RNEXT_LATE(U, RNEXT)                                                                         \
   }
-#if NFI_TILE_SMEM_SAFE
-// the next step's records issued after this step's last region (a memory clobber keeps them there):
-// no scalar load is in flight while an indexed region is open — the next step's row wait
-// (lgkmcnt(0): scalar loads return out of order) completes them first (probe pattern 19)
-#define NFI_RNEXT_EARLY(U, RNEXT)
-#define NFI_RNEXT_LATE(U, RNEXT)                                                                     \
-    asm volatile("" ::: "memory");                                                                   \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];
-#else
-#define NFI_RNEXT_EARLY(U, RNEXT) _Pragma("unroll") for (int k = 0; k < 8; ++k) RNEXT[k] = L[base_ + (U) + 8 + k];
-#define NFI_RNEXT_LATE(U, RNEXT)
-#endif
-#endif
       // Rows loaded coalesced: lane l holds float4 (l & 7) of entry 8j + (l >> 3), j = 0..6 (the
       // entry's row index comes from its lane's record by ds_bpermute): each b128 load reads 8
       // whole 128-B rows instead of one 16-B piece of 56 different rows.
@@ -2793,7 +2604,7 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
   {                                                                                                  \
     int row_ = __shfl((SX), 8 * (J) + (l >> 3));                                                    \
     NFI_ROW_CHECK(J, RB)                                                                             \
-    V = tile_row_load(reinterpret_cast<const float4*>(A.gfeat + (long long)row_ * NC + 4 * (l & 7))); \
+    V = *reinterpret_cast<const float4*>(A.gfeat + (long long)row_ * NC + 4 * (l & 7));              \
   }
 #define NFI_LOAD_ROWC(REC, RB)                                                                       \
   {                                                                                                  \
@@ -2835,15 +2646,9 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
 #define NFI_G_VERIFY(CODE)
 #define NFI_CREC(VREC)
 #endif
-#if NFI_TILE_LDSREC
-#define NFI_REC_ST(VREC) if (l < BATCH) lds_st(reinterpret_cast<int4*>(G + l * XS + NC), make_int4((VREC).y, (VREC).z, (VREC).w, (VREC).x));
-#define NFI_REC_FIRST()
-#else
-#define NFI_REC_ST(VREC)
 #define NFI_REC_FIRST()                                                                              \
     iv4 ra[8], rb[8];                                                                                \
     _Pragma("unroll") for (int k = 0; k < 8; ++k) ra[k] = L[base_ + k];
-#endif
 #define NFI_NEXT_REC(VREC, AHEAD)                                                                    \
     VREC = vnext;                                                                                    \
     vnext = A.list[min(base_ + 2 * (AHEAD) + l, b1 - 1)];
@@ -2852,7 +2657,6 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
     const int base_ = (BASE);                                                                        \
     const int n = min(BATCH, b1 - base_);                                                            \
     _Pragma("unroll") for (int j = 0; j < BATCH / 8; ++j) NFI_ST1(j, rc[j])                         \
-    NFI_REC_ST(VREC)                                                                                 \
     wave_lds_sync();                                                                                 \
     NFI_CREC(VREC)                                                                                   \
     NFI_BATCH_CHECK()                                                                                \
@@ -2880,21 +2684,17 @@ __device__ __forceinline__ void tile_chunk(const TileArgs& A, float* __restrict_
       for (int bb = b0; bb < b1; bb += BATCH) NFI_BATCHC(bb, vrec, BATCH)
 #undef NFI_BATCHC
 #undef NFI_NEXT_REC
-#undef NFI_REC_ST
 #undef NFI_REC_FIRST
 #undef NFI_ST1
 #undef NFI_LOAD_ROWC
 #undef NFI_LD1
 #undef NFI_STEP
-#undef NFI_RNEXT_EARLY
-#undef NFI_RNEXT_LATE
 #undef NFI_ENTRY
 #undef NFI_STEP_CHECK
 #undef NFI_ROW_CHECK
 #undef NFI_BATCH_CHECK
 #undef NFI_G_VERIFY
 #undef NFI_CREC
-      NFI_TILE_FLUSH(img, cur, a0, a1);
     }
     NFI_STAMP(26)
 #if NFI_TILE_CHECK

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 16
+ABI_VERSION = 17
 DEC_SIZE = 7200
 DEC_SIZE_VIEWDIR = 14384
 
@@ -125,10 +125,11 @@ SIGNATURES = {
     'nfi_split16_pack': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int64, c_void_p, c_void_p, c_void_p,
                                           c_void_p]),
     'nfi_wino_input_transform_max': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
-    'nfi_absmax_slots': (ctypes.c_int32, [c_void_p, ctypes.c_int64, c_void_p, c_void_p]),
-    'nfi_gemm_split16': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 4 + [c_void_p]),
+    'nfi_split16_slot_words': (ctypes.c_int32, []),
+    'nfi_absmax_slots': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int64, c_void_p, c_void_p]),
+    'nfi_gemm_split16': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p]),
     'nfi_gemm_split16_shared_a': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
-    'nfi_gemm_split16_ksplit': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 5 + [c_void_p] * 2),
+    'nfi_gemm_split16_ksplit': (ctypes.c_int32, [c_void_p] * 6 + [ctypes.c_int32] * 6 + [c_void_p] * 2),
     'nfi_syn_cond_norm_act_forward': (ctypes.c_int32, [c_void_p] * 3 + [ctypes.c_int32] * 3 + [c_void_p] * 3),
     'nfi_syn_cond_norm_act_backward': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 3 + [c_void_p] * 4),
     'nfi_syn_act_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,

@@ -55,14 +55,11 @@ RELU_IN_TRANSFORM = os.environ.get('NFI_RELU_IN_TRANSFORM', '1') != '0'
 # the three-pass layers' 36 products on the f16 matrix cores at fp32 accuracy (csrc/nfi_gemm.hip:
 # hi / lo splits, three products each; the weights split once, V's scale from the input
 # transform's running maximum); 0: torch.bmm (hipBLASLt fp32)
-# Batch coupling: V's power-of-two scale is ONE per call, from the maximum over all 36 x K
-# x P entries, and P spans every image of the batch.  An image whose activations / gradients sit 2^k
-# below the batch maximum gets 2^-(39-k) of its own magnitude as operand precision (fp32-level for k up
-# to ~15), so per-image results depend on the rest of the batch beyond that; the inversion's producer
-# batches images of one dataset (activations within a few powers of two of each other) and a sharded
-# run feeds each rank its own chunk, which can differ from the unsharded batch's rounding.  The
-# decoder's split (nfi_render.hip) scales per point / per wave instead; a per-image column-block scale
-# here would need one maximum slot set per image (not built).
+# B's power-of-two scale is PER IMAGE (round 6; csrc/nfi_gemm.hip): the input transform leaves each
+# image's maximum |V| in that image's slots and the GEMM splits and unscales every column with its own
+# image's scale, so an image's operand precision — and its result — does not depend on the other
+# images of the batch, and a sharded run matches the unsharded one per image
+# (tests/test_gpu_gemm.py::test_split16_per_image_scale).
 SPLIT16 = os.environ.get('NFI_SPLIT16', '1') != '0'
 SPLIT16_BK = 32       # the split GEMM's K step: channel counts must be multiples of it
 KSPLIT = os.environ.get('NFI_KSPLIT', '1') != '0'   # K split of the Winograd products with few tiles
@@ -149,6 +146,18 @@ def split_matrix(A):
     return _split(A.detach().contiguous()[None], A.shape[1], _stream(A.device))
 
 
+_slot_words = None
+
+
+def slot_words() -> int:
+    """uint32 words of a split product's maxima buffer (nfi_split16_slot_words: 256 images x 4 slots
+    + the completion counter)."""
+    global _slot_words
+    if _slot_words is None:
+        _slot_words = int(_lib.load().nfi_split16_slot_words())
+    return _slot_words
+
+
 def split_matmul_shared(As, X, slots=None):
     """C[b] = A X[b] for X [B, K, N] on the split GEMM, A's halves from split_matrix (one A for every
     image: nfi_gemm_split16_shared_a); X's scale from its maximum (nfi_absmax_slots), or from `slots`
@@ -160,8 +169,8 @@ def split_matmul_shared(As, X, slots=None):
     assert hi.shape[2] == K, (hi.shape, X.shape)
     st = _stream(X.device)
     if slots is None:
-        slots = torch.empty((128,), device=X.device, dtype=torch.int32)   # 64 maxima + the GEMM's counter
-        _call('nfi_absmax_slots', _p(X), X.numel(), _p(slots), st)
+        slots = torch.empty((slot_words(),), device=X.device, dtype=torch.int32)   # per-image maxima + counter
+        _call('nfi_absmax_slots', _p(X), B, K * N, _p(slots), st)
     C = torch.empty((B, Mrows, N), device=X.device)
     ks = ksplit(B * -(-Mrows // 128) * -(-N // 128), K) if (Mrows * N) % 4 == 0 else 1
     work = torch.empty((ks, B, Mrows, N), device=X.device) if ks > 1 else None
@@ -179,24 +188,24 @@ def ksplit(tiles, K):
 
 
 def stream_slots(owner: dict, device):
-    """A self-clearing maxima buffer (64 slots + the GEMM's counter, zeroed once) per stream, kept in
+    """A self-clearing maxima buffer (per-image slots + the GEMM's counter, zeroed once) per stream, kept in
     `owner` — for producers that fill the maxima of a split product's B operand themselves."""
     key = torch.cuda.current_stream(device).cuda_stream
     buf = owner.get(key)
     if buf is None:
-        buf = owner[key] = torch.zeros((128,), device=device, dtype=torch.int32)
+        buf = owner[key] = torch.zeros((slot_words(),), device=device, dtype=torch.int32)
     return buf
 
 
 def _slots(Uw: WeightSet, device):
-    """The maxima slots of this layer's split products on the current stream: 64 running maxima + a
-    completion counter, zeroed once; the input transform fills them and the GEMM's last workgroup
+    """The maxima slots of this layer's split products on the current stream: per-image running maxima +
+    a completion counter, zeroed once; the input transform fills them and the GEMM's last workgroup
     returns them to zero (include/nfi_producer.h), so no memset per call.  One buffer per stream: the
     LPIPS target features run the same layers on a side stream."""
     key = torch.cuda.current_stream(device).cuda_stream
     buf = Uw.vmax.get(key)
     if buf is None:
-        buf = Uw.vmax[key] = torch.zeros((128,), device=device, dtype=torch.int32)
+        buf = Uw.vmax[key] = torch.zeros((slot_words(),), device=device, dtype=torch.int32)
     return buf
 
 
@@ -216,10 +225,10 @@ def _product(Uw: WeightSet, x, scale=None, relu_y=None):
         ks = ksplit(36 * -(-Mrows // 128) * -(-P // 128), K) if KSPLIT and (Mrows * P) % 4 == 0 else 1
         if ks > 1:
             work = torch.empty((ks, 36, Mrows, P), device=x.device)
-            _call('nfi_gemm_split16_ksplit', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, ks,
-                  _p(work), st)
+            _call('nfi_gemm_split16_ksplit', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, P // N,
+                  ks, _p(work), st)
         else:
-            _call('nfi_gemm_split16', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, st)
+            _call('nfi_gemm_split16', _p(hi), _p(lo), _p(inv), _p(V), _p(vmax), _p(M), 36, Mrows, P, K, P // N, st)
         return M
     if relu_y is not None:
         _call('nfi_wino_input_transform_relu_grad', _p(x), _p(relu_y), _p(V), N, K, H, W, st)

@@ -428,7 +428,13 @@ class _VolumeRender(torch.autograd.Function):
         per_img = None
         if tile_counts is not None:
             per_img = tile_counts.numel() // B
-        lib.nfi_set_deterministic(1 if _deterministic() else 0)   # (workspace size and launches follow it)
+        # (per host thread: this is the thread running the backward — autograd's device thread for
+        # .backward() — whatever the caller's thread set; restored below.  Workspace size and launches
+        # follow it.)
+        det = 1 if _deterministic() else 0
+        prev_det = lib.nfi_set_deterministic(det)
+        if DEBUG_BACKWARD is not None:
+            DEBUG_BACKWARD['deterministic'] = int(lib.nfi_set_deterministic(-1))
 
         def part(b0, nb):
             """C-ABI arguments of the backward of images b0 .. b0+nb-1 (every per-image / per-ray
@@ -462,36 +468,39 @@ class _VolumeRender(torch.autograd.Function):
                                                          ctypes.c_void_p(strm.cuda_stream)),
                            'nfi_render_backward_stage')
 
-        main = torch.cuda.current_stream(dev)
-        if BACKWARD_PIPELINE and B >= 2 and DEBUG_BACKWARD is None:
-            # two image halves: the tile pass of half 0 (VALU / LDS / gather bound) runs on a side
-            # stream beside the field backward of half 1 (matrix-core bound)
-            parts = [part(0, B // 2), part(B // 2, B - B // 2)]
-            side = _side_stream(dev)
-            events = []
-            for p in parts:
-                stage(p, 0, 'bwd_bins', main)
-                stage(p, 1, 'bwd_field', main)
-                ev = torch.cuda.Event()
-                ev.record(main)
-                events.append(ev)
-            for p, ev in zip(parts, events):
-                side.wait_event(ev)
-                stage(p, 2, 'bwd_tiles', side)
-                p[2].record_stream(side)
-            for t in (d_planes, g_ro, g_rd, t_saved, tile_counts, planes_tm, ro, rd, near, far):
-                if t is not None:
-                    t.record_stream(side)
-            main.wait_stream(side)
-        elif 0 < BACKWARD_SLAB < B and DEBUG_BACKWARD is None:
-            for b0 in range(0, B, BACKWARD_SLAB):
-                p = part(b0, min(BACKWARD_SLAB, B - b0))
+        try:
+            main = torch.cuda.current_stream(dev)
+            if BACKWARD_PIPELINE and B >= 2 and DEBUG_BACKWARD is None:
+                # two image halves: the tile pass of half 0 (VALU / LDS / gather bound) runs on a side
+                # stream beside the field backward of half 1 (matrix-core bound)
+                parts = [part(0, B // 2), part(B // 2, B - B // 2)]
+                side = _side_stream(dev)
+                events = []
+                for p in parts:
+                    stage(p, 0, 'bwd_bins', main)
+                    stage(p, 1, 'bwd_field', main)
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                    events.append(ev)
+                for p, ev in zip(parts, events):
+                    side.wait_event(ev)
+                    stage(p, 2, 'bwd_tiles', side)
+                    p[2].record_stream(side)
+                for t in (d_planes, g_ro, g_rd, t_saved, tile_counts, planes_tm, ro, rd, near, far):
+                    if t is not None:
+                        t.record_stream(side)
+                main.wait_stream(side)
+            elif 0 < BACKWARD_SLAB < B and DEBUG_BACKWARD is None:
+                for b0 in range(0, B, BACKWARD_SLAB):
+                    p = part(b0, min(BACKWARD_SLAB, B - b0))
+                    for k, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
+                        stage(p, k, name, main)
+            else:
+                p = part(0, B)
                 for k, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
                     stage(p, k, name, main)
-        else:
-            p = part(0, B)
-            for k, name in enumerate(('bwd_bins', 'bwd_field', 'bwd_tiles')):
-                stage(p, k, name, main)
+        finally:
+            lib.nfi_set_deterministic(prev_det)
         st = _stream(dev)
         d_pal = None
         if pal is not None:

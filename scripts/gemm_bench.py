@@ -51,11 +51,11 @@ def main():
         hi = torch.empty(A.shape, device=DEV, dtype=torch.int16)
         lo = torch.empty(A.shape, device=DEV, dtype=torch.int16)
         inv = torch.empty((36,), device=DEV)
-        slots = torch.empty((128,), device=DEV, dtype=torch.int32)   # 64 maxima + counter
+        slots = torch.empty((int(lib.nfi_split16_slot_words()),), device=DEV, dtype=torch.int32)   # per-image maxima + counter
         t_pack = timeit(lambda: _lib.check(lib.nfi_split16_pack(_p(A), 36, Co * Ci, _p(hi), _p(lo), _p(inv), st), 'pack'))
-        _lib.check(lib.nfi_absmax_slots(_p(B), B.numel(), _p(slots), st), 'absmax')
+        _lib.check(lib.nfi_absmax_slots(_p(B), 1, B.numel(), _p(slots), st), 'absmax')
         C = torch.empty((36, Co, P), device=DEV)
-        gemm = lambda: _lib.check(lib.nfi_gemm_split16(_p(hi), _p(lo), _p(inv), _p(B), _p(slots), _p(C), 36, Co, P, Ci, st),
+        gemm = lambda: _lib.check(lib.nfi_gemm_split16(_p(hi), _p(lo), _p(inv), _p(B), _p(slots), _p(C), 36, Co, P, Ci, P, st),
                                   'gemm')
         fl = 2 * 36 * Co * Ci * P
         ref = torch.bmm(A.double(), B.double()).float()

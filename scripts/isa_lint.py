@@ -8,12 +8,18 @@ but models no DS data hazard, and it does not look inside inline asm at all.  Th
 wide DS store whose data registers are rewritten within WINDOW instructions (straight-line order;
 labels do not stop the scan, an unconditional branch or s_endpgm does), says whether the writer sits
 inside an inline-asm block (;;#ASMSTART .. ;;#ASMEND), and exits 1 if any is found.
-Rule 2 (lint_gpr_idx): the M0-indexed register-image regions of the tile pass.
-Rule 5 (valu_sgpr_near_region): no v_readfirstlane / v_readlane shortly before a region (probes 16-18).
-Rule 4 (lds_return_in_region): no LDS load and no scalar load may be outstanding at an
-s_set_gpr_idx_on — data returning while GPR-index mode is on corrupts registers outside its
-destination (round 5: scripts/ubench/gpr_idx_probe.hip patterns 15 (LDS) and 19 (scalar) fault the
-GPU; the same with a global load, pattern 14, is exact).
+Rule 2 (no_index_mode): no GPR-index mode (s_set_gpr_idx_*) and no M0-relative register moves
+(v_movrel*, s_movrel*) anywhere in the build.  Round 5 measured register writes returning while
+index mode was on land outside their destination (scripts/ubench/gpr_idx_probe.hip patterns 15, 16,
+19: LDS returns, VALU-written index SGPRs, scalar-load returns); from round 6 the tile
+pass's register image is updated through jump tables instead, and no kernel uses index mode.
+Rule 6 (jump_tables): every indirect jump (s_setpc_b64) of the build other than a function return
+is a jump table of the tile pass (nfi_render.hip tile_entry), checked on the ASSEMBLED code object
+(llvm-objdump of the gfx950 ELF): s_getpc_b64 P; s_lshl4_add_u32 T, S, OFF; s_add_u32 P.lo, P.lo, T;
+s_addc_u32 P.hi, P.hi, 0; s_setpc_b64 P — the slot SGPR S last written by s_min_u32 S, X, 30 before
+it (so the jump stays inside the table); getpc's PC + OFF is the address right after the s_setpc;
+case k (k = 0..30) at table + 16 k is v_fmac_f32 v(40+k) then v_fmac_f32 v(41+k) (the register
+image's two texels of slot k) and an s_branch to the one exit, which lies after case 30.
 
 Usage: python scripts/isa_lint.py [--window N] [--keep DIR] [source.hip ...]
 (default: every nfi_*.hip in nerf-from-image_amd/csrc, compiled exactly as nfi/build.py compiles them,
@@ -137,187 +143,138 @@ def lint_asm(path: str, window: int):
     return findings
 
 
-def lint_gpr_idx(path: str):
-    """Rule 2 (the tile pass's register image, nfi_render.hip img_add / img_fma2): every M0-indexed
-    region (s_set_gpr_idx_on .. s_set_gpr_idx_off) holds only 32-bit VOP2 v_add_f32 vD, vD, vX under
-    gpr_idx(SRC0,DST) on the pinned image base vD = v40 / v41 (no packed or 64-bit operand: an odd
-    index would address an unaligned VGPR pair; no VOP3 form: a VOP3 v_fma_f32 under gpr_idx(SRC2,DST)
-    broke the pass on MI355X), and
-    its index SGPR was clamped to <= 30 by an s_min just before (v40 + 31 + 1 = v72 is outside the
-    image), so no index reaches past v71."""
-    bad = []
-    lines = open(path).read().splitlines()
-    kernel = None
-    for i, ln in enumerate(lines):
+INDEX_MODE = re.compile(r'^\s*(s_set_gpr_idx_\w+|v_movrel\w*|s_movrel\w*)\b')
+
+
+def no_index_mode(path: str):
+    """Rule 2: (kernel, line, instruction) of every GPR-index-mode / M0-relative register instruction
+    in an assembler text file (there must be none)."""
+    out, kernel = [], None
+    for i, ln in enumerate(open(path).read().splitlines()):
         if re.match(r'^_Z\S+:', ln):
             kernel = ln.split(':')[0]
-        m = re.match(r'^\s*s_set_gpr_idx_on\s+(s\d+)', ln)
-        if not m:
-            continue
-        idx = m.group(1)
-        prev = [x.split(';')[0].strip() for x in lines[max(0, i - 30):i]]
-        prev = [x for x in prev if x and not x.startswith('.') and not x.endswith(':')]
-        if not any(re.match(rf's_min_[iu]32\s+{idx},\s*{idx},\s*30$', x) or
-                   re.match(rf's_min_[iu]32\s+{idx},\s*s\d+,\s*30$', x) for x in prev):
-            bad.append((kernel, i + 1, f'index {idx} not clamped to 30 before the region'))
-        j = i + 1
-        while j < len(lines) and 's_set_gpr_idx_off' not in lines[j]:
-            t = lines[j].split(';')[0].strip()
-            j += 1
-            if not t or t.startswith('.'):
-                continue
-            mode = re.search(r'gpr_idx\(([A-Z0-9,]+)\)', ln)
-            mode = mode.group(1) if mode else ''
-            ok_add = mode == 'SRC0,DST' and re.match(r'v_add_f32(_e32)?\s+(v4[01]),\s*\2,\s*v\d+$', t)
-            # (rejected: NFI_TILE_AB 2's VOP3 v_fma_f32 vD, vA, vB, vD under gpr_idx(SRC2,DST) gave wrong
-            #  d planes and a faulting launch on MI355X — DESIGN.md §3)
-            if not ok_add:
-                bad.append((kernel, j, f'unexpected instruction in an indexed region ({mode}): {t}'))
-    return bad
-
-
-LDS_RET = ('ds_read', 'ds_load', 'ds_bpermute', 'ds_permute', 'ds_swizzle', 'ds_consume', 'ds_append')
-
-
-SMEM_RET = ('s_load', 's_buffer_load')
-
-
-def lds_return_in_region(path: str, depth: int = 600, smem: bool = False):
-    """Rule 4: for every s_set_gpr_idx_on, walk back (along the fall-through path and, at a loop
-    header, from each backward branch to it) to the wait that covers it: an LDS load issued after the
-    last s_waitcnt lgkmcnt(0) — or among the N most recent lgkm instructions before an lgkmcnt(N) —
-    may still return its data while the region's index mode is on.  Returns (kernel, line, load)."""
-    lines = open(path).read().splitlines()
-    out = []
-    # kernel bodies: (name, [(line no, kind, text)])
-    bodies, cur = [], None
-    for i, ln in enumerate(lines):
-        if re.match(r'^_Z\S+:', ln):
-            cur = (ln.split(':')[0], [])
-            bodies.append(cur)
-            continue
-        if cur is None:
-            continue
-        if ln.startswith('.Lfunc_end'):
-            cur = None
-            continue
-        m = re.match(r'^(\.LBB\w+):', ln)
-        if m:
-            cur[1].append((i + 1, 'label', m.group(1)))
-            continue
-        t = ln.split(';')[0].strip()
-        if t and not t.startswith('.') and ln.startswith('\t'):
-            cur[1].append((i + 1, 'op', t))
-    for kernel, ins in bodies:
-        if not any(k == 'op' and t.startswith('s_set_gpr_idx_on') for _, k, t in ins):
-            continue
-        labels = {t: j for j, (_, k, t) in enumerate(ins) if k == 'label'}
-        back = {}
-        for j, (_, k, t) in enumerate(ins):
-            if k == 'op':
-                m = re.match(r's_(?:cbranch_\w+|branch)\s+(\.LBB\w+)', t)
-                if m and m.group(1) in labels and labels[m.group(1)] < j:
-                    back.setdefault(labels[m.group(1)], []).append(j)
-
-        def lgkm(t):
-            return t.startswith(('ds_', 's_load', 's_buffer_load'))
-
-        for j, (lno, k, t) in enumerate(ins):
-            if k != 'op' or not t.startswith('s_set_gpr_idx_on'):
-                continue
-            stack, seen, hit = [(j - 1, 0)], set(), None
-            while stack and hit is None:
-                p, n = stack.pop()
-                while p >= 0 and n < depth and hit is None:
-                    _, kk, tt = ins[p]
-                    if kk == 'label':
-                        for b in back.get(p, []):
-                            if b not in seen:
-                                seen.add(b)
-                                stack.append((b, n))
-                        p -= 1
-                        continue
-                    if tt.startswith('s_waitcnt'):
-                        mm = re.search(r'lgkmcnt\((\d+)\)', tt)
-                        if mm:
-                            left, q = int(mm.group(1)), p - 1
-                            if left and smem:   # scalar loads return out of order: only lgkmcnt(0) completes them
-                                n += 1
-                                p -= 1
-                                continue
-                            while left > 0 and q >= 0:
-                                if ins[q][1] == 'op' and lgkm(ins[q][2]):
-                                    left -= 1
-                                    if ins[q][2].startswith(LDS_RET):
-                                        hit = ins[q]
-                                q -= 1
-                            break
-                    if tt.startswith(LDS_RET) or (smem and tt.startswith(SMEM_RET)):
-                        hit = ins[p]
-                    n += 1
-                    p -= 1
-            if hit:
-                what = 'scalar' if hit[2].startswith(SMEM_RET) else 'LDS'
-                out.append((kernel, lno, f'{what} load possibly in flight at the region: line {hit[0]} {hit[2]}'))
+        if INDEX_MODE.match(ln.split(';')[0]):
+            out.append((kernel, i + 1, ln.strip()))
     return out
 
 
-def valu_sgpr_near_region(path: str, window: int = 30):
-    """Rule 5: no VALU instruction writing an SGPR from a VGPR lane (v_readfirstlane / v_readlane)
-    within `window` instructions before an s_set_gpr_idx_on, along the fall-through path and loop back
-    edges — an index SGPR made that way gave wrong register images in a region train (probe patterns
-    16-18).  Returns (kernel, line, message)."""
-    lines = open(path).read().splitlines()
-    out, bodies, cur = [], [], None
-    for i, ln in enumerate(lines):
-        if re.match(r'^_Z\S+:', ln):
-            cur = (ln.split(':')[0], [])
-            bodies.append(cur)
-            continue
-        if cur is None:
-            continue
-        if ln.startswith('.Lfunc_end'):
-            cur = None
-            continue
-        m = re.match(r'^(\.LBB\w+):', ln)
+DIS_FN = re.compile(r'^([0-9a-f]+) <(\S+)>:')
+DIS_INS = re.compile(r'^\s+([a-z_0-9]+)(?:\s+([^/]*?))?\s*//\s*([0-9A-F]+):')
+
+
+def parse_disassembly(text: str):
+    """llvm-objdump -d text -> {function: [(address, mnemonic, operands)]} (branch operands as
+    objdump prints them, with the absolute target appended as <fn+0xOFF>)."""
+    fns, cur = {}, None
+    for ln in text.splitlines():
+        m = DIS_FN.match(ln)
         if m:
-            cur[1].append((i + 1, 'label', m.group(1)))
+            cur = fns.setdefault(m.group(2), [])
             continue
-        t = ln.split(';')[0].strip()
-        if t and not t.startswith('.') and ln.startswith('\t'):
-            cur[1].append((i + 1, 'op', t))
-    for kernel, ins in bodies:
-        labels = {t: j for j, (_, k, t) in enumerate(ins) if k == 'label'}
-        back = {}
-        for j, (_, k, t) in enumerate(ins):
-            if k == 'op':
-                m = re.match(r's_(?:cbranch_\w+|branch)\s+(\.LBB\w+)', t)
-                if m and m.group(1) in labels and labels[m.group(1)] < j:
-                    back.setdefault(labels[m.group(1)], []).append(j)
-        for j, (lno, k, t) in enumerate(ins):
-            if k != 'op' or not t.startswith('s_set_gpr_idx_on'):
+        m = DIS_INS.match(ln)
+        if m and cur is not None:
+            ops = (m.group(2) or '').strip()
+            t = re.search(r'<(\S+)\+0x([0-9a-f]+)>', ln)
+            cur.append((int(m.group(3), 16), m.group(1), ops, (t.group(1), int(t.group(2), 16)) if t else None))
+    starts = {}
+    for ln in text.splitlines():
+        m = DIS_FN.match(ln)
+        if m:
+            starts[m.group(2)] = int(m.group(1), 16)
+    return fns, starts
+
+
+CASE_BYTES, CASES, IMG_BASE = 16, 31, 40
+
+
+def jump_tables(text: str):
+    """Rule 6 over llvm-objdump text: returns (number of tables checked, [(function, address, message)])."""
+    fns, starts = parse_disassembly(text)
+    bad, checked = [], 0
+    for fn, ins in fns.items():
+        at = {a: j for j, (a, _, _, _) in enumerate(ins)}
+        for jj, (saddr, smn, sops, _) in enumerate(ins):
+            # every indirect jump: a function return (s[30:31], set by the caller's s_swappc_b64) or a
+            # table dispatch, which must verify below
+            if smn != 's_setpc_b64' or sops == 's[30:31]':
                 continue
-            stack, seen, hit = [(j - 1, 0)], set(), None
-            while stack and hit is None:
-                p, n = stack.pop()
-                while p >= 0 and n < window:
-                    _, kk, tt = ins[p]
-                    if kk == 'label':
-                        for b in back.get(p, []):
-                            if b not in seen:
-                                seen.add(b)
-                                stack.append((b, n))
-                        p -= 1
-                        continue
-                    if tt.startswith(('v_readfirstlane', 'v_readlane')):
-                        hit = ins[p]
-                        break
-                    n += 1
-                    p -= 1
-            if hit:
-                out.append((kernel, lno, f'VALU-written SGPR {window} instructions or fewer before the region: '
-                                         f'line {hit[0]} {hit[2]}'))
-    return out
+            checked += 1
+            j = jj - 4
+            if j < 0 or ins[j][1] != 's_getpc_b64' or ins[j][2] != sops:
+                bad.append((fn, saddr, f'indirect jump s_setpc_b64 {sops} is not a table dispatch'))
+                continue
+            addr, mn, ops = ins[j][0], ins[j][1], ins[j][2]
+            err = lambda msg: bad.append((fn, addr, msg))
+            seq = ins[j + 1:j + 5]
+            if [x[1] for x in seq] != ['s_lshl4_add_u32', 's_add_u32', 's_addc_u32', 's_setpc_b64']:
+                err('not the table dispatch sequence: ' + ' ; '.join(f'{x[1]} {x[2]}' for x in seq))
+                continue
+            pm = re.match(r's\[(\d+):(\d+)\]$', ops)
+            sh = [o.strip() for o in seq[0][2].split(',')]
+            lo = [o.strip() for o in seq[1][2].split(',')]
+            hi = [o.strip() for o in seq[2][2].split(',')]
+            tmp, slot = sh[0], sh[1]
+            ok = (pm and len(sh) == 3 and lo == [f's{pm.group(1)}', f's{pm.group(1)}', tmp]
+                  and hi == [f's{pm.group(2)}', f's{pm.group(2)}', '0'] and seq[3][2] == ops)
+            if not ok:
+                err('dispatch operands do not form PC + (slot << 4) + OFF: ' + ' ; '.join(f'{x[1]} {x[2]}' for x in seq))
+                continue
+            try:
+                off = int(sh[2], 0)
+            except ValueError:
+                err(f'table offset is not a literal: {sh[2]}')
+                continue
+            base = seq[0][0] + off            # s_getpc_b64 returns the address of the next instruction
+            if j + 5 >= len(ins) or ins[j + 5][0] != base:
+                err(f'table base {base:#x} is not the instruction after s_setpc_b64')
+                continue
+            # the slot SGPR's last write before the dispatch: s_min_u32 slot, X, 30
+            clamp = None
+            for q in range(j - 1, max(-1, j - 64), -1):
+                qm, qo = ins[q][1], [o.strip() for o in ins[q][2].split(',')]
+                if qm.startswith('s_') and not qm.startswith(('s_cmp', 's_bitcmp', 's_cbranch', 's_waitcnt', 's_nop',
+                                                              's_branch', 's_setprio', 's_barrier')) and qo and qo[0] == slot:
+                    clamp = (qm, qo)
+                    break
+            if not clamp or clamp[0] != 's_min_u32' or clamp[1][2:] != ['30']:
+                err(f'slot {slot} not clamped to 30 by s_min_u32 before the dispatch (last write: {clamp})')
+                continue
+            exits = set()
+            for k in range(CASES):
+                c = at.get(base + CASE_BYTES * k)
+                if c is None or c + 2 >= len(ins):
+                    err(f'case {k}: no instruction at {base + CASE_BYTES * k:#x}')
+                    break
+                f0, f1, br = ins[c], ins[c + 1], ins[c + 2]
+                fmac = ('v_fmac_f32', 'v_fmac_f32_e32')
+                d0 = f0[2].split(',')[0].strip() if f0[1] in fmac else None
+                d1 = f1[2].split(',')[0].strip() if f1[1] in fmac else None
+                want0, want1 = f'v{IMG_BASE + k}', f'v{IMG_BASE + k + 1}'
+                if (d0, d1) != (want0, want1) or br[1] != 's_branch' or br[3] is None:
+                    err(f'case {k}: expected v_fmac_f32 {want0}; v_fmac_f32 {want1}; s_branch — got '
+                        f'{f0[1]} {f0[2]} ; {f1[1]} {f1[2]} ; {br[1]} {br[2]}')
+                    break
+                exits.add(starts[br[3][0]] + br[3][1])
+            else:
+                end = base + CASE_BYTES * (CASES - 1)
+                if len(exits) != 1 or not (end < next(iter(exits)) <= end + CASE_BYTES):
+                    err(f'cases do not branch to one exit after the table: {sorted(hex(e) for e in exits)}')
+    return checked, bad
+
+
+def disassemble(src: str, extra=()):
+    """llvm-objdump text of src's gfx950 code object, compiled as nfi/build.py compiles it."""
+    from nfi.build import FLAGS
+    flags = [f for f in FLAGS if f not in ('-shared', '-fPIC')]
+    with tempfile.TemporaryDirectory() as d:
+        obj = os.path.join(d, 'k.o')
+        subprocess.run([os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')] + flags + ['-w', '--cuda-device-only',
+                        '--no-gpu-bundle-output', '-c', '-o', obj, src] + list(extra), check=True)
+        objdump = os.path.join(os.path.dirname(os.path.realpath(os.environ.get('HIPCC', '/opt/rocm/bin/hipcc'))), '..',
+                               'lib', 'llvm', 'bin', 'llvm-objdump')
+        if not os.path.exists(objdump):
+            objdump = '/opt/rocm/lib/llvm/bin/llvm-objdump'
+        return subprocess.run([objdump, '-d', '--mcpu=gfx950', obj], check=True, capture_output=True, text=True).stdout
 
 
 DS_ANY = re.compile(r'^\s*(ds_(?:write|read|bpermute|permute|add|swizzle)\w*)\s+(.*)$')
@@ -398,12 +355,20 @@ def main():
                   f"      -> +{x['distance']} {x['writer']}"
                   f"{'  [writer inside inline asm]' if x['writer_in_inline_asm'] else ''}")
         total += f
-        g = lint_gpr_idx(out) + lds_return_in_region(out, smem=True) + valu_sgpr_near_region(out)
-        nreg = sum(1 for ln in open(out) if 's_set_gpr_idx_on' in ln)
-        print(f'{os.path.basename(s)}: {nreg} M0-indexed regions, {len(g)} violations')
+        g = no_index_mode(out)
+        print(f'{os.path.basename(s)}: {len(g)} GPR-index-mode / movrel instructions')
         for k, ln, msg in g:
             print(f'  {k[:70]}  line {ln}: {msg}')
         total += g
+        if 'tile_entry' in open(s).read():
+            n, jt = jump_tables(disassemble(s, ['-D' + d for d in a.D]))
+            print(f'{os.path.basename(s)}: {n} jump tables, {len(jt)} violations')
+            for fn, ad, msg in jt:
+                print(f'  {fn[:70]}  {ad:#x}: {msg}')
+            total += jt
+            if n == 0:
+                print('  (no jump table found: the tile pass was not compiled?)')
+                total.append(('', 0, 'no jump table'))
     print('isa lint:', 'FAIL' if total else 'ok')
     return 1 if total else 0
 

@@ -66,10 +66,24 @@ def test_follows_torch_deterministic_algorithms(det_mode):
     """ops.DETERMINISTIC None: torch.use_deterministic_algorithms(True) selects the deterministic form
     (set in the thread that runs the backward: autograd's device thread)."""
     prev = torch.are_deterministic_algorithms_enabled()
+    lib = _lib.load()
+    before = lib.nfi_set_deterministic(-1)             # this (the caller's) thread's setting
     torch.use_deterministic_algorithms(True, warn_only=True)
+    seen = []
     try:
-        p1, _ = _full_step(None)
-        p2, _ = _full_step(None)
+        for _ in range(2):
+            ops.DEBUG_BACKWARD = {}
+            p, _ = _full_step(None)
+            seen.append(ops.DEBUG_BACKWARD.get('deterministic'))
+            if len(seen) == 1:
+                p1 = p
+            else:
+                p2 = p
     finally:
+        ops.DEBUG_BACKWARD = None
         torch.use_deterministic_algorithms(prev)
+    # the mode was in effect on the thread that ran each backward (autograd's device thread), and the
+    # caller's thread setting is untouched (nfi_set_deterministic is per host thread, include/nfi.h)
+    assert seen == [1, 1], seen
+    assert lib.nfi_set_deterministic(-1) == before
     assert torch.equal(p1, p2)
