@@ -236,8 +236,8 @@ int32_t nfi_aug_affine_grid(const float* theta, int32_t N, int32_t H, int32_t W,
  * nfi_split16_pack: A [batch][per] -> hi, lo [batch][per] (fp16 bits) and a_inv [batch] = 2^-e, with
  *   the largest |A[b]| 2^e in [2^14, 2^15) (one workgroup per batch entry; frozen operands: once).
  * Maxima slots (b_max / vmax / slots below): NFI_SPLIT16_SLOT_WORDS uint32 (= nfi_split16_slot_words()):
- *   image i's running maximum of |B| in words [4 (i mod 256), 4 (i mod 256) + 4) (float bits), a
- *   completion counter in word 1024.  B's power-of-two scale is PER IMAGE, so an image's operand
+ *   image i's running maximum of |B| in words [64 (i mod 256), 64 (i mod 256) + 64) (float bits), a
+ *   completion counter in word 16384.  B's power-of-two scale is PER IMAGE, so an image's operand
  *   precision (and result) does not depend on the other images of its batch (sharded = unsharded).
  * nfi_wino_input_transform_max: nfi_wino_input_transform_scaled (scale may be NULL) or, with relu_y,
  *   the ReLU-masked gradient transform, also leaving each image's running maximum of |V| in its
@@ -253,7 +253,7 @@ int32_t nfi_aug_affine_grid(const float* theta, int32_t N, int32_t H, int32_t W,
  *   (stylegan.py:99-101) — and K split in ksplit ranges when ksplit > 1 (few output tiles, long K: the
  *   data gradient W9^T dP), the partial products in work [ksplit][batch][M][N] summed in order
  *   (deterministic). */
-#define NFI_SPLIT16_SLOT_WORDS 1025
+#define NFI_SPLIT16_SLOT_WORDS 16385
 int32_t nfi_split16_slot_words(void);
 int32_t nfi_split16_pack(const float* A, int32_t batch, int64_t per, uint16_t* Ah, uint16_t* Al, float* a_inv,
                          void* stream);

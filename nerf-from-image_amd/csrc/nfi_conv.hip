@@ -3,15 +3,18 @@
 //   y = A^T [ (G g G^T) (.) (B^T d B) ] A      per 4x4 output tile, 6x6 input patch
 //
 // The 36 element-wise products of a layer form 36 independent [Co x Ci] x [Ci x P] matrix
-// products (P = N * H/4 * W/4 tiles), which run as one batched fp32 GEMM on the matrix cores
-// (hipBLASLt through PyTorch-ROCm: 100-137 TFLOP/s measured on these shapes).  This file holds
-// the memory-bound parts around it:
+// products (P = N * H/4 * W/4 tiles), which run as one batched fp32-accurate GEMM on the f16 matrix
+// cores — nfi's split-f16 product (nfi_gemm.hip, nfi_gemm_split16[_ksplit]: 200-256 TFLOP/s
+// fp32-equivalent on these shapes; torch.bmm / hipBLASLt fp32 only with NFI_SPLIT16=0) — or, for the
+// 64-channel layers, inside the fused kernel below (fp32 MFMAs).  This file holds the transforms
+// around the products and the fused kernels:
 //
 //   weight_kernel   w [Co][Ci][3][3] -> U [36][Co][Ci]; or, for the data gradient (the
 //                   transposed convolution = correlation with rot180(w), channels swapped),
 //                   U [36][Ci][Co].  Once per frozen weight.
 //   input_kernel    x [N][C][H][W] -> V [36][C][P]: one lane per (channel, tile); each patch row
-//                   is a float4 plus its two neighbour columns (L1-served); 36 coalesced stores.
+//                   is a float4 plus its two neighbour columns (L1-served); 36 coalesced stores;
+//                   optionally each image's max |V| for the split product's per-image B scale.
 //   output_kernel   M [36][Co][P] -> y [N][Co][H][W] (+ bias, ReLU, 2x2 max pool fused: the
 //                   LPIPS VGG16 block epilogue, nfi_vgg_bias_relu_forward's contract — a 4x4
 //                   tile holds whole pool windows).
@@ -220,7 +223,7 @@ __global__ void __launch_bounds__(256) input_kernel(const float* __restrict__ x,
       if (m > 0.f) atomicMax(ired + (n - nb0), __float_as_uint(m));
       __syncthreads();
       for (int i = threadIdx.x; i < ni; i += 256)
-        if (ired[i] != 0u) atomicMax(vmax + split_slot(nb0 + i, blockIdx.y), ired[i]);
+        if (ired[i] != 0u) atomicMax(vmax + split_slot(nb0 + i, blockIdx.x + blockIdx.y), ired[i]);
     }
   }
 }

@@ -106,12 +106,24 @@ struct Args {
   int nslot;                  // slots the last workgroup returns to zero (images used x SPLIT_ISLOTS)
 };
 
-// B's scale for one image: the largest of its slots
+// B's scale of this lane's image (images non-decreasing across the wave's lanes): per image of the
+// wave, its 64 slots read one per lane and reduced across the wave
 __device__ __forceinline__ void image_scale(const unsigned* b_max, int img, float& s, float& inv) {
-  float m = 0.f;
+  static_assert(SPLIT_ISLOTS == 64, "one slot per lane");
+  const int i0 = __builtin_amdgcn_readfirstlane(img);
+  const int i1 = __builtin_amdgcn_readlane(img, 63);
+  float mine = 0.f;
+  for (int i = i0; i <= i1; i += 4) {   // (four images' loads in flight per pass: small maps span many)
+    float v[4];
 #pragma unroll
-  for (int j = 0; j < SPLIT_ISLOTS; ++j) m = fmaxf(m, __uint_as_float(b_max[split_slot(img, j)]));
-  pow2_scale15(m, s, inv);
+    for (int u = 0; u < 4; ++u) v[u] = __uint_as_float(b_max[split_slot(min(i + u, i1), lane_id())]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float m = wave_max(v[u]);
+      if (img == i + u) mine = m;
+    }
+  }
+  pow2_scale15(mine, s, inv);
 }
 
 // The B maxima are consumed, not copied: the used slots of b_max (float bits) + b_max[SPLIT_SLOTS] (a
@@ -190,11 +202,11 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
   const int bn = tid % TBN, bk = (tid / TBN) * KB;
   const int bcol = min(n0 + bn, N - 1);
   const bool b_ok = n0 + bn < N;
-  // B's scale: this thread's column's image; the epilogue unscales each column by its own
-  __shared__ float col_scale[TBN];
+  // B's scale: this thread's column's image; the epilogue unscales each column by its own (the
+  // column scales go through the operand LDS once the K loop is done: a separate array would take
+  // the LDS past 4 workgroups per CU)
   float sb, isb;
   image_scale(g.b_max, g.a_shared ? b : bcol / g.cpi, sb, isb);
-  if (tid < TBN) col_scale[bn] = g.a_inv[ba] * isb;   // (read after the K loop's barriers)
   u4v RA[PF][2 * CA];
   float RB[PF][KB];
   auto load = [&](int k0, u4v (&ra)[2 * CA], float (&rb)[KB]) {
@@ -288,6 +300,9 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
     if (k0 < kend) step(k0, RA[0], RB[0]);
   }
   // C rows m0 + 16 RX wm + 16 x + 4 kg + r, column n0 + 16 RY wn + 16 y + i16
+  float* col_scale = reinterpret_cast<float*>(lds);   // (the K loop ended on a barrier)
+  if (tid < TBN) col_scale[bn] = g.a_inv[ba] * isb;
+  __syncthreads();
   float* Cg = (g.ksplit > 1 ? g.work + (long long)ks * (gridDim.z / g.ksplit) * M * N : g.C) + (long long)b * M * N;
 #pragma unroll
   for (int x = 0; x < RX; ++x)

@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(256) up_bwd_fused_kernel(const float* __restri
     if ((threadIdx.x & 63) == 0) pmax[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0)
-      atomicMax(vmax + split_slot(b, blockIdx.x), __float_as_uint(fmaxf(fmaxf(pmax[0], pmax[1]), fmaxf(pmax[2], pmax[3]))));
+      atomicMax(vmax + split_slot(b, blockIdx.x + blockIdx.y), __float_as_uint(fmaxf(fmaxf(pmax[0], pmax[1]), fmaxf(pmax[2], pmax[3]))));
   }
 }
 

@@ -3,9 +3,10 @@ LPIPS VGG16 trunk (lpips 0.1 via lib/metrics.py:107) and the s
 (models/stylegan.py:130-145, §8(f) #1) call F.conv2d(x, w, padding=1) with frozen weights
 (run.py:630-632; LPIPS is never trained), in fp32 (TF32 off, run.py:59-60).
 
-Per layer: input transform (HIP) -> 36 batched [Co x Ci] x [Ci x P] fp32 GEMMs on the matrix cores
-(torch.bmm -> hipBLASLt, a plain library GEMM) -> output transform (HIP, with the VGG block's
-bias + ReLU + 2x2 max pool fused).  Weight transforms are computed once per frozen weight.  The
+Per layer: input transform (HIP) -> 36 batched [Co x Ci] x [Ci x P] fp32-accurate GEMMs on the f16
+matrix cores (nfi's split-f16 product, csrc/nfi_gemm.hip; torch.bmm / hipBLASLt with NFI_SPLIT16=0)
+-> output transform (HIP, with the VGG block's bias + ReLU + 2x2 max pool fused); the 64-channel
+layers as one fused HIP kernel.  Weight transforms are computed once per frozen weight.  The
 data gradient is the same pipeline with the rot180 / channel-swapped weights (the weights
 receive no gradient: asking for one raises).  csrc/nfi_conv.hip, include/nfi_producer.h.
 
