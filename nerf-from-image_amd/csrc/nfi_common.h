@@ -174,6 +174,16 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
   return v;
 }
+// the same on DPP inside rows, then across rows (one ds_bpermute instead of six)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  v = fmaxf(v, __shfl_xor(v, 16));
+  auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(s[0]), __int_as_float(s[1]));
+}
 
 // Inclusive prefix sum / product over lanes 0..63 (Hillis-Steele).
 __device__ __forceinline__ float wave_incl_sum(float v) {

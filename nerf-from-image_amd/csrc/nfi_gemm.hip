@@ -45,9 +45,13 @@ typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int BK = 32;
+// NFI_GEMM_BUF 1: the general kernel's operands through buffer loads (32-bit offsets, out-of-range rows
+// and columns read as zeros) and B split by v_cvt_pk_f16_f32 + v_fma_mix; 0: flat loads + selects
+#ifndef NFI_GEMM_BUF
+#define NFI_GEMM_BUF 1
+#endif
 constexpr int LDK = BK + 8;                    // halves per LDS row (80 B)
-constexpr int TILE_H = BM * LDK;               // halves per operand image (A and B^T: BM == BN)
 
 __device__ __forceinline__ f4v mfma_h(u4v a, u4v b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
@@ -113,14 +117,18 @@ __device__ __forceinline__ void image_scale(const unsigned* b_max, int img, floa
   const int i0 = __builtin_amdgcn_readfirstlane(img);
   const int i1 = __builtin_amdgcn_readlane(img, 63);
   float mine = 0.f;
-  for (int i = i0; i <= i1; i += 4) {   // (four images' loads in flight per pass: small maps span many)
-    float v[4];
+  if (i0 == i1) {   // (wave-uniform) the wave's columns in one image: one load per lane
+    mine = wave_max_dpp(__uint_as_float(b_max[split_slot(i0, lane_id())]));
+  } else {
+    for (int i = i0; i <= i1; i += 4) {   // (four images' loads in flight per pass: small maps span many)
+      float v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __uint_as_float(b_max[split_slot(min(i + u, i1), lane_id())]);
+      for (int u = 0; u < 4; ++u) v[u] = __uint_as_float(b_max[split_slot(min(i + u, i1), lane_id())]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float m = wave_max(v[u]);
-      if (img == i + u) mine = m;
+      for (int u = 0; u < 4; ++u) {
+        const float m = wave_max_dpp(v[u]);
+        if (img == i + u) mine = m;
+      }
     }
   }
   pow2_scale15(mine, s, inv);
@@ -197,7 +205,6 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
   // global -> register staging: A (row ar, halves ak .. ak + 8 CA - 1 of the K-step: CA b128 loads
   // each of hi and lo), B column bn, k = bk .. bk + KB - 1 (coalesced rows across the wave)
   const int ar = (tid * CA) >> 2, ak = 8 * ((tid * CA) & 3);
-  const int arow = min(m0 + ar, M - 1);
   const bool a_ok = m0 + ar < M;
   const int bn = tid % TBN, bk = (tid / TBN) * KB;
   const int bcol = min(n0 + bn, N - 1);
@@ -207,6 +214,63 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
   // the LDS past 4 workgroups per CU)
   float sb, isb;
   image_scale(g.b_max, g.a_shared ? b : bcol / g.cpi, sb, isb);
+#if NFI_GEMM_BUF
+  // Buffer loads on the batch entry's A halves and B: 32-bit offsets (no 64-bit address arithmetic
+  // per load), the K-step and the row i of B in the scalar offset, and rows / columns past the matrix
+  // given an offset at the buffer's end, so they load zeros (no selects)
+  const __amdgpu_buffer_rsrc_t rah = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(Ahg), (short)0,
+                                                                       M * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ral = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(Alg), (short)0,
+                                                                       M * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Bg), (short)0, K * N * 4,
+                                                                       0x00020000);
+  const int va = a_ok ? ((m0 + ar) * K + ak) * 2 : M * K * 2;
+  const int vb = b_ok ? (bk * N + n0 + bn) * 4 : K * N * 4;
+  u4v RA[PF][2 * CA];
+  float RB[PF][KB];
+  auto load = [&](int k0, u4v (&ra)[2 * CA], float (&rb)[KB]) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      ra[i] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rah, va + 16 * i, k0 * 2, 0));
+      ra[CA + i] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(ral, va + 16 * i, k0 * 2, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < KB; ++i)
+      rb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbs, vb, (k0 + i) * N * 4, 0));
+  };
+  auto store = [&](const u4v (&ra)[2 * CA], const float (&rb)[KB]) {
+    u4v* dh = reinterpret_cast<u4v*>(Ahs + ar * LDK + ak);
+    u4v* dl = reinterpret_cast<u4v*>(Als + ar * LDK + ak);
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      lds_st_fenced(dh + i, ra[i]);
+      lds_st_fenced(dl + i, ra[CA + i]);
+    }
+    // hi = f16(v), lo = f16(v - hi) of v = B sb, two values per register: v_cvt_pk_f16_f32 for hi,
+    // v_fma_mix (f16(hi * -1 + v)) for lo into a copy of hi (a register the compiler writes itself)
+    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+    u4v hv[KB / 8], lv[KB / 8];
+#pragma unroll
+    for (int i = 0; i < KB; i += 2) {
+      const float v0 = rb[i] * sb, v1 = rb[i + 1] * sb;
+      const unsigned h = __builtin_bit_cast(unsigned, h2v{(_Float16)v0, (_Float16)v1});
+      unsigned o = h;
+      asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+          "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+          : "+v"(o) : "v"(h), "v"(v0), "v"(v1));
+      hv[i >> 3][(i >> 1) & 3] = h;
+      lv[i >> 3][(i >> 1) & 3] = o;
+    }
+    u4v* eh = reinterpret_cast<u4v*>(Bhs + bn * LDK + bk);
+    u4v* el = reinterpret_cast<u4v*>(Bls + bn * LDK + bk);
+#pragma unroll
+    for (int i = 0; i < KB / 8; ++i) {
+      lds_st_fenced(eh + i, hv[i]);
+      lds_st_fenced(el + i, lv[i]);
+    }
+  };
+#else
+  const int arow = min(m0 + ar, M - 1);
   u4v RA[PF][2 * CA];
   float RB[PF][KB];
   auto load = [&](int k0, u4v (&ra)[2 * CA], float (&rb)[KB]) {
@@ -247,6 +311,7 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
       lds_st_fenced(el + i, lv[i]);
     }
   };
+#endif
 
   // wave (wm, wn) computes rows 16 RX wm.., columns 16 RY wn.. of the tile
   const int wm = wv / WN, wn = wv % WN;
@@ -304,18 +369,38 @@ __global__ void __launch_bounds__(64 * WM * WN, RX * RY > 32 ? 1 : RX * RY > 16 
   if (tid < TBN) col_scale[bn] = g.a_inv[ba] * isb;
   __syncthreads();
   float* Cg = (g.ksplit > 1 ? g.work + (long long)ks * (gridDim.z / g.ksplit) * M * N : g.C) + (long long)b * M * N;
+#if NFI_GEMM_BUF
+  if (m0 + TBM <= M && n0 + TBN <= N) {   // (workgroup-uniform) an interior tile: no bounds tests, buffer
+                                          // stores at 32-bit offsets (rows 16 apart in the scalar offset)
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(Cg, (short)0, M * N * 4, 0x00020000);
+    const int vc = ((m0 + 16 * RX * wm + 4 * kg) * N + n0 + 16 * RY * wn + i16) * 4;
+    float cs[RY];
 #pragma unroll
-  for (int x = 0; x < RX; ++x)
+    for (int y = 0; y < RY; ++y) cs[y] = col_scale[16 * RY * wn + 16 * y + i16];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + 16 * RX * wm + 16 * x + 4 * kg + r;
-      if (m >= M) continue;
+    for (int x = 0; x < RX; ++x)
 #pragma unroll
-      for (int y = 0; y < RY; ++y) {
-        const int n = n0 + 16 * RY * wn + 16 * y + i16;
-        if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * col_scale[n - n0];
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int y = 0; y < RY; ++y)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[x][y][r] * cs[y]), rc, vc + 64 * y,
+                                                (16 * x + r) * N * 4, 0);
+  } else
+#endif
+  {
+#pragma unroll
+    for (int x = 0; x < RX; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 16 * RX * wm + 16 * x + 4 * kg + r;
+        if (m >= M) continue;
+#pragma unroll
+        for (int y = 0; y < RY; ++y) {
+          const int n = n0 + 16 * RY * wn + 16 * y + i16;
+          if (n < N) Cg[(long long)m * N + n] = acc[x][y][r] * col_scale[n - n0];
+        }
       }
-    }
+  }
   release_slots(g.b_max, g.nslot);
 }
 
@@ -382,8 +467,9 @@ static int32_t gemm_split16_impl(const uint16_t* Ah, const uint16_t* Al, const f
   NFI_REQUIRE(a_shared || (cpi > 0 && N % cpi == 0), "gemm_split16: cols_per_image=%d must divide N=%d", cpi, N);
   NFI_REQUIRE(batch > 0 && batch <= 65535 && M > 0 && N > 0 && K > 0 && K % gemm::BK == 0,
               "gemm_split16: bad shape batch=%d M=%d N=%d K=%d (K a multiple of %d)", batch, M, N, K, gemm::BK);
-  NFI_REQUIRE((long long)M * K < (1ll << 31) && (long long)K * N < (1ll << 31) && (long long)M * N < (1ll << 31),
-              "gemm_split16: matrix too large");
+  // (each operand and result matrix addressed by 32-bit byte offsets: buffer loads / stores)
+  NFI_REQUIRE((long long)M * K * 2 < (1ll << 31) && (long long)K * N * 4 < (1ll << 31) && (long long)M * N * 4 < (1ll << 31),
+              "gemm_split16: matrix too large (each operand < 2 GiB)");
   NFI_REQUIRE(((uintptr_t)Ah & 15) == 0 && ((uintptr_t)Al & 15) == 0, "gemm_split16: A halves must be 16-B aligned");
   gemm::Args g{reinterpret_cast<const unsigned short*>(Ah), reinterpret_cast<const unsigned short*>(Al), a_inv, B,
                b_max, C, M, N, K, a_shared, 1, K, nullptr, 1, a_shared ? N : cpi, 0};

@@ -654,16 +654,6 @@ __device__ __forceinline__ void split8(const float (&v)[8], u4v& hi, u4v& lo) {
     lo[w] = o;
   }
 }
-// max over the 64 lanes (DPP inside rows, then across rows)
-__device__ __forceinline__ float wave_max_dpp(float v) {
-  v = fmaxf(v, dpp_mov<0xB1>(v));
-  v = fmaxf(v, dpp_mov<0x4E>(v));
-  v = fmaxf(v, dpp_mov<0x141>(v));
-  v = fmaxf(v, dpp_mov<0x140>(v));
-  v = fmaxf(v, __shfl_xor(v, 16));
-  auto s = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
-  return fmaxf(__int_as_float(s[0]), __int_as_float(s[1]));
-}
 // s = 2^e, inv = 2^-e with m s in [2^(top-1), 2^top) (e = 0 for m = 0 or not finite; |e| <= 100)
 __device__ __forceinline__ void pow2_scale(float m, int top, float& s, float& inv) {
   int e = top - __builtin_amdgcn_frexp_expf(m);
