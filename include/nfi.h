@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define NFI_ABI_VERSION 17
+#define NFI_ABI_VERSION 18
 #define NFI_DEC_SIZE 7200   /* floats in the packed decoder buffer (11 outputs: split-f16 tables) */
 #define NFI_DEC_SIZE_VIEWDIR 14384 /* ... with the view-direction mapper (33 outputs) */
 

@@ -204,6 +204,23 @@ int32_t nfi_wino_conv_fused_split(const float* x, const uint16_t* Uh, const uint
 int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, float* y, float* pooled,
                             int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W, void* stream);
 
+/* ---- Direct 3x3 convolution on the f16 matrix cores (csrc/nfi_dconv.hip), for the large-map layers
+ * (F.conv2d(x, w, b, padding=1), lpips VGG16 via metrics.py:107, stylegan.py:130-145 shapes): the
+ * products as the split-f16 GEMM's (fp32-level error), x's power-of-two scale PER IMAGE.
+ * nfi_dconv_pack: w [Co][Ci][3][3] fp32 -> wp [2][9][Ci'/8][Co'][8] fp16 bits (hi planes, then lo) and
+ *   w_inv [1]; flip = 0: the forward weight (Co' = Co, Ci' = Ci); flip = 1: the data gradient's
+ *   w'[ci][co][ky][kx] = w[co][ci][2-ky][2-kx] (Co' = Ci, Ci' = Co).  Ci' % 8 == 0.  Once per frozen
+ *   weight.
+ * nfi_dconv3x3: y [N][Co][H][W] = conv3x3(x', w) with x' = x (relu_y NULL) or x where relu_y > 0
+ *   (threshold_backward of the block's output: the data gradient through the ReLU), then, when bias
+ *   is given, relu(y + bias) and, when pooled is given, pooled = MaxPool2d(2, 2)(y).  slots: each image's
+ *   max |x| (nfi_absmax_slots of x; read, not consumed).  Ci % 16 == 0, Co % 64 == 0, H % 8 == 0,
+ *   W % 64 == 0; wp 16-B aligned. */
+int32_t nfi_dconv_pack(const float* w, int32_t Co, int32_t Ci, int32_t flip, uint16_t* wp, float* w_inv, void* stream);
+int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
+                     const float* bias, float* y, float* pooled, int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W,
+                     void* stream);
+
 /* The 'vgg' inversion loss's augmented copies (run.py:720-767 augment_impl as optimize_iter calls
  * it, run.py:2211-2235): img [B][H][W][3] (the rendered / target image, channels last), grid
  * [B*K][Ho][Wo][2] (affine_grid of each copy's rotation / scale / translation, copy j = b*K + k)

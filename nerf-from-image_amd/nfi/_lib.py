@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('NFI_LIBRARY') or os.path.join(_HERE, 'libnfi_hip.so')
-ABI_VERSION = 17
+ABI_VERSION = 18
 DEC_SIZE = 7200
 DEC_SIZE_VIEWDIR = 14384
 
@@ -194,6 +194,9 @@ SIGNATURES = {
     'nfi_wino_conv_fused': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                              c_void_p]),
+    'nfi_dconv_pack': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p, c_void_p,
+                                        c_void_p]),
+    'nfi_dconv3x3': (ctypes.c_int32, [c_void_p] * 8 + [ctypes.c_int32] * 5 + [c_void_p]),
 }
 
 _lib = None

@@ -9,7 +9,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), 'csrc')
 OUT = os.path.join(HERE, 'libnfi_hip.so')
-SOURCES = ['nfi_rays.hip', 'nfi_render.hip', 'nfi_producer.hip', 'nfi_conv.hip', 'nfi_gemm.hip']
+SOURCES = ['nfi_rays.hip', 'nfi_render.hip', 'nfi_producer.hip', 'nfi_conv.hip', 'nfi_gemm.hip', 'nfi_dconv.hip']
 HEADERS = ['nfi_common.h', 'nfi_host.h']
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-shared', '-munsafe-fp-atomics',
          '-Wall', '-Wno-unused-result']

@@ -68,16 +68,23 @@ KSPLIT = os.environ.get('NFI_KSPLIT', '1') != '0'   # K split of the Winograd pr
 # transform one Winograd row at a time) where the shapes allow — measured slower than fused_kernel's
 # fp32 MFMAs (0.68 vs 0.48-0.51 ms on the 64->64 @128^2 layer), so off unless NFI_FUSED_SPLIT=1
 FUSED_SPLIT = os.environ.get('NFI_FUSED_SPLIT', '0') != '0'
+# Direct convolution on the f16 matrix cores (csrc/nfi_dconv.hip, nfi_dconv3x3) for the large maps: the
+# products as the split GEMM's, x's scale per image, no Winograd round trips through HBM.  Taken for
+# layers with Ci % 16 == 0, Co % 64 == 0, H % 8 == 0, W % 64 == 0 and H*W >= DIRECT_MIN_HW (the LPIPS
+# 128^2 and 64^2 maps) and no modulation scale (NFI_DCONV=0: the Winograd forms everywhere).
+DIRECT = os.environ.get('NFI_DCONV', '1') != '0'
+DIRECT_MIN_HW = int(os.environ.get('NFI_DCONV_MIN_HW', str(64 * 64)))
 
 
 class WeightSet:
     """One orientation of a frozen 3x3 weight, transformed: U [36, M, K] fp32 (the hipBLASLt
-    product), `packed` (the fused kernel's MFMA operands, or None) and `split` = (hi, lo, inverse
-    scales) f16 halves for the split-f16 product (or None)."""
-    __slots__ = ('U', 'packed', 'split', 'vmax')
+    product), `packed` (the fused kernel's MFMA operands, or None), `split` = (hi, lo, inverse
+    scales) f16 halves for the split-f16 product (or None) and `direct` = (packed halves, inverse
+    scale) for the direct convolution nfi_dconv3x3 (or None)."""
+    __slots__ = ('U', 'packed', 'split', 'direct', 'vmax')
 
-    def __init__(self, U, packed, split):
-        self.U, self.packed, self.split = U, packed, split
+    def __init__(self, U, packed, split, direct=None):
+        self.U, self.packed, self.split, self.direct = U, packed, split, direct
         self.vmax = {}   # stream -> the split product's maxima slots (self-clearing: see _slots)
 
 
@@ -122,8 +129,8 @@ def weights(weight: torch.Tensor):
     st = _stream(w.device)
     _call('nfi_wino_weight_transform', _p(w), _p(U), Co, Ci, 0, st)
     _call('nfi_wino_weight_transform', _p(w), _p(Ut), Co, Ci, 1, st)
-    out = (WeightSet(U, _pack(U, Co, Ci, st), _split(U, Ci, st)),
-           WeightSet(Ut, _pack(Ut, Ci, Co, st), _split(Ut, Co, st)))
+    out = (WeightSet(U, _pack(U, Co, Ci, st), _split(U, Ci, st), _direct_pack(w, Co, Ci, False, st)),
+           WeightSet(Ut, _pack(Ut, Ci, Co, st), _split(Ut, Co, st), _direct_pack(w, Co, Ci, True, st)))
     weight._nfi_winograd = (tag, out)          # cached on the (frozen) parameter itself
     return out
 
@@ -137,6 +144,48 @@ def _split(U, K, st):
     inv = torch.empty((U.shape[0],), device=U.device)
     _call('nfi_split16_pack', _p(U), U.shape[0], U.shape[1] * U.shape[2], _p(hi), _p(lo), _p(inv), st)
     return hi, lo, inv
+
+
+def _direct_pack(w, Co, Ci, flip, st):
+    """w [Co, Ci, 3, 3] -> (wp [2 * 9 * Ci * Co] f16 bits, w_inv [1]) for nfi_dconv3x3: the forward weight,
+    or (flip) the data gradient's; None when its input channels are not a multiple of 16."""
+    if not DIRECT or (Co if flip else Ci) % 16:
+        return None
+    wp = torch.empty((2 * 9 * Co * Ci,), device=w.device, dtype=torch.int16)
+    winv = torch.empty((1,), device=w.device)
+    _call('nfi_dconv_pack', _p(w), Co, Ci, 1 if flip else 0, _p(wp), _p(winv), st)
+    return wp, winv
+
+
+def _direct_ok(Uw, x):
+    """Whether conv3x3(x) with this weight orientation runs as nfi_dconv3x3."""
+    N, Ci, H, W = x.shape
+    Co = Uw.U.shape[1]
+    return (DIRECT and Uw.direct is not None and Ci % 16 == 0 and Co % 64 == 0 and H % 8 == 0 and W % 64 == 0
+            and H * W >= DIRECT_MIN_HW)
+
+
+def _direct(x, Uw, bias=None, pool=False, relu_y=None):
+    """conv3x3(x') on the direct kernel, x' = x or x where relu_y > 0; with bias the VGG epilogue
+    (and the pooled map when pool): y or (y, pooled)."""
+    N, Ci, H, W = x.shape
+    Co = Uw.U.shape[1]
+    st = _stream(x.device)
+    slots = torch.empty((slot_words(),), device=x.device, dtype=torch.int32)
+    _call('nfi_absmax_slots', _p(x), N, Ci * H * W, _p(slots), st)
+    y = torch.empty((N, Co, H, W), device=x.device)
+    m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
+    wp, winv = Uw.direct
+    _call('nfi_dconv3x3', _p(x), _p(relu_y), _p(slots), _p(wp), _p(winv), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
+    return (y, m) if pool else y
+
+
+def _conv(x, Uw, bias=None, pool=False, scale=None):
+    """The layer's convolution on its fastest form: the direct kernel where _direct_ok, else
+    Winograd (fused or three-pass)."""
+    if scale is None and _direct_ok(Uw, x):
+        return _direct(x, Uw, bias, pool)
+    return _winograd(x, Uw, bias, pool, scale)
 
 
 def split_matrix(A):
@@ -276,7 +325,7 @@ def _winograd(x, Uw, bias=None, pool=False, scale=None):
 
 def _dgrad(g, ctx):
     if DGRAD:
-        return _winograd(g, ctx.Ut)
+        return _conv(g, ctx.Ut)
     return torch.nn.grad.conv2d_input(ctx.xshape, ctx.weight, g, 1, 1)
 
 
@@ -293,7 +342,7 @@ class _Conv(torch.autograd.Function):
         x = x.contiguous()
         U, Ut = weights(weight)
         ctx.Ut, ctx.xshape, ctx.weight = Ut, x.shape, weight.detach()
-        return _winograd(x, U)
+        return _conv(x, U)
 
     @staticmethod
     def backward(ctx, g):
@@ -314,7 +363,7 @@ class _ModConv(torch.autograd.Function):
         U, Ut = weights(weight)
         ctx.save_for_backward(x, s)
         ctx.Ut, ctx.xshape, ctx.weight = Ut, x.shape, weight.detach()
-        return _winograd(x, U, scale=s)
+        return _conv(x, U, scale=s)
 
     @staticmethod
     def backward(ctx, g):
@@ -344,7 +393,7 @@ class _VggBlock(torch.autograd.Function):
         _require_device(x, weight, bias)
         x = x.contiguous()
         U, Ut = weights(weight)
-        r = _winograd(x, U, bias.detach().contiguous(), pool)
+        r = _conv(x, U, bias.detach().contiguous(), pool)
         y = r[0] if pool else r
         ctx.save_for_backward(y)
         ctx.Ut, ctx.xshape, ctx.weight = Ut, x.shape, weight.detach()
@@ -359,6 +408,9 @@ class _VggBlock(torch.autograd.Function):
         N, C, H, W = y.shape
         gy = None if gy is None else gy.contiguous()
         gm = None if gm is None else gm.contiguous()
+        if gm is None and DGRAD and _direct_ok(ctx.Ut, y):
+            # no pool gradient: the ReLU threshold inside the direct kernel's staging
+            return _direct(gy, ctx.Ut, relu_y=y), None, None, None
         if RELU_IN_TRANSFORM and gm is None and DGRAD and not _fused_ok(ctx.Ut, C, ctx.Ut.U.shape[1]):
             # no pool gradient: the ReLU threshold inside the data gradient's input transform
             st = _stream(y.device)

@@ -1,0 +1,143 @@
+"""The direct 3x3 convolution on the f16 matrix cores (nfi_dconv3x3, csrc/nfi_dconv.hip; nfi.conv's
+form for the LPIPS 128^2 / 64^2 layers) against fp64 convolutions: forward, the VGG block epilogue
+(bias, ReLU, 2x2 max pool), the data gradient with the ReLU mask in the staging, per-image operand
+scales, and the dispatch through conv3x3 / vgg_block.  Bar: the largest error relative to the largest
+output <= max(4 x MIOpen fp32's own, 2e-6) (split-f16 products: 3 2^-22 |a||b| each at worst)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from nfi import conv
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+SHAPES = [(2, 16, 64, 8, 64), (3, 64, 64, 16, 64), (2, 64, 128, 16, 128), (1, 128, 64, 8, 128),
+          (2, 32, 192, 24, 64), (9, 48, 64, 8, 64)]
+
+
+def _err(a, ref):
+    ref = ref.detach()
+    return float((a.detach().double().cpu() - ref).abs().max() / ref.abs().max())
+
+
+def _wset(w):
+    U, Ut = conv.weights(w)
+    assert U.direct is not None and Ut.direct is not None
+    return U, Ut
+
+
+@pytest.mark.parametrize('N,Ci,Co,H,W', SHAPES)
+def test_dconv_forward(N, Ci, Co, H, W):
+    g = torch.Generator(device=DEV).manual_seed(Ci * Co + H + N)
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    U, _ = _wset(w)
+    y = conv._direct(x, U)
+    yd = F.conv2d(x.double().cpu(), w.double().cpu(), padding=1)
+    ym = F.conv2d(x, w, padding=1)
+    e, em = _err(y, yd), _err(ym, yd)
+    print(f'direct {e:.2e}, miopen {em:.2e}')
+    assert e <= max(4 * em, 2e-6), (e, em)
+
+
+@pytest.mark.parametrize('pool', [False, True])
+@pytest.mark.parametrize('N,Ci,Co,H,W', [(2, 64, 64, 16, 64), (3, 32, 128, 8, 128)])
+def test_dconv_vgg_epilogue(N, Ci, Co, H, W, pool):
+    g = torch.Generator(device=DEV).manual_seed(N + Ci + Co + H + pool)
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    U, _ = _wset(w)
+    out = conv._direct(x, U, b, pool)
+    yd = torch.relu(F.conv2d(x.double().cpu(), w.double().cpu(), b.double().cpu(), padding=1))
+    y = out[0] if pool else out
+    assert _err(y, yd) <= 2e-6
+    if pool:
+        assert out[1].shape == (N, Co, H // 2, W // 2)
+        assert _err(out[1], F.max_pool2d(yd, 2, 2)) <= 2e-6
+
+
+@pytest.mark.parametrize('masked', [False, True])
+@pytest.mark.parametrize('N,C,Co,H,W', [(2, 64, 64, 16, 64), (2, 128, 64, 8, 128), (1, 64, 128, 8, 64)])
+def test_dconv_data_gradient(N, C, Co, H, W, masked):
+    """The flipped / transposed pack: conv3x3(g', w') = conv_transpose2d(g', w, padding=1), g' = g or,
+    with relu_y, g where relu_y > 0 (threshold_backward in the staging)."""
+    gen = torch.Generator(device=DEV).manual_seed(N * C + Co + H + masked)
+    w = torch.randn((Co, C, 3, 3), device=DEV, generator=gen) / (3 * C ** 0.5)
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=gen)
+    yv = torch.randn((N, Co, H, W), device=DEV, generator=gen) if masked else None
+    _, Ut = _wset(w)
+    gx = conv._direct(gy, Ut, relu_y=yv)
+    gm = gy * (yv > 0) if masked else gy
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.double().cpu(), gm.double().cpu(), 1, 1)
+    refm = torch.nn.grad.conv2d_input((N, C, H, W), w, gm, 1, 1)
+    e, em = _err(gx, ref), _err(refm, ref)
+    print(f'direct dgrad {e:.2e}, miopen {em:.2e}')
+    assert e <= max(4 * em, 2e-6), (e, em)
+
+
+@pytest.mark.parametrize('small', [1e-6, 1e-9])
+def test_dconv_per_image_scale(small):
+    """One image far below the others keeps its own precision, and its result equals the same image
+    run alone bit for bit (its scale is its own: sharded = unsharded)."""
+    N, Ci, Co, H, W = 4, 64, 64, 16, 64
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    x[2] *= small
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / (3 * Ci ** 0.5)
+    U, _ = _wset(w)
+    y = conv._direct(x, U)
+    yd = F.conv2d(x[2:3].double().cpu(), w.double().cpu(), padding=1)
+    assert _err(y[2:3], yd) <= 2e-6
+    alone = conv._direct(x[2:3].contiguous(), U)
+    assert torch.equal(alone, y[2:3])
+
+
+def test_dconv_lpips_shape_against_miopen():
+    """The LPIPS conv1_2 layer at full size (64 images of 128^2, 64 -> 64, bias, ReLU, pool) against
+    MIOpen fp32 (both near fp32 rounding; relative to the largest output)."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.relu(torch.randn((64, 64, 128, 128), device=DEV, generator=g))
+    w = torch.randn((64, 64, 3, 3), device=DEV, generator=g) / 24.0
+    b = torch.randn((64,), device=DEV, generator=g) * 0.1
+    U, _ = _wset(w)
+    y, m = conv._direct(x, U, b, True)
+    ym = torch.relu(F.conv2d(x, w, b, padding=1))
+    scale = float(ym.abs().max())
+    assert float((y - ym).abs().max()) <= 4e-6 * scale
+    assert torch.equal(m, F.max_pool2d(y, 2, 2))
+
+
+def test_dconv_dispatch_and_autograd(monkeypatch):
+    """vgg_block / conv3x3 take the direct kernel on eligible shapes, forward and backward (the ReLU
+    mask in the staging when there is no pool gradient), and match fp64 autograd."""
+    calls = []
+    real = conv._direct
+
+    def spy(*a, **k):
+        calls.append(a[0].shape)
+        return real(*a, **k)
+
+    monkeypatch.setattr(conv, '_direct', spy)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    N, Ci, Co, H, W = 2, 64, 64, 64, 64
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / 24.0
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=g)
+    xa = x.clone().requires_grad_()
+    y = conv.vgg_block(xa, w, b, False)
+    y.backward(gy)
+    assert len(calls) == 2, calls    # forward + data gradient
+    xd = x.double().cpu().requires_grad_()
+    yd = torch.relu(F.conv2d(xd, w.double().cpu(), b.double().cpu(), padding=1))
+    yd.backward(gy.double().cpu())
+    assert _err(y, yd) <= 2e-6
+    rel = float((xa.grad.double().cpu() - xd.grad).norm() / xd.grad.norm())
+    assert rel < 1e-5, rel
+    calls.clear()
+    xb = x.clone().requires_grad_()
+    conv.conv3x3(xb, w).backward(gy)
+    assert len(calls) == 2, calls
