@@ -130,6 +130,10 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
  * per output: bound by writing y).  W % 4 == 0. */
 int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
                               int32_t H, int32_t W, void* stream);
+/* The same, also leaving each image's max of y in its split-f16 slots ymax (split_slot; zero on entry,
+ * may be NULL): the x scale of the next layer's nfi_dconv3x3 without a maxima pass. */
+int32_t nfi_vgg_first_forward_max(const float* x, const float* w, const float* bias, float* y, uint32_t* ymax,
+                                  int32_t N, int32_t Co, int32_t H, int32_t W, void* stream);
 
 /* Its backward to the image: gx [N,3,H,W] = conv_transpose(gy * (y > 0), w) (threshold_backward then
  * the data gradient; overwritten).  H % 16 == 0, W % 64 == 0. */
@@ -214,12 +218,14 @@ int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, 
  * nfi_dconv3x3: y [N][Co][H][W] = conv3x3(x', w) with x' = x (relu_y NULL) or x where relu_y > 0
  *   (threshold_backward of the block's output: the data gradient through the ReLU), then, when bias
  *   is given, relu(y + bias) and, when pooled is given, pooled = MaxPool2d(2, 2)(y).  slots: each image's
- *   max |x| (nfi_absmax_slots of x; read, not consumed).  Ci % 16 == 0, Co % 64 == 0, H % 8 == 0,
- *   W % 64 == 0; wp 16-B aligned. */
+ *   max |x| (nfi_absmax_slots of x, or the ymax of the dconv that produced x; read, not consumed).
+ *   ymax (may be NULL; zero on entry): each image's max |y| atomically maxed into its slots, the next
+ *   layer's slots (a bound for pooled too).  Ci % 16 == 0, Co % 64 == 0, H % 8 == 0, W % 64 == 0; wp
+ *   16-B aligned. */
 int32_t nfi_dconv_pack(const float* w, int32_t Co, int32_t Ci, int32_t flip, uint16_t* wp, float* w_inv, void* stream);
 int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
-                     const float* bias, float* y, float* pooled, int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W,
-                     void* stream);
+                     const float* bias, float* y, float* pooled, uint32_t* ymax, int32_t N, int32_t Ci, int32_t Co,
+                     int32_t H, int32_t W, void* stream);
 
 /* The 'vgg' inversion loss's augmented copies (run.py:720-767 augment_impl as optimize_iter calls
  * it, run.py:2211-2235): img [B][H][W][3] (the rendered / target image, channels last), grid

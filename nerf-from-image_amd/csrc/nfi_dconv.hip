@@ -75,6 +75,8 @@ struct Args {
   const float* bias;       // null (plain convolution) or [Co]: relu(conv + bias)
   float* y;                // [N][Co][H][W]
   float* pooled;           // null or [N][Co][H/2][W/2]: MaxPool2d(2, 2) of y (needs bias)
+  unsigned* ymax;          // null, or per-image max |y| slots (split_slot layout; atomicMax): the next
+                           // layer's x scale without a maxima pass
   int N, Ci, Co, H, W;
   int tw, th, tco, T;      // tiles per row / per column / channel blocks; total
 };
@@ -287,7 +289,7 @@ __device__ __forceinline__ void chunk(const u4v* __restrict__ cur, u4v* __restri
 // column pairs by DPP (no wait inside the store sequence).
 template <int EPI>
 __device__ __forceinline__ void epilogue(const Args& g, const Tile& d, int cb, int rp, const f16v (&acc)[2][2],
-                                         float f) {
+                                         float f, int t) {
   const int l = lane_id(), kg = l >> 5, lr = l & 31;
   const int HW = g.H * g.W, H2 = g.H >> 1, W2 = g.W >> 1, HW2 = H2 * W2;
   const long long img = (long long)d.n * g.Co;
@@ -306,6 +308,7 @@ __device__ __forceinline__ void epilogue(const Args& g, const Tile& d, int cb, i
     rpool = __builtin_amdgcn_make_buffer_rsrc(g.pooled + img * HW2, (short)0, g.Co * HW2 * 4, 0x00020000);
     vp = (c0 * HW2 + ((d.y0 >> 1) + rp) * W2 + ((d.x0 + lr) >> 1)) * 4;
   }
+  float ym = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int cr = (r & 3) + 8 * (r >> 2);
@@ -316,6 +319,7 @@ __device__ __forceinline__ void epilogue(const Args& g, const Tile& d, int cb, i
       for (int i = 0; i < 2; ++i) {
         v[i] = acc[i][j][r] * f;
         if constexpr (EPI >= 1) v[i] = fmaxf(v[i] + bias[r], 0.f);
+        ym = fmaxf(ym, fabsf(v[i]));
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[i]), ry, vy + (i * g.W + 32 * j) * 4,
                                               cr * HW * 4, 0);
       }
@@ -326,6 +330,10 @@ __device__ __forceinline__ void epilogue(const Args& g, const Tile& d, int cb, i
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rpool, vp + 16 * j * 4, cr * HW2 * 4, 0);
       }
     }
+  }
+  if (g.ymax) {   // one atomic per wave and tile, spread over the image's 64 slots
+    ym = wave_max_dpp(ym);
+    if (l == 0) atomicMax(g.ymax + split_slot(d.n, t * NW + (threadIdx.x >> 6)), __float_as_uint(ym));
   }
 }
 
@@ -404,7 +412,7 @@ __global__ void __launch_bounds__(NT, 1) dconv_kernel(Args g) {
       if (v == 12345.f) g.y[threadIdx.x] = v;
     }
 #else
-    epilogue<EPI>(g, decode(g, t), cb, rp, acc, isx * w_inv);
+    epilogue<EPI>(g, decode(g, t), cb, rp, acc, isx * w_inv, t);
 #endif
     t += tstep;
     if (t >= tend) break;
@@ -472,8 +480,8 @@ int32_t nfi_dconv_pack(const float* w, int32_t Co, int32_t Ci, int32_t flip, uin
 }
 
 int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
-                     const float* bias, float* y, float* pooled, int32_t N, int32_t Ci, int32_t Co, int32_t H, int32_t W,
-                     void* stream) {
+                     const float* bias, float* y, float* pooled, uint32_t* ymax, int32_t N, int32_t Ci, int32_t Co,
+                     int32_t H, int32_t W, void* stream) {
   using namespace dconv;
   NFI_REQUIRE(x && slots && wp && w_inv && y, "dconv3x3: null pointer");
   NFI_REQUIRE(N > 0 && Ci > 0 && Ci % KC == 0 && Co > 0 && Co % CT == 0 && H > 0 && H % TR == 0 && W > 0 && W % TC == 0,
@@ -484,7 +492,7 @@ int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots,
   NFI_REQUIRE(pooled == nullptr || bias != nullptr, "dconv3x3: pooling needs the bias/ReLU epilogue");
   NFI_REQUIRE(pooled == nullptr || relu_y == nullptr, "dconv3x3: the masked (data-gradient) form has no pool epilogue");
   NFI_REQUIRE(((uintptr_t)wp & 15) == 0, "dconv3x3: the packed weight must be 16-B aligned");
-  Args g{x, relu_y, slots, reinterpret_cast<const u4v*>(wp), w_inv, bias, y, pooled, N, Ci, Co, H, W,
+  Args g{x, relu_y, slots, reinterpret_cast<const u4v*>(wp), w_inv, bias, y, pooled, ymax, N, Ci, Co, H, W,
          W / TC, H / TR, Co / CT, 0};
   const long long T = (long long)N * g.th * g.tw * g.tco;
   NFI_REQUIRE(T < (1ll << 30), "dconv3x3: too many tiles");

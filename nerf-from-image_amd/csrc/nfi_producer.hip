@@ -829,11 +829,16 @@ __global__ void __launch_bounds__(64 * LP_WAVES) lpips_bwd_regs_kernel(const flo
 // workgroup per 16 x 64 pixel block: the masked gradient of FB channels at a time is staged in
 // LDS with a 1-pixel halo, each thread accumulates its 4 pixels x 3 input channels.
 // ---------------------------------------------------------------------------------------
+// ymax (optional): each image's max of y (>= 0 after the ReLU) into its split-f16 slots (split_slot):
+// the next layer's direct convolution (nfi_dconv3x3) takes its x scale from them, no maxima pass
 __global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float4* __restrict__ y,
-                                                            int64_t total, int Co, int H, int W) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
+                                                            int64_t total, int Co, int H, int W,
+                                                            unsigned* __restrict__ ymax) {
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = i0 < total;
+  if (!live && ymax == nullptr) return;
+  const int64_t i = live ? i0 : total - 1;   // (lanes past the end: a clamped pixel quad, no store)
   const int W4 = W / 4;
   const int64_t row = i / W4;                // n * H + yy
   const int x0 = (int)(i - row * W4) * 4;
@@ -856,6 +861,7 @@ __global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restr
   }
   float4* yo = y + (((int64_t)n * Co) * H + yy) * W4 + x0 / 4;
   const int64_t plane4 = (int64_t)H * W4;
+  float ym = 0.f;
   for (int co = 0; co < Co; ++co) {
     const float* wc = w + co * 27;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -870,8 +876,20 @@ __global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restr
           for (int k = 0; k < 4; ++k) a[k] = fmaf(wv, v[c][r][k + kx], a[k]);
         }
     const float b = bias[co];
-    yo[co * plane4] = make_float4(fmaxf(a[0] + b, 0.f), fmaxf(a[1] + b, 0.f), fmaxf(a[2] + b, 0.f),
-                                  fmaxf(a[3] + b, 0.f));
+    const float4 o = make_float4(fmaxf(a[0] + b, 0.f), fmaxf(a[1] + b, 0.f), fmaxf(a[2] + b, 0.f), fmaxf(a[3] + b, 0.f));
+    ym = fmaxf(ym, fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w)));
+    if (live) yo[co * plane4] = o;
+  }
+  if (ymax != nullptr) {
+    ym = live ? ym : 0.f;
+    const int n0 = __builtin_amdgcn_readfirstlane(n), n63 = __builtin_amdgcn_readlane(n, 63);
+    if (n0 == n63) {   // (wave-uniform) the wave inside one image: one atomic
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) ym = fmaxf(ym, __shfl_xor(ym, o));
+      if ((threadIdx.x & 63) == 0) atomicMax(ymax + split_slot(n0, blockIdx.x * 4 + (threadIdx.x >> 6)), __float_as_uint(ym));
+    } else if (live) {
+      atomicMax(ymax + split_slot(n, threadIdx.x), __float_as_uint(ym));
+    }
   }
 }
 
@@ -1528,14 +1546,20 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
   return NFI_OK;
 }
 
-int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
-                              int32_t H, int32_t W, void* stream) {
+int32_t nfi_vgg_first_forward_max(const float* x, const float* w, const float* bias, float* y, uint32_t* ymax,
+                                  int32_t N, int32_t Co, int32_t H, int32_t W, void* stream) {
   NFI_REQUIRE(x && w && bias && y, "vgg_first_forward: null pointer");
   NFI_REQUIRE(N > 0 && Co > 0 && H > 0 && W > 0 && W % 4 == 0, "vgg_first_forward: bad shape");
   const int64_t total = (int64_t)N * H * (W / 4);
-  vgg_first_fwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(x, w, bias, (float4*)y, total, Co, H, W);
+  vgg_first_fwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(x, w, bias, (float4*)y, total, Co, H, W,
+                                                                       (unsigned*)ymax);
   NFI_CHECK_LAUNCH("vgg_first_fwd_kernel");
   return NFI_OK;
+}
+
+int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
+                              int32_t H, int32_t W, void* stream) {
+  return nfi_vgg_first_forward_max(x, w, bias, y, nullptr, N, Co, H, W, stream);
 }
 
 int32_t nfi_vgg_first_backward(const float* gy, const float* y, const float* w, float* gx, int32_t N, int32_t Co,

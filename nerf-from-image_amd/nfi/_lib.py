@@ -160,6 +160,7 @@ SIGNATURES = {
     'nfi_syn_up_add_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_vgg_first_forward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 4 + [c_void_p]),
+    'nfi_vgg_first_forward_max': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_vgg_first_backward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_syn_up_add_forward_strided': (ctypes.c_int32, [c_void_p] * 7 + [ctypes.c_int32] * 3 + [c_void_p]),
     'nfi_syn_up_backward_strided': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 3 + [c_void_p]),
@@ -196,7 +197,7 @@ SIGNATURES = {
                                              c_void_p]),
     'nfi_dconv_pack': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p, c_void_p,
                                         c_void_p]),
-    'nfi_dconv3x3': (ctypes.c_int32, [c_void_p] * 8 + [ctypes.c_int32] * 5 + [c_void_p]),
+    'nfi_dconv3x3': (ctypes.c_int32, [c_void_p] * 9 + [ctypes.c_int32] * 5 + [c_void_p]),
 }
 
 _lib = None

@@ -6,7 +6,9 @@ LPIPS VGG16 trunk (lpips 0.1 via lib/metrics.py:107) and the s
 Per layer: input transform (HIP) -> 36 batched [Co x Ci] x [Ci x P] fp32-accurate GEMMs on the f16
 matrix cores (nfi's split-f16 product, csrc/nfi_gemm.hip; torch.bmm / hipBLASLt with NFI_SPLIT16=0)
 -> output transform (HIP, with the VGG block's bias + ReLU + 2x2 max pool fused); the 64-channel
-layers as one fused HIP kernel.  Weight transforms are computed once per frozen weight.  The
+layers as one fused HIP kernel.  The large maps (the LPIPS 128^2 and 64^2 layers, forward and data
+gradient) run instead as a direct convolution on the f16 matrix cores (csrc/nfi_dconv.hip, same
+split-f16 products, no Winograd round trips).  Weight transforms are computed once per frozen weight.  The
 data gradient is the same pipeline with the rot180 / channel-swapped weights (the weights
 receive no gradient: asking for one raises).  csrc/nfi_conv.hip, include/nfi_producer.h.
 
@@ -165,18 +167,37 @@ def _direct_ok(Uw, x):
             and H * W >= DIRECT_MIN_HW)
 
 
+def _maxima_of(t):
+    """The per-image max |t| slots a dconv epilogue left on t (tagged with t's version and storage), or
+    None."""
+    tag = getattr(t, '_nfi_absmax', None)
+    if tag is not None and tag[1] == t._version and tag[2] == t.data_ptr():
+        return tag[0]
+    return None
+
+
 def _direct(x, Uw, bias=None, pool=False, relu_y=None):
     """conv3x3(x') on the direct kernel, x' = x or x where relu_y > 0; with bias the VGG epilogue
-    (and the pooled map when pool): y or (y, pooled)."""
+    (and the pooled map when pool): y or (y, pooled).  x's per-image maxima come from the dconv that
+    produced it when it left them (the VGG blocks' chain), else from one maxima pass; the VGG epilogue
+    leaves y's (a bound for pooled too) on both outputs for the next layer."""
     N, Ci, H, W = x.shape
     Co = Uw.U.shape[1]
     st = _stream(x.device)
-    slots = torch.empty((slot_words(),), device=x.device, dtype=torch.int32)
-    _call('nfi_absmax_slots', _p(x), N, Ci * H * W, _p(slots), st)
+    slots = _maxima_of(x)
+    if slots is None:
+        slots = torch.empty((slot_words(),), device=x.device, dtype=torch.int32)
+        _call('nfi_absmax_slots', _p(x), N, Ci * H * W, _p(slots), st)
     y = torch.empty((N, Co, H, W), device=x.device)
     m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
+    ymax = torch.zeros((slot_words(),), device=x.device, dtype=torch.int32) if bias is not None else None
     wp, winv = Uw.direct
-    _call('nfi_dconv3x3', _p(x), _p(relu_y), _p(slots), _p(wp), _p(winv), _p(bias), _p(y), _p(m), N, Ci, Co, H, W, st)
+    _call('nfi_dconv3x3', _p(x), _p(relu_y), _p(slots), _p(wp), _p(winv), _p(bias), _p(y), _p(m), _p(ymax), N, Ci, Co,
+          H, W, st)
+    if ymax is not None:
+        for t in (y, m):
+            if t is not None:
+                t._nfi_absmax = (ymax, t._version, t.data_ptr())
     return (y, m) if pool else y
 
 

@@ -61,7 +61,8 @@ class VGG16Features(nn.Module):
             conv = f[i]
             pool = i + 2 < len(f) and isinstance(f[i + 2], nn.MaxPool2d)
             if self.winograd and wconv.applicable(x, conv.weight):
-                # Winograd F(4,3): the epilogue (bias, ReLU, pool) runs in the output transform
+                # nfi.conv: the direct split-f16 kernel on the 128^2 / 64^2 maps, Winograd F(4,3)
+                # below; the epilogue (bias, ReLU, pool) fused either way
                 r = wconv.vgg_block(x, conv.weight, conv.bias, pool)
                 y, x = r if pool else (r, r)
                 if i + 1 in TAPS:

@@ -545,8 +545,12 @@ class _VggFirst(torch.autograd.Function):
         Co = w.shape[0]
         y = torch.empty((N, Co, H, W), device=x.device, dtype=x.dtype)
         wd = w.detach().contiguous()
-        _call('nfi_vgg_first_forward', _p(x), _p(wd), _p(bias.detach().contiguous()), _p(y), N, Co, H, W,
-              _stream(x.device))
+        # each image's max of y for the next layer's direct convolution (nfi.conv._direct)
+        from .conv import slot_words
+        ymax = torch.zeros((slot_words(),), device=x.device, dtype=torch.int32)
+        _call('nfi_vgg_first_forward_max', _p(x), _p(wd), _p(bias.detach().contiguous()), _p(y), _p(ymax), N, Co, H,
+              W, _stream(x.device))
+        y._nfi_absmax = (ymax, y._version, y.data_ptr())
         ctx.save_for_backward(y, wd)
         return y
 

@@ -141,3 +141,30 @@ def test_dconv_dispatch_and_autograd(monkeypatch):
     xb = x.clone().requires_grad_()
     conv.conv3x3(xb, w).backward(gy)
     assert len(calls) == 2, calls
+
+
+def test_dconv_chained_maxima_equal_maxima_pass():
+    """The per-image maxima a producer leaves on its output (the LPIPS first layer, a dconv VGG
+    epilogue) give the next dconv the same scale as a maxima pass over that output: equal results, bit
+    for bit; a modified tensor drops them."""
+    from nfi import producer_ops
+    g = torch.Generator(device=DEV).manual_seed(5)
+    img = torch.randn((3, 3, 64, 64), device=DEV, generator=g)
+    w1 = torch.randn((64, 3, 3, 3), device=DEV, generator=g) / 5.0
+    b1 = torch.randn((64,), device=DEV, generator=g) * 0.1
+    w2 = torch.randn((64, 64, 3, 3), device=DEV, generator=g) / 24.0
+    b2 = torch.randn((64,), device=DEV, generator=g) * 0.1
+    w3 = torch.randn((128, 64, 3, 3), device=DEV, generator=g) / 24.0
+    U2, _ = _wset(w2)
+    U3, _ = _wset(w3)
+    with torch.no_grad():
+        y1 = producer_ops.vgg_first(img, w1, b1)
+        assert conv._maxima_of(y1) is not None
+        y2, m2 = conv._direct(y1, U2, b2, True)
+        y2r, m2r = conv._direct(y1.clone(), U2, b2, True)
+        assert torch.equal(y2, y2r) and torch.equal(m2, m2r)
+        assert conv._maxima_of(y2) is not None and conv._maxima_of(m2) is not None
+        y3 = conv._direct(y2, U3, b2.repeat(2))
+        assert torch.equal(y3, conv._direct(y2.clone(), U3, b2.repeat(2)))
+        y2.mul_(2.0)
+        assert conv._maxima_of(y2) is None
