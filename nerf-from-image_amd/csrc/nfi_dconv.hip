@@ -66,6 +66,10 @@ static_assert(CT == 64 && AU % 64 == 0, "weight rows of 64 channels");
 #define NFI_DCONV_EXP 0
 #endif
 
+#ifndef NFI_DCONV_STAUX
+#define NFI_DCONV_STAUX 2   // the epilogue's stores streamed (slc): 128^2 conv1_2 0.335 -> 0.302 ms (0: A/B builds)
+#endif
+
 struct Args {
   const float* x;          // [N][Ci][H][W]
   const float* relu_y;     // null, or [N][Ci][H][W]: x taken where relu_y > 0 (threshold_backward)
@@ -321,13 +325,13 @@ __device__ __forceinline__ void epilogue(const Args& g, const Tile& d, int cb, i
         if constexpr (EPI >= 1) v[i] = fmaxf(v[i] + bias[r], 0.f);
         ym = fmaxf(ym, fabsf(v[i]));
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[i]), ry, vy + (i * g.W + 32 * j) * 4,
-                                              cr * HW * 4, 0);
+                                              cr * HW * 4, NFI_DCONV_STAUX);
       }
       if constexpr (EPI == 2) {
         float m = fmaxf(v[0], v[1]);
         m = fmaxf(m, dpp_mov<0xB1>(m));   // the column pair (lanes l, l ^ 1)
         if (!(lr & 1))
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rpool, vp + 16 * j * 4, cr * HW2 * 4, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, m), rpool, vp + 16 * j * 4, cr * HW2 * 4, NFI_DCONV_STAUX);
       }
     }
   }
@@ -420,22 +424,23 @@ __global__ void __launch_bounds__(NT, 1) dconv_kernel(Args g) {
 }
 
 // w [Co][Ci][3][3] -> wp [2][9][Ci'/8][Co'][8] halves (hi, lo of w 2^e) and w_inv = 2^-e; flip: the
-// data gradient's weight w'[ci][co][ky][kx] = w[co][ci][2 - ky][2 - kx] (Co' = Ci, Ci' = Co).  One
-// workgroup (once per frozen weight).
+// data gradient's weight w'[ci][co][ky][kx] = w[co][ci][2 - ky][2 - kx] (Co' = Ci, Ci' = Co).  Three
+// launches, once per frozen weight: max |w| into w_inv[0] (float bits, atomicMax, zeroed first), the
+// pack (every block reads the maximum), then w_inv[0] = 2^-e.
+__global__ void __launch_bounds__(256) wmax_kernel(const float* __restrict__ w, int n, unsigned* __restrict__ m) {
+  float v = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) v = fmaxf(v, fabsf(w[i]));
+  v = wave_max(v);
+  if (lane_id() == 0) atomicMax(m, __float_as_uint(v));
+}
+
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, int Co, int Ci, int flip,
-                                                   unsigned short* __restrict__ wp, float* __restrict__ w_inv) {
-  __shared__ float red[4];
+                                                   unsigned short* __restrict__ wp, const float* __restrict__ wmax) {
   const int n = Co * Ci * 9;
-  float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, fabsf(w[i]));
-  m = wave_max(m);
-  if (lane_id() == 0) lds_st_fenced(red + (threadIdx.x >> 6), m);
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   float s, inv;
-  pow2_scale15(m, s, inv);
+  pow2_scale15(wmax[0], s, inv);
   const int Cop = flip ? Ci : Co, Cip = flip ? Co : Ci;
-  for (int q = threadIdx.x; q < n; q += 256) {
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) {
     // q = ((tap Ci'/8 + ci' / 8) Co' + co') 8 + ci' % 8
     const int e = q & 7, u = q >> 3;
     const int co = u % Cop, rest = u / Cop;
@@ -446,7 +451,12 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, 
     wp[q] = __builtin_bit_cast(unsigned short, h);
     wp[n + q] = __builtin_bit_cast(unsigned short, (_Float16)(v - (float)h));
   }
-  if (threadIdx.x == 0) w_inv[0] = inv;
+}
+
+__global__ void winv_kernel(float* w_inv) {
+  float s, inv;
+  pow2_scale15(w_inv[0], s, inv);
+  w_inv[0] = inv;
 }
 
 static int cu_count() {
@@ -473,8 +483,13 @@ int32_t nfi_dconv_pack(const float* w, int32_t Co, int32_t Ci, int32_t flip, uin
   NFI_REQUIRE(w && wp && w_inv, "dconv_pack: null pointer");
   NFI_REQUIRE(Co > 0 && Ci > 0 && (flip ? Co : Ci) % 8 == 0 && (long long)Co * Ci * 9 < (1ll << 30),
               "dconv_pack: bad shape Co=%d Ci=%d (input channels of the packed form a multiple of 8)", Co, Ci);
-  hipLaunchKernelGGL(dconv::pack_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, w, Co, Ci, flip ? 1 : 0,
+  hipStream_t st = (hipStream_t)stream;
+  NFI_REQUIRE(hipMemsetAsync(w_inv, 0, 4, st) == hipSuccess, "dconv_pack: memset");
+  const int n = Co * Ci * 9, nb = std::min(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(dconv::wmax_kernel, dim3(nb), dim3(256), 0, st, w, n, reinterpret_cast<unsigned*>(w_inv));
+  hipLaunchKernelGGL(dconv::pack_kernel, dim3(nb), dim3(256), 0, st, w, Co, Ci, flip ? 1 : 0,
                      reinterpret_cast<unsigned short*>(wp), w_inv);
+  hipLaunchKernelGGL(dconv::winv_kernel, dim3(1), dim3(1), 0, st, w_inv);
   NFI_CHECK_LAUNCH("dconv pack_kernel");
   return NFI_OK;
 }

@@ -83,10 +83,11 @@ class WeightSet:
     product), `packed` (the fused kernel's MFMA operands, or None), `split` = (hi, lo, inverse
     scales) f16 halves for the split-f16 product (or None) and `direct` = (packed halves, inverse
     scale) for the direct convolution nfi_dconv3x3 (or None)."""
-    __slots__ = ('U', 'packed', 'split', 'direct', 'vmax')
+    __slots__ = ('U', 'packed', 'split', 'direct', 'direct_src', 'vmax')
 
-    def __init__(self, U, packed, split, direct=None):
+    def __init__(self, U, packed, split, direct=None, direct_src=None):
         self.U, self.packed, self.split, self.direct = U, packed, split, direct
+        self.direct_src = direct_src   # (w, Co, Ci, flip): `direct` packed on first use (_direct_ok)
         self.vmax = {}   # stream -> the split product's maxima slots (self-clearing: see _slots)
 
 
@@ -131,8 +132,8 @@ def weights(weight: torch.Tensor):
     st = _stream(w.device)
     _call('nfi_wino_weight_transform', _p(w), _p(U), Co, Ci, 0, st)
     _call('nfi_wino_weight_transform', _p(w), _p(Ut), Co, Ci, 1, st)
-    out = (WeightSet(U, _pack(U, Co, Ci, st), _split(U, Ci, st), _direct_pack(w, Co, Ci, False, st)),
-           WeightSet(Ut, _pack(Ut, Ci, Co, st), _split(Ut, Co, st), _direct_pack(w, Co, Ci, True, st)))
+    out = (WeightSet(U, _pack(U, Co, Ci, st), _split(U, Ci, st), direct_src=(w, Co, Ci, False)),
+           WeightSet(Ut, _pack(Ut, Ci, Co, st), _split(Ut, Co, st), direct_src=(w, Co, Ci, True)))
     weight._nfi_winograd = (tag, out)          # cached on the (frozen) parameter itself
     return out
 
@@ -163,8 +164,13 @@ def _direct_ok(Uw, x):
     """Whether conv3x3(x) with this weight orientation runs as nfi_dconv3x3."""
     N, Ci, H, W = x.shape
     Co = Uw.U.shape[1]
-    return (DIRECT and Uw.direct is not None and Ci % 16 == 0 and Co % 64 == 0 and H % 8 == 0 and W % 64 == 0
-            and H * W >= DIRECT_MIN_HW)
+    if not (DIRECT and Ci % 16 == 0 and Co % 64 == 0 and H % 8 == 0 and W % 64 == 0 and H * W >= DIRECT_MIN_HW):
+        return False
+    if Uw.direct is None and Uw.direct_src is not None:   # packed on the layer's first direct call
+        w, co, ci, flip = Uw.direct_src
+        Uw.direct = _direct_pack(w, co, ci, flip, _stream(w.device))
+        Uw.direct_src = None
+    return Uw.direct is not None
 
 
 def _maxima_of(t):

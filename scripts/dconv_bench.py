@@ -41,10 +41,10 @@ def main():
         U, Ut = conv.weights(w)
         flops = 2.0 * N * Co * Ci * 9 * H * H
         row = [f'{N:3d}x{Ci:3d}->{Co:3d} @{H:3d}^2']
-        if U.direct is not None and conv._direct_ok(U, x):
+        if conv._direct_ok(U, x):
             t = timeit(lambda: conv._direct(x, U, b, True))
             row.append(f'direct fwd {t:.3f} ms ({flops / t / 1e9:.0f} TF)')
-        if Ut.direct is not None and conv._direct_ok(Ut, gy):
+        if conv._direct_ok(Ut, gy):
             t = timeit(lambda: conv._direct(gy, Ut, relu_y=yv))
             row.append(f'direct dgrad {t:.3f} ms')
         t = timeit(lambda: conv._winograd(x, U, b, True))

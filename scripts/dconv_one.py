@@ -24,6 +24,7 @@ def main():
     b = torch.randn((Co,), device=DEV, generator=g) * 0.1
     yv = torch.randn((N, Ci, H, H), device=DEV, generator=g) if mask else None
     U, _ = conv.weights(w)
+    assert conv._direct_ok(U, x)   # (packs the direct weight)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for i in range(reps + 2):
         if i == 2:

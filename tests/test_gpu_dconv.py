@@ -24,6 +24,10 @@ def _err(a, ref):
 
 def _wset(w):
     U, Ut = conv.weights(w)
+    for ws in (U, Ut):    # (packed on first use)
+        if ws.direct is None:
+            w_, co, ci, flip = ws.direct_src
+            ws.direct = conv._direct_pack(w_, co, ci, flip, conv._stream(w.device))
     assert U.direct is not None and Ut.direct is not None
     return U, Ut
 
