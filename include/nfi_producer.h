@@ -219,11 +219,16 @@ int32_t nfi_wino_conv_fused(const float* x, const float* Ua, const float* bias, 
  *   (threshold_backward of the block's output: the data gradient through the ReLU), then, when bias
  *   is given, relu(y + bias) and, when pooled is given, pooled = MaxPool2d(2, 2)(y).  slots: each image's
  *   max |x| (nfi_absmax_slots of x, or the ymax of the dconv that produced x; read, not consumed).
+ *   xscale (may be NULL; then no relu_y and no bias): [N][Ci], the convolution of x * xscale[n][c] (the
+ *   synthesis layers' modulation, stylegan.py:130); slots then bound max |x xscale| per image
+ *   (nfi_absmax_scaled_slots).
  *   ymax (may be NULL; zero on entry): each image's max |y| atomically maxed into its slots, the next
  *   layer's slots (a bound for pooled too).  Ci % 16 == 0, Co % 64 == 0, H % 8 == 0, W % 64 == 0; wp
  *   16-B aligned. */
 int32_t nfi_dconv_pack(const float* w, int32_t Co, int32_t Ci, int32_t flip, uint16_t* wp, float* w_inv, void* stream);
-int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
+int32_t nfi_absmax_scaled_slots(const float* x, const float* scale, int32_t N, int32_t C, int32_t HW, uint32_t* slots,
+                                void* stream);
+int32_t nfi_dconv3x3(const float* x, const float* xscale, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
                      const float* bias, float* y, float* pooled, uint32_t* ymax, int32_t N, int32_t Ci, int32_t Co,
                      int32_t H, int32_t W, void* stream);
 

@@ -73,6 +73,7 @@ static_assert(CT == 64 && AU % 64 == 0, "weight rows of 64 channels");
 struct Args {
   const float* x;          // [N][Ci][H][W]
   const float* relu_y;     // null, or [N][Ci][H][W]: x taken where relu_y > 0 (threshold_backward)
+  const float* xscale;     // null, or [N][Ci]: x taken times xscale[n][c] (the synthesis layers' modulation)
   const unsigned* slots;   // per-image max |x| (split_slot layout, float bits)
   const u4v* wp;           // [2 (hi, lo)][9][Ci / 8][Co] 16-B units: 8 halves = channels 8k .. 8k + 7
   const float* w_inv;      // [1]: 2^-e of the weight's split
@@ -118,15 +119,16 @@ __device__ __forceinline__ Tile decode(const Args& g, int t) {
 
 // the next chunk's x in registers: unit u = tid + r NT of round r is (k-group, pixel) = channels
 // 8 kg .. 8 kg + 7 of one region pixel
-template <bool MASK>
+template <bool MASK, bool SCALE = false>
 struct Stage {
   float b[BRD][8];
   float m[MASK ? BRD : 1][8];
+  float xs[SCALE ? KC : 1];   // the chunk's 16 channel scales (wave-uniform: scalar registers)
   float smax;
 };
 
-template <bool MASK>
-__device__ __forceinline__ void stage_load(const Args& g, Stage<MASK>& st, int t, int c) {
+template <bool MASK, bool SCALE>
+__device__ __forceinline__ void stage_load(const Args& g, Stage<MASK, SCALE>& st, int t, int c) {
   const Tile d = decode(g, t);
   const int tid = threadIdx.x;
   const int HW = g.H * g.W;
@@ -154,12 +156,17 @@ __device__ __forceinline__ void stage_load(const Args& g, Stage<MASK>& st, int t
         st.m[r][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ry, vo, (c * KC + i) * HW * 4, 0));
     }
   }
+  if constexpr (SCALE) {
+    const float* xs = g.xscale + (long long)d.n * g.Ci + c * KC;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) st.xs[i] = xs[i];
+  }
   st.smax = __uint_as_float(g.slots[split_slot(d.n, lane_id())]);
 }
 
 // round R of the staged x, split with scale s into buffer dst
-template <int R, bool MASK>
-__device__ __forceinline__ void stage_store(const Stage<MASK>& st, float s, u4v* __restrict__ dst) {
+template <int R, bool MASK, bool SCALE>
+__device__ __forceinline__ void stage_store(const Stage<MASK, SCALE>& st, float s, u4v* __restrict__ dst) {
   const int u = threadIdx.x + R * NT;
   if (u < BU) {
     const int kg = u >= NPX ? 1 : 0, p = u - kg * NPX;
@@ -167,6 +174,10 @@ __device__ __forceinline__ void stage_store(const Stage<MASK>& st, float s, u4v*
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
       float v0 = st.b[R][i] * s, v1 = st.b[R][i + 1] * s;
+      if constexpr (SCALE) {   // (x s_c) 2^e: the image scale bounds max |x s_c|
+        v0 *= kg ? st.xs[8 + i] : st.xs[i];
+        v1 *= kg ? st.xs[9 + i] : st.xs[i + 1];
+      }
       if constexpr (MASK) {
         v0 = st.m[R][i] > 0.f ? v0 : 0.f;
         v1 = st.m[R][i + 1] > 0.f ? v1 : 0.f;
@@ -241,9 +252,9 @@ __device__ __forceinline__ void tap_products(const Ops& o, f16v (&acc)[2][2]) {
 // previous tap's 12 MFMAs run (two operand sets; scheduling barriers keep further reads from being
 // hoisted) — with, when `more`, the next chunk's x split into buffer nxt in three rounds behind the
 // MFMAs of taps 6, 7 and 8 (its loads were issued at the chunk's start).
-template <bool MASK>
+template <bool MASK, bool SCALE>
 __device__ __forceinline__ void chunk(const u4v* __restrict__ cur, u4v* __restrict__ nxt, int cb, int rp,
-                                      f16v (&acc)[2][2], const Stage<MASK>& st, bool more, float& inv) {
+                                      f16v (&acc)[2][2], const Stage<MASK, SCALE>& st, bool more, float& inv) {
   const int l = lane_id(), kg = l >> 5, lr = l & 31;
   const u4v* bx = cur + kg * NPXP + (2 * rp) * RC + lr;
   const u4v* aw = cur + OA + kg * CT + 32 * cb + lr;
@@ -341,7 +352,7 @@ __device__ __forceinline__ void epilogue(const Args& g, const Tile& d, int cb, i
   }
 }
 
-template <bool MASK, int EPI>
+template <bool MASK, int EPI, bool SCALE = false>
 __global__ void __launch_bounds__(NT, 1) dconv_kernel(Args g) {
   __shared__ __attribute__((aligned(16))) u4v lds[2 * BUFU];
   const int w = threadIdx.x >> 6;
@@ -363,7 +374,7 @@ __global__ void __launch_bounds__(NT, 1) dconv_kernel(Args g) {
   }
   if (t >= tend) return;   // (workgroup-uniform, before any barrier)
   const int nk = g.Ci / KC;
-  Stage<MASK> st;
+  Stage<MASK, SCALE> st;
   float isx_next;
   {   // the first chunk, staged before the loop
     stage_load(g, st, t, 0);
@@ -459,6 +470,22 @@ __global__ void winv_kernel(float* w_inv) {
   w_inv[0] = inv;
 }
 
+// per-image max |x[n][c][p] s[n][c]| into the split slots (zeroed by the caller): grid (blocks, N)
+__global__ void __launch_bounds__(256) absmax_scaled_kernel(const float* __restrict__ x, const float* __restrict__ sc,
+                                                            int C, int HW, unsigned* __restrict__ slots) {
+  const int n = blockIdx.y;
+  const long long per = (long long)C * HW;
+  const float4* x4 = reinterpret_cast<const float4*>(x + (long long)n * per);
+  float m = 0.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < per / 4; i += (long long)gridDim.x * 256) {
+    const float4 v = x4[i];
+    const float s = fabsf(sc[(long long)n * C + (int)(4 * i / HW)]);
+    m = fmaxf(m, s * fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  m = wave_max(m);
+  if (lane_id() == 0) atomicMax(slots + split_slot(n, blockIdx.x * 4 + (threadIdx.x >> 6)), __float_as_uint(m));
+}
+
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -494,7 +521,21 @@ int32_t nfi_dconv_pack(const float* w, int32_t Co, int32_t Ci, int32_t flip, uin
   return NFI_OK;
 }
 
-int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
+int32_t nfi_absmax_scaled_slots(const float* x, const float* scale, int32_t N, int32_t C, int32_t HW, uint32_t* slots,
+                                void* stream) {
+  NFI_REQUIRE(x && scale && slots && N > 0 && N <= 65535 && C > 0 && HW > 0 && HW % 4 == 0 && ((uintptr_t)x & 15) == 0,
+              "absmax_scaled_slots: bad arguments (HW %% 4 == 0, x 16-B aligned)");
+  hipStream_t st = (hipStream_t)stream;
+  NFI_REQUIRE(hipMemsetAsync(slots, 0, (SPLIT_SLOTS + 1) * 4, st) == hipSuccess, "absmax_scaled_slots: memset");
+  const long long per4 = (long long)C * HW / 4;
+  const int nb = (int)std::max<long long>(1, std::min<long long>((per4 + 255) / 256, std::max(1, 4096 / N)));
+  hipLaunchKernelGGL(dconv::absmax_scaled_kernel, dim3((unsigned)nb, (unsigned)N), dim3(256), 0, st, x, scale, C, HW,
+                     reinterpret_cast<unsigned*>(slots));
+  NFI_CHECK_LAUNCH("absmax_scaled_kernel");
+  return NFI_OK;
+}
+
+int32_t nfi_dconv3x3(const float* x, const float* xscale, const float* relu_y, const uint32_t* slots, const uint16_t* wp, const float* w_inv,
                      const float* bias, float* y, float* pooled, uint32_t* ymax, int32_t N, int32_t Ci, int32_t Co,
                      int32_t H, int32_t W, void* stream) {
   using namespace dconv;
@@ -506,8 +547,10 @@ int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots,
               "dconv3x3: an image or the weight past 2 GiB (32-bit buffer offsets)");
   NFI_REQUIRE(pooled == nullptr || bias != nullptr, "dconv3x3: pooling needs the bias/ReLU epilogue");
   NFI_REQUIRE(pooled == nullptr || relu_y == nullptr, "dconv3x3: the masked (data-gradient) form has no pool epilogue");
+  NFI_REQUIRE(xscale == nullptr || (relu_y == nullptr && bias == nullptr),
+              "dconv3x3: the scaled (modulated) form is a plain convolution (no mask, no epilogue)");
   NFI_REQUIRE(((uintptr_t)wp & 15) == 0, "dconv3x3: the packed weight must be 16-B aligned");
-  Args g{x, relu_y, slots, reinterpret_cast<const u4v*>(wp), w_inv, bias, y, pooled, ymax, N, Ci, Co, H, W,
+  Args g{x, relu_y, xscale, slots, reinterpret_cast<const u4v*>(wp), w_inv, bias, y, pooled, ymax, N, Ci, Co, H, W,
          W / TC, H / TR, Co / CT, 0};
   const long long T = (long long)N * g.th * g.tw * g.tco;
   NFI_REQUIRE(T < (1ll << 30), "dconv3x3: too many tiles");
@@ -516,7 +559,9 @@ int32_t nfi_dconv3x3(const float* x, const float* relu_y, const uint32_t* slots,
   int G = (int)std::min<long long>(T, cus);   // one workgroup per CU
   if (G >= 8) G &= ~7;
   const dim3 grid((unsigned)G), block(NT);
-  if (relu_y && !bias)
+  if (xscale)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(dconv::dconv_kernel<false, 0, true>), grid, block, 0, (hipStream_t)stream, g);
+  else if (relu_y && !bias)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(dconv::dconv_kernel<true, 0>), grid, block, 0, (hipStream_t)stream, g);
   else if (relu_y)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(dconv::dconv_kernel<true, 1>), grid, block, 0, (hipStream_t)stream, g);

@@ -197,7 +197,8 @@ SIGNATURES = {
                                              c_void_p]),
     'nfi_dconv_pack': (ctypes.c_int32, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_void_p, c_void_p,
                                         c_void_p]),
-    'nfi_dconv3x3': (ctypes.c_int32, [c_void_p] * 9 + [ctypes.c_int32] * 5 + [c_void_p]),
+    'nfi_dconv3x3': (ctypes.c_int32, [c_void_p] * 10 + [ctypes.c_int32] * 5 + [c_void_p]),
+    'nfi_absmax_scaled_slots': (ctypes.c_int32, [c_void_p, c_void_p] + [ctypes.c_int32] * 3 + [c_void_p, c_void_p]),
 }
 
 _lib = None

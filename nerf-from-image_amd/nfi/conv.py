@@ -76,6 +76,11 @@ FUSED_SPLIT = os.environ.get('NFI_FUSED_SPLIT', '0') != '0'
 # 128^2 and 64^2 maps) and no modulation scale (NFI_DCONV=0: the Winograd forms everywhere).
 DIRECT = os.environ.get('NFI_DCONV', '1') != '0'
 DIRECT_MIN_HW = int(os.environ.get('NFI_DCONV_MIN_HW', str(64 * 64)))
+# ... and the modulated synthesis layers (the scale folded into the staging, csrc/nfi_dconv.hip xscale):
+# measured SLOWER on the inversion step's 4-image producer (l1 8.32-8.35 vs 8.04-8.12 ms: the Winograd
+# products of 4 images of 128 channels cost no more than the direct form's maxima pass + scale backward
+# pass), so off unless NFI_DCONV_MOD=1 (tests/test_gpu_dconv.py covers it)
+DIRECT_MOD = os.environ.get('NFI_DCONV_MOD', '0') != '0'
 
 
 class WeightSet:
@@ -182,23 +187,27 @@ def _maxima_of(t):
     return None
 
 
-def _direct(x, Uw, bias=None, pool=False, relu_y=None):
+def _direct(x, Uw, bias=None, pool=False, relu_y=None, scale=None):
     """conv3x3(x') on the direct kernel, x' = x or x where relu_y > 0; with bias the VGG epilogue
     (and the pooled map when pool): y or (y, pooled).  x's per-image maxima come from the dconv that
     produced it when it left them (the VGG blocks' chain), else from one maxima pass; the VGG epilogue
-    leaves y's (a bound for pooled too) on both outputs for the next layer."""
+    leaves y's (a bound for pooled too) on both outputs for the next layer.  scale [N, Ci]: the
+    convolution of x * scale[n, c] (the modulated synthesis layers), folded into the staging."""
     N, Ci, H, W = x.shape
     Co = Uw.U.shape[1]
     st = _stream(x.device)
-    slots = _maxima_of(x)
-    if slots is None:
+    slots = _maxima_of(x) if scale is None else None
+    if scale is not None:
+        slots = torch.empty((slot_words(),), device=x.device, dtype=torch.int32)
+        _call('nfi_absmax_scaled_slots', _p(x), _p(scale), N, Ci, H * W, _p(slots), st)
+    elif slots is None:
         slots = torch.empty((slot_words(),), device=x.device, dtype=torch.int32)
         _call('nfi_absmax_slots', _p(x), N, Ci * H * W, _p(slots), st)
     y = torch.empty((N, Co, H, W), device=x.device)
     m = torch.empty((N, Co, H // 2, W // 2), device=x.device) if pool else None
     ymax = torch.zeros((slot_words(),), device=x.device, dtype=torch.int32) if bias is not None else None
     wp, winv = Uw.direct
-    _call('nfi_dconv3x3', _p(x), _p(relu_y), _p(slots), _p(wp), _p(winv), _p(bias), _p(y), _p(m), _p(ymax), N, Ci, Co,
+    _call('nfi_dconv3x3', _p(x), _p(scale), _p(relu_y), _p(slots), _p(wp), _p(winv), _p(bias), _p(y), _p(m), _p(ymax), N, Ci, Co,
           H, W, st)
     if ymax is not None:
         for t in (y, m):
@@ -210,8 +219,8 @@ def _direct(x, Uw, bias=None, pool=False, relu_y=None):
 def _conv(x, Uw, bias=None, pool=False, scale=None):
     """The layer's convolution on its fastest form: the direct kernel where _direct_ok, else
     Winograd (fused or three-pass)."""
-    if scale is None and _direct_ok(Uw, x):
-        return _direct(x, Uw, bias, pool)
+    if (scale is None or (DIRECT_MOD and bias is None and not pool)) and _direct_ok(Uw, x):
+        return _direct(x, Uw, bias, pool, scale=scale)
     return _winograd(x, Uw, bias, pool, scale)
 
 
@@ -401,6 +410,11 @@ class _ModConv(torch.autograd.Function):
         ds = torch.empty((B, C), device=x.device, dtype=x.dtype)
         st = _stream(x.device)
         Co = g.shape[1]
+        if DGRAD and DIRECT_MOD and _direct_ok(ctx.Ut, g):
+            # the data gradient on the direct kernel, then gx = g' s and ds = sum_hw g' x in one pass
+            gxs = _direct(g, ctx.Ut)
+            _call('nfi_syn_scale_backward', _p(gxs), _p(x), _p(s), _p(gx), _p(ds), B * C, H * W, st)
+            return gx, ds, None
         if DGRAD and not _fused_ok(ctx.Ut, Co, C):
             # three-pass data gradient, the scale backward in its output transform
             M = _product(ctx.Ut, g)

@@ -172,3 +172,36 @@ def test_dconv_chained_maxima_equal_maxima_pass():
         assert torch.equal(y3, conv._direct(y2.clone(), U3, b2.repeat(2)))
         y2.mul_(2.0)
         assert conv._maxima_of(y2) is None
+
+
+def test_dconv_modulated_forward_backward(monkeypatch):
+    """modulated_conv3x3 (conv2d(x * s[:, :, None, None], w), stylegan.py:130) on the direct kernel: the
+    scale folded into the staging (per-image maxima of |x s|), the backward as the direct data
+    gradient + nfi_syn_scale_backward; against fp64 autograd."""
+    calls = []
+    real = conv._direct
+
+    def spy(*a, **k):
+        calls.append(k.get('scale') is not None)
+        return real(*a, **k)
+
+    monkeypatch.setattr(conv, '_direct', spy)
+    monkeypatch.setattr(conv, 'DIRECT_MOD', True)
+    g = torch.Generator(device=DEV).manual_seed(13)
+    N, Ci, Co, H, W = 2, 64, 128, 64, 64
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    s = torch.rand((N, Ci), device=DEV, generator=g) * 1.5 + 0.25
+    s[1] *= 1e-3
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / 24.0
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=g)
+    xa, sa = x.clone().requires_grad_(), s.clone().requires_grad_()
+    y = conv.modulated_conv3x3(xa, sa, w)
+    y.backward(gy)
+    assert calls == [True, False], calls
+    xd, sd = x.double().cpu().requires_grad_(), s.double().cpu().requires_grad_()
+    yd = F.conv2d(xd * sd[:, :, None, None], w.double().cpu(), padding=1)
+    yd.backward(gy.double().cpu())
+    for n in range(N):   # each image on its own scale
+        assert _err(y[n], yd[n]) <= 2e-6, n
+    assert float((xa.grad.double().cpu() - xd.grad).norm() / xd.grad.norm()) < 1e-5
+    assert float((sa.grad.double().cpu() - sd.grad).norm() / sd.grad.norm()) < 1e-5
