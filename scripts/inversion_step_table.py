@@ -29,6 +29,8 @@ def group(name):
         return 'LPIPS distance head (nfi HIP)'
     if 'nfi::wino::' in name:
         return 'Winograd transforms (nfi HIP)'
+    if 'nfi::dconv::' in name:
+        return 'direct convolutions (nfi split-f16)'
     if 'nfi::syn::' in name:
         return 'producer epilogues (nfi HIP)'
     if 'nfi::' in name:
