@@ -302,9 +302,18 @@ class _ModConv1x1(torch.autograd.Function):
                 Wq = Wt[:, 32 * q:32 * (q + 1)]
                 gxs = torch.matmul(Wq, gq) if gxs is None else gxs.baddbmm_(Wq.expand(B, -1, -1), gq)
         elif gy.dim() == 5:   # texel-major planes [B, Q, 32, H, W]: the Q planes' channels are one
-            # K = 32 Q contraction (a view: plane and channel strides merge in the texel-major layout) —
-            # one product instead of a product + Q - 1 in-place accumulations over the [B, C, HW] result
-            gxs = torch.matmul(Wt, gy.reshape(B, gy.shape[1] * gy.shape[2], H * W))
+            # K = 32 Q contraction — one product instead of a product + Q - 1 in-place accumulations over
+            # the [B, C, HW] result.  The texel-major gradient ([B][Q][HW][32] in memory) is not a K x HW
+            # matrix (plane stride HW*32, channel stride 1): it goes channel-major by the renderer's
+            # LDS-tiled conversion (nfi_planes_to_channel_major) — a reshape here made ATen's strided
+            # copy, 113 us per step for the 100 MB at B = 4
+            Q = gy.shape[1]
+            if Q == 3 and H == W and gy.permute(0, 1, 3, 4, 2).is_contiguous():
+                gc = torch.empty((B, 3 * 32, H * W), device=gy.device, dtype=gy.dtype)
+                _call('nfi_planes_to_channel_major', _p(gy), B, H, _p(gc), _stream(gy.device))
+            else:
+                gc = gy.reshape(B, Q * gy.shape[2], H * W)
+            gxs = torch.matmul(Wt, gc)
         elif gy.is_contiguous():
             gxs = torch.matmul(Wt, gy.view(B, -1, H * W))
         else:                 # channels-last: [B, HW, O] seen as [B, O, HW] (a transposed operand, no copy)
