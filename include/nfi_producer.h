@@ -130,10 +130,16 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
  * per output: bound by writing y).  W % 4 == 0. */
 int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
                               int32_t H, int32_t W, void* stream);
-/* The same, also leaving each image's max of y in its split-f16 slots ymax (split_slot; zero on entry,
- * may be NULL): the x scale of the next layer's nfi_dconv3x3 without a maxima pass. */
-int32_t nfi_vgg_first_forward_max(const float* x, const float* w, const float* bias, float* y, uint32_t* ymax,
-                                  int32_t N, int32_t Co, int32_t H, int32_t W, void* stream);
+/* The same on the LPIPS ScalingLayer's output (nshift / nscale [3], both NULL: none): the convolution of
+ * (x - nshift[c]) / nscale[c] (metrics.py via lpips 0.1, ATen's operation order; zero padding of the
+ * normalised image), also leaving each image's max of y in its split-f16 slots ymax (split_slot; zero on
+ * entry, may be NULL): the x scale of the next layer's nfi_dconv3x3 without a maxima pass. */
+int32_t nfi_vgg_first_forward_max(const float* x, const float* nshift, const float* nscale, const float* w,
+                                  const float* bias, float* y, uint32_t* ymax, int32_t N, int32_t Co, int32_t H, int32_t W,
+                                  void* stream);
+/* The backward through the ScalingLayer as well: gx = d(conv input) / nscale[c] (nscale NULL: none). */
+int32_t nfi_vgg_first_backward_scaled(const float* gy, const float* y, const float* w, const float* nscale, float* gx,
+                                      int32_t N, int32_t Co, int32_t H, int32_t W, void* stream);
 
 /* Its backward to the image: gx [N,3,H,W] = conv_transpose(gy * (y > 0), w) (threshold_backward then
  * the data gradient; overwritten).  H % 16 == 0, W % 64 == 0. */
@@ -270,7 +276,8 @@ int32_t nfi_aug_affine_grid(const float* theta, int32_t N, int32_t H, int32_t W,
  * nfi_wino_input_transform_max: nfi_wino_input_transform_scaled (scale may be NULL) or, with relu_y,
  *   the ReLU-masked gradient transform, also leaving each image's running maximum of |V| in its
  *   slots.  vmax must hold zeros on entry: a zeroed buffer, or one a split GEMM has consumed.
- * nfi_absmax_slots: the same per-image maxima of any x [nimg][per_image] (zeroes the slots first).
+ * nfi_absmax_slots: the same per-image maxima of any x [nimg][per_image] (every used slot and the counter
+ *   rewritten: no prior zeroing needed).
  * nfi_gemm_split16: A halves [batch][M][K], B [batch][K][N] fp32, b_max from one of the above, C
  *   [batch][M][N] fp32 (written); K a multiple of 32; column n of every B[b] belongs to image
  *   n / cols_per_image (cols_per_image divides N; the Winograd products: tiles per image; N: one image).

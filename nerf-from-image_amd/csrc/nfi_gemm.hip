@@ -416,6 +416,10 @@ __global__ void __launch_bounds__(256) ksum_kernel(const float* __restrict__ wor
 
 // running maximum of |x| per image, x [nimg][per], into the images' slots (generic callers; the
 // Winograd input transform keeps its own, nfi_conv.hip).  grid (blocks per image, nimg)
+// STORE: a grid of exactly SPLIT_ISLOTS blocks per image (<= SPLIT_IMAGES images), block j writing
+// slot j of its image (every slot of the used images written: no memset) and block (0, 0) the
+// completion counter's zero; else atomicMax into zeroed slots
+template <bool STORE>
 __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ x, long long per,
                                                      unsigned* __restrict__ slots) {
   __shared__ float red[4];
@@ -443,8 +447,15 @@ __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ x
   m = wave_max(m);
   if (lane_id() == 0) lds_st_fenced(red + (threadIdx.x >> 6), m);
   __syncthreads();
-  if (threadIdx.x == 0)
-    atomicMax(slots + split_slot(blockIdx.y, blockIdx.x), __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (threadIdx.x == 0) {
+    const unsigned v = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+    if constexpr (STORE) {
+      slots[split_slot(blockIdx.y, blockIdx.x)] = v;
+      if (blockIdx.x == 0 && blockIdx.y == 0) slots[SPLIT_SLOTS] = 0u;
+    } else {
+      atomicMax(slots + split_slot(blockIdx.y, blockIdx.x), v);
+    }
+  }
 }
 
 }  // namespace gemm
@@ -469,10 +480,15 @@ int32_t nfi_split16_slot_words(void) { return SPLIT_SLOTS + 1; }
 
 int32_t nfi_absmax_slots(const float* x, int32_t nimg, int64_t per_image, uint32_t* slots, void* stream) {
   NFI_REQUIRE(x && slots && nimg > 0 && nimg <= 65535 && per_image > 0, "absmax_slots: bad arguments");
-  NFI_REQUIRE(hipMemsetAsync(slots, 0, (SPLIT_SLOTS + 1) * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
-  const long long blocks = std::max<long long>(1, std::min<long long>((per_image + 255) / 256, 4096 / nimg));
-  hipLaunchKernelGGL(gemm::absmax_kernel, dim3((unsigned)blocks, (unsigned)nimg), dim3(256), 0, (hipStream_t)stream, x,
-                     (long long)per_image, slots);
+  if (nimg >= 4096 / SPLIT_ISLOTS && nimg <= SPLIT_IMAGES) {   // (64-256 images) one block per slot: no memset
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::absmax_kernel<true>), dim3(SPLIT_ISLOTS, (unsigned)nimg), dim3(256), 0,
+                       (hipStream_t)stream, x, (long long)per_image, slots);
+  } else {
+    NFI_REQUIRE(hipMemsetAsync(slots, 0, (SPLIT_SLOTS + 1) * 4, (hipStream_t)stream) == hipSuccess, "absmax_slots: memset");
+    const long long blocks = std::max<long long>(1, std::min<long long>((per_image + 255) / 256, 4096 / nimg));
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm::absmax_kernel<false>), dim3((unsigned)blocks, (unsigned)nimg), dim3(256), 0,
+                       (hipStream_t)stream, x, (long long)per_image, slots);
+  }
   NFI_CHECK_LAUNCH("absmax_kernel");
   return NFI_OK;
 }

@@ -834,7 +834,11 @@ __global__ void __launch_bounds__(64 * LP_WAVES) lpips_bwd_regs_kernel(const flo
 __global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ bias, float4* __restrict__ y,
                                                             int64_t total, int Co, int H, int W,
-                                                            unsigned* __restrict__ ymax) {
+                                                            unsigned* __restrict__ ymax, const float* __restrict__ nsh,
+                                                            const float* __restrict__ nsc) {
+  // nsh / nsc (optional, [3]): the LPIPS ScalingLayer (x - shift[c]) / scale[c] (lpips 0.1) applied to the
+  // map's pixels as they load, in ATen's order (subtract, then a correctly rounded division); the zero
+  // padding is the normalised image's, as the reference pads it
   const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool live = i0 < total;
   if (!live && ymax == nullptr) return;
@@ -854,7 +858,8 @@ __global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restr
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int cx = x0 - 1 + j;
-        const float t = xr[min(max(cx, 0), W - 1)];
+        float t = xr[min(max(cx, 0), W - 1)];
+        if (nsh != nullptr) t = __fdiv_rn(t - nsh[c], nsc[c]);
         v[c][r][j] = (ry >= 0 && ry < H && cx >= 0 && cx < W) ? t : 0.f;
       }
     }
@@ -894,9 +899,11 @@ __global__ void __launch_bounds__(256) vgg_first_fwd_kernel(const float* __restr
 }
 
 constexpr int VF_TY = 16, VF_TX = 64, VF_FB = 4;   // pixel block, channels per LDS stage
+// nsc (optional, [3]): the gradient leaves through the ScalingLayer's division (d x = g / scale[c], ATen's
+// div backward)
 __global__ void __launch_bounds__(256) vgg_first_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ y,
                                                             const float* __restrict__ w, float* __restrict__ gx,
-                                                            int Co, int H, int W) {
+                                                            int Co, int H, int W, const float* __restrict__ nsc) {
   __shared__ float M[VF_FB][VF_TY + 2][VF_TX + 3];
   const int tiles_x = W / VF_TX;
   const int Y0 = (blockIdx.x / tiles_x) * VF_TY, X0 = (blockIdx.x % tiles_x) * VF_TX;
@@ -951,9 +958,15 @@ __global__ void __launch_bounds__(256) vgg_first_bwd_kernel(const float* __restr
     }
   }
 #pragma unroll
-  for (int ci = 0; ci < 3; ++ci)
+  for (int ci = 0; ci < 3; ++ci) {
+    if (nsc != nullptr) {
+      const float sc = nsc[ci];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[ci][k] = __fdiv_rn(acc[ci][k], sc);
+    }
     *reinterpret_cast<float4*>(gx + ((int64_t)n * 3 + ci) * HW + (int64_t)(Y0 + ty) * W + X0 + tx4) =
         make_float4(acc[ci][0], acc[ci][1], acc[ci][2], acc[ci][3]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1546,30 +1559,38 @@ int32_t nfi_lpips_head_backward(const float* g, const float* f0, const float* f1
   return NFI_OK;
 }
 
-int32_t nfi_vgg_first_forward_max(const float* x, const float* w, const float* bias, float* y, uint32_t* ymax,
-                                  int32_t N, int32_t Co, int32_t H, int32_t W, void* stream) {
+int32_t nfi_vgg_first_forward_max(const float* x, const float* nshift, const float* nscale, const float* w,
+                                  const float* bias, float* y, uint32_t* ymax, int32_t N, int32_t Co, int32_t H, int32_t W,
+                                  void* stream) {
+  NFI_REQUIRE((nshift == nullptr) == (nscale == nullptr), "vgg_first_forward: shift and scale go together");
   NFI_REQUIRE(x && w && bias && y, "vgg_first_forward: null pointer");
   NFI_REQUIRE(N > 0 && Co > 0 && H > 0 && W > 0 && W % 4 == 0, "vgg_first_forward: bad shape");
   const int64_t total = (int64_t)N * H * (W / 4);
   vgg_first_fwd_kernel<<<blocks(total), 256, 0, (hipStream_t)stream>>>(x, w, bias, (float4*)y, total, Co, H, W,
-                                                                       (unsigned*)ymax);
+                                                                       (unsigned*)ymax, nshift, nscale);
   NFI_CHECK_LAUNCH("vgg_first_fwd_kernel");
   return NFI_OK;
 }
 
 int32_t nfi_vgg_first_forward(const float* x, const float* w, const float* bias, float* y, int32_t N, int32_t Co,
                               int32_t H, int32_t W, void* stream) {
-  return nfi_vgg_first_forward_max(x, w, bias, y, nullptr, N, Co, H, W, stream);
+  return nfi_vgg_first_forward_max(x, nullptr, nullptr, w, bias, y, nullptr, N, Co, H, W, stream);
 }
 
-int32_t nfi_vgg_first_backward(const float* gy, const float* y, const float* w, float* gx, int32_t N, int32_t Co,
+int32_t nfi_vgg_first_backward_scaled(const float* gy, const float* y, const float* w, const float* nscale, float* gx,
+                                      int32_t N, int32_t Co,
                                int32_t H, int32_t W, void* stream) {
   NFI_REQUIRE(gy && y && w && gx, "vgg_first_backward: null pointer");
   NFI_REQUIRE(N > 0 && Co > 0 && H % VF_TY == 0 && W % VF_TX == 0, "vgg_first_backward: bad shape");
   vgg_first_bwd_kernel<<<dim3((unsigned)((H / VF_TY) * (W / VF_TX)), (unsigned)N), 256, 0, (hipStream_t)stream>>>(
-      gy, y, w, gx, Co, H, W);
+      gy, y, w, gx, Co, H, W, nscale);
   NFI_CHECK_LAUNCH("vgg_first_bwd_kernel");
   return NFI_OK;
+}
+
+int32_t nfi_vgg_first_backward(const float* gy, const float* y, const float* w, float* gx, int32_t N, int32_t Co,
+                               int32_t H, int32_t W, void* stream) {
+  return nfi_vgg_first_backward_scaled(gy, y, w, nullptr, gx, N, Co, H, W, stream);
 }
 
 int32_t nfi_vgg_bias_relu_forward(const float* x, const float* bias, float* y, float* pooled,

@@ -160,7 +160,8 @@ SIGNATURES = {
     'nfi_syn_up_add_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_vgg_first_forward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 4 + [c_void_p]),
-    'nfi_vgg_first_forward_max': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
+    'nfi_vgg_first_forward_max': (ctypes.c_int32, [c_void_p] * 7 + [ctypes.c_int32] * 4 + [c_void_p]),
+    'nfi_vgg_first_backward_scaled': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_vgg_first_backward': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_syn_up_add_forward_strided': (ctypes.c_int32, [c_void_p] * 7 + [ctypes.c_int32] * 3 + [c_void_p]),
     'nfi_syn_up_backward_strided': (ctypes.c_int32, [c_void_p] * 4 + [ctypes.c_int32] * 3 + [c_void_p]),

@@ -22,6 +22,8 @@ from __future__ import annotations
 
 import ctypes
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -51,8 +53,13 @@ class VGG16Features(nn.Module):
                 c = v
         self.features = nn.Sequential(*layers)
 
-    def forward(self, x):
+    def forward(self, x, shift=None, scale=None):
+        """The feature taps of x; with shift / scale, of the ScalingLayer's (x - shift) / scale, folded
+        into the first layer's kernels when they apply (else computed here)."""
         out = []
+        from . import producer_ops as _po
+        if shift is not None and not (self.winograd and _po.vgg_first_applicable(x, self.features[0].weight)):
+            x, shift, scale = (x - shift) / scale, None, None
         # each conv block as MIOpen's bias-free convolution + one HIP epilogue pass (bias, ReLU and
         # the following MaxPool2d when there is one; producer_ops.vgg_epilogue)
         from . import conv as wconv, producer_ops
@@ -70,7 +77,7 @@ class VGG16Features(nn.Module):
                 i += 3 if pool else 2
                 continue
             if i == 0 and not pool and producer_ops.vgg_first_applicable(x, conv.weight):
-                x = producer_ops.vgg_first(x, conv.weight, conv.bias)     # conv1_1 + ReLU, one pass
+                x = producer_ops.vgg_first(x, conv.weight, conv.bias, shift, scale)   # (normalise) conv1_1 + ReLU
                 if i + 1 in TAPS:
                     out.append(x)
                 i += 2
@@ -87,6 +94,11 @@ class VGG16Features(nn.Module):
                 out.append(y)
             i += 3 if pool else 2
         return out
+
+
+# the ScalingLayer inside the first VGG layer's kernels (nfi_vgg_first_forward_max / _backward_scaled);
+# NFI_LPIPS_FOLD=0: the two ATen ops each way (A/B)
+FOLD_SCALING = os.environ.get('NFI_LPIPS_FOLD', '1') != '0'
 
 
 class LPIPS(nn.Module):
@@ -116,6 +128,8 @@ class LPIPS(nn.Module):
         return self
 
     def features(self, im):
+        if FOLD_SCALING:   # the ScalingLayer folded into the first layer's pass
+            return self.net(im, self.shift, self.scale)
         return self.net((im - self.shift) / self.scale)
 
     def target_features(self, in1):

@@ -548,29 +548,31 @@ class _VggEpilogue(torch.autograd.Function):
 
 class _VggFirst(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias):
+    def forward(ctx, x, w, bias, shift=None, scale=None):
         x = x.contiguous()
         N, _, H, W = x.shape
         Co = w.shape[0]
         y = torch.empty((N, Co, H, W), device=x.device, dtype=x.dtype)
         wd = w.detach().contiguous()
+        sh = None if shift is None else shift.detach().reshape(3).contiguous()
+        sc = None if scale is None else scale.detach().reshape(3).contiguous()
         # each image's max of y for the next layer's direct convolution (nfi.conv._direct)
         from .conv import slot_words
         ymax = torch.zeros((slot_words(),), device=x.device, dtype=torch.int32)
-        _call('nfi_vgg_first_forward_max', _p(x), _p(wd), _p(bias.detach().contiguous()), _p(y), _p(ymax), N, Co, H,
-              W, _stream(x.device))
+        _call('nfi_vgg_first_forward_max', _p(x), _p(sh), _p(sc), _p(wd), _p(bias.detach().contiguous()), _p(y),
+              _p(ymax), N, Co, H, W, _stream(x.device))
         y._nfi_absmax = (ymax, y._version, y.data_ptr())
-        ctx.save_for_backward(y, wd)
+        ctx.save_for_backward(y, wd, sc)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        y, wd = ctx.saved_tensors
+        y, wd, sc = ctx.saved_tensors
         N, Co, H, W = y.shape
         gx = torch.empty((N, 3, H, W), device=y.device, dtype=y.dtype)
-        _call('nfi_vgg_first_backward', _p(gy.contiguous()), _p(y), _p(wd), _p(gx), N, Co, H, W,
+        _call('nfi_vgg_first_backward_scaled', _p(gy.contiguous()), _p(y), _p(wd), _p(sc), _p(gx), N, Co, H, W,
               _stream(y.device))
-        return gx, None, None
+        return gx, None, None, None, None
 
 
 def vgg_first_applicable(x, w) -> bool:
@@ -578,13 +580,15 @@ def vgg_first_applicable(x, w) -> bool:
             and x.shape[-1] % 64 == 0 and not (torch.is_grad_enabled() and w.requires_grad))
 
 
-def vgg_first(x, w, bias):
-    """relu(conv2d(x, w, bias, padding=1)) for the LPIPS trunk's 3-channel first layer
-    (vgg16.features[0:2]): one direct-convolution pass with the epilogue each way
-    (nfi_vgg_first_forward / _backward); frozen weights (the LPIPS net is not trained)."""
+def vgg_first(x, w, bias, shift=None, scale=None):
+    """relu(conv2d(x', w, bias, padding=1)) for the LPIPS trunk's 3-channel first layer
+    (vgg16.features[0:2]), x' = x or, with shift / scale ([3] or [1, 3, 1, 1]), the ScalingLayer's
+    (x - shift) / scale (lpips 0.1) folded into the same pass: one direct-convolution pass with the
+    epilogue each way (nfi_vgg_first_forward_max / _backward_scaled); frozen weights (the LPIPS net is
+    not trained)."""
     _require_device(x, w, bias)
     _frozen(bias)
-    return _VggFirst.apply(x, w, bias)
+    return _VggFirst.apply(x, w, bias, shift, scale)
 
 
 def vgg_epilogue(x, bias, pool: bool = False):

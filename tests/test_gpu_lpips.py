@@ -190,6 +190,33 @@ def test_vgg_first_layer(N, Co, H, W):
         assert err <= max(1e-6 * m, 4 * err32), (err, err32, m)
 
 
+def test_vgg_first_layer_with_scaling_layer():
+    """The LPIPS ScalingLayer folded into the first layer (lpips 0.1: (x - shift) / scale, then conv1_1 +
+    ReLU): forward equal to the unfolded ops up to one rounding of the normalised input, and the image
+    gradient through the division against fp64 torch."""
+    g = torch.Generator(device=DEV).manual_seed(21)
+    N, Co, H, W = 2, 64, 32, 64
+    net = lpips.LPIPS().to(DEV)
+    x = torch.rand((N, 3, H, W), device=DEV, generator=g) * 2 - 1
+    w = torch.randn((Co, 3, 3, 3), device=DEV, generator=g) * 0.3
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=g)
+    xa = x.clone().requires_grad_()
+    y = producer_ops.vgg_first(xa, w, b, net.shift, net.scale)
+    y.backward(gy)
+    xb = x.clone().requires_grad_()
+    yb = producer_ops.vgg_first((xb - net.shift) / net.scale, w, b)
+    yb.backward(gy)
+    assert float((y - yb).abs().max()) <= 1e-6 * float(yb.abs().max())
+    x64 = x.double().requires_grad_()
+    y64 = torch.relu(torch.nn.functional.conv2d((x64 - net.shift.double()) / net.scale.double(), w.double(),
+                                                b.double(), padding=1))
+    y64.backward(gy.double())
+    m = float(x64.grad.abs().max())
+    assert float((xa.grad.double() - x64.grad).abs().max()) <= 4 * max(
+        float((xb.grad.double() - x64.grad).abs().max()), 1e-7 * m)
+
+
 def test_vgg_target_on_side_stream_matches_inline():
     """The target half of the 'vgg' loss (grid + target features) computed on a side stream gives
     the inline loss and gradient (same device draws, same kernels); the inversion
