@@ -157,6 +157,10 @@ int32_t nfi_vgg_bias_relu_forward(const float* x, const float* bias, float* y, f
  * the first maximum of each 2x2 window, row-major).  gy or gpooled may be NULL (not both). */
 int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float* y, float* gx,
                               int32_t P, int32_t H, int32_t W, void* stream);
+/* The pooled form, also leaving each image's max |gx| (C planes per image) in its split-f16 slots gmax
+ * (split_slot; zero on entry): the data gradient's nfi_dconv3x3 without a maxima pass. */
+int32_t nfi_vgg_relu_backward_max(const float* gy, const float* gpooled, const float* y, float* gx, uint32_t* gmax,
+                                  int32_t P, int32_t C, int32_t H, int32_t W, void* stream);
 
 /* Winograd F(4x4, 3x3) convolution (stride 1, padding 1), the 3x3 convolutions of the LPIPS VGG16
  * trunk (lpips 0.1 via metrics.py:107) and of the synthesis layers (stylegan.py:130-145), i.e.

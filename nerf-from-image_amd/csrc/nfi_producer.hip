@@ -1039,9 +1039,13 @@ __global__ void __launch_bounds__(256) vgg_relu_pool_bwd_kernel(const float* __r
                                                                 const float* __restrict__ gm,
                                                                 const float* __restrict__ y,
                                                                 float* __restrict__ gx, int64_t npatch,
-                                                                int H, int W) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= npatch) return;
+                                                                int H, int W, unsigned* __restrict__ gmax, int C) {
+  // gmax (optional): each image's max |gx| (C planes per image) into its split-f16 slots, for the data
+  // gradient's direct convolution (nfi_dconv3x3) without a maxima pass
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = i0 < npatch;
+  if (!live && gmax == nullptr) return;
+  const int64_t i = live ? i0 : npatch - 1;
   const int W4 = W >> 2, H2 = H >> 1;
   const int qx = (int)(i % W4);
   const int64_t t = i / W4;
@@ -1064,10 +1068,28 @@ __global__ void __launch_bounds__(256) vgg_relu_pool_bwd_kernel(const float* __r
     if (k0 == 0) gu.x += g2.x; else if (k0 == 1) gu.y += g2.x; else if (k0 == 2) gv.x += g2.x; else gv.y += g2.x;
     if (k1 == 0) gu.z += g2.y; else if (k1 == 1) gu.w += g2.y; else if (k1 == 2) gv.z += g2.y; else gv.w += g2.y;
   }
-  *reinterpret_cast<float4*>(gx + o0) = make_float4(yu.x > 0.f ? gu.x : 0.f, yu.y > 0.f ? gu.y : 0.f,
-                                                    yu.z > 0.f ? gu.z : 0.f, yu.w > 0.f ? gu.w : 0.f);
-  *reinterpret_cast<float4*>(gx + o0 + W) = make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f,
-                                                        yv.z > 0.f ? gv.z : 0.f, yv.w > 0.f ? gv.w : 0.f);
+  const float4 ou = make_float4(yu.x > 0.f ? gu.x : 0.f, yu.y > 0.f ? gu.y : 0.f, yu.z > 0.f ? gu.z : 0.f,
+                                yu.w > 0.f ? gu.w : 0.f);
+  const float4 ov = make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f, yv.z > 0.f ? gv.z : 0.f,
+                                yv.w > 0.f ? gv.w : 0.f);
+  if (live) {
+    *reinterpret_cast<float4*>(gx + o0) = ou;
+    *reinterpret_cast<float4*>(gx + o0 + W) = ov;
+  }
+  if (gmax != nullptr) {
+    float m = fmaxf(fmaxf(fmaxf(fabsf(ou.x), fabsf(ou.y)), fmaxf(fabsf(ou.z), fabsf(ou.w))),
+                    fmaxf(fmaxf(fabsf(ov.x), fabsf(ov.y)), fmaxf(fabsf(ov.z), fabsf(ov.w))));
+    m = live ? m : 0.f;
+    const int n = (int)(p / C);
+    const int n0 = __builtin_amdgcn_readfirstlane(n), n63 = __builtin_amdgcn_readlane(n, 63);
+    if (n0 == n63) {   // (wave-uniform) the wave inside one image: one atomic
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      if ((threadIdx.x & 63) == 0) atomicMax(gmax + split_slot(n0, blockIdx.x * 4 + (threadIdx.x >> 6)), __float_as_uint(m));
+    } else if (live) {
+      atomicMax(gmax + split_slot(n, threadIdx.x), __float_as_uint(m));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1612,6 +1634,16 @@ int32_t nfi_vgg_bias_relu_forward(const float* x, const float* bias, float* y, f
   return NFI_OK;
 }
 
+int32_t nfi_vgg_relu_backward_max(const float* gy, const float* gpooled, const float* y, float* gx, uint32_t* gmax,
+                                  int32_t P, int32_t C, int32_t H, int32_t W, void* stream) {
+  NFI_REQUIRE(y && gx && gpooled && gmax && C > 0 && P % C == 0, "vgg_relu_backward_max: bad arguments");
+  NFI_REQUIRE(P > 0 && H > 0 && W > 0 && W % 4 == 0 && H % 2 == 0, "vgg_relu_backward_max: bad shape");
+  const int64_t np = (int64_t)P * (H / 2) * (W / 4);
+  vgg_relu_pool_bwd_kernel<<<blocks(np), 256, 0, (hipStream_t)stream>>>(gy, gpooled, y, gx, np, H, W, (unsigned*)gmax, C);
+  NFI_CHECK_LAUNCH("vgg_relu_pool_bwd_kernel");
+  return NFI_OK;
+}
+
 int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float* y, float* gx,
                               int32_t P, int32_t H, int32_t W, void* stream) {
   NFI_REQUIRE(y && gx && (gy || gpooled), "vgg_relu_backward: null pointer");
@@ -1620,7 +1652,7 @@ int32_t nfi_vgg_relu_backward(const float* gy, const float* gpooled, const float
   hipStream_t st = (hipStream_t)stream;
   if (gpooled) {
     const int64_t np = (int64_t)P * (H / 2) * (W / 4);
-    vgg_relu_pool_bwd_kernel<<<blocks(np), 256, 0, st>>>(gy, gpooled, y, gx, np, H, W);
+    vgg_relu_pool_bwd_kernel<<<blocks(np), 256, 0, st>>>(gy, gpooled, y, gx, np, H, W, nullptr, 1);
     NFI_CHECK_LAUNCH("vgg_relu_pool_bwd_kernel");
   } else {
     const int64_t n4 = (int64_t)P * H * W / 4;

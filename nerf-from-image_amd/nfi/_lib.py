@@ -178,6 +178,7 @@ SIGNATURES = {
     'nfi_vgg_bias_relu_forward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p,
                                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                    ctypes.c_int32, c_void_p]),
+    'nfi_vgg_relu_backward_max': (ctypes.c_int32, [c_void_p] * 5 + [ctypes.c_int32] * 4 + [c_void_p]),
     'nfi_vgg_relu_backward': (ctypes.c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, c_void_p]),
     'nfi_wino_weight_transform': (ctypes.c_int32, [c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32,

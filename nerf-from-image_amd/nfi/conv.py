@@ -461,7 +461,14 @@ class _VggBlock(torch.autograd.Function):
             _call('nfi_wino_output_transform', _p(M), None, _p(gx), None, N, Ci, H, W, st)
             return gx, None, None, None
         gz = torch.empty_like(y)
-        _call('nfi_vgg_relu_backward', _p(gy), _p(gm), _p(y), _p(gz), N * C, H, W, _stream(y.device))
+        if gm is not None and DGRAD and _direct_ok(ctx.Ut, y):
+            # the pool routing + ReLU pass leaves gz's per-image maxima for the direct data gradient
+            gmax = torch.zeros((slot_words(),), device=y.device, dtype=torch.int32)
+            _call('nfi_vgg_relu_backward_max', _p(gy), _p(gm), _p(y), _p(gz), _p(gmax), N * C, C, H, W,
+                  _stream(y.device))
+            gz._nfi_absmax = (gmax, gz._version, gz.data_ptr())
+        else:
+            _call('nfi_vgg_relu_backward', _p(gy), _p(gm), _p(y), _p(gz), N * C, H, W, _stream(y.device))
         return _dgrad(gz, ctx), None, None, None
 
 

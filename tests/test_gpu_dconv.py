@@ -205,3 +205,25 @@ def test_dconv_modulated_forward_backward(monkeypatch):
         assert _err(y[n], yd[n]) <= 2e-6, n
     assert float((xa.grad.double().cpu() - xd.grad).norm() / xd.grad.norm()) < 1e-5
     assert float((sa.grad.double().cpu() - sd.grad).norm() / sd.grad.norm()) < 1e-5
+
+
+def test_dconv_vgg_block_pool_backward():
+    """vgg_block with the pool on the direct path: the pool routing + ReLU backward leaves gz's per-image
+    maxima for the direct data gradient (no maxima pass), against fp64 autograd."""
+    g = torch.Generator(device=DEV).manual_seed(17)
+    N, Ci, Co, H, W = 2, 64, 64, 64, 64
+    x = torch.randn((N, Ci, H, W), device=DEV, generator=g)
+    w = torch.randn((Co, Ci, 3, 3), device=DEV, generator=g) / 24.0
+    b = torch.randn((Co,), device=DEV, generator=g) * 0.1
+    gy = torch.randn((N, Co, H, W), device=DEV, generator=g)
+    gm = torch.randn((N, Co, H // 2, W // 2), device=DEV, generator=g)
+    xa = x.clone().requires_grad_()
+    y, m = conv.vgg_block(xa, w, b, True)
+    torch.autograd.backward([y, m], [gy, gm])
+    xd = x.double().cpu().requires_grad_()
+    yd = torch.relu(F.conv2d(xd, w.double().cpu(), b.double().cpu(), padding=1))
+    md = F.max_pool2d(yd, 2, 2)
+    torch.autograd.backward([yd, md], [gy.double().cpu(), gm.double().cpu()])
+    assert _err(y, yd) <= 2e-6 and _err(m, md) <= 2e-6
+    rel = float((xa.grad.double().cpu() - xd.grad).norm() / xd.grad.norm())
+    assert rel < 1e-4, rel    # (a pool argmax can flip on a near-tie)
